@@ -1,0 +1,131 @@
+// api.cpp — C-ABI entry points of libfccf (context, errors, stage exports).
+// The registration driver itself lives in pipeline.cpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "ctx.h"
+#include "kernels.h"
+#include "pipeline.h"
+
+using namespace fccf;
+
+extern "C" void fccf_params_default(fccf_params* p) {
+  if (!p) return;
+  // FCCF.cpp:126-175
+  p->parameter_l1 = 0.5f; p->parameter_l2 = 1.0f; p->parameter_k1 = 5.0f; p->parameter_k2 = 2.0f;
+  p->normal_vector_threshold1 = 5.0f; p->normal_vector_threshold2 = 8.0f;
+  p->face_voxel_size = 1.0f;
+  p->voxel_point_threshold = 5;
+  p->curvature_threshold = 0.05f;
+  p->select_plane_number = 15;
+  p->quick_verify_angel_threshold = 10.0f; p->quick_verify_distance_threshold = 2.0f;
+  p->required_optimize_plane = 4.0f;
+  p->fine_verify_voxel_size = 0.5f; p->fine_verify_number = 4;
+  p->included_angle_same_threshold = 5.0f; p->included_angle_min_threshold = 30.0f;
+  p->included_angle_max_threshold = 150.0f;
+  p->third_plane_threshold = 0.5f; p->third_plane_normal_threshold = 5.0f;
+  p->cluster_number_threshold = 10; p->cluster_angel_threshold = 2.0f; p->cluster_distance_threshold = 0.8f;
+  p->seclct_cluster_number = 200;
+  p->rough_threshold_gl = 2;
+}
+
+extern "C" const char* fccf_strerror(int code) {
+  switch (code) {
+    case FCCF_OK: return "ok";
+    case FCCF_E_ARG: return "invalid argument";
+    case FCCF_E_HIP: return "HIP runtime error";
+    case FCCF_E_RCCL: return "collective error";
+    case FCCF_E_OOM: return "out of memory";
+    case FCCF_E_IO: return "I/O error";
+    case FCCF_E_INTERNAL: return "internal error";
+    case FCCF_E_NODEVICE: return "no usable HIP device";
+    default: return "unknown error";
+  }
+}
+
+extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
+  if (!out) return FCCF_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return FCCF_E_NODEVICE;
+  if (device < 0 || device >= n) return FCCF_E_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCCF_E_HIP;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return FCCF_E_NODEVICE;  // code objects are gfx950-only
+  fccf_ctx* c = new fccf_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) { delete c; return FCCF_E_HIP; }
+  for (auto& s : c->st)
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { delete c; return FCCF_E_HIP; }
+  *out = c;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
+  if (!c) return FCCF_E_ARG;
+  (void)hipSetDevice(c->device);
+  for (auto& s : c->st)
+    if (s) (void)hipStreamDestroy(s);
+  delete c;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_ctx_set_debug(fccf_ctx* c, int on) {
+  if (!c) return FCCF_E_ARG;
+  c->debug = on != 0;
+  if (!c->debug) c->dbg.clear();
+  return FCCF_OK;
+}
+
+extern "C" int fccf_debug_get(fccf_ctx* c, const char* name, void* buf, int64_t cap, int64_t* nbytes) {
+  if (!c || !name) return FCCF_E_ARG;
+  auto it = c->dbg.find(name);
+  if (it == c->dbg.end()) return FCCF_E_ARG;
+  const int64_t n = (int64_t)it->second.size();
+  if (nbytes) *nbytes = n;
+  if (buf && cap > 0) std::memcpy(buf, it->second.data(), (size_t)std::min(n, cap));
+  return FCCF_OK;
+}
+
+template <class F>
+static int guarded(fccf_ctx* c, F&& f) {
+  try {
+    HIP_CHECK(hipSetDevice(c->device));
+    f();
+    return FCCF_OK;
+  } catch (const Error& e) {
+    c->last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    return FCCF_E_OOM;
+  } catch (...) {
+    return FCCF_E_INTERNAL;
+  }
+}
+
+extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out, int64_t* m) {
+  if (!c || (!xyz && n) || !out || !m || n < 0 || n > (int64_t)0x7FFFFFFF || !(leaf > 0.f)) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    hipStream_t st = c->st[0];
+    const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
+    c->arena.ensure(voxel_grid_bytes(cap) + 12 * (size_t)cap * 2 + (1 << 20));
+    c->arena.reset();
+    float* d_in = c->arena.take_n<float>(3 * (size_t)cap);
+    float* d_out = c->arena.take_n<float>(3 * (size_t)cap);
+    uint32_t* d_sc = c->arena.take_n<uint32_t>(64);
+    VGBufs b = voxel_grid_carve(c->arena, cap);
+    uint32_t hn = (uint32_t)n;
+    HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
+    voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st);
+    HIP_CHECK(hipGetLastError());
+    uint32_t hm = 0;
+    HIP_CHECK(hipMemcpyAsync(&hm, d_sc + 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    HIP_CHECK(hipMemcpyAsync(out, d_out, 12 * (size_t)hm, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    *m = hm;
+  });
+}

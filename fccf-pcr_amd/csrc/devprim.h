@@ -1,0 +1,48 @@
+// devprim.h — device-wide primitives used by the FCCF kernels (gfx950, wave64).
+// Every size is read from device memory (d_n) so the whole pipeline can be
+// enqueued without host round-trips; grids are sized for the capacity.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fccf {
+
+constexpr int RS_THREADS = 256;               // 4 waves
+constexpr int RS_CHUNKS = 8;                  // 64-key chunks per wave
+constexpr int RS_TILE = RS_THREADS * RS_CHUNKS;  // 2048 keys per block
+
+inline uint32_t rs_blocks(uint32_t cap) { return (cap + RS_TILE - 1) / RS_TILE; }
+
+// Scratch for radix_sort_pairs / segment_heads: hist needs 256*blocks u32,
+// tot 256 u32, blk blocks+1 u32.
+struct SortScratch {
+  uint32_t* hist;
+  uint32_t* tot;
+  uint32_t* blk;
+};
+size_t sort_scratch_bytes(uint32_t cap);
+SortScratch sort_scratch_carve(void* base, uint32_t cap);
+
+// Stable LSD radix sort of (key, val) by the low *d_nbits bits of key (8-bit
+// digits).  The sorted result is always left in (k0, v0); (k1, v1) are temporaries.
+// If vals_iota, v0 is ignored on input and the values are the input positions.
+void radix_sort_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* d_n,
+                    uint32_t cap, const uint32_t* d_nbits, int max_bits, bool vals_iota,
+                    SortScratch s, hipStream_t st);
+void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, const uint32_t* d_n,
+                    uint32_t cap, const uint32_t* d_nbits, int max_bits, bool vals_iota,
+                    SortScratch s, hipStream_t st);
+
+// Run-length segmentation of sorted keys[0..*d_n): starts[s] = first index of
+// segment s, starts[S] = *d_n, *d_nseg = S.  Keys equal to `invalid` (which sort
+// last) are excluded: the valid prefix ends at the first invalid key.
+void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid,
+                       uint32_t* starts, uint32_t* d_nseg, SortScratch s, hipStream_t st);
+void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts,
+                       uint32_t* d_nseg, SortScratch s, hipStream_t st);
+
+// Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
+void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap,
+                        uint32_t* d_total, SortScratch s, hipStream_t st);
+
+}  // namespace fccf

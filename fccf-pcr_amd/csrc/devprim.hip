@@ -1,0 +1,320 @@
+// devprim.hip — stable LSD radix sort, run-length segmentation and exclusive scan
+// for gfx950.  Wave64-native: per-digit ranks come from 8 ballots per 64-key
+// chunk (no 32-lane warp idioms), block = 4 waves, tile = 2048 keys.
+#include "devprim.h"
+
+namespace fccf {
+
+namespace {
+
+constexpr int T = RS_THREADS;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+// popcount(mask & lanes_below_me)
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Exclusive scan over the 256 threads of a block; sh needs 4 u32.
+__device__ __forceinline__ uint32_t block_scan_256(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint32_t wp = 0;
+  for (uint32_t w = 0; w < wave; ++w) wp += sh[w];
+  const uint32_t tot = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
+__device__ __forceinline__ uint32_t passes_of(uint32_t nbits) { return (nbits + 7u) / 8u; }
+
+template <class K>
+__global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
+                                               const uint32_t* __restrict__ d_nbits, int shift,
+                                               uint32_t* __restrict__ hist, uint32_t nblocks) {
+  if ((uint32_t)shift >= *d_nbits) return;
+  __shared__ uint32_t cnt[256];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t n = *d_n;
+  const uint32_t base = blockIdx.x * RS_TILE;
+  const uint32_t end = min(base + (uint32_t)RS_TILE, n);
+  for (uint32_t i = base + threadIdx.x; i < end; i += T) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+  __syncthreads();
+  hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// One block per digit: exclusive scan of that digit's per-block counts in place.
+__global__ void __launch_bounds__(T) k_rs_rowscan(uint32_t* __restrict__ hist, uint32_t nblocks,
+                                                  uint32_t* __restrict__ tot, const uint32_t* __restrict__ d_nbits,
+                                                  int shift) {
+  if ((uint32_t)shift >= *d_nbits) return;
+  __shared__ uint32_t sh[4];
+  const uint32_t d = blockIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nblocks; b0 += T) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nblocks ? hist[d * nblocks + i] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_scan_256(v, sh, &t);
+    if (i < nblocks) hist[d * nblocks + i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) tot[d] = carry;
+}
+
+template <class K>
+__global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                  const uint32_t* __restrict__ d_n,
+                                                  const uint32_t* __restrict__ d_nbits, int shift,
+                                                  const uint32_t* __restrict__ hist,
+                                                  const uint32_t* __restrict__ tot, uint32_t nblocks, int iota) {
+  if ((uint32_t)shift >= *d_nbits) return;
+  __shared__ uint32_t dbase[256];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t sh[4];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  {
+    uint32_t t;
+    dbase[tid] = block_scan_256(tot[tid], sh, &t);
+  }
+  for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+  __syncthreads();
+  const uint32_t n = *d_n;
+  const uint32_t base = blockIdx.x * RS_TILE + wave * (RS_CHUNKS * 64);
+  K kk[RS_CHUNKS];
+  uint32_t vv[RS_CHUNKS], rk[RS_CHUNKS], dg[RS_CHUNKS];
+  bool ok[RS_CHUNKS];
+#pragma unroll
+  for (int c = 0; c < RS_CHUNKS; ++c) {
+    const uint32_t i = base + c * 64 + lane;
+    ok[c] = i < n;
+    kk[c] = ok[c] ? kin[i] : (K)0;
+    vv[c] = ok[c] ? (iota ? i : vin[i]) : 0u;
+    const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
+    dg[c] = d;
+    const uint64_t valid = __ballot(ok[c]);
+    uint64_t m = valid;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t r = mbcnt(m);
+    const uint32_t pre = wcnt[wave][d];
+    rk[c] = pre + r;
+    if (ok[c] && r == 0) wcnt[wave][d] = pre + (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  {
+    uint32_t s = 0;
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t t = wcnt[w][tid];
+      wcnt[w][tid] = s;
+      s += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < RS_CHUNKS; ++c) {
+    if (!ok[c]) continue;
+    const uint32_t d = dg[c];
+    const uint32_t pos = dbase[d] + hist[d * nblocks + blockIdx.x] + wcnt[wave][d] + rk[c];
+    kout[pos] = kk[c];
+    vout[pos] = vv[c];
+  }
+}
+
+template <class K>
+__global__ void k_rs_copyback(const K* __restrict__ k1, const uint32_t* __restrict__ v1, K* __restrict__ k0,
+                              uint32_t* __restrict__ v0, const uint32_t* __restrict__ d_n,
+                              const uint32_t* __restrict__ d_nbits, int max_passes) {
+  const uint32_t p = min(passes_of(*d_nbits), (uint32_t)max_passes);
+  if ((p & 1u) == 0u) return;
+  const uint32_t n = *d_n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    k0[i] = k1[i];
+    v0[i] = v1[i];
+  }
+}
+
+template <class K>
+void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
+                const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
+  const uint32_t nb = rs_blocks(cap);
+  if (nb == 0) return;
+  const int max_passes = (max_bits + 7) / 8;
+  K* kb[2] = {k0, k1};
+  uint32_t* vb[2] = {v0, v1};
+  for (int p = 0; p < max_passes; ++p) {
+    const int shift = 8 * p;
+    const int src = p & 1, dst = src ^ 1;
+    k_rs_hist<K><<<nb, T, 0, st>>>(kb[src], d_n, d_nbits, shift, s.hist, nb);
+    k_rs_rowscan<<<256, T, 0, st>>>(s.hist, nb, s.tot, d_nbits, shift);
+    k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb,
+                                      (iota && p == 0) ? 1 : 0);
+  }
+  const uint32_t g = min(nb * 8u, 2048u);
+  k_rs_copyback<K><<<g, 256, 0, st>>>(k1, v1, k0, v0, d_n, d_nbits, max_passes);
+}
+
+// ---------------------------------------------------------------- segments / scan
+template <class K, bool HasInvalid>
+__device__ __forceinline__ bool is_head(const K* keys, uint32_t i, uint32_t n, K invalid) {
+  if (i >= n) return false;
+  const K k = keys[i];
+  if (HasInvalid && k == invalid) return false;
+  return i == 0 || keys[i - 1] != k;
+}
+
+template <class K, bool HasInvalid>
+__global__ void __launch_bounds__(T) k_seg_count(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
+                                                 K invalid, uint32_t* __restrict__ blk) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = *d_n;
+  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  uint32_t c = 0;
+  for (int j = 0; j < RS_CHUNKS; ++j) c += is_head<K, HasInvalid>(keys, i0 + j, n, invalid) ? 1u : 0u;
+  uint32_t t;
+  block_scan_256(c, sh, &t);
+  if (threadIdx.x == 0) blk[blockIdx.x] = t;
+}
+
+// single block: exclusive scan of blk[0..nb) in place, blk[nb] = total, *d_out = total
+__global__ void __launch_bounds__(T) k_scan_blocks(uint32_t* __restrict__ blk, uint32_t nb, uint32_t* __restrict__ d_out) {
+  __shared__ uint32_t sh[4];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += T) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? blk[i] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_scan_256(v, sh, &t);
+    if (i < nb) blk[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) {
+    blk[nb] = carry;
+    if (d_out) *d_out = carry;
+  }
+}
+
+template <class K, bool HasInvalid>
+__global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
+                                                 K invalid, const uint32_t* __restrict__ blk,
+                                                 uint32_t* __restrict__ starts) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = *d_n;
+  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  bool h[RS_CHUNKS];
+  uint32_t c = 0;
+  for (int j = 0; j < RS_CHUNKS; ++j) {
+    h[j] = is_head<K, HasInvalid>(keys, i0 + j, n, invalid);
+    c += h[j] ? 1u : 0u;
+  }
+  uint32_t t;
+  uint32_t pos = blk[blockIdx.x] + block_scan_256(c, sh, &t);
+  for (int j = 0; j < RS_CHUNKS; ++j) {
+    const uint32_t i = i0 + j;
+    if (h[j]) starts[pos++] = i;
+    // end of the valid prefix: close the last segment
+    if (i < n) {
+      const bool valid = !HasInvalid || keys[i] != invalid;
+      const bool next_valid = (i + 1 < n) && (!HasInvalid || keys[i + 1] != invalid);
+      if (valid && !next_valid) starts[pos] = i + 1;  // pos == segment count here
+    }
+  }
+}
+
+template <class K, bool HasInvalid>
+void segment_heads(const K* keys, const uint32_t* d_n, uint32_t cap, K invalid, uint32_t* starts, uint32_t* d_nseg,
+                   SortScratch s, hipStream_t st) {
+  const uint32_t nb = rs_blocks(cap);
+  if (nb == 0) return;
+  k_seg_count<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk);
+  k_scan_blocks<<<1, T, 0, st>>>(s.blk, nb, d_nseg);
+  k_seg_write<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk, starts);
+}
+
+__global__ void __launch_bounds__(T) k_sum_tiles(const uint32_t* __restrict__ in, const uint32_t* __restrict__ d_n,
+                                                 uint32_t* __restrict__ blk) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = *d_n;
+  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  uint32_t c = 0;
+  for (int j = 0; j < RS_CHUNKS; ++j) c += (i0 + j < n) ? in[i0 + j] : 0u;
+  uint32_t t;
+  block_scan_256(c, sh, &t);
+  if (threadIdx.x == 0) blk[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(T) k_scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                  const uint32_t* __restrict__ d_n, const uint32_t* __restrict__ blk) {
+  __shared__ uint32_t sh[4];
+  const uint32_t n = *d_n;
+  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  uint32_t v[RS_CHUNKS], c = 0;
+  for (int j = 0; j < RS_CHUNKS; ++j) {
+    v[j] = (i0 + j < n) ? in[i0 + j] : 0u;
+    c += v[j];
+  }
+  uint32_t t;
+  uint32_t run = blk[blockIdx.x] + block_scan_256(c, sh, &t);
+  for (int j = 0; j < RS_CHUNKS; ++j) {
+    if (i0 + j < n) out[i0 + j] = run;
+    run += v[j];
+  }
+}
+
+}  // namespace
+
+size_t sort_scratch_bytes(uint32_t cap) {
+  const size_t nb = rs_blocks(cap) + 1;
+  return sizeof(uint32_t) * (256 * nb + 256 + nb + 1) + 256;
+}
+
+SortScratch sort_scratch_carve(void* base, uint32_t cap) {
+  const size_t nb = rs_blocks(cap) + 1;
+  uint32_t* p = (uint32_t*)base;
+  SortScratch s;
+  s.hist = p;
+  s.tot = p + 256 * nb;
+  s.blk = s.tot + 256;
+  return s;
+}
+
+void radix_sort_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
+                    const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
+  radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, max_bits, iota, s, st);
+}
+void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
+                    const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
+  radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, max_bits, iota, s, st);
+}
+void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid, uint32_t* starts,
+                       uint32_t* d_nseg, SortScratch s, hipStream_t st) {
+  segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st);
+}
+void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts, uint32_t* d_nseg,
+                       SortScratch s, hipStream_t st) {
+  segment_heads<uint64_t, false>(keys, d_n, cap, (uint64_t)0, starts, d_nseg, s, st);
+}
+void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap, uint32_t* d_total,
+                        SortScratch s, hipStream_t st) {
+  const uint32_t nb = rs_blocks(cap);
+  if (nb == 0) return;
+  k_sum_tiles<<<nb, T, 0, st>>>(in, d_n, s.blk);
+  k_scan_blocks<<<1, T, 0, st>>>(s.blk, nb, d_total);
+  k_scan_tiles<<<nb, T, 0, st>>>(in, out, d_n, s.blk);
+}
+
+}  // namespace fccf

@@ -1,0 +1,82 @@
+// kernels.h — launchers of the FCCF HIP kernels (one .hip file per stage).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "devprim.h"
+#include "fccf_math.h"
+
+namespace fccf {
+
+// ------------------------------------------------ K1: VoxelGrid (FCCF.cpp:1668-1678, :1377-1387)
+struct VGParams {
+  float mn[3], mx[3];
+  float inv;
+  uint32_t nfinite;
+  int32_t min_b[3];
+  int32_t div_b[3];
+  int64_t mul1, mul2;
+  uint32_t overflow;  // int32 index guard tripped: output = input
+  uint32_t nbits;     // radix bits (0 when overflow / empty)
+  uint32_t pad[2];
+};
+
+constexpr int VG_BBOX_BLOCKS = 512;
+
+struct VGBufs {
+  uint32_t *k0, *v0, *k1, *v1;  // cap each
+  uint32_t* starts;             // cap + 1
+  float* part;                  // VG_BBOX_BLOCKS * 8
+  VGParams* params;
+  uint32_t* nseg;
+  SortScratch ss;
+};
+
+// xyz[0..*d_n) -> out[0..*d_m), PCL VoxelGrid<PointXYZ> semantics with stable
+// (ascending input index) accumulation inside a leaf.
+void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf, float* out, uint32_t* d_m,
+                VGBufs b, hipStream_t st);
+
+// ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
+struct VoxRec {  // one occupied octree leaf, Morton order
+  float c[3];
+  float n[3];   // oriented normal (planar) / raw eigenvector
+  int32_t count;
+  float curvature;
+};
+
+struct FaceBufs {
+  uint64_t *c0, *c1;       // codes, cap each
+  uint32_t *v0, *v1;       // cap each
+  uint32_t* starts;        // cap + 1
+  float* aggr;             // per 1024-point block: min xyz, max xyz (6 floats)
+  OctState* oct;
+  float* centroid;         // 4 floats
+  VoxRec* recs;            // cap (all leaves)
+  uint32_t* flag_planar;   // cap
+  uint32_t* resid_cnt;     // cap
+  uint32_t* planar_off;    // cap
+  uint32_t* resid_off;     // cap
+  uint32_t* nleaf;         // scalars
+  uint32_t* nbits;
+  uint32_t* nplanar;
+  uint32_t* nresid;
+  SortScratch ss;
+};
+
+// Launch the sequential cloud-centroid reduction (PCL compute3DCentroid order).
+void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, hipStream_t st);
+// Octree leaves + per-leaf plane fit + compaction.  `centroid` must be ready
+// before the fit kernel runs (the caller orders the streams).
+void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
+                         hipStream_t st);
+void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float voxel_point_threshold,
+                     float curvature_threshold, VoxRec* planar_out, float* resid_out, FaceBufs b, hipStream_t st);
+
+// Octree bound simulation over xyz[0..*d_n) starting from *state (single workgroup).
+void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr,
+                OctState* state, hipStream_t st);
+void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st);
+constexpr uint32_t AGGR_BLOCK = 4096;
+
+}  // namespace fccf

@@ -1,0 +1,215 @@
+"""fccf_amd — ctypes binding of libfccf (include/fccf.h) for tests and bench.
+
+This is the Python mirror of the reference's operator surface for the path: the
+reference itself is a C++ CLI (`./FCCF src tar voxel`, FCCF.cpp:1646-1689) around
+`computer_transform_guess` (FCCF.cpp:1370).  `register()` is that driver plus
+main's VoxelGrid pass, on the GPU.  There is no CPU fallback: loading fails loudly
+if lib/libfccf.so is missing, and Ctx() raises when no gfx950 device is present.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfccf.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libfccf not built: {LIB_PATH} missing (run `make -C fccf-pcr_amd` or __graft_entry__.build())")
+_lib = ctypes.CDLL(LIB_PATH)
+
+FCCF_OK = 0
+E_ARG, E_HIP, E_RCCL, E_OOM, E_IO, E_INTERNAL, E_NODEVICE = -1, -2, -3, -4, -5, -6, -7
+T_NAMES = ["downsample", "voxelfit", "grow", "select", "match", "cluster", "verify", "fine", "fuse", "h2d"]
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in (
+        "parameter_l1", "parameter_l2", "parameter_k1", "parameter_k2",
+        "normal_vector_threshold1", "normal_vector_threshold2", "face_voxel_size",
+        "voxel_point_threshold", "curvature_threshold", "select_plane_number",
+        "quick_verify_angel_threshold", "quick_verify_distance_threshold", "required_optimize_plane",
+        "fine_verify_voxel_size", "fine_verify_number", "included_angle_same_threshold",
+        "included_angle_min_threshold", "included_angle_max_threshold", "third_plane_threshold",
+        "third_plane_normal_threshold", "cluster_number_threshold", "cluster_angel_threshold",
+        "cluster_distance_threshold", "seclct_cluster_number", "rough_threshold_gl")]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "n_src", "n_tar", "m_src", "m_tar", "vox1", "vox2", "res1", "res2", "groups1", "groups2",
+        "planes1", "planes2", "bases1", "bases2", "K", "K_pass")] + [
+        ("cand", ctypes.c_int64 * 3), ("fine", ctypes.c_int64 * 3), ("lm_solves", ctypes.c_int64),
+        ("overflow_passthrough", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double)]
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "reserved")}
+        d["cand"] = list(self.cand)
+        d["fine"] = list(self.fine)
+        d["ms"] = dict(zip(T_NAMES, list(self.ms)))
+        return d
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("fccf_params_default", None, ctypes.POINTER(Params))
+_sig("fccf_strerror", ctypes.c_char_p, ctypes.c_int)
+_sig("fccf_ctx_create", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int)
+_sig("fccf_ctx_destroy", ctypes.c_int, _P)
+_sig("fccf_ctx_set_debug", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
+     ctypes.POINTER(Stats))
+_sig("fccf_register_device", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
+     ctypes.POINTER(Stats))
+_sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
+_sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
+_sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
+     ctypes.POINTER(_I64))
+_sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
+_sig("fccf_free", None, _P)
+_sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
+     ctypes.c_double, _P)
+_sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P, _P, _P)
+
+
+class FCCFError(RuntimeError):
+    def __init__(self, code, where=""):
+        self.code = code
+        super().__init__(f"{where}: {_lib.fccf_strerror(code).decode()} ({code})")
+
+
+def _check(rc, where):
+    if rc != FCCF_OK:
+        raise FCCFError(rc, where)
+
+
+def default_params() -> Params:
+    p = Params()
+    _lib.fccf_params_default(ctypes.byref(p))
+    return p
+
+
+def _f32(a):
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 3)
+    return a
+
+
+class Ctx:
+    """One fccf_ctx (bound to one HIP device and its own streams)."""
+
+    def __init__(self, device: int = 0, debug: bool = False):
+        self._h = _P()
+        _check(_lib.fccf_ctx_create(ctypes.byref(self._h), int(device)), "fccf_ctx_create")
+        if debug:
+            _check(_lib.fccf_ctx_set_debug(self._h, 1), "fccf_ctx_set_debug")
+
+    def close(self):
+        if self._h:
+            _lib.fccf_ctx_destroy(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def register(self, src, tar, leaf: float, params: Params | None = None):
+        """T (4x4 float32) mapping src-file points to the tar-file frame, and stats."""
+        s, t = _f32(src), _f32(tar)
+        T = np.zeros(16, np.float32)
+        st = Stats()
+        rc = _lib.fccf_register(self._h, s.ctypes.data, s.shape[0], t.ctypes.data, t.shape[0], float(leaf),
+                                ctypes.byref(params) if params is not None else None, T.ctypes.data,
+                                ctypes.byref(st))
+        _check(rc, "fccf_register")
+        return T.reshape(4, 4), st
+
+    def register_device(self, d_src: int, n_src: int, d_tar: int, n_tar: int, leaf: float,
+                        params: Params | None = None):
+        """Same, with both clouds already resident in HBM (device pointers as ints)."""
+        T = np.zeros(16, np.float32)
+        st = Stats()
+        rc = _lib.fccf_register_device(self._h, _P(d_src), int(n_src), _P(d_tar), int(n_tar), float(leaf),
+                                       ctypes.byref(params) if params is not None else None, T.ctypes.data,
+                                       ctypes.byref(st))
+        _check(rc, "fccf_register_device")
+        return T.reshape(4, 4), st
+
+    def downsample(self, xyz, leaf: float):
+        a = _f32(xyz)
+        out = np.zeros_like(a) if a.shape[0] else np.zeros((1, 3), np.float32)
+        m = _I64()
+        _check(_lib.fccf_stage_downsample(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data,
+                                          ctypes.byref(m)), "fccf_stage_downsample")
+        return out[: m.value].copy()
+
+    def debug(self, name: str, dtype=np.float32):
+        n = _I64()
+        rc = _lib.fccf_debug_get(self._h, name.encode(), None, 0, ctypes.byref(n))
+        if rc != FCCF_OK:
+            return None
+        buf = np.zeros(n.value // np.dtype(dtype).itemsize, dtype)
+        _check(_lib.fccf_debug_get(self._h, name.encode(), buf.ctypes.data, n.value, ctypes.byref(n)), "debug")
+        return buf
+
+
+def strerror(code: int) -> str:
+    return _lib.fccf_strerror(code).decode()
+
+
+def ply_read(path: str) -> np.ndarray:
+    p = ctypes.POINTER(ctypes.c_float)()
+    n = _I64()
+    _check(_lib.fccf_ply_read(path.encode(), ctypes.byref(p), ctypes.byref(n)), f"fccf_ply_read({path})")
+    try:
+        return np.ctypeslib.as_array(p, shape=(n.value * 3,)).reshape(-1, 3).copy() if n.value else np.zeros((0, 3), np.float32)
+    finally:
+        _lib.fccf_free(p)
+
+
+def ply_write(path: str, xyz, binary: bool = True):
+    a = _f32(xyz)
+    _check(_lib.fccf_ply_write(path.encode(), a.ctypes.data, a.shape[0], 1 if binary else 0), "fccf_ply_write")
+
+
+def synth_scene(n: int, room=(20.0, 15.0, 4.0), seed: int = 1, crop_x_frac: float = 0.0) -> np.ndarray:
+    out = np.zeros((max(n, 1), 3), np.float32)
+    _check(_lib.fccf_synth_scene(n, *map(float, room), seed, crop_x_frac, out.ctypes.data), "fccf_synth_scene")
+    return out[:n]
+
+
+def synth_pair(n: int, room=(20.0, 15.0, 4.0)):
+    """(src, tar, T_gt): tar = scene cropped to x <= 0.8 Lx, src = scene mapped by T_gt^-1."""
+    src = np.zeros((max(n, 1), 3), np.float32)
+    tar = np.zeros((max(n, 1), 3), np.float32)
+    T = np.zeros(16, np.float32)
+    _check(_lib.fccf_synth_pair(n, *map(float, room), src.ctypes.data, tar.ctypes.data, T.ctypes.data),
+           "fccf_synth_pair")
+    return src[:n], tar[:n], T.reshape(4, 4)
+
+
+# Workloads of BASELINE.json configs[1..4]; configs[0] is the ETH PLY pair.
+CONFIGS = {
+    "c2": dict(n=100_000, room=(20.0, 15.0, 4.0), leaf=0.1),
+    "c3": dict(n=1_000_000, room=(20.0, 15.0, 4.0), leaf=0.05),
+    "c4": dict(n=5_000_000, room=(30.0, 24.0, 6.0), leaf=0.05),
+    "c5": dict(n=10_000_000, room=(30.0, 24.0, 6.0), leaf=0.02),
+}

@@ -1,0 +1,136 @@
+/* fccf.h — C-ABI of libfccf, the MI355X-native FCCF-PCR registration path.
+ *
+ * Drop-in boundary.  The reference has no library surface of
+ * its own: its only entry points are the CLI `./FCCF src.ply tar.ply voxel`
+ * (/root/reference/FCCF.cpp:1646-1689) and the in-process driver
+ *   void computer_transform_guess(PointCloud<PointXYZ>::Ptr source,
+ *                                 PointCloud<PointXYZ>::Ptr target,
+ *                                 Eigen::Matrix4f& best)            (FCCF.cpp:1370)
+ * which `main` calls as (cloud_tar, cloud_src) after one VoxelGrid pass per cloud
+ * (FCCF.cpp:1668-1683).  fccf_register() replaces the whole of main's compute
+ * (both VoxelGrid passes + the driver) with plain pointers: inputs in FILE order
+ * (src, tar), output T maps src-file points into the tar-file frame, exactly the
+ * matrix the reference prints.  Inputs are never mutated (the reference's driver
+ * mutates its clouds via removeNaNFromPointCloud, FCCF.cpp:1374-1375).
+ *
+ * All functions return 0 (FCCF_OK) or a negative FCCF_E_* code; no C++ exception
+ * crosses this boundary.  One fccf_ctx per host thread; a ctx is bound to one HIP
+ * device and stream.  There is no CPU fallback: fccf_ctx_create fails with
+ * FCCF_E_NODEVICE when no gfx950 device is present.
+ */
+#ifndef FCCF_H_
+#define FCCF_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  FCCF_OK = 0,
+  FCCF_E_ARG = -1,      /* bad argument (null pointer, leaf <= 0, n < 0 ...)        */
+  FCCF_E_HIP = -2,      /* a HIP runtime call failed                                 */
+  FCCF_E_RCCL = -3,     /* a collective failed                                       */
+  FCCF_E_OOM = -4,      /* device or host allocation failed                          */
+  FCCF_E_IO = -5,       /* PLY read/write failed                                     */
+  FCCF_E_INTERNAL = -6, /* capacity / invariant violation inside the pipeline        */
+  FCCF_E_NODEVICE = -7  /* no usable HIP device                                      */
+};
+
+/* The 26 tunables of FCCF.cpp:120-176, same names and reference defaults
+ * (fccf_params_default).  Passed explicitly instead of globals. */
+typedef struct fccf_params {
+  float parameter_l1, parameter_l2, parameter_k1, parameter_k2;          /* :126-129 */
+  float normal_vector_threshold1, normal_vector_threshold2;              /* :131-132 */
+  float face_voxel_size;                                                 /* :134 (1.0 m; only 1.0 and 0.5 are exact) */
+  float voxel_point_threshold;                                           /* :136 */
+  float curvature_threshold;                                             /* :138 */
+  float select_plane_number;                                             /* :141 */
+  float quick_verify_angel_threshold, quick_verify_distance_threshold;   /* :145-146 */
+  float required_optimize_plane;                                         /* :147 */
+  float fine_verify_voxel_size, fine_verify_number;                      /* :150-151 */
+  float included_angle_same_threshold, included_angle_min_threshold,
+        included_angle_max_threshold;                                    /* :156-158 */
+  float third_plane_threshold, third_plane_normal_threshold;             /* :160,162 */
+  float cluster_number_threshold, cluster_angel_threshold,
+        cluster_distance_threshold;                                      /* :166-168 */
+  float seclct_cluster_number;                                           /* :171 */
+  float rough_threshold_gl;                                              /* :175 */
+} fccf_params;
+
+/* Per-call counters and per-stage device/host timings (ms). */
+enum {
+  FCCF_T_DOWNSAMPLE = 0, FCCF_T_VOXELFIT, FCCF_T_GROW, FCCF_T_SELECT, FCCF_T_MATCH,
+  FCCF_T_CLUSTER, FCCF_T_VERIFY, FCCF_T_FINE, FCCF_T_FUSE, FCCF_T_H2D, FCCF_T_COUNT
+};
+typedef struct fccf_stats {
+  int64_t n_src, n_tar;          /* input points                                  */
+  int64_t m_src, m_tar;          /* after both VoxelGrid passes                   */
+  int64_t vox1, vox2;            /* planar 1 m voxels (driver source / target)    */
+  int64_t res1, res2;            /* residual (non-planar) points S1, S2           */
+  int64_t groups1, groups2;      /* region-growing groups after stage 2           */
+  int64_t planes1, planes2;      /* selected planes F1, F2 (<= 16)                */
+  int64_t bases1, bases2;        /* coplane pairs B1, B2                          */
+  int64_t K;                     /* coplane-pair correspondence tests = B1*B2     */
+  int64_t K_pass;                /* tests that passed (computer_transform calls)  */
+  int64_t cand[3];               /* candidate transforms per roughness type       */
+  int64_t fine[3];               /* cluster-fused candidates per type             */
+  int64_t lm_solves;             /* quick_verify refinements run                  */
+  int32_t overflow_passthrough;  /* VoxelGrid int32 guard tripped (any pass)      */
+  int32_t reserved;
+  double ms[FCCF_T_COUNT];       /* stage wall times                              */
+  double ms_total;               /* host arrays (or resident device arrays) -> T  */
+} fccf_stats;
+
+typedef struct fccf_ctx fccf_ctx;
+
+void fccf_params_default(fccf_params* p);
+const char* fccf_strerror(int code);
+
+/* device: HIP ordinal (the ctx creates its own non-blocking stream). */
+int fccf_ctx_create(fccf_ctx** ctx, int device);
+int fccf_ctx_destroy(fccf_ctx* ctx);
+/* Keep per-stage intermediates for fccf_debug_get (tests). Off by default. */
+int fccf_ctx_set_debug(fccf_ctx* ctx, int on);
+
+/* Whole registration from host arrays (xyz float32, 3*n, FILE order src/tar).
+ * leaf = the CLI voxel argument (FCCF.cpp:1650).  params may be NULL (defaults).
+ * T_rowmajor receives the 4x4 the reference prints (FCCF.cpp:1687).  stats may be NULL. */
+int fccf_register(fccf_ctx* ctx, const float* src_xyz, int64_t n_src, const float* tar_xyz,
+                  int64_t n_tar, float leaf, const fccf_params* params, float T_rowmajor[16],
+                  fccf_stats* stats);
+
+/* Same, with both clouds already resident in device memory of ctx's device. */
+int fccf_register_device(fccf_ctx* ctx, const float* d_src_xyz, int64_t n_src,
+                         const float* d_tar_xyz, int64_t n_tar, float leaf,
+                         const fccf_params* params, float T_rowmajor[16], fccf_stats* stats);
+
+/* Stage export: PCL VoxelGrid<PointXYZ> (FCCF.cpp:1668-1678) on the GPU.
+ * out_xyz capacity 3*n floats; *m receives the output count.  Output order is
+ * ascending leaf index; points of one leaf are summed in ascending input order. */
+int fccf_stage_downsample(fccf_ctx* ctx, const float* xyz, int64_t n, float leaf, float* out_xyz,
+                          int64_t* m);
+
+/* Named intermediate of the last fccf_register call with debug on (see DESIGN.md
+ * "Debug names").  Copies min(cap_bytes, size) bytes; *n_bytes = full size. */
+int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes,
+                   int64_t* n_bytes);
+
+/* PLY I/O (the reference's pcl::io::loadPLYFile<PointXYZ> surface, FCCF.cpp:1655-1665):
+ * ascii / binary_little_endian / binary_big_endian, float x,y,z (double converted).
+ * *xyz is malloc'd by the library; release with fccf_free. */
+int fccf_ply_read(const char* path, float** xyz, int64_t* n);
+int fccf_ply_write(const char* path, const float* xyz, int64_t n, int binary);
+void fccf_free(void* p);
+
+/* Deterministic synthetic scenes; used by tests and bench. */
+int fccf_synth_scene(int64_t n, double Lx, double Ly, double Lz, uint64_t seed,
+                     double crop_x_frac, float* out_xyz);
+int fccf_synth_pair(int64_t n, double Lx, double Ly, double Lz, float* src_xyz,
+                    float* tar_xyz, float T_gt_rowmajor[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FCCF_H_ */

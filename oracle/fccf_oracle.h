@@ -1,0 +1,56 @@
+/* fccf_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of /root/reference/FCCF.cpp (the whole registration path) used
+ * as the parity oracle by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg.  The product (libfccf, fccf-pcr_amd/) never links it.
+ *
+ * Parity status: the reference cannot be compiled here (PCL/Eigen/Ceres/FLANN
+ * absent) and ships no tests or fixtures, so this restatement is
+ * "parity unpinned" against the original binary; it is pinned by known-answer
+ * tests (tests/test_oracle_kat.py) and by recovering the ground-truth transform
+ * of the synthetic scenes.  See DESIGN.md §Oracle.
+ */
+#ifndef FCCF_ORACLE_H_
+#define FCCF_ORACLE_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Within-leaf summation order of the VoxelGrid centroid (PCL sorts (leaf, index)
+ * pairs with std::sort, which is unstable; FCCF.cpp:1668-1678 / App. A2). */
+enum { ORC_ORDER_STABLE = 0, ORC_ORDER_INTROSORT = 1 };
+
+typedef struct orc_ctx orc_ctx;
+
+/* Full registration exactly as `./FCCF src tar leaf` computes it: VoxelGrid on
+ * both clouds (main), then computer_transform_guess(tar, src).  Keeps every
+ * intermediate for orc_get.  Returns NULL on bad arguments. */
+orc_ctx* orc_register(const float* src_xyz, int64_t n_src, const float* tar_xyz, int64_t n_tar,
+                      float leaf, int order);
+void orc_free(orc_ctx* c);
+/* Copy a named intermediate (see oracle/README in DESIGN.md); returns its byte size. */
+int64_t orc_get(orc_ctx* c, const char* name, void* buf, int64_t cap_bytes);
+/* Per-stage host milliseconds of the last run: [downsample, voxelfit, grow+select,
+ * match, cluster, verify, fine, fuse, total]. */
+void orc_times(orc_ctx* c, double out_ms[9]);
+
+/* Single stages (known-answer tests). */
+int64_t orc_voxel_grid(const float* xyz, int64_t n, float leaf, int order, float* out_xyz,
+                       int* overflow);
+/* pcl::eigen33 + curvature on a symmetric 3x3 (row-major) covariance. */
+void orc_eigen33(const float cov[9], float* eigenvalue, float vec[3]);
+/* compute_normal_angel (FCCF.cpp:369-377). */
+float orc_normal_angle(float x1, float y1, float z1, float x2, float y2, float z2);
+/* Eigen::Quaternionf(Matrix3f) and toRotationMatrix (row-major). */
+void orc_quat_from_rot(const float R[9], float q_wxyz[4]);
+void orc_rot_from_quat(const float q_wxyz[4], float R[9]);
+/* Ceres-1.14-style LM of ceres_refine (FCCF.cpp:210-249) on P plane pairs laid out
+ * as 13 floats each: p1[3] n1[3] p2[3] n2[3] weight.  Outputs q (x,y,z,w), t. */
+int orc_lm_refine(const float* pairs, int P, double q_xyzw[4], double t[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

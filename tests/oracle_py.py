@@ -1,0 +1,115 @@
+"""TEST INFRASTRUCTURE: ctypes loader for the CPU oracle (oracle/build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this; the
+product (fccf-pcr_amd/) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+STABLE, INTROSORT = 0, 1
+
+
+def _load():
+    if not os.path.exists(LIB):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")])
+    lib = ctypes.CDLL(LIB)
+    P, I64 = ctypes.c_void_p, ctypes.c_int64
+    lib.orc_register.restype = P
+    lib.orc_register.argtypes = [P, I64, P, I64, ctypes.c_float, ctypes.c_int]
+    lib.orc_free.argtypes = [P]
+    lib.orc_get.restype = I64
+    lib.orc_get.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.orc_times.argtypes = [P, P]
+    lib.orc_voxel_grid.restype = I64
+    lib.orc_voxel_grid.argtypes = [P, I64, ctypes.c_float, ctypes.c_int, P, ctypes.POINTER(ctypes.c_int)]
+    lib.orc_eigen33.argtypes = [P, P, P]
+    lib.orc_normal_angle.restype = ctypes.c_float
+    lib.orc_normal_angle.argtypes = [ctypes.c_float] * 6
+    lib.orc_quat_from_rot.argtypes = [P, P]
+    lib.orc_rot_from_quat.argtypes = [P, P]
+    lib.orc_lm_refine.restype = ctypes.c_int
+    lib.orc_lm_refine.argtypes = [P, ctypes.c_int, P, P]
+    return lib
+
+
+lib = _load()
+
+
+class Run:
+    """One oracle registration (FCCF.cpp main + computer_transform_guess)."""
+
+    def __init__(self, src, tar, leaf, order=STABLE):
+        s = np.ascontiguousarray(src, np.float32)
+        t = np.ascontiguousarray(tar, np.float32)
+        self.h = lib.orc_register(s.ctypes.data, s.shape[0], t.ctypes.data, t.shape[0], float(leaf), int(order))
+        if not self.h:
+            raise ValueError("orc_register rejected its arguments")
+
+    def get(self, name, dtype=np.float32):
+        n = lib.orc_get(self.h, name.encode(), None, 0)
+        if n < 0:
+            return None
+        a = np.zeros(n // np.dtype(dtype).itemsize, dtype)
+        lib.orc_get(self.h, name.encode(), a.ctypes.data, n)
+        return a
+
+    @property
+    def T(self):
+        return self.get("T").reshape(4, 4)
+
+    def times(self):
+        ms = np.zeros(9)
+        lib.orc_times(self.h, ms.ctypes.data)
+        return ms
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.orc_free(self.h)
+            self.h = None
+
+
+def voxel_grid(xyz, leaf, order=STABLE):
+    a = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    out = np.zeros((max(a.shape[0], 1), 3), np.float32)
+    ovf = ctypes.c_int(0)
+    m = lib.orc_voxel_grid(a.ctypes.data, a.shape[0], float(leaf), int(order), out.ctypes.data, ctypes.byref(ovf))
+    return out[:m].copy(), bool(ovf.value)
+
+
+def eigen33(cov):
+    c = np.ascontiguousarray(cov, np.float32).reshape(9)
+    ev = np.zeros(1, np.float32)
+    v = np.zeros(3, np.float32)
+    lib.orc_eigen33(c.ctypes.data, ev.ctypes.data, v.ctypes.data)
+    return float(ev[0]), v
+
+
+def normal_angle(a, b):
+    return lib.orc_normal_angle(*[float(x) for x in list(a) + list(b)])
+
+
+def quat_from_rot(R):
+    r = np.ascontiguousarray(R, np.float32).reshape(9)
+    q = np.zeros(4, np.float32)
+    lib.orc_quat_from_rot(r.ctypes.data, q.ctypes.data)
+    return q
+
+
+def rot_from_quat(q):
+    qq = np.ascontiguousarray(q, np.float32).reshape(4)
+    R = np.zeros(9, np.float32)
+    lib.orc_rot_from_quat(qq.ctypes.data, R.ctypes.data)
+    return R.reshape(3, 3)
+
+
+def lm_refine(pairs):
+    p = np.ascontiguousarray(pairs, np.float32).reshape(-1, 13)
+    q = np.zeros(4)
+    t = np.zeros(3)
+    lib.orc_lm_refine(p.ctypes.data, p.shape[0], q.ctypes.data, t.ctypes.data)
+    return q, t
