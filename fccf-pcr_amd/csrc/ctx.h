@@ -74,7 +74,9 @@ struct PinnedBuf {
 struct fccf_ctx {
   int device = 0;
   hipStream_t st[2] = {nullptr, nullptr};
-  fccf::Arena arena;
+  fccf::Arena arena;   // per-cloud buffers
+  fccf::Arena arena2;  // matching
+  fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
   bool debug = false;
   std::map<std::string, std::vector<uint8_t>> dbg;

@@ -306,7 +306,7 @@ void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, 
 }
 void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts, uint32_t* d_nseg,
                        SortScratch s, hipStream_t st) {
-  segment_heads<uint64_t, false>(keys, d_n, cap, (uint64_t)0, starts, d_nseg, s, st);
+  segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st);
 }
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap, uint32_t* d_total,
                         SortScratch s, hipStream_t st) {

@@ -1,0 +1,344 @@
+// facefit.hip — K2/K3: the voxel pass of face_extrate (FCCF.cpp:470-534) on gfx950.
+//
+//  * cloud centroid: pcl::compute3DCentroid, a *sequential* float sum (:473);
+//  * OctreePointCloudSearch(1.0): the dynamic bounding box grows as points are
+//    inserted in cloud order (App. A3).  Only its final bounds matter for the leaf
+//    keys, and bounds change only at "violating" points, so one workgroup finds
+//    them with block aggregates + parallel find-first, replaying adoptBoundingBox;
+//  * leaves in getOccupiedVoxelCenters DFS order = stable sort by Morton code;
+//  * per leaf with > 5 points: centroid, unshifted single-pass covariance
+//    (PCL 1.10 computeMeanAndCovarianceMatrix), pcl::eigen33, curvature, planar
+//    test and normal orientation towards the cloud centroid (:486-531);
+//  * compaction: planar leaves (Morton order) and the residual cloud cloud_sub
+//    (points of non-planar leaves, Morton then index order, :527-530).
+// Sums run over each leaf's points in ascending index, the reference's order.
+#include "kernels.h"
+
+namespace fccf {
+namespace {
+
+constexpr uint32_t INV_U32 = 0xFFFFFFFFu;
+
+// ---------------------------------------------------------------- centroid
+// One lane per component; the sum order is the reference's (index order), so this
+// is a dependent chain by construction.  Loads are batched to stay off the chain.
+__global__ void __launch_bounds__(64) k_seqsum3(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
+                                                float* __restrict__ out4) {
+  const uint32_t c = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const uint32_t n = *d_n;
+  float s = 0.f;
+  uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = xyz[3 * (i + j) + c];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
+  for (; i < n; ++i) s += xyz[3 * i + c];
+  out4[c] = n ? s / (float)n : 0.f;
+  if (c == 0) out4[3] = 1.f;
+}
+
+// ---------------------------------------------------------------- octree bounds
+// Batched over blockIdx.y = sequence e.
+__global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
+                                                    float* __restrict__ aggr0, size_t xyz_stride,
+                                                    size_t aggr_stride) {
+  __shared__ float sh[4][6];
+  const uint32_t n = *d_n;
+  const float* xyz = xyz0 + blockIdx.y * xyz_stride;
+  float* aggr = aggr0 + blockIdx.y * aggr_stride;
+  const uint32_t b0 = blockIdx.x * AGGR_BLOCK, b1 = min(b0 + AGGR_BLOCK, n);
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    if (!finite3(x, y, z)) continue;
+    mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
+    mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
+  }
+  for (int a = 0; a < 3; ++a)
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) { sh[w][a] = mn[a]; sh[w][3 + a] = mx[a]; }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    float r = sh[0][a];
+    for (int ww = 1; ww < 4; ++ww) r = a < 3 ? fminf(r, sh[ww][a]) : fmaxf(r, sh[ww][a]);
+    aggr[6 * blockIdx.x + a] = r;
+  }
+}
+
+// Replays adoptBoundingBoxToPoint over xyz[0..n) in order, starting from *state.
+// Batched over blockIdx.x = sequence e: xyz + e*xyz_stride, aggr + e*aggr_stride, state[e].
+__global__ void __launch_bounds__(1024) k_oct_sim(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
+                                                  const float* __restrict__ aggr0, double res,
+                                                  OctState* __restrict__ state0, size_t xyz_stride,
+                                                  size_t aggr_stride) {
+  __shared__ OctState S;
+  __shared__ uint32_t first_pt, first_blk;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = *d_n;
+  const float* xyz = xyz0 + blockIdx.x * xyz_stride;
+  const float* aggr = aggr0 + blockIdx.x * aggr_stride;
+  OctState* state = state0 + blockIdx.x;
+  const uint32_t nblk = (n + AGGR_BLOCK - 1) / AGGR_BLOCK;
+  if (tid == 0) S = *state;
+  __syncthreads();
+  uint32_t cur = 0;
+  while (cur < n) {
+    if (tid == 0) { first_pt = INV_U32; first_blk = INV_U32; }
+    __syncthreads();
+    const uint32_t blk = cur / AGGR_BLOCK;
+    const uint32_t bend = min((blk + 1) * AGGR_BLOCK, n);
+    for (uint32_t i = cur + tid; i < bend; i += 1024) {
+      const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+      if (finite3(x, y, z) && (!S.defined || !oct_inside(S, x, y, z))) atomicMin(&first_pt, i);
+    }
+    __syncthreads();
+    uint32_t fp = first_pt;
+    if (fp == INV_U32) {
+      for (uint32_t b = blk + 1 + tid; b < nblk; b += 1024) {
+        const float* a = aggr + 6 * b;
+        const bool nonempty = a[0] <= a[3];
+        if (nonempty && (!S.defined || !oct_inside(S, a[0], a[1], a[2]) || !oct_inside(S, a[3], a[4], a[5])))
+          atomicMin(&first_blk, b);
+      }
+      __syncthreads();
+      const uint32_t fb = first_blk;
+      __syncthreads();
+      if (fb == INV_U32) break;
+      cur = fb * AGGR_BLOCK;
+      continue;
+    }
+    if (tid == 0) {
+      const float p[3] = {xyz[3 * fp], xyz[3 * fp + 1], xyz[3 * fp + 2]};
+      oct_adopt(S, res, p);
+    }
+    __syncthreads();
+    cur = fp + 1;
+  }
+  __syncthreads();
+  if (tid == 0) *state = S;
+}
+
+__global__ void __launch_bounds__(256) k_oct_codes(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
+                                                   const OctState* __restrict__ state, double res,
+                                                   uint64_t* __restrict__ codes, uint32_t* __restrict__ d_nbits) {
+  const OctState S = *state;
+  const uint32_t n = *d_n;
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+  if (gid == 0) *d_nbits = S.defined ? 3u * S.depth + 1u : 1u;
+  for (uint32_t i = gid; i < n; i += gridDim.x * 256) {
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    codes[i] = finite3(x, y, z) ? oct_code(S, res, x, y, z) : ~(uint64_t)0;
+  }
+}
+
+// ---------------------------------------------------------------- plane fit
+__device__ __forceinline__ void roots2(float b, float c, float r[3]) {
+  r[0] = 0.f;
+  float d = (float)((double)(b * b) - 4.0 * (double)c);
+  if (d < 0.0) d = 0.0;
+  const float sd = sqrtf(d);
+  r[2] = 0.5f * (b + sd);
+  r[1] = 0.5f * (b - sd);
+}
+
+// pcl::computeRoots (closed-form cubic; float transcendental := f64 evaluation rounded)
+__device__ void roots3(const float m[3][3], float r[3]) {
+  const float c0 = m[0][0] * m[1][1] * m[2][2] + 2.f * m[0][1] * m[0][2] * m[1][2] - m[0][0] * m[1][2] * m[1][2] -
+                   m[1][1] * m[0][2] * m[0][2] - m[2][2] * m[0][1] * m[0][1];
+  const float c1 = m[0][0] * m[1][1] - m[0][1] * m[0][1] + m[0][0] * m[2][2] - m[0][2] * m[0][2] +
+                   m[1][1] * m[2][2] - m[1][2] * m[1][2];
+  const float c2 = m[0][0] + m[1][1] + m[2][2];
+  if (fabsf(c0) < 1.1920928955078125e-07f) {
+    roots2(c2, c1, r);
+    return;
+  }
+  const float inv3 = (float)(1.0 / 3.0);
+  const float sqrt3 = sqrtf(3.0f);
+  const float c2o3 = c2 * inv3;
+  float a3 = (c1 - c2 * c2o3) * inv3;
+  if (a3 > 0.f) a3 = 0.f;
+  const float hb = 0.5f * (c0 + c2o3 * (2.f * c2o3 * c2o3 - c1));
+  float q = hb * hb + a3 * a3 * a3;
+  if (q > 0.f) q = 0.f;
+  const float rho = sqrtf(-a3);
+  const float th = (float)atan2((double)sqrtf(-q), (double)hb) * inv3;
+  const float ct = (float)cos((double)th), sn = (float)sin((double)th);
+  r[0] = c2o3 + 2.f * rho * ct;
+  r[1] = c2o3 - rho * (ct + sqrt3 * sn);
+  r[2] = c2o3 - rho * (ct - sqrt3 * sn);
+  float t;
+  if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+  if (r[1] >= r[2]) {
+    t = r[1]; r[1] = r[2]; r[2] = t;
+    if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+  }
+  if (r[0] <= 0.f) roots2(c2, c1, r);
+}
+
+// pcl::eigen33(mat, eigenvalue, eigenvector): smallest eigenpair.
+__device__ void eig_min(const float A[3][3], float& ev, f3& v) {
+  float scale = 0.f;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) scale = fmaxf(scale, fabsf(A[i][j]));
+  if (scale <= 1.17549435e-38f) scale = 1.0f;
+  float s[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) s[i][j] = A[i][j] / scale;
+  float r[3];
+  roots3(s, r);
+  ev = r[0] * scale;
+  for (int i = 0; i < 3; ++i) s[i][i] -= r[0];
+  const f3 a = {s[0][0], s[0][1], s[0][2]}, b = {s[1][0], s[1][1], s[1][2]}, c = {s[2][0], s[2][1], s[2][2]};
+  const f3 v1 = cross3(a, b), v2 = cross3(a, c), v3 = cross3(b, c);
+  const float l1 = sqn3(v1), l2 = sqn3(v2), l3 = sqn3(v3);
+  f3 w;
+  float d;
+  if (l1 >= l2 && l1 >= l3) { w = v1; d = sqrtf(l1); }
+  else if (l2 >= l1 && l2 >= l3) { w = v2; d = sqrtf(l2); }
+  else { w = v3; d = sqrtf(l3); }
+  v = {w.x / d, w.y / d, w.z / d};
+}
+
+__global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
+                                                   const uint32_t* __restrict__ starts, const uint32_t* __restrict__ d_nleaf,
+                                                   const float* __restrict__ cc, float vpt, float cthr,
+                                                   VoxRec* __restrict__ recs, uint32_t* __restrict__ planar,
+                                                   uint32_t* __restrict__ resid) {
+  const uint32_t nl = *d_nleaf;
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
+    const uint32_t b = starts[s], e = starts[s + 1];
+    const uint32_t cnt = e - b;
+    VoxRec r;
+    r.count = (int32_t)cnt;
+    r.curvature = 0.f;
+    r.c[0] = r.c[1] = r.c[2] = 0.f;
+    r.n[0] = r.n[1] = r.n[2] = 0.f;
+    uint32_t flag = 0;
+    if ((float)cnt > vpt) {
+      const float fc = (float)cnt;
+      float cx = 0.f, cy = 0.f, cz = 0.f;
+      float ac[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (uint32_t k = b; k < e; ++k) {
+        const uint32_t j = vals[k];
+        const float x = xyz[3 * j], y = xyz[3 * j + 1], z = xyz[3 * j + 2];
+        cx += x; cy += y; cz += z;
+        ac[0] += x * x; ac[1] += x * y; ac[2] += x * z;
+        ac[3] += y * y; ac[4] += y * z; ac[5] += z * z;
+        ac[6] += x; ac[7] += y; ac[8] += z;
+      }
+      cx /= fc; cy /= fc; cz /= fc;
+      for (int i = 0; i < 9; ++i) ac[i] /= fc;
+      float cov[3][3];
+      cov[0][0] = ac[0] - ac[6] * ac[6];
+      cov[0][1] = ac[1] - ac[6] * ac[7];
+      cov[0][2] = ac[2] - ac[6] * ac[8];
+      cov[1][1] = ac[3] - ac[7] * ac[7];
+      cov[1][2] = ac[4] - ac[7] * ac[8];
+      cov[2][2] = ac[5] - ac[8] * ac[8];
+      cov[1][0] = cov[0][1]; cov[2][0] = cov[0][2]; cov[2][1] = cov[1][2];
+      float ev;
+      f3 nv;
+      eig_min(cov, ev, nv);
+      const float es = cov[0][0] + cov[1][1] + cov[2][2];
+      const float curv = (es != 0.f) ? fabsf(ev / es) : 0.f;
+      r.curvature = curv;
+      r.c[0] = cx; r.c[1] = cy; r.c[2] = cz;
+      if (curv < cthr) {
+        const f3 to = {cx - cc[0], cy - cc[1], cz - cc[2]};
+        if (dot3(to, nv) < 0.f) { r.n[0] = nv.x; r.n[1] = nv.y; r.n[2] = nv.z; }
+        else { r.n[0] = -nv.x; r.n[1] = -nv.y; r.n[2] = -nv.z; }
+        flag = 1;
+      } else {
+        r.n[0] = nv.x; r.n[1] = nv.y; r.n[2] = nv.z;
+        flag = 2;
+      }
+    }
+    recs[s] = r;
+    planar[s] = flag == 1 ? 1u : 0u;
+    resid[s] = flag == 2 ? cnt : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_compact(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
+                                                 const uint32_t* __restrict__ starts, const uint32_t* __restrict__ d_nleaf,
+                                                 const VoxRec* __restrict__ recs, const uint32_t* __restrict__ planar,
+                                                 const uint32_t* __restrict__ poff, const uint32_t* __restrict__ resid,
+                                                 const uint32_t* __restrict__ roff, VoxRec* __restrict__ pout,
+                                                 float* __restrict__ rout) {
+  const uint32_t nl = *d_nleaf;
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
+    if (planar[s]) pout[poff[s]] = recs[s];
+    if (resid[s]) {
+      const uint32_t b = starts[s], o = roff[s];
+      for (uint32_t k = 0; k < resid[s]; ++k) {
+        const uint32_t j = vals[b + k];
+        rout[3 * (o + k)] = xyz[3 * j];
+        rout[3 * (o + k) + 1] = xyz[3 * j + 1];
+        rout[3 * (o + k) + 2] = xyz[3 * j + 2];
+      }
+    }
+  }
+}
+
+__global__ void k_oct_reset(OctState* s) {
+  OctState z;
+  for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
+  z.depth = 0;
+  z.defined = 0;
+  *s = z;
+}
+
+inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
+  uint32_t g = (cap + per - 1) / per;
+  return g < 1 ? 1 : (g > mx ? mx : g);
+}
+
+}  // namespace
+
+void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, hipStream_t st) {
+  k_seqsum3<<<3, 64, 0, st>>>(xyz, d_n, out4);
+}
+
+void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
+                size_t xyz_stride, size_t aggr_stride) {
+  const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
+  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, xyz_stride, aggr_stride);
+}
+
+void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
+                hipStream_t st, int batch, size_t xyz_stride, size_t aggr_stride) {
+  (void)cap;
+  k_oct_sim<<<batch, 1024, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride);
+}
+
+void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
+                         hipStream_t st) {
+  k_oct_reset<<<1, 1, 0, st>>>(b.oct);
+  block_aggr(xyz, d_n, cap, b.aggr, st);
+  octree_sim(xyz, d_n, cap, res, b.aggr, b.oct, st);
+  k_oct_codes<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.oct, res, b.c0, b.nbits);
+  radix_sort_u64(b.c0, b.v0, b.c1, b.v1, d_n, cap, b.nbits, 64, true, b.ss, st);
+  segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st);
+}
+
+void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, VoxRec* planar_out,
+                     float* resid_out, FaceBufs b, hipStream_t st) {
+  k_voxel_fit<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, b.starts, b.nleaf, b.centroid, vpt, cthr, b.recs,
+                                             b.flag_planar, b.resid_cnt);
+  exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
+  exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
+  k_compact<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, b.starts, b.nleaf, b.recs, b.flag_planar, b.planar_off,
+                                           b.resid_cnt, b.resid_off, planar_out, resid_out);
+}
+
+}  // namespace fccf

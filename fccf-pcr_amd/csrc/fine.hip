@@ -1,0 +1,161 @@
+// fine.hip — K7: fine_verify (FCCF.cpp:785-839) for all <= 12 candidate transforms
+// of one registration in one batch.
+//
+// Per evaluation e: S2' = T_e * S2 (PCL SSE transformer), fused cloud S1 ++ S2',
+// OctreePointCloudSearch(0.5) anchored at the fused cloud's first point, then for
+// each occupied leaf in DFS (Morton) order: s/t counts and the sequential float sums
+//   allinvec += s + t ;  similar += (s+t) * (min/max)   (if s >= 1 and t >= 1)
+// score = similar / allinvec.  The S1 half of the octree bound replay is shared by
+// all evaluations.  Sort key = (e | morton | is_target); counts are exact integers,
+// the two float sums run in the reference's leaf order (one lane per evaluation).
+#include "kernels.h"
+#include "match.h"
+
+namespace fccf {
+namespace {
+
+__global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ s2, uint32_t n2,
+                                                      const m44* __restrict__ T, float* __restrict__ s2t) {
+  const int e = blockIdx.y;
+  const m44 M = T[e];
+  float* o = s2t + (size_t)e * 3 * n2;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += gridDim.x * 256) {
+    const f3 p = tf_se3(M, s2[3 * i], s2[3 * i + 1], s2[3 * i + 2]);
+    o[3 * i] = p.x; o[3 * i + 1] = p.y; o[3 * i + 2] = p.z;
+  }
+}
+
+__global__ void k_fv_init(OctState* st, int E, uint32_t* scal, uint32_t n1, uint32_t n2) {
+  // st[E] := undefined; after the S1 replay it is copied to st[0..E)
+  if (threadIdx.x == 0) {
+    scal[4] = n1;
+    scal[5] = n2;
+    OctState z;
+    for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
+    z.depth = 0;
+    z.defined = 0;
+    st[E] = z;
+  }
+}
+
+__global__ void k_fv_fork(OctState* st, int E) {
+  const int e = threadIdx.x;
+  if (e < E) st[e] = st[E];
+}
+
+// scal: [0] total keys, [1] nbits, [3] shift = 3*Dmax+1, [4] n1, [5] n2, [6] E
+__global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict__ scal, uint32_t n1, uint32_t n2,
+                          int E) {
+  if (threadIdx.x != 0) return;
+  uint32_t D = 0;
+  for (int e = 0; e < E; ++e)
+    if (st[e].defined && st[e].depth > D) D = st[e].depth;
+  uint32_t eb = 1;
+  while ((1u << eb) <= (uint32_t)E) ++eb;
+  scal[0] = (uint32_t)E * (n1 + n2);
+  scal[2] = 0u;  // segment count (stays 0 when there are no keys)
+  scal[3] = 3u * D + 1u;
+  scal[1] = 3u * D + 1u + eb;
+  scal[4] = n1;
+  scal[5] = n2;
+  scal[6] = (uint32_t)E;
+}
+
+__global__ void __launch_bounds__(256) k_fv_keys(const float* __restrict__ s1, const float* __restrict__ s2t,
+                                                 const OctState* __restrict__ st, const uint32_t* __restrict__ scal,
+                                                 double res, uint64_t* __restrict__ keys) {
+  const int e = blockIdx.y;
+  const OctState S = st[e];
+  const uint32_t n1 = scal[4], n2 = scal[5], shift = scal[3];
+  const uint32_t n = n1 + n2;
+  uint64_t* out = keys + (size_t)e * n;
+  const float* b = s2t + (size_t)e * 3 * n2;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const bool tgt = i >= n1;
+    const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
+    uint64_t k = ~(uint64_t)0;
+    if (finite3(p[0], p[1], p[2]))
+      k = ((uint64_t)e << shift) | (oct_code(S, res, p[0], p[1], p[2]) << 1) | (tgt ? 1ull : 0ull);
+    out[i] = k;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_fv_leafkeys(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ scal,
+                                                     uint64_t* __restrict__ vk) {
+  const uint32_t n = scal[0];
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint64_t k = keys[i];
+    vk[i] = k == ~(uint64_t)0 ? k : (k >> 1);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ starts,
+                                                   const uint32_t* __restrict__ d_nseg, uint32_t* __restrict__ cnt) {
+  const uint32_t ns = *d_nseg;
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
+    const uint32_t b = starts[s], e = starts[s + 1];
+    uint32_t src = 0;
+    for (uint32_t k = b; k < e; ++k) src += (keys[k] & 1ull) ? 0u : 1u;
+    cnt[2 * s] = src;
+    cnt[2 * s + 1] = (e - b) - src;
+  }
+}
+
+// One lane per evaluation: the reference's sequential float sums in leaf order.
+__global__ void __launch_bounds__(64) k_fv_score(const uint64_t* __restrict__ vk, const uint32_t* __restrict__ starts,
+                                                 const uint32_t* __restrict__ d_nseg, const uint32_t* __restrict__ cnt,
+                                                 const uint32_t* __restrict__ scal, float* __restrict__ scores) {
+  const int e = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const uint32_t ns = *d_nseg, sh = scal[3] - 1u;  // e of a leaf key = vk >> (shift - 1)
+  uint32_t lo = 0, hi = ns;                        // first segment with e' >= e
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if ((vk[starts[mid]] >> sh) < (uint64_t)e) lo = mid + 1;
+    else hi = mid;
+  }
+  float similar = 0.f, all = 0.f;
+  for (uint32_t s = lo; s < ns && (vk[starts[s]] >> sh) == (uint64_t)e; ++s) {
+    const float sn = (float)cnt[2 * s], tn = (float)cnt[2 * s + 1];
+    all = all + sn + tn;
+    if (sn >= 1.f && tn >= 1.f) {
+      const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
+      similar = similar + (sn + tn) * (mn / mx);
+    }
+  }
+  scores[e] = similar / all;
+}
+
+inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
+  uint32_t g = (cap + per - 1) / per;
+  return g < 1 ? 1 : (g > mx ? mx : g);
+}
+
+}  // namespace
+
+void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
+                       hipStream_t st) {
+  if (E <= 0) return;
+  const uint32_t nb2 = (n2 + AGGR_BLOCK - 1) / AGGR_BLOCK;
+  const size_t astride = 6 * (size_t)(nb2 ? nb2 : 1);
+  k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t);
+  k_fv_init<<<1, 64, 0, st>>>(b.state, E, b.scal, n1, n2);
+  // scal[4], scal[5] hold n1, n2 for the device-count interfaces
+  uint32_t* d_n1 = b.scal + 4;
+  uint32_t* d_n2 = b.scal + 5;
+  block_aggr(s1, d_n1, n1, b.aggr1, st);
+  octree_sim(s1, d_n1, n1, res, b.aggr1, b.state + E, st);
+  k_fv_fork<<<1, 64, 0, st>>>(b.state, E);
+  block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, 3 * (size_t)n2, astride);
+  octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, 3 * (size_t)n2, astride);
+  k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, n1, n2, E);
+  const uint32_t n = (uint32_t)E * (n1 + n2);
+  k_fv_keys<<<dim3(grid_for(n1 + n2, 256, 1024), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0);
+  radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 64, true, b.ss, st);
+  k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
+  segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
+  k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.starts, b.scal + 2, b.st_counts);
+  k_fv_score<<<E, 64, 0, st>>>(b.k1, b.starts, b.scal + 2, b.st_counts, b.scal, b.scores);
+}
+
+}  // namespace fccf

@@ -1,0 +1,621 @@
+// host_stages.cpp — serial stages of the FCCF-PCR driver kept on the host in
+// round 1 (see host_stages.h).  Every expression is written in the evaluation
+// order of the reference binary (fccf_math.h conventions).
+#include "host_stages.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+
+namespace fccf {
+
+static inline float angle_deg(float x1, float y1, float z1, float x2, float y2, float z2) {
+  return theta_of_cos_host(normal_cos(x1, y1, z1, x2, y2, z2));
+}
+
+// ------------------------------------------------------------------ growing
+namespace {
+struct Group {
+  std::vector<int> mem;             // voxel indices in voxelgrothnode order
+  float s = 0, sc[3] = {0, 0, 0}, sn[3] = {0, 0, 0};  // running recompute sums
+  float ac[3], an[3], fps;
+  bool alloc = false;
+};
+
+inline void add_member(Group& g, const VoxRec& v) {
+  g.s = g.s + (float)v.count;
+  for (int a = 0; a < 3; ++a) {
+    g.sc[a] = g.sc[a] + v.c[a] * (float)v.count;
+    g.sn[a] = g.sn[a] + v.n[a] * (float)v.count;
+  }
+}
+inline void set_avg(Group& g) {  // the recompute's averages (:580-586)
+  g.fps = g.s;
+  for (int a = 0; a < 3; ++a) {
+    g.ac[a] = g.sc[a] / g.s;
+    g.an[a] = g.sn[a] / g.s;
+  }
+}
+}  // namespace
+
+GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
+  std::vector<char> va(nv, 0);
+  std::vector<Group> G;
+  // stage 1 (:536-593): recompute-from-scratch == running sums in member order (App. B Q7)
+  for (int i = 0; i < nv; ++i) {
+    if (va[i]) continue;
+    Group g;
+    va[i] = 1;
+    g.mem.push_back(i);
+    add_member(g, vox[i]);
+    g.fps = (float)vox[i].count;
+    for (int a = 0; a < 3; ++a) { g.an[a] = vox[i].n[a]; g.ac[a] = vox[i].c[a]; }
+    for (int j = 0; j < nv; ++j) {
+      if (va[j]) continue;
+      const VoxRec& v = vox[j];
+      const bool same = !(angle_deg(g.an[0], g.an[1], g.an[2], v.n[0], v.n[1], v.n[2]) > P.normal_vector_threshold1);
+      const bool cop = compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]},
+                                     f3{v.n[0], v.n[1], v.n[2]}, f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1,
+                                     P.parameter_k1);
+      if (same && cop) {
+        g.mem.push_back(j);
+        va[j] = 1;
+        add_member(g, v);
+        set_avg(g);
+      }
+    }
+    G.push_back(std::move(g));
+  }
+  // stage 2 (:595-648): seeds never mark themselves allocated (Q6)
+  for (size_t i = 0; i < G.size(); ++i) {
+    if (G[i].alloc) continue;
+    bool newadd = true;
+    while (newadd) {
+      newadd = false;
+      for (size_t j = 0; j < G.size(); ++j) {
+        if (j == i || G[j].alloc) continue;
+        Group& a = G[i];
+        Group& b = G[j];
+        const bool same = !(angle_deg(a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2]) > P.normal_vector_threshold2);
+        const bool cop = compare_plane(f3{a.an[0], a.an[1], a.an[2]}, f3{a.ac[0], a.ac[1], a.ac[2]},
+                                       f3{b.an[0], b.an[1], b.an[2]}, f3{b.ac[0], b.ac[1], b.ac[2]}, P.parameter_l2,
+                                       P.parameter_k2);
+        if (same && cop) {
+          newadd = true;
+          b.alloc = true;
+          for (int m : b.mem) {
+            a.mem.push_back(m);
+            add_member(a, vox[m]);
+          }
+          set_avg(a);
+        }
+      }
+    }
+  }
+  // range_face (:409-427): exchange sort on voxel counts, emulated on indices
+  std::vector<int> ord(G.size());
+  for (size_t i = 0; i < G.size(); ++i) ord[i] = (int)i;
+  for (size_t i = 0; i + 1 < ord.size(); ++i)
+    for (size_t j = i + 1; j < ord.size(); ++j)
+      if (G[ord[i]].mem.size() < G[ord[j]].mem.size()) std::swap(ord[i], ord[j]);
+  GrowOut out;
+  for (int k : ord) {
+    const Group& g = G[k];
+    Plane p;
+    std::memcpy(p.c, g.ac, 12);
+    std::memcpy(p.n, g.an, 12);
+    p.fps = g.fps;
+    p.nvox = (int32_t)g.mem.size();
+    out.groups.push_back(p);
+    out.galloc.push_back(g.alloc ? 1 : 0);
+  }
+  int cur = 0;
+  for (size_t r = 0; r < ord.size(); ++r) {
+    const Group& g = G[ord[r]];
+    if (!g.alloc) {
+      out.planes.push_back(out.groups[r]);
+      double sum = 0;
+      for (int m : g.mem) {
+        const double th = angle_deg(g.an[0], g.an[1], g.an[2], vox[m].n[0], vox[m].n[1], vox[m].n[2]);
+        sum += std::fabs(th);
+      }
+      sum /= (double)g.mem.size();
+      out.theta.push_back(sum);
+      cur++;
+    }
+    if ((float)cur > P.select_plane_number) break;
+  }
+  return out;
+}
+
+std::vector<Base> select_base(const std::vector<Plane>& F, const std::vector<double>& th, const fccf_params& P,
+                              int side) {
+  std::vector<Base> base;
+  std::vector<int32_t> type;
+  const double t1 = P.rough_threshold_gl;
+  for (size_t i = 0; i < F.size(); ++i)
+    for (size_t j = i + 1; j < F.size(); ++j) {
+      const float ang = angle_deg(F[i].n[0], F[i].n[1], F[i].n[2], F[j].n[0], F[j].n[1], F[j].n[2]);
+      if (P.included_angle_min_threshold < ang && ang < P.included_angle_max_threshold) {
+        base.push_back({(int32_t)i, (int32_t)j, ang, 0});
+        if (th[i] <= t1 && th[j] <= t1) type.push_back(0);
+        else if (th[i] > t1 && th[j] > t1) type.push_back(1);
+        else if (th[i] <= t1 && th[j] > t1) type.push_back(2);
+        else if (th[i] > t1 && th[j] <= t1) type.push_back(2);
+      }
+    }
+  // type_index is indexed by the pair's position even when NaN roughness made it
+  // shorter (Q5); positions past its end get a sentinel that matches nothing.
+  for (size_t k = 0; k < base.size(); ++k) base[k].type = k < type.size() ? type[k] : (side == 1 ? -1 : -2);
+  return base;
+}
+
+// ------------------------------------------------------------------ clustering
+QT qt_from_T(const m44& T) {
+  m33 R;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R.m[i][j] = T.m[i][j];
+  const quatf q = quat_from_rot(R);
+  return {q.w, q.x, q.y, q.z, T.m[0][3], T.m[1][3], T.m[2][3], 0u};
+}
+
+m44 T_from_qt(const QT& t) {
+  const m33 R = rot_from_quat(quatf{t.qw, t.qx, t.qy, t.qz});
+  m44 T = eye44();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T.m[i][j] = R.m[i][j];
+  T.m[0][3] = t.tx; T.m[1][3] = t.ty; T.m[2][3] = t.tz;
+  return T;
+}
+
+void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
+                       int64_t* ncl) {
+  const int n = (int)in.size();
+  if (ncl) *ncl = 0;
+  if ((float)n <= P.cluster_number_threshold) {
+    if (n == 0) fine.push_back({1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1u});
+    else fine.insert(fine.end(), in.begin(), in.end());
+    return;
+  }
+  // KdTreeFLANN::radiusSearch(q, r): every j with L2_Simple d2 < float(r*r), sorted by (d2, j)
+  const float r2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
+  const double cell = std::max(1.0, (double)P.cluster_distance_threshold * 1.25);
+  struct KH {
+    size_t operator()(const int64_t k) const { return std::hash<int64_t>()(k); }
+  };
+  auto key = [&](const QT& t) {
+    const int64_t x = (int64_t)std::floor(t.tx / cell), y = (int64_t)std::floor(t.ty / cell),
+                  z = (int64_t)std::floor(t.tz / cell);
+    return (x * 73856093) ^ (y * 19349663) ^ (z * 83492791);
+  };
+  auto cell_of = [&](const QT& t, int64_t* c) {
+    c[0] = (int64_t)std::floor(t.tx / cell);
+    c[1] = (int64_t)std::floor(t.ty / cell);
+    c[2] = (int64_t)std::floor(t.tz / cell);
+  };
+  std::unordered_map<int64_t, std::vector<int>, KH> grid;
+  for (int i = 0; i < n; ++i) grid[key(in[i])].push_back(i);
+  std::vector<f3> xaxis(n);
+  for (int i = 0; i < n; ++i) xaxis[i] = quat_rotate(quatf{in[i].qw, in[i].qx, in[i].qy, in[i].qz}, f3{1.f, 0.f, 0.f});
+  std::vector<std::vector<int>> clusters;
+  std::vector<std::pair<float, int>> nb;
+  for (int i = 0; i + 1 < n; ++i) {  // the last candidate never seeds (:1084)
+    if (in[i].alloc) continue;
+    nb.clear();
+    int64_t c[3];
+    cell_of(in[i], c);
+    for (int64_t dx = -1; dx <= 1; ++dx)
+      for (int64_t dy = -1; dy <= 1; ++dy)
+        for (int64_t dz = -1; dz <= 1; ++dz) {
+          const int64_t k = ((c[0] + dx) * 73856093) ^ ((c[1] + dy) * 19349663) ^ ((c[2] + dz) * 83492791);
+          auto it = grid.find(k);
+          if (it == grid.end()) continue;
+          for (int j : it->second) {
+            int64_t cj[3];
+            cell_of(in[j], cj);
+            if (cj[0] != c[0] + dx || cj[1] != c[1] + dy || cj[2] != c[2] + dz) continue;  // hash collision
+            const float ex = in[i].tx - in[j].tx, ey = in[i].ty - in[j].ty, ez = in[i].tz - in[j].tz;
+            float d2 = 0.0f;
+            d2 += ex * ex;
+            d2 += ey * ey;
+            d2 += ez * ez;
+            if (d2 < r2) nb.push_back({d2, j});
+          }
+        }
+    std::sort(nb.begin(), nb.end());
+    std::vector<int> cl;
+    for (auto& e : nb) {
+      const f3 a = xaxis[i], b = xaxis[e.second];
+      if (angle_deg(a.x, a.y, a.z, b.x, b.y, b.z) < P.cluster_angel_threshold) {
+        in[e.second].alloc = 1u;
+        cl.push_back(e.second);
+      }
+    }
+    clusters.push_back(std::move(cl));
+  }
+  if (ncl) *ncl = (int64_t)clusters.size();
+  // range_cluster (:1020-1038): exchange sort by size, emulated on indices
+  std::vector<int> ord(clusters.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+  auto sz = [&](int k) { return clusters[k].size(); };
+  // Only the first positions are consumed below; run passes lazily.
+  size_t sorted_upto = 0;
+  auto ensure_sorted = [&](size_t pos) {
+    while (sorted_upto <= pos && sorted_upto + 1 < ord.size()) {
+      const size_t i = sorted_upto;
+      for (size_t j = i + 1; j < ord.size(); ++j)
+        if (sz(ord[i]) < sz(ord[j])) std::swap(ord[i], ord[j]);
+      ++sorted_upto;
+    }
+  };
+  ensure_sorted(0);
+  int clusternum = (int)sz(ord[0]);
+  bool stop = false;
+  for (size_t r = 0; r < ord.size(); ++r) {
+    if (stop) break;  // nothing else happens once stop is set
+    ensure_sorted(r);
+    const std::vector<int>& cl = clusters[ord[r]];
+    if ((int)cl.size() >= clusternum) {
+      float ax = 0, ay = 0, az = 0;
+      for (int k : cl) { ax = ax + in[k].tx; ay = ay + in[k].ty; az = az + in[k].tz; }
+      const float cs = (float)cl.size();
+      ax = ax / cs; ay = ay / cs; az = az / cs;
+      float s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
+      for (int k : cl) {
+        const quatf q = {in[k].qw, in[k].qx, in[k].qy, in[k].qz};
+        const f3 u = quat_rotate(q, f3{1.f, 0.f, 0.f}), v = quat_rotate(q, f3{0.f, 1.f, 0.f});
+        s1[0] = s1[0] + u.x; s1[1] = s1[1] + u.y; s1[2] = s1[2] + u.z;
+        s2[0] = s2[0] + v.x; s2[1] = s2[1] + v.y; s2[2] = s2[2] + v.z;
+      }
+      const f3 nt1 = normalize3(f3{s1[0] / cs, s1[1] / cs, s1[2] / cs});
+      const f3 nt2 = normalize3(f3{s2[0] / cs, s2[1] / cs, s2[2] / cs});
+      const quatf q = quat_from_rot(axes_to_rot(nt1, nt2));
+      fine.push_back({q.w, q.x, q.y, q.z, ax, ay, az, 1u});
+      if (fine.size() > (size_t)cluster_num) break;
+    } else {
+      if ((double)fine.size() < (cluster_num / 2.0)) {
+        clusternum--;
+        if (clusternum < 2) break;
+      } else {
+        stop = true;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ Ceres 1.14 LM
+namespace {
+inline void crossd(const double a[3], const double b[3], double r[3]) {
+  r[0] = a[1] * b[2] - a[2] * b[1];
+  r[1] = a[2] * b[0] - a[0] * b[2];
+  r[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Eigen Quaterniond product, SSE2 Packet2d grouping; coefficients (x,y,z,w).
+inline void qmul(const double a[4], const double b[4], double r[4]) {
+  const double ax = a[0], ay = a[1], az = a[2], aw = a[3], bx = b[0], by = b[1], bz = b[2], bw = b[3];
+  r[0] = (aw * bx + ay * bz) - (az * by - ax * bw);
+  r[1] = (aw * by + ay * bw) + (az * bx - ax * bz);
+  r[2] = (aw * bz - ay * bx) + (az * bw + ax * by);
+  r[3] = (aw * bw - ay * by) - (az * bz + ax * bx);
+}
+// EigenQuaternionParameterization::Plus (q) and Euclidean plus (t).
+inline void plus7(const double x[7], const double d[6], double o[7]) {
+  const double nd = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  if (nd > 0.0) {
+    const double s = std::sin(nd) / nd;
+    const double dq[4] = {s * d[0], s * d[1], s * d[2], std::cos(nd)};
+    qmul(dq, x, o);
+  } else {
+    o[0] = x[0]; o[1] = x[1]; o[2] = x[2]; o[3] = x[3];
+  }
+  for (int i = 0; i < 3; ++i) o[4 + i] = x[4 + i] + d[3 + i];
+}
+// v' = v + w*uv + u x uv, uv = 2(u x v); Jacobian wrt (x,y,z,w).
+inline void rotq(const double q[4], const double v[3], double f[3], double (*J)[4]) {
+  const double u[3] = {q[0], q[1], q[2]}, w = q[3];
+  double a[3], uv[3], c[3];
+  crossd(u, v, a);
+  uv[0] = a[0] + a[0]; uv[1] = a[1] + a[1]; uv[2] = a[2] + a[2];
+  crossd(u, uv, c);
+  for (int i = 0; i < 3; ++i) f[i] = (v[i] + w * uv[i]) + c[i];
+  if (!J) return;
+  for (int k = 0; k < 3; ++k) {
+    double e[3] = {0, 0, 0};
+    e[k] = 1.0;
+    double ekv[3], eka[3], uekv[3];
+    crossd(e, v, ekv);
+    crossd(e, a, eka);
+    crossd(u, ekv, uekv);
+    for (int i = 0; i < 3; ++i) J[i][k] = 2.0 * w * ekv[i] + 2.0 * (eka[i] + uekv[i]);
+  }
+  for (int i = 0; i < 3; ++i) J[i][3] = uv[i];
+}
+
+// LidarPlaneFactor (FCCF.cpp:178-208): residuals and local (6-column) Jacobian.
+bool lm_eval(const float* pf, int P, const double x[7], double* cost, double* r, double* J) {
+  const double* q = x;
+  const double* t = x + 4;
+  const double Pj[4][3] = {{q[3], q[2], -q[1]}, {-q[2], q[3], q[0]}, {q[1], -q[0], q[3]}, {-q[0], -q[1], -q[2]}};
+  double c = 0.0;
+  for (int b = 0; b < P; ++b) {
+    const float* s = pf + 13 * b;
+    const double p1[3] = {s[0], s[1], s[2]}, n1[3] = {s[3], s[4], s[5]};
+    const double p2[3] = {s[6], s[7], s[8]}, n2[3] = {s[9], s[10], s[11]};
+    const double w = s[12];
+    double n2r[3], p2r[3], Jn[3][4], Jp[3][4];
+    rotq(q, n2, n2r, J ? Jn : nullptr);
+    rotq(q, p2, p2r, J ? Jp : nullptr);
+    for (int i = 0; i < 3; ++i) p2r[i] = p2r[i] + t[i];
+    double cr[3];
+    crossd(n1, n2r, cr);
+    const double nrm = std::sqrt((cr[0] * cr[0] + cr[1] * cr[1]) + cr[2] * cr[2]);
+    const double d = ((n1[0] * p1[0] + n1[1] * p1[1]) + n1[2] * p1[2]) -
+                     ((n2r[0] * p2r[0] + n2r[1] * p2r[1]) + n2r[2] * p2r[2]);
+    const double r0 = w * nrm, r1 = w * std::sqrt(d * d);
+    r[2 * b] = r0;
+    r[2 * b + 1] = r1;
+    c += 0.5 * (r0 * r0 + r1 * r1);
+    if (!std::isfinite(r0) || !std::isfinite(r1)) return false;
+    if (J) {
+      double g0[7] = {0, 0, 0, 0, 0, 0, 0}, g1[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < 4; ++k) {
+        const double col[3] = {Jn[0][k], Jn[1][k], Jn[2][k]};
+        double dc[3];
+        crossd(n1, col, dc);
+        g0[k] = w * (((cr[0] * dc[0] + cr[1] * dc[1]) + cr[2] * dc[2]) / nrm);
+        const double dd = -(((Jn[0][k] * p2r[0] + Jn[1][k] * p2r[1]) + Jn[2][k] * p2r[2]) +
+                            ((n2r[0] * Jp[0][k] + n2r[1] * Jp[1][k]) + n2r[2] * Jp[2][k]));
+        g1[k] = w * ((d * dd) / std::sqrt(d * d));
+      }
+      for (int k = 0; k < 3; ++k) g1[4 + k] = w * ((d * -n2r[k]) / std::sqrt(d * d));
+      double* J0 = J + (2 * b) * 6;
+      double* J1 = J + (2 * b + 1) * 6;
+      for (int j = 0; j < 3; ++j) {
+        J0[j] = ((g0[0] * Pj[0][j] + g0[1] * Pj[1][j]) + g0[2] * Pj[2][j]) + g0[3] * Pj[3][j];
+        J1[j] = ((g1[0] * Pj[0][j] + g1[1] * Pj[1][j]) + g1[2] * Pj[2][j]) + g1[3] * Pj[3][j];
+        J0[3 + j] = 0.0;
+        J1[3 + j] = g1[4 + j];
+      }
+      for (int j = 0; j < 6; ++j)
+        if (!std::isfinite(J0[j]) || !std::isfinite(J1[j])) return false;
+    }
+  }
+  *cost = c;
+  return true;
+}
+
+// DENSE_QR: min || [A; diag(D)] y - [b; 0] || by Householder QR (HouseholderQR form).
+bool qr_solve(const double* A, int m, const double D[6], const double* b, double y[6]) {
+  const int n = 6, M = m + n;
+  std::vector<double> Q((size_t)M * n, 0.0), rhs(M, 0.0);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < n; ++j) Q[(size_t)i * n + j] = A[(size_t)i * n + j];
+  for (int j = 0; j < n; ++j) Q[(size_t)(m + j) * n + j] = D[j];
+  for (int i = 0; i < m; ++i) rhs[i] = b[i];
+  for (int k = 0; k < n; ++k) {
+    const double c0 = Q[(size_t)k * n + k];
+    double tail = 0.0;
+    for (int i = k + 1; i < M; ++i) tail += Q[(size_t)i * n + k] * Q[(size_t)i * n + k];
+    double tau, beta;
+    if (tail <= DBL_MIN) {
+      tau = 0.0;
+      beta = c0;
+      for (int i = k + 1; i < M; ++i) Q[(size_t)i * n + k] = 0.0;
+    } else {
+      beta = std::sqrt(c0 * c0 + tail);
+      if (c0 >= 0.0) beta = -beta;
+      for (int i = k + 1; i < M; ++i) Q[(size_t)i * n + k] = Q[(size_t)i * n + k] / (c0 - beta);
+      tau = (beta - c0) / beta;
+    }
+    Q[(size_t)k * n + k] = beta;
+    for (int j = k + 1; j <= n; ++j) {  // j == n: the right-hand side
+      auto at = [&](int i) -> double& { return j < n ? Q[(size_t)i * n + j] : rhs[i]; };
+      double tmp = 0.0;
+      for (int i = k + 1; i < M; ++i) tmp += Q[(size_t)i * n + k] * at(i);
+      tmp += at(k);
+      at(k) = at(k) - tau * tmp;
+      for (int i = k + 1; i < M; ++i) at(i) = at(i) - tau * Q[(size_t)i * n + k] * tmp;
+    }
+  }
+  for (int i = 0; i < n; ++i) y[i] = rhs[i];
+  for (int k = n - 1; k >= 0; --k) {
+    y[k] = y[k] / Q[(size_t)k * n + k];
+    for (int i = 0; i < k; ++i) y[i] = y[i] - y[k] * Q[(size_t)i * n + k];
+  }
+  for (int i = 0; i < n; ++i)
+    if (!std::isfinite(y[i])) return false;
+  return true;
+}
+}  // namespace
+
+// TrustRegionMinimizer + LevenbergMarquardtStrategy (Ceres 1.14 defaults, App. A10):
+// jacobi scaling from iteration 0, LM diagonal clamp [1e-6,1e32], radius 1e4,
+// function/gradient/parameter tolerances 1e-6/1e-10/1e-8, 50 iterations, returns
+// the parameters of the lowest cost seen at an iteration boundary.
+void lm_solve(const float* pf, int P, double best[7]) {
+  const int m = 2 * P;
+  double x[7] = {0, 0, 0, 1, 0, 0, 0};
+  for (int i = 0; i < 7; ++i) best[i] = x[i];
+  std::vector<double> r(m), J((size_t)m * 6), rc(m);
+  double cost;
+  if (!lm_eval(pf, P, x, &cost, r.data(), J.data())) return;
+  double scale[6], gmax = 0.0;
+  for (int j = 0; j < 6; ++j) {
+    double s = 0.0;
+    for (int i = 0; i < m; ++i) s += J[(size_t)i * 6 + j] * J[(size_t)i * 6 + j];
+    scale[j] = 1.0 / (1.0 + std::sqrt(s));
+  }
+  auto finish = [&]() {
+    double g[6], ng[6], xp[7];
+    for (int j = 0; j < 6; ++j) {
+      double s = 0.0;
+      for (int i = 0; i < m; ++i) s += J[(size_t)i * 6 + j] * r[i];
+      g[j] = s;
+      ng[j] = -g[j];
+    }
+    plus7(x, ng, xp);
+    double mx = 0.0;
+    for (int j = 0; j < 7; ++j) mx = std::max(mx, std::fabs(x[j] - xp[j]));
+    gmax = mx;
+    for (int i = 0; i < m; ++i)
+      for (int j = 0; j < 6; ++j) J[(size_t)i * 6 + j] *= scale[j];
+  };
+  finish();
+  double min_cost = cost;
+  auto norm7 = [](const double* v) {
+    double s = 0.0;
+    for (int i = 0; i < 7; ++i) s += v[i] * v[i];
+    return std::sqrt(s);
+  };
+  double x_norm = norm7(x);
+  double radius = 1e4, decrease = 2.0, diag[6];
+  bool reuse = false;
+  int iteration = 0, invalid = 0;
+  if (gmax <= 1e-10) return;
+  while (true) {
+    ++iteration;
+    bool successful = false;
+    if (!reuse)
+      for (int j = 0; j < 6; ++j) {
+        double s = 0.0;
+        for (int i = 0; i < m; ++i) s += J[(size_t)i * 6 + j] * J[(size_t)i * 6 + j];
+        diag[j] = std::min(std::max(s, 1e-6), 1e32);
+      }
+    double D[6], y[6], step[6];
+    for (int j = 0; j < 6; ++j) D[j] = std::sqrt(diag[j] / radius);
+    const bool solved = qr_solve(J.data(), m, D, r.data(), y);
+    reuse = true;
+    bool valid = false;
+    double mcc = 0.0;
+    if (solved) {
+      for (int j = 0; j < 6; ++j) step[j] = -y[j];
+      double dot = 0.0;
+      for (int i = 0; i < m; ++i) {
+        double mr = 0.0;
+        for (int j = 0; j < 6; ++j) mr += J[(size_t)i * 6 + j] * step[j];
+        dot += mr * (r[i] + mr / 2.0);
+      }
+      mcc = -dot;
+      valid = mcc > 0.0;
+    }
+    if (!valid) {
+      if (++invalid >= 5) return;
+      radius = radius / decrease;
+      decrease *= 2.0;
+    } else {
+      invalid = 0;
+      double delta[6], cand[7];
+      for (int j = 0; j < 6; ++j) delta[j] = step[j] * scale[j];
+      plus7(x, delta, cand);
+      double ccost;
+      if (!lm_eval(pf, P, cand, &ccost, rc.data(), nullptr)) ccost = DBL_MAX;
+      double sn = 0.0;
+      for (int i = 0; i < 7; ++i) sn += (x[i] - cand[i]) * (x[i] - cand[i]);
+      sn = std::sqrt(sn);
+      if (sn <= 1e-8 * (x_norm + 1e-8)) return;
+      if (std::fabs(cost - ccost) <= 1e-6 * cost) return;
+      const double rho = (cost - ccost) / mcc;
+      if (rho > 1e-3) {
+        for (int i = 0; i < 7; ++i) x[i] = cand[i];
+        x_norm = norm7(x);
+        if (!lm_eval(pf, P, x, &cost, r.data(), J.data())) return;
+        finish();
+        successful = true;
+        radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3));
+        radius = std::min(1e16, radius);
+        decrease = 2.0;
+        reuse = false;
+      } else {
+        radius = radius / decrease;
+        decrease *= 2.0;
+      }
+    }
+    if (successful && cost < min_cost) {
+      min_cost = cost;
+      for (int i = 0; i < 7; ++i) best[i] = x[i];
+    }
+    if (iteration >= 50) return;
+    if (successful && gmax <= 1e-10) return;
+    if (radius <= 1e-32) return;
+  }
+}
+
+float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2, const fccf_params& P,
+                   int* npairs) {
+  int fs1 = 0, fs2 = 0;
+  for (const Plane& f : F1) fs1 = (int)((float)fs1 + f.fps);
+  for (const Plane& f : F2) fs2 = (int)((float)fs2 + f.fps);
+  std::vector<f3> c2(F2.size()), n2(F2.size());
+  for (size_t k = 0; k < F2.size(); ++k) {
+    c2[k] = tf_se3(T, F2[k].c[0], F2[k].c[1], F2[k].c[2]);
+    n2[k] = tf_so3(T, F2[k].n[0], F2[k].n[1], F2[k].n[2]);
+  }
+  std::vector<float> pairs;
+  int np = 0;
+  for (size_t i = 0; i < F1.size(); ++i) {
+    const Plane& a = F1[i];
+    bool find = false;
+    int best = 0;
+    float best_imp = 0, best_score = 0;
+    for (size_t j = 0; j < F2.size(); ++j) {
+      const float ang = angle_deg(a.n[0], a.n[1], a.n[2], n2[j].x, n2[j].y, n2[j].z);
+      const float d1 = (float)dot3d(a.n[0], a.n[1], a.n[2], a.c[0], a.c[1], a.c[2]);
+      const float d2 = (float)dot3d(n2[j].x, n2[j].y, n2[j].z, c2[j].x, c2[j].y, c2[j].z);
+      const float dist = std::fabs(d1 - d2);
+      if (ang < P.quick_verify_angel_threshold && dist < P.quick_verify_distance_threshold) {
+        find = true;
+        const float s1 = a.fps, s2 = F2[j].fps;
+        const float mn = s1 < s2 ? s1 : s2, mx = s1 > s2 ? s1 : s2;
+        const float sc = mn / mx;
+        const float imp = (2 * mn) / (float)(fs1 + fs2);
+        if (sc > best_score) { best_imp = imp; best_score = sc; best = (int)j; }
+      }
+    }
+    if (find) {
+      const float rec[13] = {a.c[0], a.c[1], a.c[2], a.n[0], a.n[1], a.n[2], c2[best].x, c2[best].y, c2[best].z,
+                             n2[best].x, n2[best].y, n2[best].z, best_imp};
+      pairs.insert(pairs.end(), rec, rec + 13);
+      ++np;
+    }
+  }
+  if (npairs) *npairs = np;
+  if ((float)np >= P.required_optimize_plane) {
+    double b[7];
+    lm_solve(pairs.data(), np, b);
+    const m33 R = rot_from_quat(quatf{(float)b[3], (float)b[0], (float)b[1], (float)b[2]});
+    m44 dT = eye44();
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) dT.m[i][j] = R.m[i][j];
+    dT.m[0][3] = (float)b[4]; dT.m[1][3] = (float)b[5]; dT.m[2][3] = (float)b[6];
+    T = mul44(dT, T);
+  }
+  float score = 0;
+  for (int k = 0; k < np; ++k) score = score + pairs[13 * k + 12];
+  return score;
+}
+
+m44 fuse_answer(const std::vector<High>& hs, float sum) {
+  float tx = 0, ty = 0, tz = 0;
+  for (const High& h : hs) {
+    tx = tx + h.qt.tx * (h.score / sum);
+    ty = ty + h.qt.ty * (h.score / sum);
+    tz = tz + h.qt.tz * (h.score / sum);
+  }
+  float a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+  for (const High& h : hs) {
+    const quatf q = {h.qt.qw, h.qt.qx, h.qt.qy, h.qt.qz};
+    const f3 u = quat_rotate(q, f3{1.f, 0.f, 0.f}), v = quat_rotate(q, f3{0.f, 1.f, 0.f});
+    a[0] = a[0] + u.x * (h.score / sum); a[1] = a[1] + u.y * (h.score / sum); a[2] = a[2] + u.z * (h.score / sum);
+    b[0] = b[0] + v.x * (h.score / sum); b[1] = b[1] + v.y * (h.score / sum); b[2] = b[2] + v.z * (h.score / sum);
+  }
+  const m33 R = axes_to_rot(normalize3(f3{a[0], a[1], a[2]}), normalize3(f3{b[0], b[1], b[2]}));
+  m44 T = eye44();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T.m[i][j] = R.m[i][j];
+  T.m[0][3] = tx; T.m[1][3] = ty; T.m[2][3] = tz;
+  return T;
+}
+
+}  // namespace fccf

@@ -1,0 +1,65 @@
+// host_stages.h — the serial, tiny-cardinality stages of FCCF-PCR that libfccf
+// runs on the host CPU in round 1 (<= a few thousand items each).  Bit-level
+// arithmetic follows fccf_math.h, the same conventions as the device kernels.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../../include/fccf.h"
+#include "fccf_math.h"
+#include "kernels.h"
+
+namespace fccf {
+
+struct Plane {        // facenode of a selected plane (FCCF.cpp:47-58)
+  float c[3], n[3];   // average_centry_*, average_normal_* (never renormalised, App. B Q3)
+  float fps;          // face_point_size
+  int32_t nvox;       // voxelgrothnode.size()
+};
+
+struct Base {         // face_base + type (FCCF.cpp:60-65, :454-461)
+  int32_t i1, i2;
+  float angle;
+  int32_t type;       // 0 smooth/smooth, 1 rough/rough, 2 mixed; -1/-2 = no type (NaN roughness, Q5)
+};
+
+struct GrowOut {
+  std::vector<Plane> planes;     // <= select_plane_number + 1
+  std::vector<double> theta;     // roughness per selected plane
+  std::vector<Plane> groups;     // all groups after stage 2 + range_face (debug)
+  std::vector<int32_t> galloc;   // their is_allocate flags
+};
+
+// face_extrate region growing (:536-648), range_face (:409-427), selection (:650-677).
+GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P);
+// select_base (:429-468); `side` picks the out-of-range type sentinel (-1 / -2).
+std::vector<Base> select_base(const std::vector<Plane>& F, const std::vector<double>& theta, const fccf_params& P,
+                              int side);
+
+struct QT {  // transform_q_t (FCCF.cpp:74-84)
+  float qw, qx, qy, qz, tx, ty, tz;
+  uint32_t alloc;
+};
+
+// transform_cluster (:1040-1231) incl. range_cluster and average_normal.
+void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
+                       int64_t* nclusters);
+
+// quick_verify (:680-783) with ceres_refine (:210-249): refines T in place, returns score.
+float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2, const fccf_params& P,
+                   int* npairs);
+
+// Ceres-1.14-style LM on plane pairs (13 floats each: p1 n1 p2 n2 w); best x = q(xyzw), t.
+void lm_solve(const float* pairs, int P, double best[7]);
+
+struct High {
+  QT qt;
+  float score;
+};
+// weight_normal + fuse_answer (:1253-1368)
+m44 fuse_answer(const std::vector<High>& hs, float sum);
+
+QT qt_from_T(const m44& T);
+m44 T_from_qt(const QT& q);
+
+}  // namespace fccf

@@ -73,10 +73,12 @@ void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, do
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float voxel_point_threshold,
                      float curvature_threshold, VoxRec* planar_out, float* resid_out, FaceBufs b, hipStream_t st);
 
-// Octree bound simulation over xyz[0..*d_n) starting from *state (single workgroup).
+// Octree bound simulation over xyz[0..*d_n) starting from *state (one workgroup per
+// sequence; `batch` sequences at xyz + e*xyz_stride with state[e]).
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr,
-                OctState* state, hipStream_t st);
-void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st);
+                OctState* state, hipStream_t st, int batch = 1, size_t xyz_stride = 0, size_t aggr_stride = 0);
+void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
+                size_t xyz_stride = 0, size_t aggr_stride = 0);
 constexpr uint32_t AGGR_BLOCK = 4096;
 
 }  // namespace fccf

@@ -1,0 +1,51 @@
+// match.h — device-side tables of K5 (coplane-pair matching) and K7 (fine verify).
+#pragma once
+#include <stdint.h>
+
+#include "devprim.h"
+#include "fccf_math.h"
+
+namespace fccf {
+
+constexpr int MAX_PLANES = 17;   // select_plane_number + 1 planes are kept (:670)
+constexpr int MAX_BASES = 136;   // C(17, 2)
+
+struct MPlane { float c[3], n[3], fps; int32_t nvox; };
+struct MBase { int32_t i1, i2; float angle; int32_t type; };
+
+struct MatchIn {
+  MPlane F1[MAX_PLANES], F2[MAX_PLANES];
+  MBase B1[MAX_BASES], B2[MAX_BASES];
+  int32_t nF1, nF2, nB1, nB2;
+  float ang_same;    // included_angle_same_threshold
+  float third_thr;   // third_plane_threshold
+  AngleCut third_cut;  // theta < third_plane_normal_threshold
+};
+
+struct MCand { float R[9]; float t[3]; };
+struct QTd { float qw, qx, qy, qz, tx, ty, tz; uint32_t alloc; };
+
+// counts/types/offsets need K entries; totals 3; c[t]/q[t] sized by the caller.
+void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
+                      MCand* c[3], QTd* q[3], hipStream_t st);
+
+// ------------------------------------------------ K7: fine_verify (FCCF.cpp:785-839)
+constexpr int MAX_EVAL = 16;
+struct FineBufs {
+  float* s2t;          // E * n2 * 3
+  float* aggr1;        // aggregates of S1
+  float* aggr2;        // E * blocks(n2) * 6
+  OctState* state;     // E + 1 (slot E = after S1)
+  uint64_t *k0, *k1;   // E * (n1 + n2)
+  uint32_t *v0, *v1;
+  uint32_t* starts;    // E * (n1 + n2) + 1
+  uint32_t* st_counts; // per segment: source, target counts (2 u32)
+  uint32_t* scal;      // [0]=n total keys, [1]=nbits, [2]=nseg, [3]=shift, [4]=n1, [5]=n2, [6]=E
+  float* scores;       // E
+  m44* T;              // E
+  SortScratch ss;
+};
+void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
+                       hipStream_t st);
+
+}  // namespace fccf

@@ -1,0 +1,218 @@
+// match.hip — K5: all-pairs coplane-pair correspondence search (FCCF.cpp:1410-1428)
+// fused with the closed-form transform of each match (computer_transform, :841-1018).
+//
+// One lane per test k = i1 * B2 + i2 (b1-major, the reference loop order).  A test
+// passes when |angle1 - angle2| < 5 deg and the roughness types agree; it then emits
+// one transform per (third source plane, matching target plane) in loop order, or
+// the weighted-centroid fallback (:1000-1017).  Emission is two-pass: counts ->
+// per-type exclusive scan -> write, so each type's list is in exactly the order
+// transformation_vecter[type] receives push_backs.  The plane/pair tables (<= 16
+// planes, <= 120 pairs per cloud) live in LDS.
+#include "kernels.h"
+#include "match.h"
+
+namespace fccf {
+namespace {
+
+struct Ctx {
+  m33 rot;
+  f3 n1, m1, n2, m2r, n1cm1, n2cm2;
+};
+
+__device__ void prep(const MatchIn& M, int i11, int i12, int i21, int i22, Ctx& c) {
+  const MPlane *A = M.F1, *B = M.F2;
+  c.n1 = {A[i11].n[0], A[i11].n[1], A[i11].n[2]};
+  c.m1 = {A[i12].n[0], A[i12].n[1], A[i12].n[2]};
+  c.n2 = {B[i21].n[0], B[i21].n[1], B[i21].n[2]};
+  f3 m2 = {B[i22].n[0], B[i22].n[1], B[i22].n[2]};
+  const f3 r1 = normalize3(cross3(c.n2, c.n1));
+  const float n2dn1 = dot3(c.n2, c.n1);
+  const float r1cn2dn1 = dot3(cross3(r1, c.n2), c.n1);
+  const m33 R1 = rodrigues(n2dn1, r1cn2dn1, r1);
+  m2 = mul3v(R1, m2);
+  const f3 r2 = c.n1;
+  const float m2dm1 = dot3(m2, c.m1), m2dr2 = dot3(m2, r2), m1dr2 = dot3(c.m1, r2);
+  const float r2cm2dm1 = dot3(cross3(r2, m2), c.m1);
+  const float cos2 = (m2dm1 - (m2dr2 * m1dr2)) / (1.f - (m2dr2 * m1dr2));
+  const float sin2 = (r2cm2dm1) / (1.f - (m2dr2 * m1dr2));
+  c.rot = mul33(rodrigues(cos2, sin2, r2), R1);
+  c.m2r = m2;
+  c.n1cm1 = normalize3(cross3(c.n1, c.m1));
+  c.n2cm2 = normalize3(cross3(c.n2, m2));
+}
+
+__device__ __forceinline__ m44 rot_only(const m33& R) {
+  m44 T = eye44();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T.m[i][j] = R.m[i][j];
+  return T;
+}
+
+// ((A^T A)^-1 A^T) D with Eigen's 3x3 cofactor inverse (compute_inverse<...,3>).
+__device__ f3 ls3(f3 n1, f3 m1, f3 k1, f3 D) {
+  m33 A, AT;
+  const f3 rows[3] = {n1, m1, k1};
+  for (int i = 0; i < 3; ++i) {
+    A.m[i][0] = rows[i].x; A.m[i][1] = rows[i].y; A.m[i][2] = rows[i].z;
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) AT.m[i][j] = A.m[j][i];
+  const m33 M = mul33(AT, A);
+#define COF(i, j) (M.m[((i) + 1) % 3][((j) + 1) % 3] * M.m[((i) + 2) % 3][((j) + 2) % 3] - \
+                   M.m[((i) + 1) % 3][((j) + 2) % 3] * M.m[((i) + 2) % 3][((j) + 1) % 3])
+  const float c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
+  const float det = c0 * M.m[0][0] + (c1 * M.m[1][0] + c2 * M.m[2][0]);
+  const float inv = 1.f / det;
+  m33 Mi;
+  Mi.m[0][0] = c0 * inv; Mi.m[0][1] = c1 * inv; Mi.m[0][2] = c2 * inv;
+  Mi.m[1][0] = COF(0, 1) * inv; Mi.m[1][1] = COF(1, 1) * inv; Mi.m[1][2] = COF(2, 1) * inv;
+  Mi.m[2][0] = COF(0, 2) * inv; Mi.m[2][1] = COF(1, 2) * inv; Mi.m[2][2] = COF(2, 2) * inv;
+#undef COF
+  return mul3v(mul33(Mi, AT), D);
+}
+
+// Returns the number of transforms the test emits; writes them when out != null.
+__device__ int match_test(const MatchIn& M, int k, MCand* out) {
+  const int i1 = k / M.nB2, i2 = k % M.nB2;
+  const MBase& b1 = M.B1[i1];
+  const MBase& b2 = M.B2[i2];
+  if (!(fabsf(b1.angle - b2.angle) < M.ang_same && b1.type == b2.type)) return 0;
+  Ctx c;
+  prep(M, b1.i1, b1.i2, b2.i1, b2.i2, c);
+  const m44 T0 = rot_only(c.rot);
+  const MPlane *A = M.F1, *B = M.F2;
+  int cnt = 0;
+  for (int k3 = 0; k3 < M.nF1; ++k3) {
+    if (k3 == b1.i1 || k3 == b1.i2) continue;
+    const f3 kn = {A[k3].n[0], A[k3].n[1], A[k3].n[2]};
+    if (!(fabsf(dot3(c.n1cm1, kn)) > M.third_thr)) continue;
+    for (int q = 0; q < M.nF2; ++q) {
+      if (q == b2.i1 || q == b2.i2) continue;
+      const f3 pn = tf_so3(T0, B[q].n[0], B[q].n[1], B[q].n[2]);
+      const float cs = normal_cos(kn, pn);
+      if (angle_lt(cs, M.third_cut) && fabsf(dot3(c.n2cm2, pn)) > M.third_thr) {
+        if (out) {
+          const f3 pc = tf_se3(T0, B[q].c[0], B[q].c[1], B[q].c[2]);
+          const f3 c11 = {A[b1.i1].c[0], A[b1.i1].c[1], A[b1.i1].c[2]};
+          const f3 c12 = {A[b1.i2].c[0], A[b1.i2].c[1], A[b1.i2].c[2]};
+          const f3 c13 = {A[k3].c[0], A[k3].c[1], A[k3].c[2]};
+          const f3 c21 = {B[b2.i1].c[0], B[b2.i1].c[1], B[b2.i1].c[2]};
+          const f3 c22 = {B[b2.i2].c[0], B[b2.i2].c[1], B[b2.i2].c[2]};
+          const f3 D = {dot3(c11, c.n1) - dot3(c21, c.n2), dot3(c12, c.m1) - dot3(c22, c.m2r),
+                        dot3(c13, kn) - dot3(pc, pn)};
+          const f3 t = ls3(c.n1, c.m1, kn, D);
+          MCand& o = out[cnt];
+          for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) o.R[3 * i + j] = c.rot.m[i][j];
+          o.t[0] = t.x; o.t[1] = t.y; o.t[2] = t.z;
+        }
+        ++cnt;
+      }
+    }
+  }
+  if (cnt == 0) {
+    if (out) {
+      const MPlane &a = A[b1.i1], &b = A[b1.i2], &d = B[b2.i1], &e = B[b2.i2];
+      const float sx = (a.c[0] * a.fps + b.c[0] * b.fps) / (a.fps + b.fps);
+      const float sy = (a.c[1] * a.fps + b.c[1] * b.fps) / (a.fps + b.fps);
+      const float sz = (a.c[2] * a.fps + b.c[2] * b.fps) / (a.fps + b.fps);
+      const float tx = (d.c[0] * d.fps + e.c[0] * e.fps) / (d.fps + e.fps);
+      const float ty = (d.c[1] * d.fps + e.c[1] * e.fps) / (d.fps + e.fps);
+      const float tz = (d.c[2] * d.fps + e.c[2] * e.fps) / (d.fps + e.fps);
+      const f3 tc = mul3v(c.rot, f3{tx, ty, tz});
+      MCand& o = out[0];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) o.R[3 * i + j] = c.rot.m[i][j];
+      o.t[0] = sx - tc.x; o.t[1] = sy - tc.y; o.t[2] = sz - tc.z;
+    }
+    cnt = 1;
+  }
+  return cnt;
+}
+
+__global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__ Mp, uint32_t* __restrict__ cnt,
+                                                     int32_t* __restrict__ type) {
+  __shared__ MatchIn M;
+  if (threadIdx.x == 0) M = *Mp;
+  __syncthreads();
+  const int K = M.nB1 * M.nB2;
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
+    const int n = match_test(M, k, nullptr);
+    cnt[k] = (uint32_t)n;
+    type[k] = n ? M.B1[k / M.nB2].type : -1;
+  }
+}
+
+// single block: per-type exclusive scan in test order
+__global__ void __launch_bounds__(256) k_match_scan(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ type, uint32_t* __restrict__ off,
+                                                    uint32_t* __restrict__ totals) {
+  __shared__ uint32_t sh[4][3];
+  const int K = Mp->nB1 * Mp->nB2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t carry[3] = {0, 0, 0};
+  for (int b0 = 0; b0 < K; b0 += 256) {
+    const int k = b0 + threadIdx.x;
+    const uint32_t c = k < K ? cnt[k] : 0u;
+    const int t = k < K ? type[k] : -1;
+    uint32_t ex = 0;
+    for (int ty = 0; ty < 3; ++ty) {
+      uint32_t x = (t == ty) ? c : 0u;
+      const uint32_t v = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) sh[w][ty] = x;
+      __syncthreads();
+      uint32_t wp = 0;
+      for (int ww = 0; ww < w; ++ww) wp += sh[ww][ty];
+      const uint32_t tot = sh[0][ty] + sh[1][ty] + sh[2][ty] + sh[3][ty];
+      __syncthreads();
+      if (t == ty) ex = carry[ty] + wp + x - v;
+      carry[ty] += tot;
+    }
+    if (k < K) off[k] = ex;
+  }
+  if (threadIdx.x < 3) totals[threadIdx.x] = carry[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ type, const uint32_t* __restrict__ off,
+                                                    MCand* __restrict__ c0, MCand* __restrict__ c1,
+                                                    MCand* __restrict__ c2, QTd* __restrict__ q0,
+                                                    QTd* __restrict__ q1, QTd* __restrict__ q2) {
+  __shared__ MatchIn M;
+  if (threadIdx.x == 0) M = *Mp;
+  __syncthreads();
+  const int K = M.nB1 * M.nB2;
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
+    if (!cnt[k]) continue;
+    const int t = type[k];
+    MCand* cb = t == 0 ? c0 : (t == 1 ? c1 : c2);
+    QTd* qb = t == 0 ? q0 : (t == 1 ? q1 : q2);
+    const uint32_t o = off[k];
+    const int n = match_test(M, k, cb + o);
+    for (int j = 0; j < n; ++j) {  // fused R -> quaternion (FCCF.cpp:1437-1462)
+      const MCand& c = cb[o + j];
+      m33 R;
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) R.m[a][b] = c.R[3 * a + b];
+      const quatf q = quat_from_rot(R);
+      qb[o + j] = {q.w, q.x, q.y, q.z, c.t[0], c.t[1], c.t[2], 0u};
+    }
+  }
+}
+
+}  // namespace
+
+void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
+                      MCand* c[3], QTd* q[3], hipStream_t st) {
+  if (K <= 0) return;
+  const int g = (K + 255) / 256;
+  k_match_count<<<g, 256, 0, st>>>(d_in, cnt, type);
+  k_match_scan<<<1, 256, 0, st>>>(d_in, cnt, type, off, totals);
+  k_match_emit<<<g, 256, 0, st>>>(d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]);
+}
+
+}  // namespace fccf

@@ -1,6 +1,585 @@
-// pipeline.cpp — fccf_register: placeholder until the full driver lands.
+// pipeline.cpp — fccf_register / fccf_register_device: the whole FCCF-PCR
+// registration (FCCF.cpp main :1668-1683 + computer_transform_guess :1370-1608).
+//
+// Device (two HIP streams, one per cloud, no host round-trip inside a cloud):
+//   K1 VoxelGrid x2 -> remove-NaN -> K2/K3 octree leaves + plane fit + compaction
+// Host (round 1; <= a few thousand items): region growing / plane selection,
+//   select_base, clustering, quick_verify + LM, score ranking, fusion.
+// Device: K5 coplane-pair matching + closed-form transforms, K7 fine verify (batched).
+//
+// Cloud roles follow the reference's swapped call (FCCF.cpp:1683): driver
+// "source" (index 0 here, F1/S1) is the TAR file, driver "target" (index 1, F2/S2)
+// is the SRC file; the output T maps src-file points into the tar frame.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+#include "host_stages.h"
+#include "kernels.h"
+#include "match.h"
 #include "pipeline.h"
-extern "C" int fccf_register(fccf_ctx*, const float*, int64_t, const float*, int64_t, float, const fccf_params*,
-                             float*, fccf_stats*) { return FCCF_E_INTERNAL; }
-extern "C" int fccf_register_device(fccf_ctx*, const float*, int64_t, const float*, int64_t, float,
-                                    const fccf_params*, float*, fccf_stats*) { return FCCF_E_INTERNAL; }
+
+namespace fccf {
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); }
+
+// ------------------------------------------------------------ remove-NaN (:1374-1375)
+__global__ void k_finite_flags(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
+                               uint32_t* __restrict__ f) {
+  const uint32_t n = *d_n;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    f[i] = finite3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]) ? 1u : 0u;
+}
+__global__ void k_finite_scatter(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
+                                 const uint32_t* __restrict__ f, const uint32_t* __restrict__ off,
+                                 float* __restrict__ out) {
+  const uint32_t n = *d_n;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    if (f[i]) {
+      const uint32_t o = off[i];
+      out[3 * o] = xyz[3 * i]; out[3 * o + 1] = xyz[3 * i + 1]; out[3 * o + 2] = xyz[3 * i + 2];
+    }
+}
+
+inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
+  uint32_t g = (cap + per - 1) / per;
+  return g < 1 ? 1 : (g > mx ? mx : g);
+}
+
+// ------------------------------------------------------------ exact angle cuts
+// theta(c) is monotone non-increasing on [-1,1]; find c* with theta(c) > thr <=> c < gt
+// and theta(c) < thr <=> c > lt, then verify the claim around the cut.
+uint32_t okey(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+float okey_inv(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+AngleCut make_cut(float thr) {
+  auto first_true = [](uint32_t lo, uint32_t hi, auto pred) {  // pred monotone false..true on [lo,hi]
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (pred(mid)) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  const uint32_t lo = okey(-1.0f), hi = okey(1.0f);
+  const uint32_t kg = first_true(lo, hi + 1, [&](uint32_t k) { return !(theta_of_cos_host(okey_inv(k)) > thr); });
+  const uint32_t kl = first_true(lo, hi + 1, [&](uint32_t k) { return theta_of_cos_host(okey_inv(k)) < thr; });
+  AngleCut c;
+  c.gt = okey_inv(kg);
+  c.lt = okey_inv(kl - 1);
+  for (int64_t d = -4096; d <= 4096; ++d) {  // monotonicity check around both cuts
+    for (uint32_t base : {kg, kl}) {
+      const int64_t k = (int64_t)base + d;
+      if (k < (int64_t)lo || k > (int64_t)hi) continue;
+      const float v = okey_inv((uint32_t)k);
+      const float th = theta_of_cos_host(v);
+      if ((th > thr) != (v >= -1.0f && v < c.gt) || (th < thr) != (v > c.lt && v <= 1.0f))
+        throw Error(FCCF_E_INTERNAL, "angle cut not monotone");
+    }
+  }
+  return c;
+}
+
+// ------------------------------------------------------------ per-cloud device state
+struct CloudWS {
+  uint32_t cap = 0;
+  const float* in = nullptr;
+  float* in_copy = nullptr;
+  uint32_t* sc = nullptr;  // [0] n_in, [1] m1, [2] m1 finite, [3] m2
+  float *ds1 = nullptr, *ds1f = nullptr, *ds2 = nullptr;
+  uint32_t *fflag = nullptr, *foff = nullptr;
+  VGBufs vg;
+  FaceBufs fb;
+  VoxRec* planar = nullptr;
+  float* resid = nullptr;
+};
+
+size_t cloud_bytes(uint32_t cap, bool host_input) {
+  const size_t N = cap;
+  size_t b = 0;
+  b += host_input ? 12 * N : 0;                               // input copy
+  b += 12 * N * 3 + 8 * N + 64;                                // ds1, ds1f, ds2, flags, offsets
+  b += voxel_grid_bytes(cap);                                  // K1
+  b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
+  b += 6 * 4 * ((N + AGGR_BLOCK - 1) / AGGR_BLOCK + 1) + 256;  // aggregates, state, centroid
+  b += sizeof(VoxRec) * N + 4 * 4 * N + 64;                    // leaf records, flags, offsets
+  b += sizeof(VoxRec) * N + 12 * N;                            // planar out, residual out
+  b += sort_scratch_bytes(cap) + 64 * 256;                     // sort scratch + alignment slack
+  return b;
+}
+
+void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
+  w.cap = cap;
+  if (host_input) w.in_copy = a.take_n<float>(3 * (size_t)cap);
+  w.sc = a.take_n<uint32_t>(16);
+  w.ds1 = a.take_n<float>(3 * (size_t)cap);
+  w.ds1f = a.take_n<float>(3 * (size_t)cap);
+  w.ds2 = a.take_n<float>(3 * (size_t)cap);
+  w.fflag = a.take_n<uint32_t>(cap);
+  w.foff = a.take_n<uint32_t>(cap);
+  w.vg = voxel_grid_carve(a, cap);
+  FaceBufs& f = w.fb;
+  f.c0 = a.take_n<uint64_t>(cap);
+  f.c1 = a.take_n<uint64_t>(cap);
+  f.v0 = a.take_n<uint32_t>(cap);
+  f.v1 = a.take_n<uint32_t>(cap);
+  f.starts = a.take_n<uint32_t>((size_t)cap + 1);
+  f.aggr = a.take_n<float>(6 * ((size_t)(cap + AGGR_BLOCK - 1) / AGGR_BLOCK + 1));
+  f.oct = a.take_n<OctState>(1);
+  f.centroid = a.take_n<float>(4);
+  f.recs = a.take_n<VoxRec>(cap);
+  f.flag_planar = a.take_n<uint32_t>(cap);
+  f.resid_cnt = a.take_n<uint32_t>(cap);
+  f.planar_off = a.take_n<uint32_t>(cap);
+  f.resid_off = a.take_n<uint32_t>(cap);
+  uint32_t* s = a.take_n<uint32_t>(16);
+  f.nleaf = s;
+  f.nbits = s + 1;
+  f.nplanar = s + 2;
+  f.nresid = s + 3;
+  f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
+  w.planar = a.take_n<VoxRec>(cap);
+  w.resid = a.take_n<float>(3 * (size_t)cap);
+}
+
+// Device part of one cloud: both VoxelGrid passes, remove-NaN, face voxels.
+void enqueue_cloud(CloudWS& w, float leaf, const fccf_params& P, hipStream_t st) {
+  voxel_grid(w.in, w.sc, w.cap, leaf, w.ds1, w.sc + 1, w.vg, st);  // main :1668-1678
+  k_finite_flags<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag);  // driver :1374-1375
+  exclusive_scan_u32(w.fflag, w.foff, w.sc + 1, w.cap, w.sc + 2, w.vg.ss, st);
+  k_finite_scatter<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag, w.foff, w.ds1f);
+  voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st);  // driver :1377-1387
+  cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, st);
+  face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
+  face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.planar, w.resid, w.fb,
+                  st);
+}
+
+template <class T>
+std::vector<T> d2h(const T* d, size_t n, hipStream_t st) {
+  std::vector<T> v(n);
+  if (n) HIP_CHECK(hipMemcpyAsync(v.data(), d, sizeof(T) * n, hipMemcpyDeviceToHost, st));
+  return v;
+}
+
+void dump_planes(fccf_ctx* c, const std::string& k, const std::vector<Plane>& F) {
+  if (!c->debug) return;
+  std::vector<float> v;
+  for (const Plane& p : F) {
+    v.insert(v.end(), p.c, p.c + 3);
+    v.insert(v.end(), p.n, p.n + 3);
+    v.push_back(p.fps);
+    v.push_back((float)p.nvox);
+  }
+  c->dbg_put(k, v);
+}
+
+}  // namespace
+
+void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
+                  float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
+  fccf_stats S;
+  std::memset(&S, 0, sizeof S);
+  S.n_src = n_src;
+  S.n_tar = n_tar;
+  if (c->debug) c->dbg.clear();
+  const auto t_all = clk::now();
+  auto t0 = clk::now();
+  hipStream_t st0 = c->st[0], st1 = c->st[1];
+  // cloud 0 = driver source = TAR file; cloud 1 = driver target = SRC file (:1683)
+  CloudWS w[2];
+  const int64_t nin[2] = {n_tar, n_src};
+  const float* hin[2] = {tar, src};
+  const uint32_t cap[2] = {(uint32_t)std::max<int64_t>(nin[0], 1), (uint32_t)std::max<int64_t>(nin[1], 1)};
+  c->arena.ensure(cloud_bytes(cap[0], !on_device) + cloud_bytes(cap[1], !on_device) + (1 << 20));
+  c->arena.reset();
+  for (int k = 0; k < 2; ++k) {
+    carve_cloud(c->arena, w[k], cap[k], !on_device);
+    hipStream_t st = c->st[k];
+    const uint32_t n = (uint32_t)nin[k];
+    if (on_device) {
+      w[k].in = hin[k];
+    } else {
+      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n, hipMemcpyHostToDevice, st));
+      w[k].in = w[k].in_copy;
+    }
+    uint32_t* hn = (uint32_t*)c->pinned.get(64) + k;
+    *hn = n;
+    HIP_CHECK(hipMemcpyAsync(w[k].sc, hn, 4, hipMemcpyHostToDevice, st));
+    enqueue_cloud(w[k], leaf, P, st);
+    HIP_CHECK(hipGetLastError());
+  }
+  // counts of both clouds
+  uint32_t sc[2][4], fsc[2][4];
+  for (int k = 0; k < 2; ++k) {
+    HIP_CHECK(hipMemcpyAsync(sc[k], w[k].sc, 16, hipMemcpyDeviceToHost, c->st[k]));
+    HIP_CHECK(hipMemcpyAsync(fsc[k], w[k].fb.nleaf, 16, hipMemcpyDeviceToHost, c->st[k]));
+  }
+  HIP_CHECK(hipStreamSynchronize(st0));
+  HIP_CHECK(hipStreamSynchronize(st1));
+  S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
+  t0 = clk::now();
+  S.m_tar = sc[0][3];
+  S.m_src = sc[1][3];
+  std::vector<VoxRec> vox[2];
+  for (int k = 0; k < 2; ++k) vox[k] = d2h(w[k].planar, fsc[k][2], c->st[k]);
+  HIP_CHECK(hipStreamSynchronize(st0));
+  HIP_CHECK(hipStreamSynchronize(st1));
+  S.vox1 = fsc[0][2]; S.vox2 = fsc[1][2];
+  S.res1 = fsc[0][3]; S.res2 = fsc[1][3];
+  if (c->debug) {
+    const char* dsn[2] = {"ds_tar", "ds_src"};
+    for (int k = 0; k < 2; ++k) {
+      const std::string s = std::to_string(k + 1);
+      auto a = d2h(w[k].ds1, 3 * (size_t)sc[k][1], c->st[k]);
+      auto b = d2h(w[k].ds2, 3 * (size_t)sc[k][3], c->st[k]);
+      auto ce = d2h(w[k].fb.centroid, 4, c->st[k]);
+      auto oc = d2h(w[k].fb.oct, 1, c->st[k]);
+      auto recs = d2h(w[k].fb.recs, fsc[k][0], c->st[k]);
+      auto pl = d2h(w[k].fb.flag_planar, fsc[k][0], c->st[k]);
+      auto rc = d2h(w[k].fb.resid_cnt, fsc[k][0], c->st[k]);
+      auto res = d2h(w[k].resid, 3 * (size_t)fsc[k][3], c->st[k]);
+      HIP_CHECK(hipStreamSynchronize(c->st[k]));
+      c->dbg_put(dsn[k], a);
+      c->dbg_put("ds" + s, b);
+      c->dbg_put("centroid" + s, ce);
+      std::vector<double> o = {oc[0].min[0], oc[0].min[1], oc[0].min[2], (double)oc[0].depth};
+      c->dbg_put("oct" + s, o);
+      std::vector<float> vv;
+      for (const VoxRec& r : vox[k]) {
+        vv.insert(vv.end(), r.c, r.c + 3);
+        vv.insert(vv.end(), r.n, r.n + 3);
+        vv.push_back((float)r.count);
+        vv.push_back(0.f);
+      }
+      c->dbg_put("vox" + s, vv);
+      std::vector<int32_t> vs;
+      std::vector<float> vc;
+      for (uint32_t i = 0; i < fsc[k][0]; ++i) {
+        vs.push_back(recs[i].count);
+        vs.push_back(pl[i] ? 1 : (rc[i] ? 2 : 0));
+        vc.push_back(recs[i].curvature);
+      }
+      c->dbg_put("vstat" + s, vs);
+      c->dbg_put("vcurv" + s, vc);
+      c->dbg_put("res" + s, res);
+    }
+  }
+
+  // ---------------- host: growing + selection + select_base
+  GrowOut g[2];
+  std::vector<Base> base[2];
+  for (int k = 0; k < 2; ++k) {
+    g[k] = grow_and_select(vox[k].data(), (int)vox[k].size(), P);
+    base[k] = select_base(g[k].planes, g[k].theta, P, k + 1);
+  }
+  S.groups1 = (int64_t)g[0].groups.size();
+  S.groups2 = (int64_t)g[1].groups.size();
+  S.planes1 = (int64_t)g[0].planes.size();
+  S.planes2 = (int64_t)g[1].planes.size();
+  S.bases1 = (int64_t)base[0].size();
+  S.bases2 = (int64_t)base[1].size();
+  S.ms[FCCF_T_GROW] = ms_since(t0);
+  if (c->debug)
+    for (int k = 0; k < 2; ++k) {
+      const std::string s = std::to_string(k + 1);
+      dump_planes(c, "groups" + s, g[k].groups);
+      dump_planes(c, "planes" + s, g[k].planes);
+      c->dbg_put("theta" + s, g[k].theta);
+      c->dbg_put("galloc" + s, g[k].galloc);
+      std::vector<int32_t> bv;
+      for (const Base& b : base[k]) {
+        int32_t ab;
+        std::memcpy(&ab, &b.angle, 4);
+        bv.push_back(b.i1); bv.push_back(b.i2); bv.push_back(ab); bv.push_back(b.type < 0 ? -1 : b.type);
+      }
+      c->dbg_put("bases" + s, bv);
+    }
+
+  // ---------------- device: K5 matching + closed-form transforms
+  t0 = clk::now();
+  const int K = (int)(base[0].size() * base[1].size());
+  S.K = K;
+  if (g[0].planes.size() > (size_t)MAX_PLANES || g[1].planes.size() > (size_t)MAX_PLANES ||
+      base[0].size() > (size_t)MAX_BASES || base[1].size() > (size_t)MAX_BASES)
+    throw Error(FCCF_E_INTERNAL, "plane table capacity");
+  MatchIn M;
+  std::memset(&M, 0, sizeof M);
+  for (int k = 0; k < 2; ++k) {
+    MPlane* dst = k == 0 ? M.F1 : M.F2;
+    for (size_t i = 0; i < g[k].planes.size(); ++i) {
+      const Plane& p = g[k].planes[i];
+      std::memcpy(dst[i].c, p.c, 12);
+      std::memcpy(dst[i].n, p.n, 12);
+      dst[i].fps = p.fps;
+      dst[i].nvox = p.nvox;
+    }
+    MBase* bd = k == 0 ? M.B1 : M.B2;
+    for (size_t i = 0; i < base[k].size(); ++i) bd[i] = {base[k][i].i1, base[k][i].i2, base[k][i].angle, base[k][i].type};
+  }
+  M.nF1 = (int)g[0].planes.size();
+  M.nF2 = (int)g[1].planes.size();
+  M.nB1 = (int)base[0].size();
+  M.nB2 = (int)base[1].size();
+  M.ang_same = P.included_angle_same_threshold;
+  M.third_thr = P.third_plane_threshold;
+  M.third_cut = make_cut(P.third_plane_normal_threshold);
+  const size_t per = (size_t)std::max(1, std::max(0, M.nF1 - 2) * std::max(0, M.nF2 - 2));
+  const size_t ccap = std::max<size_t>(1, (size_t)K * per);
+  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + 3 * ccap * (sizeof(MCand) + sizeof(QTd)) +
+                   (1 << 16));
+  c->arena2.reset();
+  MatchIn* dM = c->arena2.take_n<MatchIn>(1);
+  uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
+  int32_t* dtype = c->arena2.take_n<int32_t>(std::max(K, 1));
+  uint32_t* doff = c->arena2.take_n<uint32_t>(std::max(K, 1));
+  uint32_t* dtot = c->arena2.take_n<uint32_t>(4);
+  MCand* dc[3];
+  QTd* dq[3];
+  for (int t = 0; t < 3; ++t) {
+    dc[t] = c->arena2.take_n<MCand>(ccap);
+    dq[t] = c->arena2.take_n<QTd>(ccap);
+  }
+  uint32_t tot[4] = {0, 0, 0, 0};
+  HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
+  HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
+  match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st0);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(tot, dtot, 12, hipMemcpyDeviceToHost, st0));
+  HIP_CHECK(hipStreamSynchronize(st0));
+  std::vector<QTd> qraw[3];
+  for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
+  std::vector<uint32_t> hcnt = d2h(dcnt, (size_t)K, st0);
+  HIP_CHECK(hipStreamSynchronize(st0));
+  int64_t kpass = 0;
+  for (int k = 0; k < K; ++k) kpass += hcnt[k] ? 1 : 0;
+  S.K_pass = kpass;
+  for (int t = 0; t < 3; ++t) S.cand[t] = tot[t];
+  S.ms[FCCF_T_MATCH] = ms_since(t0);
+  if (c->debug)
+    for (int t = 0; t < 3; ++t) {
+      auto cv = d2h(dc[t], tot[t], st0);
+      HIP_CHECK(hipStreamSynchronize(st0));
+      std::vector<float> v;
+      for (const MCand& m : cv) {
+        for (int i = 0; i < 3; ++i) {
+          v.insert(v.end(), m.R + 3 * i, m.R + 3 * i + 3);
+          v.push_back(m.t[i]);
+        }
+        v.insert(v.end(), {0.f, 0.f, 0.f, 1.f});
+      }
+      c->dbg_put("cand" + std::to_string(t), v);
+    }
+
+  // ---------------- host: clustering, quick_verify (LM), score ranking
+  const int transformation_num = (int)(tot[0] + tot[1] + tot[2]);
+  const int analyse_max = (int)P.fine_verify_number;
+  struct TS { m44 T; float score, score2; };
+  std::vector<TS> ctv[3];
+  std::vector<int64_t> counts = {(int64_t)K, kpass, (int64_t)tot[0], (int64_t)tot[1], (int64_t)tot[2]};
+  for (int t = 0; t < 3; ++t) {
+    auto tc = clk::now();
+    std::vector<QT> qv(qraw[t].size());
+    for (size_t i = 0; i < qv.size(); ++i) {
+      const QTd& a = qraw[t][i];
+      qv[i] = {a.qw, a.qx, a.qy, a.qz, a.tx, a.ty, a.tz, 0u};
+    }
+    std::vector<QT> fine;
+    const int cluster_num =
+        transformation_num ? (int)(P.seclct_cluster_number * (float)qv.size() / (float)transformation_num) : 0;
+    int64_t ncl = 0;
+    transform_cluster(qv, fine, cluster_num, P, &ncl);
+    counts.push_back(ncl);
+    S.fine[t] = (int64_t)fine.size();
+    S.ms[FCCF_T_CLUSTER] += ms_since(tc);
+    tc = clk::now();
+    std::vector<float> fdump, qdump;
+    for (const QT& q : fine) {
+      const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
+      fdump.insert(fdump.end(), a, a + 8);
+      TS ts;
+      ts.T = T_from_qt(q);
+      int np = 0;
+      ts.score = quick_verify(ts.T, g[0].planes, g[1].planes, P, &np);
+      ts.score2 = 0.f;
+      if ((float)np >= P.required_optimize_plane) ++S.lm_solves;
+      ctv[t].push_back(ts);
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) qdump.push_back(ts.T.m[i][j]);
+      qdump.push_back(ts.score);
+      qdump.push_back((float)np);
+    }
+    // score_range (:1233-1251): exchange sort; only the first analyse_max positions matter
+    auto& cv = ctv[t];
+    for (size_t i = 0; i + 1 < cv.size() && (int)i < analyse_max; ++i)
+      for (size_t j = i + 1; j < cv.size(); ++j)
+        if (cv[i].score < cv[j].score) std::swap(cv[i], cv[j]);
+    S.ms[FCCF_T_VERIFY] += ms_since(tc);
+    c->dbg_put("fine" + std::to_string(t), fdump);
+    c->dbg_put("qv" + std::to_string(t), qdump);
+  }
+
+  // ---------------- device: K7 fine verify of the top analyse_max per type
+  t0 = clk::now();
+  std::vector<m44> evals;
+  std::vector<std::pair<int, int>> who;
+  for (int t = 0; t < 3; ++t)
+    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
+      evals.push_back(ctv[t][i].T);
+      who.push_back({t, i});
+    }
+  const int E = (int)evals.size();
+  if (E > MAX_EVAL) throw Error(FCCF_E_INTERNAL, "too many fine-verify evaluations");
+  std::vector<float> scores(E, 0.f);
+  if (E > 0) {
+    const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
+    const size_t nk = (size_t)E * (n1 + n2);
+    const size_t nb2 = (n2 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1, nb1 = (n1 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1;
+    const size_t need = 12 * (size_t)E * n2 + 24 * (nb1 + E * nb2) + sizeof(OctState) * (E + 1) +
+                        (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
+                        sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256;
+    c->arena3.ensure(need);
+    c->arena3.reset();
+    FineBufs fb;
+    fb.s2t = c->arena3.take_n<float>(3 * (size_t)E * n2);
+    fb.aggr1 = c->arena3.take_n<float>(6 * nb1);
+    fb.aggr2 = c->arena3.take_n<float>(6 * (size_t)E * nb2);
+    fb.state = c->arena3.take_n<OctState>(E + 1);
+    fb.k0 = c->arena3.take_n<uint64_t>(nk);
+    fb.k1 = c->arena3.take_n<uint64_t>(nk);
+    fb.v0 = c->arena3.take_n<uint32_t>(nk);
+    fb.v1 = c->arena3.take_n<uint32_t>(nk);
+    fb.starts = c->arena3.take_n<uint32_t>(nk + 1);
+    fb.st_counts = c->arena3.take_n<uint32_t>(2 * nk);
+    fb.scal = c->arena3.take_n<uint32_t>(16);
+    fb.scores = c->arena3.take_n<float>(E);
+    fb.T = c->arena3.take_n<m44>(E);
+    fb.ss = sort_scratch_carve(c->arena3.take(sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1))),
+                               (uint32_t)std::max<size_t>(nk, 1));
+    HIP_CHECK(hipMemcpyAsync(fb.T, evals.data(), sizeof(m44) * E, hipMemcpyHostToDevice, st0));
+    fine_verify_batch(w[0].resid, n1, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(scores.data(), fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st0));
+    HIP_CHECK(hipStreamSynchronize(st0));
+  }
+  S.ms[FCCF_T_FINE] = ms_since(t0);
+
+  // ---------------- host: score sums (over all types) and fusion (:1539-1606)
+  t0 = clk::now();
+  float score1_sum = 0.f, score2_sum = 0.f;
+  {
+    int e = 0;
+    for (int t = 0; t < 3; ++t) {
+      std::vector<float> fv;
+      for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i, ++e) {
+        ctv[t][i].score2 = scores[e];
+        score2_sum += ctv[t][i].score2;
+        score1_sum += ctv[t][i].score;
+        for (int a = 0; a < 4; ++a)
+          for (int b = 0; b < 4; ++b) fv.push_back(ctv[t][i].T.m[a][b]);
+        fv.push_back(ctv[t][i].score);
+        fv.push_back(ctv[t][i].score2);
+      }
+      c->dbg_put("fv" + std::to_string(t), fv);
+    }
+  }
+  std::vector<High> tmp;
+  float best_best = 0.f;
+  for (int t = 0; t < 3; ++t) {
+    float bs = 0.f;
+    m44 bt = eye44();
+    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
+      const float s = ctv[t][i].score / score1_sum + ctv[t][i].score2 / score2_sum;
+      if (s > bs) { bs = s; bt = ctv[t][i].T; }
+    }
+    if (best_best < bs) best_best = bs;
+    tmp.push_back({qt_from_T(bt), bs});
+  }
+  std::vector<High> hs;
+  float score_sum = 0.f;
+  for (const High& h : tmp)
+    if (h.score > best_best * 0.8) {
+      hs.push_back(h);
+      score_sum += h.score;
+    }
+  const m44 T = fuse_answer(hs, score_sum);
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) T_out[4 * i + j] = T.m[i][j];
+  S.ms[FCCF_T_FUSE] = ms_since(t0);
+  S.ms_total = ms_since(t_all);
+  counts.push_back(S.lm_solves);
+  counts.push_back(0);
+  if (c->debug) {
+    std::vector<float> hv;
+    for (const High& h : tmp) {
+      const float a[8] = {h.qt.qw, h.qt.qx, h.qt.qy, h.qt.qz, h.qt.tx, h.qt.ty, h.qt.tz, h.score};
+      hv.insert(hv.end(), a, a + 8);
+    }
+    c->dbg_put("high", hv);
+    c->dbg_put("T", T_out, 16);
+    c->dbg_put("counts", counts);
+  }
+  if (stats) *stats = S;
+}
+
+}  // namespace fccf
+
+using namespace fccf;
+
+template <class F>
+static int guarded2(fccf_ctx* c, F&& f) {
+  try {
+    HIP_CHECK(hipSetDevice(c->device));
+    f();
+    return FCCF_OK;
+  } catch (const Error& e) {
+    c->last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    return FCCF_E_OOM;
+  } catch (...) {
+    return FCCF_E_INTERNAL;
+  }
+}
+
+static int check_args(fccf_ctx* c, const float* s, int64_t ns, const float* t, int64_t nt, float leaf, float* T) {
+  if (!c || !T || (!s && ns) || (!t && nt) || ns < 0 || nt < 0 || ns > 0x7FFFFFFF || nt > 0x7FFFFFFF ||
+      !(leaf > 0.f) || !std::isfinite(leaf))
+    return FCCF_E_ARG;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_register(fccf_ctx* c, const float* src, int64_t ns, const float* tar, int64_t nt, float leaf,
+                             const fccf_params* params, float T[16], fccf_stats* stats) {
+  if (int rc = check_args(c, src, ns, tar, nt, leaf, T)) return rc;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded2(c, [&] { run_register(c, src, ns, tar, nt, false, leaf, P, T, stats); });
+}
+
+extern "C" int fccf_register_device(fccf_ctx* c, const float* d_src, int64_t ns, const float* d_tar, int64_t nt,
+                                    float leaf, const fccf_params* params, float T[16], fccf_stats* stats) {
+  if (int rc = check_args(c, d_src, ns, d_tar, nt, leaf, T)) return rc;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded2(c, [&] { run_register(c, d_src, ns, d_tar, nt, true, leaf, P, T, stats); });
+}
