@@ -129,3 +129,21 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
     *m = hm;
   });
 }
+
+extern "C" int fccf_device_upload(fccf_ctx* c, const float* xyz, int64_t n, float** d) {
+  if (!c || !d || (!xyz && n) || n < 0) return FCCF_E_ARG;
+  *d = nullptr;
+  return guarded(c, [&] {
+    float* p = nullptr;
+    if (hipMalloc((void**)&p, 12 * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
+    if (n) HIP_CHECK(hipMemcpy(p, xyz, 12 * (size_t)n, hipMemcpyHostToDevice));
+    *d = p;
+  });
+}
+
+extern "C" int fccf_device_free(fccf_ctx* c, float* d) {
+  if (!c) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    if (d) HIP_CHECK(hipFree(d));
+  });
+}

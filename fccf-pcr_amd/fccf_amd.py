@@ -72,6 +72,8 @@ _sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctyp
      ctypes.POINTER(Stats))
 _sig("fccf_register_device", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
      ctypes.POINTER(Stats))
+_sig("fccf_device_upload", ctypes.c_int, _P, _P, _I64, ctypes.POINTER(_P))
+_sig("fccf_device_free", ctypes.c_int, _P, _P)
 _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
@@ -152,6 +154,16 @@ class Ctx:
                                        ctypes.byref(st))
         _check(rc, "fccf_register_device")
         return T.reshape(4, 4), st
+
+    def upload(self, xyz) -> int:
+        """Copy xyz into a new HBM buffer of this ctx's device; returns the device pointer."""
+        a = _f32(xyz)
+        d = _P()
+        _check(_lib.fccf_device_upload(self._h, a.ctypes.data, a.shape[0], ctypes.byref(d)), "fccf_device_upload")
+        return int(d.value or 0)
+
+    def free(self, dptr: int):
+        _check(_lib.fccf_device_free(self._h, _P(dptr)), "fccf_device_free")
 
     def downsample(self, xyz, leaf: float):
         a = _f32(xyz)

@@ -106,6 +106,11 @@ int fccf_register_device(fccf_ctx* ctx, const float* d_src_xyz, int64_t n_src,
                          const float* d_tar_xyz, int64_t n_tar, float leaf,
                          const fccf_params* params, float T_rowmajor[16], fccf_stats* stats);
 
+/* Device-resident inputs for fccf_register_device (bench / batch users): copy n
+ * xyz points to a new HBM buffer on ctx's device; release with fccf_device_free. */
+int fccf_device_upload(fccf_ctx* ctx, const float* xyz, int64_t n, float** d_xyz);
+int fccf_device_free(fccf_ctx* ctx, float* d_xyz);
+
 /* Stage export: PCL VoxelGrid<PointXYZ> (FCCF.cpp:1668-1678) on the GPU.
  * out_xyz capacity 3*n floats; *m receives the output count.  Output order is
  * ascending leaf index; points of one leaf are summed in ascending input order. */

@@ -67,13 +67,14 @@ def test_register_bit_exact(ctx, oracle, fccf, cfg):
 
 
 def test_register_device_resident_matches_host_path(ctx, fccf):
-    import torch
     src, tar, _ = fccf.synth_pair(60_000)
     T1, _ = ctx.register(src, tar, 0.1)
-    ds = torch.from_numpy(src).cuda()
-    dt = torch.from_numpy(tar).cuda()
-    torch.cuda.synchronize()
-    T2, _ = ctx.register_device(ds.data_ptr(), src.shape[0], dt.data_ptr(), tar.shape[0], 0.1)
+    ds, dt = ctx.upload(src), ctx.upload(tar)
+    try:
+        T2, _ = ctx.register_device(ds, src.shape[0], dt, tar.shape[0], 0.1)
+    finally:
+        ctx.free(ds)
+        ctx.free(dt)
     np.testing.assert_array_equal(T1.view(np.uint32), T2.view(np.uint32))
 
 
