@@ -59,6 +59,8 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   if (hipSetDevice(device) != hipSuccess) { delete c; return FCCF_E_HIP; }
   for (auto& s : c->st)
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { delete c; return FCCF_E_HIP; }
+  for (auto& e : c->ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { delete c; return FCCF_E_HIP; }
   *out = c;
   return FCCF_OK;
 }
@@ -68,6 +70,8 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& s : c->st)
     if (s) (void)hipStreamDestroy(s);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return FCCF_OK;
 }
@@ -128,6 +132,41 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
     HIP_CHECK(hipStreamSynchronize(st));
     *m = hm;
   });
+}
+
+namespace {
+// Shared body of the sum stage exports: S-float elements, K components.
+int stage_sum(fccf_ctx* c, const float* x, int64_t n, int S, bool divide, float* out) {
+  if (!c || (!x && n) || !out || n < 0 || n > (int64_t)0x7FFFFFFF) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    hipStream_t st = c->st[0];
+    const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
+    c->arena.ensure(4 * (size_t)S * cap + exact_sum_bytes(S, cap) + (1 << 16));
+    c->arena.reset();
+    float* d_in = c->arena.take_n<float>((size_t)S * cap);
+    uint32_t* d_sc = c->arena.take_n<uint32_t>(64);
+    float* d_out = c->arena.take_n<float>(4);
+    XsBufs xs = exact_sum_carve(c->arena.take(exact_sum_bytes(S, cap)), S, cap);
+    uint32_t hn = (uint32_t)n;
+    if (n) HIP_CHECK(hipMemcpyAsync(d_in, x, 4 * (size_t)S * n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
+    exact_sum(d_in, S, S, nullptr, d_sc, 1, d_out, divide, xs, st);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(out, d_out, 4 * (size_t)S, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+}  // namespace
+
+extern "C" int fccf_stage_centroid(fccf_ctx* c, const float* xyz, int64_t n, float out[4]) {
+  if (!out) return FCCF_E_ARG;
+  const int rc = stage_sum(c, xyz, n, 3, true, out);
+  if (rc == FCCF_OK) out[3] = 1.f;
+  return rc;
+}
+
+extern "C" int fccf_stage_seqsum(fccf_ctx* c, const float* x, int64_t n, float* out) {
+  return stage_sum(c, x, n, 1, false, out);
 }
 
 extern "C" int fccf_device_upload(fccf_ctx* c, const float* xyz, int64_t n, float** d) {

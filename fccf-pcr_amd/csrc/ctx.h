@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/fccf.h"
+#include "pool.h"
 
 namespace fccf {
 
@@ -73,11 +74,13 @@ struct PinnedBuf {
 
 struct fccf_ctx {
   int device = 0;
-  hipStream_t st[2] = {nullptr, nullptr};
+  hipStream_t st[4] = {nullptr, nullptr, nullptr, nullptr};  // [0,1] per-cloud main, [2,3] side
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   fccf::Arena arena;   // per-cloud buffers
   fccf::Arena arena2;  // matching
   fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
+  fccf::Pool pool;
   bool debug = false;
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "exactsum.h"
+
 namespace fccf {
 
 constexpr int RS_THREADS = 256;               // 4 waves
@@ -36,10 +38,23 @@ void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, cons
 // Run-length segmentation of sorted keys[0..*d_n): starts[s] = first index of
 // segment s, starts[S] = *d_n, *d_nseg = S.  Keys equal to `invalid` (which sort
 // last) are excluded: the valid prefix ends at the first invalid key.
+// seg_of (optional): segment index of every valid element.
 void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid,
-                       uint32_t* starts, uint32_t* d_nseg, SortScratch s, hipStream_t st);
+                       uint32_t* starts, uint32_t* d_nseg, SortScratch s, hipStream_t st,
+                       uint32_t* seg_of = nullptr);
 void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts,
-                       uint32_t* d_nseg, SortScratch s, hipStream_t st);
+                       uint32_t* d_nseg, SortScratch s, hipStream_t st, uint32_t* seg_of = nullptr);
+
+// Sequential float sums in the reference's left-to-right order, s = ((0 + v0) + v1) + ...
+// bit-exact, computed in parallel (exactsum.h).  Problem b sums elements
+// [off[b], off[b] + cnt[b]) of `data` (off may be null = 0); an element is S
+// consecutive floats (S = 1 or 3) and its first K components are summed
+// independently into out[b*K + k] (divided by the count if `divide`).
+// Scratch: exact_sum_carve(rows = nprob*K, cap = max elements per problem).
+size_t exact_sum_bytes(int rows, uint32_t cap);
+XsBufs exact_sum_carve(void* base, int rows, uint32_t cap);
+void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint32_t* cnt, int nprob, float* out,
+               bool divide, XsBufs x, hipStream_t st);
 
 // Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap,

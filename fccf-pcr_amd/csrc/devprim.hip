@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(T) k_scan_blocks(uint32_t* __restrict__ blk, u
 template <class K, bool HasInvalid>
 __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
                                                  K invalid, const uint32_t* __restrict__ blk,
-                                                 uint32_t* __restrict__ starts) {
+                                                 uint32_t* __restrict__ starts, uint32_t* __restrict__ seg_of) {
   __shared__ uint32_t sh[4];
   const uint32_t n = *d_n;
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
@@ -229,6 +229,7 @@ __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, con
     // end of the valid prefix: close the last segment
     if (i < n) {
       const bool valid = !HasInvalid || keys[i] != invalid;
+      if (seg_of && valid) seg_of[i] = pos - 1;
       const bool next_valid = (i + 1 < n) && (!HasInvalid || keys[i + 1] != invalid);
       if (valid && !next_valid) starts[pos] = i + 1;  // pos == segment count here
     }
@@ -237,12 +238,12 @@ __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, con
 
 template <class K, bool HasInvalid>
 void segment_heads(const K* keys, const uint32_t* d_n, uint32_t cap, K invalid, uint32_t* starts, uint32_t* d_nseg,
-                   SortScratch s, hipStream_t st) {
+                   SortScratch s, hipStream_t st, uint32_t* seg_of) {
   const uint32_t nb = rs_blocks(cap);
   if (nb == 0) return;
   k_seg_count<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk);
   k_scan_blocks<<<1, T, 0, st>>>(s.blk, nb, d_nseg);
-  k_seg_write<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk, starts);
+  k_seg_write<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk, starts, seg_of);
 }
 
 __global__ void __launch_bounds__(T) k_sum_tiles(const uint32_t* __restrict__ in, const uint32_t* __restrict__ d_n,
@@ -301,12 +302,12 @@ void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, cons
   radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, max_bits, iota, s, st);
 }
 void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid, uint32_t* starts,
-                       uint32_t* d_nseg, SortScratch s, hipStream_t st) {
-  segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st);
+                       uint32_t* d_nseg, SortScratch s, hipStream_t st, uint32_t* seg_of) {
+  segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st, seg_of);
 }
 void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts, uint32_t* d_nseg,
-                       SortScratch s, hipStream_t st) {
-  segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st);
+                       SortScratch s, hipStream_t st, uint32_t* seg_of) {
+  segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st, seg_of);
 }
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap, uint32_t* d_total,
                         SortScratch s, hipStream_t st) {

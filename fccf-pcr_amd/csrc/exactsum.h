@@ -1,0 +1,155 @@
+// exactsum.h — exact emulation of a left-to-right float32 sum, in parallel.
+//
+// The reference computes several sums as s = ((0 + x0) + x1) + ... in float
+// (pcl::compute3DCentroid, FCCF.cpp:473; fine_verify's similar_num, :830-835).  The
+// bits of s depend on every intermediate rounding, so the GPU must reproduce the
+// sequence exactly.  Within one binade the sequence is translation-equivariant:
+// if s is a multiple of the quantum u = 2^(E-23) and the exact partial r = s + x
+// lies in binade E (2^E <= |r| < 2^(E+1)), then
+//      fl(s + x) = s + q*u,  q = RNE(x/u) with ties broken towards even s/u + q.
+// A run of inputs is therefore summarised, for a hypothesis (E, parity p of s/u),
+// by Q = sum of q and the integer envelope [lo, hi] of Q_k + floor(x_k/u) (units
+// of u); "every partial of this run stays in binade E" is then a pure integer
+// test on the actual start M = s/u.  Summaries of consecutive runs compose
+// (xs_compose is associative), so a wave reduces a 256-input chunk, and 64 chunk
+// summaries reduce to a group summary, in O(log) depth.  Hypotheses cover the 3
+// binades around a double-precision prefix prediction.  A short serial chain then
+// applies one group (16384 inputs) per step, descends to chunks where a group does
+// not validate (binade crossings, zero/subnormal starts, non-finite inputs), and
+// replays a chunk with plain float adds where no chunk hypothesis validates.
+// Result bits are identical to the naive loop (tests/test_exactsum.py fuzzes it).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "fccf_math.h"
+
+namespace fccf {
+
+constexpr int XS_L = 256;   // inputs per chunk (one wave x 4)
+constexpr int XS_G = 64;    // chunks per group
+constexpr int XS_NE = 3;    // binade hypotheses per table: Ebase, Ebase+1, Ebase+2
+constexpr int64_t XS_INF = (int64_t)1 << 62;   // empty-envelope sentinel
+constexpr double XS_YMAX = 33554432.0;          // 2^25: a step this large always leaves binade E
+constexpr int XS_NOE = -100000;                 // "no prediction" Ebase
+
+struct XsSum {          // summary of a run under one binade E, for start parity 0 / 1
+  int64_t Q[2], lo[2], hi[2];
+  int32_t ok, pad;
+};
+
+FH XsSum xs_identity() {
+  XsSum s;
+  for (int p = 0; p < 2; ++p) { s.Q[p] = 0; s.lo[p] = XS_INF; s.hi[p] = -XS_INF; }
+  s.ok = 1;
+  s.pad = 0;
+  return s;
+}
+
+FH XsSum xs_bad() {
+  XsSum s = xs_identity();
+  s.ok = 0;
+  return s;
+}
+
+// one input x under binade E (inv_u = 2^(23-E)); x/u is exact in double
+FH XsSum xs_elem(float x, double inv_u) {
+  if (!isfinite(x)) return xs_bad();
+  const double y = (double)x * inv_u;
+  if (!(fabs(y) < XS_YMAX)) return xs_bad();
+  const double fl = floor(y);
+  const int64_t f = (int64_t)fl;
+  const double fr = y - fl;  // exact
+  XsSum s;
+  for (int p = 0; p < 2; ++p) {
+    int64_t q;
+    if (fr < 0.5) q = f;
+    else if (fr > 0.5) q = f + 1;
+    else q = (((int64_t)p + f) & 1) ? f + 1 : f;  // tie: the new s/u is even
+    s.Q[p] = q;
+    s.lo[p] = f;
+    s.hi[p] = f;
+  }
+  s.ok = 1;
+  s.pad = 0;
+  return s;
+}
+
+// run a then run b
+FH XsSum xs_compose(const XsSum& a, const XsSum& b) {
+  XsSum r;
+  r.ok = a.ok & b.ok;
+  r.pad = 0;
+  if (!r.ok) return xs_bad();
+  for (int p = 0; p < 2; ++p) {
+    const int64_t qa = a.Q[p];
+    const int pb = (int)((p + qa) & 1);
+    r.Q[p] = qa + b.Q[pb];
+    const int64_t bl = b.lo[pb] == XS_INF ? XS_INF : qa + b.lo[pb];
+    const int64_t bh = b.hi[pb] == -XS_INF ? -XS_INF : qa + b.hi[pb];
+    r.lo[p] = a.lo[p] < bl ? a.lo[p] : bl;
+    r.hi[p] = a.hi[p] > bh ? a.hi[p] : bh;
+  }
+  return r;
+}
+
+// binade exponent and signed integer mantissa M (s = M * 2^(E-23)) of a normal float
+FH bool xs_decompose(float s, int* E, int64_t* M) {
+  uint32_t b;
+  __builtin_memcpy(&b, &s, 4);
+  const int ex = (int)((b >> 23) & 0xFF);
+  if (ex == 0 || ex == 0xFF) return false;  // zero/subnormal/inf/nan: no binade hypothesis
+  *E = ex - 127;
+  const int64_t m = (int64_t)((b & 0x7FFFFFu) | 0x800000u);
+  *M = (b >> 31) ? -m : m;
+  return true;
+}
+
+// Does summary h (parity p = M & 1) apply at start M: every partial r_k/u in
+// [M + lo, M + hi + 1) stays inside binade E on M's side of zero?
+FH bool xs_valid(const XsSum& h, int64_t M) {
+  if (!h.ok) return false;
+  const int p = (int)(M & 1);
+  if (h.lo[p] == XS_INF) return true;  // empty run
+  const int64_t lo = M + h.lo[p], hi = M + h.hi[p];
+  if (M > 0) return lo >= ((int64_t)1 << 23) && hi + 1 <= ((int64_t)1 << 24);
+  return hi + 1 <= -((int64_t)1 << 23) && lo >= -((int64_t)1 << 24) + 1;
+}
+
+// end of the run: (M + Q) u, exact (it is the float the last rounding produced)
+FH float xs_apply(const XsSum& h, int64_t M, int E) {
+  return (float)ldexp((double)(M + h.Q[M & 1]), E - 23);
+}
+
+// Ebase (= predicted binade - 1) of a run starting at prefix value pre;
+// XS_NOE when the prefix is too close to zero to be useful.
+FH int xs_predict(double pre) {
+  const double a = fabs(pre);
+  if (!(a >= 1.1754943508222875e-38) || !(a < 3.0e38)) return XS_NOE;
+  int e;
+  frexp(a, &e);  // a = f * 2^e, f in [0.5, 1)
+  return e - 2;
+}
+
+// Device scratch of exact_sum (devprim.h): per row (problem x component) NC chunk
+// tables and NG group tables.
+struct XsBufs {
+  double* pre;     // rows x (NC + 1): chunk sums, then exclusive prefix
+  XsSum* ctab;     // rows x NC x XS_NE
+  int32_t* cE;     // rows x NC: Ebase per chunk
+  XsSum* gtab;     // rows x NG x XS_NE
+  int32_t* gE;     // rows x NG
+  uint32_t NC, NG;
+  int rows;
+};
+
+// Summary of the run x[0..n) under binade E (host / reference walk).
+FH XsSum xs_run(const float* x, int64_t stride, int n, int E) {
+  const double inv_u = ldexp(1.0, 23 - E);
+  XsSum s = xs_identity();
+  for (int k = 0; k < n; ++k) s = xs_compose(s, xs_elem(x[k * stride], inv_u));
+  return s;
+}
+
+}  // namespace fccf

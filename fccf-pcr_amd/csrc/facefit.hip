@@ -19,28 +19,6 @@ namespace {
 
 constexpr uint32_t INV_U32 = 0xFFFFFFFFu;
 
-// ---------------------------------------------------------------- centroid
-// One lane per component; the sum order is the reference's (index order), so this
-// is a dependent chain by construction.  Loads are batched to stay off the chain.
-__global__ void __launch_bounds__(64) k_seqsum3(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                                float* __restrict__ out4) {
-  const uint32_t c = blockIdx.x;
-  if (threadIdx.x != 0) return;
-  const uint32_t n = *d_n;
-  float s = 0.f;
-  uint32_t i = 0;
-  for (; i + 16 <= n; i += 16) {
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = xyz[3 * (i + j) + c];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) s += v[j];
-  }
-  for (; i < n; ++i) s += xyz[3 * i + c];
-  out4[c] = n ? s / (float)n : 0.f;
-  if (c == 0) out4[3] = 1.f;
-}
-
 // ---------------------------------------------------------------- octree bounds
 // Batched over blockIdx.y = sequence e.
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
@@ -209,34 +187,75 @@ __device__ void eig_min(const float A[3][3], float& ev, f3& v) {
   v = {w.x / d, w.y / d, w.z / d};
 }
 
-__global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
-                                                   const uint32_t* __restrict__ starts, const uint32_t* __restrict__ d_nleaf,
-                                                   const float* __restrict__ cc, float vpt, float cthr,
+// Points in leaf order (Morton, then index): the per-leaf loops below then read
+// contiguous memory instead of gathering through the sort permutation.
+__global__ void __launch_bounds__(256) k_gather(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
+                                                const uint32_t* __restrict__ d_n, float* __restrict__ sp) {
+  const uint32_t n = *d_n;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+    const uint32_t j = vals[k];
+    sp[3 * k] = xyz[3 * j]; sp[3 * k + 1] = xyz[3 * j + 1]; sp[3 * k + 2] = xyz[3 * j + 2];
+  }
+}
+
+// One wave per leaf (Morton order).  Lane k < 9 owns accumulator k of
+// computeMeanAndCovarianceMatrix (:495): [xx, xy, xz, yy, yz, zz, x, y, z], each a
+// sequential float sum over the leaf's points in index order.  Points are staged in
+// LDS as (x, y, z, 1) so every lane computes term = p[i1] * p[i2] (the linear sums
+// use i2 = w = 1, and x * 1 == x exactly).  compute3DCentroid (:490) is the same
+// sequential x/y/z sum divided by n, i.e. accumulators 6..8 / n bit-for-bit.
+__global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ sp, const uint32_t* __restrict__ starts,
+                                                   const uint32_t* __restrict__ d_nleaf, float vpt, float cthr,
                                                    VoxRec* __restrict__ recs, uint32_t* __restrict__ planar,
                                                    uint32_t* __restrict__ resid) {
+  __shared__ __attribute__((aligned(16))) float pts[4][64 * 4];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t nl = *d_nleaf;
-  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
+  const int i1t[16] = {0, 0, 0, 1, 1, 2, 0, 1, 2, 0, 0, 0, 0, 0, 0, 0};
+  const int i2t[16] = {0, 1, 2, 1, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3};
+  const int i1 = i1t[lane & 15], i2 = i2t[lane & 15];
+  float* P = pts[wave];
+  for (uint32_t s = blockIdx.x * 4 + wave; s < nl; s += gridDim.x * 4) {
     const uint32_t b = starts[s], e = starts[s + 1];
     const uint32_t cnt = e - b;
+    float acc = 0.f;
+    const bool fit = (float)cnt > vpt;
+    if (fit) {
+      for (uint32_t base = 0; base < cnt; base += 64) {
+        const uint32_t k = base + lane;
+        if (k < cnt) {
+          const float* q = sp + 3 * (size_t)(b + k);
+          *(float4*)(P + 4 * lane) = make_float4(q[0], q[1], q[2], 1.0f);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t m = min(64u, cnt - base);
+        uint32_t j = 0;
+        for (; j + 8 <= m; j += 8) {
+          float a[8], c[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { a[q] = P[4 * (j + q) + i1]; c[q] = P[4 * (j + q) + i2]; }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc += a[q] * c[q];
+        }
+        for (; j < m; ++j) acc += P[4 * j + i1] * P[4 * j + i2];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+    float ac[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) ac[q] = __shfl(acc, q, 64);
+    if (lane != 0) continue;
     VoxRec r;
     r.count = (int32_t)cnt;
     r.curvature = 0.f;
     r.c[0] = r.c[1] = r.c[2] = 0.f;
     r.n[0] = r.n[1] = r.n[2] = 0.f;
     uint32_t flag = 0;
-    if ((float)cnt > vpt) {
+    if (fit) {
       const float fc = (float)cnt;
-      float cx = 0.f, cy = 0.f, cz = 0.f;
-      float ac[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (uint32_t k = b; k < e; ++k) {
-        const uint32_t j = vals[k];
-        const float x = xyz[3 * j], y = xyz[3 * j + 1], z = xyz[3 * j + 2];
-        cx += x; cy += y; cz += z;
-        ac[0] += x * x; ac[1] += x * y; ac[2] += x * z;
-        ac[3] += y * y; ac[4] += y * z; ac[5] += z * z;
-        ac[6] += x; ac[7] += y; ac[8] += z;
-      }
-      cx /= fc; cy /= fc; cz /= fc;
+      const float cx = ac[6] / fc, cy = ac[7] / fc, cz = ac[8] / fc;
       for (int i = 0; i < 9; ++i) ac[i] /= fc;
       float cov[3][3];
       cov[0][0] = ac[0] - ac[6] * ac[6];
@@ -253,15 +272,8 @@ __global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ xyz
       const float curv = (es != 0.f) ? fabsf(ev / es) : 0.f;
       r.curvature = curv;
       r.c[0] = cx; r.c[1] = cy; r.c[2] = cz;
-      if (curv < cthr) {
-        const f3 to = {cx - cc[0], cy - cc[1], cz - cc[2]};
-        if (dot3(to, nv) < 0.f) { r.n[0] = nv.x; r.n[1] = nv.y; r.n[2] = nv.z; }
-        else { r.n[0] = -nv.x; r.n[1] = -nv.y; r.n[2] = -nv.z; }
-        flag = 1;
-      } else {
-        r.n[0] = nv.x; r.n[1] = nv.y; r.n[2] = nv.z;
-        flag = 2;
-      }
+      r.n[0] = nv.x; r.n[1] = nv.y; r.n[2] = nv.z;  // oriented later (needs the cloud centroid)
+      flag = curv < cthr ? 1u : 2u;
     }
     recs[s] = r;
     planar[s] = flag == 1 ? 1u : 0u;
@@ -269,24 +281,35 @@ __global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ xyz
   }
 }
 
-__global__ void __launch_bounds__(256) k_compact(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
-                                                 const uint32_t* __restrict__ starts, const uint32_t* __restrict__ d_nleaf,
-                                                 const VoxRec* __restrict__ recs, const uint32_t* __restrict__ planar,
-                                                 const uint32_t* __restrict__ poff, const uint32_t* __restrict__ resid,
-                                                 const uint32_t* __restrict__ roff, VoxRec* __restrict__ pout,
-                                                 float* __restrict__ rout) {
+// cloud_sub (:527-530): every point of a non-planar leaf, leaf order then index order.
+__global__ void __launch_bounds__(256) k_compact_resid(const float* __restrict__ sp, const uint32_t* __restrict__ d_n,
+                                                       const uint32_t* __restrict__ seg_of,
+                                                       const uint32_t* __restrict__ starts,
+                                                       const uint32_t* __restrict__ resid,
+                                                       const uint32_t* __restrict__ roff, float* __restrict__ rout) {
+  const uint32_t n = *d_n;
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+    const uint32_t s = seg_of[k];
+    if (!resid[s]) continue;
+    const uint32_t o = roff[s] + (k - starts[s]);
+    rout[3 * o] = sp[3 * k]; rout[3 * o + 1] = sp[3 * k + 1]; rout[3 * o + 2] = sp[3 * k + 2];
+  }
+}
+
+// Planar leaves with the normal oriented towards the cloud centroid (:504-516).
+__global__ void __launch_bounds__(256) k_compact_planar(const uint32_t* __restrict__ d_nleaf,
+                                                        const VoxRec* __restrict__ recs,
+                                                        const uint32_t* __restrict__ planar,
+                                                        const uint32_t* __restrict__ poff, const float* __restrict__ cc,
+                                                        VoxRec* __restrict__ pout) {
   const uint32_t nl = *d_nleaf;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
-    if (planar[s]) pout[poff[s]] = recs[s];
-    if (resid[s]) {
-      const uint32_t b = starts[s], o = roff[s];
-      for (uint32_t k = 0; k < resid[s]; ++k) {
-        const uint32_t j = vals[b + k];
-        rout[3 * (o + k)] = xyz[3 * j];
-        rout[3 * (o + k) + 1] = xyz[3 * j + 1];
-        rout[3 * (o + k) + 2] = xyz[3 * j + 2];
-      }
-    }
+    if (!planar[s]) continue;
+    VoxRec r = recs[s];
+    const f3 to = {r.c[0] - cc[0], r.c[1] - cc[1], r.c[2] - cc[2]};
+    const f3 nv = {r.n[0], r.n[1], r.n[2]};
+    if (!(dot3(to, nv) < 0.f)) { r.n[0] = -nv.x; r.n[1] = -nv.y; r.n[2] = -nv.z; }
+    pout[poff[s]] = r;
   }
 }
 
@@ -305,8 +328,8 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, hipStream_t st) {
-  k_seqsum3<<<3, 64, 0, st>>>(xyz, d_n, out4);
+void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs xs, hipStream_t st) {
+  exact_sum(xyz, 3, 3, nullptr, d_n, 1, out4, true, xs, st);  // compute3DCentroid (:473)
 }
 
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
@@ -328,17 +351,21 @@ void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, do
   octree_sim(xyz, d_n, cap, res, b.aggr, b.oct, st);
   k_oct_codes<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.oct, res, b.c0, b.nbits);
   radix_sort_u64(b.c0, b.v0, b.c1, b.v1, d_n, cap, b.nbits, 64, true, b.ss, st);
-  segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st);
+  segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st, b.seg_of);
+  k_gather<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, d_n, b.sp);
 }
 
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, VoxRec* planar_out,
-                     float* resid_out, FaceBufs b, hipStream_t st) {
-  k_voxel_fit<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, b.starts, b.nleaf, b.centroid, vpt, cthr, b.recs,
-                                             b.flag_planar, b.resid_cnt);
+                     float* resid_out, FaceBufs b, hipStream_t st, hipEvent_t centroid_ready) {
+  (void)xyz;
+  k_voxel_fit<<<grid_for(cap, 4, 4096), 256, 0, st>>>(b.sp, b.starts, b.nleaf, vpt, cthr, b.recs, b.flag_planar,
+                                                      b.resid_cnt);
   exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
   exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
-  k_compact<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, b.starts, b.nleaf, b.recs, b.flag_planar, b.planar_off,
-                                           b.resid_cnt, b.resid_off, planar_out, resid_out);
+  k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);
+  if (centroid_ready) (void)hipStreamWaitEvent(st, centroid_ready, 0);
+  k_compact_planar<<<grid_for(cap), 256, 0, st>>>(b.nleaf, b.recs, b.flag_planar, b.planar_off, b.centroid,
+                                                  planar_out);
 }
 
 }  // namespace fccf

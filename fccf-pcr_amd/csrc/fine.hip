@@ -30,6 +30,7 @@ __global__ void k_fv_init(OctState* st, int E, uint32_t* scal, uint32_t n1, uint
   if (threadIdx.x == 0) {
     scal[4] = n1;
     scal[5] = n2;
+    scal[7] = 0u;
     OctState z;
     for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
     z.depth = 0;
@@ -89,41 +90,49 @@ __global__ void __launch_bounds__(256) k_fv_leafkeys(const uint64_t* __restrict_
   }
 }
 
-__global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ starts,
-                                                   const uint32_t* __restrict__ d_nseg, uint32_t* __restrict__ cnt) {
-  const uint32_t ns = *d_nseg;
+// Per leaf: source/target counts (exact) and the similar_num term (:830-835):
+// (s+t)*(min/max) when both are >= 1, else +0.0f (adding +0 leaves the float
+// sum unchanged).  Also the per-evaluation segment ranges.
+__global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vk,
+                                                   const uint32_t* __restrict__ starts,
+                                                   const uint32_t* __restrict__ scal, float* __restrict__ term,
+                                                   uint32_t* __restrict__ range) {
+  const uint32_t ns = scal[2], sh = scal[3] - 1u;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
     const uint32_t b = starts[s], e = starts[s + 1];
     uint32_t src = 0;
     for (uint32_t k = b; k < e; ++k) src += (keys[k] & 1ull) ? 0u : 1u;
-    cnt[2 * s] = src;
-    cnt[2 * s + 1] = (e - b) - src;
+    const float sn = (float)src, tn = (float)((e - b) - src);
+    float t = 0.f;
+    if (sn >= 1.f && tn >= 1.f) {
+      const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
+      t = (sn + tn) * (mn / mx);
+    }
+    term[s] = t;
+    const uint32_t ev = (uint32_t)(vk[b] >> sh);
+    if (s == 0 || (uint32_t)(vk[starts[s - 1]] >> sh) != ev) range[2 * ev] = s;
+    if (s + 1 == ns || (uint32_t)(vk[starts[s + 1]] >> sh) != ev) range[2 * ev + 1] = s + 1;
   }
 }
 
-// One lane per evaluation: the reference's sequential float sums in leaf order.
-__global__ void __launch_bounds__(64) k_fv_score(const uint64_t* __restrict__ vk, const uint32_t* __restrict__ starts,
-                                                 const uint32_t* __restrict__ d_nseg, const uint32_t* __restrict__ cnt,
-                                                 const uint32_t* __restrict__ scal, float* __restrict__ scores) {
-  const int e = blockIdx.x;
-  if (threadIdx.x != 0) return;
-  const uint32_t ns = *d_nseg, sh = scal[3] - 1u;  // e of a leaf key = vk >> (shift - 1)
-  uint32_t lo = 0, hi = ns;                        // first segment with e' >= e
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) / 2;
-    if ((vk[starts[mid]] >> sh) < (uint64_t)e) lo = mid + 1;
-    else hi = mid;
-  }
-  float similar = 0.f, all = 0.f;
-  for (uint32_t s = lo; s < ns && (vk[starts[s]] >> sh) == (uint64_t)e; ++s) {
-    const float sn = (float)cnt[2 * s], tn = (float)cnt[2 * s + 1];
-    all = all + sn + tn;
-    if (sn >= 1.f && tn >= 1.f) {
-      const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
-      similar = similar + (sn + tn) * (mn / mx);
-    }
-  }
-  scores[e] = similar / all;
+// count of leaves per evaluation (exact_sum input) and allinvec: the float sum of
+// integer counts is exact below 2^24, so it equals the integer point count.
+__global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __restrict__ range,
+                            uint32_t* __restrict__ nseg_e, float* __restrict__ all, uint32_t* __restrict__ scal, int E) {
+  const int e = threadIdx.x;
+  if (e >= E) return;
+  const uint32_t f = range[2 * e], l = range[2 * e + 1];
+  nseg_e[e] = l - f;
+  nseg_e[MAX_EVAL + e] = f;  // first leaf of evaluation e (exact_sum offsets)
+  const uint32_t pts = l > f ? starts[l] - starts[f] : 0u;
+  if (pts >= (1u << 24)) atomicOr(&scal[7], 1u);  // float allinvec would round: unsupported size
+  all[e] = (float)pts;
+}
+
+__global__ void k_fv_score(const float* __restrict__ similar, const float* __restrict__ all, float* __restrict__ scores,
+                           int E) {
+  const int e = threadIdx.x;
+  if (e < E) scores[e] = similar[e] / all[e];
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -154,8 +163,11 @@ void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n
   radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 64, true, b.ss, st);
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
-  k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.starts, b.scal + 2, b.st_counts);
-  k_fv_score<<<E, 64, 0, st>>>(b.k1, b.starts, b.scal + 2, b.st_counts, b.scal, b.scores);
+  (void)hipMemsetAsync(b.range, 0, sizeof(uint32_t) * 2 * MAX_EVAL, st);
+  k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.k1, b.starts, b.scal, b.term, b.range);
+  k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
+  exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
+  k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E);
 }
 
 }  // namespace fccf

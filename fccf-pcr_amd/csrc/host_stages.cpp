@@ -7,6 +7,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <stdexcept>
 #include <unordered_map>
 
 namespace fccf {
@@ -41,6 +42,8 @@ inline void set_avg(Group& g) {  // the recompute's averages (:580-586)
 }  // namespace
 
 GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
+  // compare_normal(...) == !(theta > thr) == !angle_gt(cos, cut): no acos in the O(V^2) loops
+  const AngleCut cut1 = make_cut(P.normal_vector_threshold1), cut2 = make_cut(P.normal_vector_threshold2);
   std::vector<char> va(nv, 0);
   std::vector<Group> G;
   // stage 1 (:536-593): recompute-from-scratch == running sums in member order (App. B Q7)
@@ -55,7 +58,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
     for (int j = 0; j < nv; ++j) {
       if (va[j]) continue;
       const VoxRec& v = vox[j];
-      const bool same = !(angle_deg(g.an[0], g.an[1], g.an[2], v.n[0], v.n[1], v.n[2]) > P.normal_vector_threshold1);
+      const bool same = !angle_gt(normal_cos(g.an[0], g.an[1], g.an[2], v.n[0], v.n[1], v.n[2]), cut1);
       const bool cop = compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]},
                                      f3{v.n[0], v.n[1], v.n[2]}, f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1,
                                      P.parameter_k1);
@@ -78,7 +81,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
         if (j == i || G[j].alloc) continue;
         Group& a = G[i];
         Group& b = G[j];
-        const bool same = !(angle_deg(a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2]) > P.normal_vector_threshold2);
+        const bool same = !angle_gt(normal_cos(a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2]), cut2);
         const bool cop = compare_plane(f3{a.an[0], a.an[1], a.an[2]}, f3{a.ac[0], a.ac[1], a.ac[2]},
                                        f3{b.an[0], b.an[1], b.an[2]}, f3{b.ac[0], b.ac[1], b.ac[2]}, P.parameter_l2,
                                        P.parameter_k2);
@@ -197,6 +200,7 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
   };
   std::unordered_map<int64_t, std::vector<int>, KH> grid;
   for (int i = 0; i < n; ++i) grid[key(in[i])].push_back(i);
+  const AngleCut ccut = make_cut(P.cluster_angel_threshold);
   std::vector<f3> xaxis(n);
   for (int i = 0; i < n; ++i) xaxis[i] = quat_rotate(quatf{in[i].qw, in[i].qx, in[i].qy, in[i].qz}, f3{1.f, 0.f, 0.f});
   std::vector<std::vector<int>> clusters;
@@ -228,7 +232,7 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
     std::vector<int> cl;
     for (auto& e : nb) {
       const f3 a = xaxis[i], b = xaxis[e.second];
-      if (angle_deg(a.x, a.y, a.z, b.x, b.y, b.z) < P.cluster_angel_threshold) {
+      if (angle_lt(normal_cos(a.x, a.y, a.z, b.x, b.y, b.z), ccut)) {
         in[e.second].alloc = 1u;
         cl.push_back(e.second);
       }
@@ -387,9 +391,12 @@ bool lm_eval(const float* pf, int P, const double x[7], double* cost, double* r,
 }
 
 // DENSE_QR: min || [A; diag(D)] y - [b; 0] || by Householder QR (HouseholderQR form).
+constexpr int LM_MAXM = 2 * 17;  // <= one pair per source plane
 bool qr_solve(const double* A, int m, const double D[6], const double* b, double y[6]) {
   const int n = 6, M = m + n;
-  std::vector<double> Q((size_t)M * n, 0.0), rhs(M, 0.0);
+  double Q[(LM_MAXM + 6) * 6], rhs[LM_MAXM + 6];
+  for (int i = 0; i < M * n; ++i) Q[i] = 0.0;
+  for (int i = 0; i < M; ++i) rhs[i] = 0.0;
   for (int i = 0; i < m; ++i)
     for (int j = 0; j < n; ++j) Q[(size_t)i * n + j] = A[(size_t)i * n + j];
   for (int j = 0; j < n; ++j) Q[(size_t)(m + j) * n + j] = D[j];
@@ -438,9 +445,10 @@ void lm_solve(const float* pf, int P, double best[7]) {
   const int m = 2 * P;
   double x[7] = {0, 0, 0, 1, 0, 0, 0};
   for (int i = 0; i < 7; ++i) best[i] = x[i];
-  std::vector<double> r(m), J((size_t)m * 6), rc(m);
+  if (m > LM_MAXM) throw std::length_error("lm_solve: too many plane pairs");
+  double r[LM_MAXM], J[LM_MAXM * 6], rc[LM_MAXM];
   double cost;
-  if (!lm_eval(pf, P, x, &cost, r.data(), J.data())) return;
+  if (!lm_eval(pf, P, x, &cost, r, J)) return;
   double scale[6], gmax = 0.0;
   for (int j = 0; j < 6; ++j) {
     double s = 0.0;
@@ -485,7 +493,7 @@ void lm_solve(const float* pf, int P, double best[7]) {
       }
     double D[6], y[6], step[6];
     for (int j = 0; j < 6; ++j) D[j] = std::sqrt(diag[j] / radius);
-    const bool solved = qr_solve(J.data(), m, D, r.data(), y);
+    const bool solved = qr_solve(J, m, D, r, y);
     reuse = true;
     bool valid = false;
     double mcc = 0.0;
@@ -510,7 +518,7 @@ void lm_solve(const float* pf, int P, double best[7]) {
       for (int j = 0; j < 6; ++j) delta[j] = step[j] * scale[j];
       plus7(x, delta, cand);
       double ccost;
-      if (!lm_eval(pf, P, cand, &ccost, rc.data(), nullptr)) ccost = DBL_MAX;
+      if (!lm_eval(pf, P, cand, &ccost, rc, nullptr)) ccost = DBL_MAX;
       double sn = 0.0;
       for (int i = 0; i < 7; ++i) sn += (x[i] - cand[i]) * (x[i] - cand[i]);
       sn = std::sqrt(sn);
@@ -520,7 +528,7 @@ void lm_solve(const float* pf, int P, double best[7]) {
       if (rho > 1e-3) {
         for (int i = 0; i < 7; ++i) x[i] = cand[i];
         x_norm = norm7(x);
-        if (!lm_eval(pf, P, x, &cost, r.data(), J.data())) return;
+        if (!lm_eval(pf, P, x, &cost, r, J)) return;
         finish();
         successful = true;
         radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3));
@@ -547,6 +555,7 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
   int fs1 = 0, fs2 = 0;
   for (const Plane& f : F1) fs1 = (int)((float)fs1 + f.fps);
   for (const Plane& f : F2) fs2 = (int)((float)fs2 + f.fps);
+  const AngleCut qcut = make_cut(P.quick_verify_angel_threshold);
   std::vector<f3> c2(F2.size()), n2(F2.size());
   for (size_t k = 0; k < F2.size(); ++k) {
     c2[k] = tf_se3(T, F2[k].c[0], F2[k].c[1], F2[k].c[2]);
@@ -560,11 +569,11 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
     int best = 0;
     float best_imp = 0, best_score = 0;
     for (size_t j = 0; j < F2.size(); ++j) {
-      const float ang = angle_deg(a.n[0], a.n[1], a.n[2], n2[j].x, n2[j].y, n2[j].z);
+      const bool ang_ok = angle_lt(normal_cos(a.n[0], a.n[1], a.n[2], n2[j].x, n2[j].y, n2[j].z), qcut);
       const float d1 = (float)dot3d(a.n[0], a.n[1], a.n[2], a.c[0], a.c[1], a.c[2]);
       const float d2 = (float)dot3d(n2[j].x, n2[j].y, n2[j].z, c2[j].x, c2[j].y, c2[j].z);
       const float dist = std::fabs(d1 - d2);
-      if (ang < P.quick_verify_angel_threshold && dist < P.quick_verify_distance_threshold) {
+      if (ang_ok && dist < P.quick_verify_distance_threshold) {
         find = true;
         const float s1 = a.fps, s2 = F2[j].fps;
         const float mn = s1 < s2 ? s1 : s2, mx = s1 > s2 ? s1 : s2;

@@ -11,6 +11,9 @@
 
 namespace fccf {
 
+// Exact cut points of theta(c) for a threshold (see pipeline.cpp make_cut).
+AngleCut make_cut(float thr);
+
 struct Plane {        // facenode of a selected plane (FCCF.cpp:47-58)
   float c[3], n[3];   // average_centry_*, average_normal_* (never renormalised, App. B Q3)
   float fps;          // face_point_size

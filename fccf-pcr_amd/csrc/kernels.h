@@ -52,11 +52,14 @@ struct FaceBufs {
   float* aggr;             // per 1024-point block: min xyz, max xyz (6 floats)
   OctState* oct;
   float* centroid;         // 4 floats
+  XsBufs xs;               // centroid sum scratch (3 rows)
   VoxRec* recs;            // cap (all leaves)
   uint32_t* flag_planar;   // cap
   uint32_t* resid_cnt;     // cap
   uint32_t* planar_off;    // cap
   uint32_t* resid_off;     // cap
+  float* sp;               // points in leaf order, 3 * cap
+  uint32_t* seg_of;        // leaf index of every sorted point, cap
   uint32_t* nleaf;         // scalars
   uint32_t* nbits;
   uint32_t* nplanar;
@@ -65,13 +68,15 @@ struct FaceBufs {
 };
 
 // Launch the sequential cloud-centroid reduction (PCL compute3DCentroid order).
-void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, hipStream_t st);
+void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs xs, hipStream_t st);
 // Octree leaves + per-leaf plane fit + compaction.  `centroid` must be ready
 // before the fit kernel runs (the caller orders the streams).
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
                          hipStream_t st);
+// centroid_ready (may be null): event after which b.centroid holds the cloud centroid.
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float voxel_point_threshold,
-                     float curvature_threshold, VoxRec* planar_out, float* resid_out, FaceBufs b, hipStream_t st);
+                     float curvature_threshold, VoxRec* planar_out, float* resid_out, FaceBufs b, hipStream_t st,
+                     hipEvent_t centroid_ready);
 
 // Octree bound simulation over xyz[0..*d_n) starting from *state (one workgroup per
 // sequence; `batch` sequences at xyz + e*xyz_stride with state[e]).

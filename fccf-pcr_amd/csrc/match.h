@@ -39,11 +39,16 @@ struct FineBufs {
   uint64_t *k0, *k1;   // E * (n1 + n2)
   uint32_t *v0, *v1;
   uint32_t* starts;    // E * (n1 + n2) + 1
-  uint32_t* st_counts; // per segment: source, target counts (2 u32)
-  uint32_t* scal;      // [0]=n total keys, [1]=nbits, [2]=nseg, [3]=shift, [4]=n1, [5]=n2, [6]=E
+  float* term;         // per leaf similar_num term
+  uint32_t* range;     // per evaluation: first leaf, end leaf (2 * MAX_EVAL)
+  uint32_t* nseg_e;    // 2 * MAX_EVAL: leaf counts, then first leaves
+  float* similar;      // MAX_EVAL
+  float* all;          // MAX_EVAL
+  uint32_t* scal;      // [0]=n keys, [1]=nbits, [2]=nseg, [3]=shift, [4]=n1, [5]=n2, [6]=E, [7]=error
   float* scores;       // E
   m44* T;              // E
   SortScratch ss;
+  XsBufs xs;           // similar_num sum scratch (E rows, cap n1 + n2)
 };
 void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
                        hipStream_t st);

@@ -69,7 +69,7 @@ float okey_inv(uint32_t k) {
   std::memcpy(&f, &u, 4);
   return f;
 }
-AngleCut make_cut(float thr) {
+AngleCut make_cut_impl(float thr) {
   auto first_true = [](uint32_t lo, uint32_t hi, auto pred) {  // pred monotone false..true on [lo,hi]
     while (lo < hi) {
       const uint32_t mid = lo + (hi - lo) / 2;
@@ -97,6 +97,19 @@ AngleCut make_cut(float thr) {
   return c;
 }
 
+}  // namespace
+
+AngleCut make_cut(float thr) {  // memoised per thread: thresholds are few and fixed per call
+  static thread_local std::vector<std::pair<float, AngleCut>> memo;
+  for (const auto& m : memo)
+    if (m.first == thr) return m.second;
+  const AngleCut c = make_cut_impl(thr);
+  memo.push_back({thr, c});
+  return c;
+}
+
+namespace {
+
 // ------------------------------------------------------------ per-cloud device state
 struct CloudWS {
   uint32_t cap = 0;
@@ -120,8 +133,10 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
   b += 6 * 4 * ((N + AGGR_BLOCK - 1) / AGGR_BLOCK + 1) + 256;  // aggregates, state, centroid
   b += sizeof(VoxRec) * N + 4 * 4 * N + 64;                    // leaf records, flags, offsets
+  b += 12 * N + 4 * N;                                         // sorted points, leaf of point
   b += sizeof(VoxRec) * N + 12 * N;                            // planar out, residual out
   b += sort_scratch_bytes(cap) + 64 * 256;                     // sort scratch + alignment slack
+  b += exact_sum_bytes(3, cap) + 256;                          // centroid sum tables
   return b;
 }
 
@@ -144,11 +159,14 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   f.aggr = a.take_n<float>(6 * ((size_t)(cap + AGGR_BLOCK - 1) / AGGR_BLOCK + 1));
   f.oct = a.take_n<OctState>(1);
   f.centroid = a.take_n<float>(4);
+  f.xs = exact_sum_carve(a.take(exact_sum_bytes(3, cap)), 3, cap);
   f.recs = a.take_n<VoxRec>(cap);
   f.flag_planar = a.take_n<uint32_t>(cap);
   f.resid_cnt = a.take_n<uint32_t>(cap);
   f.planar_off = a.take_n<uint32_t>(cap);
   f.resid_off = a.take_n<uint32_t>(cap);
+  f.sp = a.take_n<float>(3 * (size_t)cap);
+  f.seg_of = a.take_n<uint32_t>(cap);
   uint32_t* s = a.take_n<uint32_t>(16);
   f.nleaf = s;
   f.nbits = s + 1;
@@ -159,17 +177,23 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.resid = a.take_n<float>(3 * (size_t)cap);
 }
 
-// Device part of one cloud: both VoxelGrid passes, remove-NaN, face voxels.
-void enqueue_cloud(CloudWS& w, float leaf, const fccf_params& P, hipStream_t st) {
+// Device part of one cloud: both VoxelGrid passes, remove-NaN, face voxels.  The
+// sequential cloud-centroid sum runs on a side stream beside the octree/sort/fit
+// work and only gates the final normal orientation.
+void enqueue_cloud(CloudWS& w, float leaf, const fccf_params& P, hipStream_t st, hipStream_t side, hipEvent_t ev_ds,
+                   hipEvent_t ev_cent) {
   voxel_grid(w.in, w.sc, w.cap, leaf, w.ds1, w.sc + 1, w.vg, st);  // main :1668-1678
   k_finite_flags<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag);  // driver :1374-1375
   exclusive_scan_u32(w.fflag, w.foff, w.sc + 1, w.cap, w.sc + 2, w.vg.ss, st);
   k_finite_scatter<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag, w.foff, w.ds1f);
   voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st);  // driver :1377-1387
-  cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, st);
+  HIP_CHECK(hipEventRecord(ev_ds, st));
+  HIP_CHECK(hipStreamWaitEvent(side, ev_ds, 0));
+  cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, w.fb.xs, side);
+  HIP_CHECK(hipEventRecord(ev_cent, side));
   face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
   face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.planar, w.resid, w.fb,
-                  st);
+                  st, ev_cent);
 }
 
 template <class T>
@@ -223,7 +247,7 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     uint32_t* hn = (uint32_t*)c->pinned.get(64) + k;
     *hn = n;
     HIP_CHECK(hipMemcpyAsync(w[k].sc, hn, 4, hipMemcpyHostToDevice, st));
-    enqueue_cloud(w[k], leaf, P, st);
+    enqueue_cloud(w[k], leaf, P, st, c->st[2 + k], c->ev[2 * k], c->ev[2 * k + 1]);
     HIP_CHECK(hipGetLastError());
   }
   // counts of both clouds
@@ -259,6 +283,7 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
       HIP_CHECK(hipStreamSynchronize(c->st[k]));
       c->dbg_put(dsn[k], a);
       c->dbg_put("ds" + s, b);
+      ce[3] = 1.f;  // Eigen::Vector4f centroid[3] (unused by the algorithm)
       c->dbg_put("centroid" + s, ce);
       std::vector<double> o = {oc[0].min[0], oc[0].min[1], oc[0].min[2], (double)oc[0].depth};
       c->dbg_put("oct" + s, o);
@@ -411,20 +436,24 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     S.ms[FCCF_T_CLUSTER] += ms_since(tc);
     tc = clk::now();
     std::vector<float> fdump, qdump;
-    for (const QT& q : fine) {
+    std::vector<TS> res(fine.size());
+    std::vector<int> npairs(fine.size());
+    c->pool.parallel_for((int)fine.size(), [&](int i) {  // independent per candidate
+      res[i].T = T_from_qt(fine[i]);
+      res[i].score = quick_verify(res[i].T, g[0].planes, g[1].planes, P, &npairs[i]);
+      res[i].score2 = 0.f;
+    });
+    for (size_t i = 0; i < fine.size(); ++i) {
+      const QT& q = fine[i];
       const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
       fdump.insert(fdump.end(), a, a + 8);
-      TS ts;
-      ts.T = T_from_qt(q);
-      int np = 0;
-      ts.score = quick_verify(ts.T, g[0].planes, g[1].planes, P, &np);
-      ts.score2 = 0.f;
-      if ((float)np >= P.required_optimize_plane) ++S.lm_solves;
+      const TS& ts = res[i];
+      if ((float)npairs[i] >= P.required_optimize_plane) ++S.lm_solves;
       ctv[t].push_back(ts);
-      for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) qdump.push_back(ts.T.m[i][j]);
+      for (int a2 = 0; a2 < 4; ++a2)
+        for (int b2 = 0; b2 < 4; ++b2) qdump.push_back(ts.T.m[a2][b2]);
       qdump.push_back(ts.score);
-      qdump.push_back((float)np);
+      qdump.push_back((float)npairs[i]);
     }
     // score_range (:1233-1251): exchange sort; only the first analyse_max positions matter
     auto& cv = ctv[t];
@@ -454,7 +483,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     const size_t nb2 = (n2 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1, nb1 = (n1 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1;
     const size_t need = 12 * (size_t)E * n2 + 24 * (nb1 + E * nb2) + sizeof(OctState) * (E + 1) +
                         (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
-                        sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256;
+                        sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256 +
+                        exact_sum_bytes(E, n1 + n2) + 256;
     c->arena3.ensure(need);
     c->arena3.reset();
     FineBufs fb;
@@ -467,17 +497,25 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     fb.v0 = c->arena3.take_n<uint32_t>(nk);
     fb.v1 = c->arena3.take_n<uint32_t>(nk);
     fb.starts = c->arena3.take_n<uint32_t>(nk + 1);
-    fb.st_counts = c->arena3.take_n<uint32_t>(2 * nk);
+    fb.term = c->arena3.take_n<float>(nk + 1);
+    fb.range = c->arena3.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.nseg_e = c->arena3.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.similar = c->arena3.take_n<float>(MAX_EVAL);
+    fb.all = c->arena3.take_n<float>(MAX_EVAL);
     fb.scal = c->arena3.take_n<uint32_t>(16);
     fb.scores = c->arena3.take_n<float>(E);
     fb.T = c->arena3.take_n<m44>(E);
     fb.ss = sort_scratch_carve(c->arena3.take(sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1))),
                                (uint32_t)std::max<size_t>(nk, 1));
+    fb.xs = exact_sum_carve(c->arena3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
     HIP_CHECK(hipMemcpyAsync(fb.T, evals.data(), sizeof(m44) * E, hipMemcpyHostToDevice, st0));
     fine_verify_batch(w[0].resid, n1, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
     HIP_CHECK(hipGetLastError());
+    uint32_t ferr = 0;
     HIP_CHECK(hipMemcpyAsync(scores.data(), fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st0));
+    HIP_CHECK(hipMemcpyAsync(&ferr, fb.scal + 7, 4, hipMemcpyDeviceToHost, st0));
     HIP_CHECK(hipStreamSynchronize(st0));
+    if (ferr) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
   }
   S.ms[FCCF_T_FINE] = ms_since(t0);
 

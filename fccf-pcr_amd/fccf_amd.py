@@ -75,6 +75,8 @@ _sig("fccf_register_device", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_floa
 _sig("fccf_device_upload", ctypes.c_int, _P, _P, _I64, ctypes.POINTER(_P))
 _sig("fccf_device_free", ctypes.c_int, _P, _P)
 _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
+_sig("fccf_stage_centroid", ctypes.c_int, _P, _P, _I64, _P)
+_sig("fccf_stage_seqsum", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
@@ -172,6 +174,20 @@ class Ctx:
         _check(_lib.fccf_stage_downsample(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data,
                                           ctypes.byref(m)), "fccf_stage_downsample")
         return out[: m.value].copy()
+
+    def centroid(self, xyz):
+        """compute3DCentroid (FCCF.cpp:473) of a dense cloud: float32[4] (x, y, z, 1)."""
+        a = _f32(xyz)
+        out = np.zeros(4, np.float32)
+        _check(_lib.fccf_stage_centroid(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_centroid")
+        return out
+
+    def seqsum(self, x) -> np.float32:
+        """Left-to-right float32 sum ((0 + x0) + x1) + ... (similar_num order, FCCF.cpp:830-835)."""
+        a = np.ascontiguousarray(np.asarray(x, np.float32).reshape(-1))
+        out = np.zeros(1, np.float32)
+        _check(_lib.fccf_stage_seqsum(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_seqsum")
+        return out[0]
 
     def debug(self, name: str, dtype=np.float32):
         n = _I64()

@@ -117,6 +117,15 @@ int fccf_device_free(fccf_ctx* ctx, float* d_xyz);
 int fccf_stage_downsample(fccf_ctx* ctx, const float* xyz, int64_t n, float leaf, float* out_xyz,
                           int64_t* m);
 
+/* Stage export: pcl::compute3DCentroid of a dense cloud (FCCF.cpp:473 via
+ * face_extrate): out = (sum x / n, sum y / n, sum z / n, 1) with each sum a
+ * left-to-right float accumulation, bit-identical to the sequential loop (computed
+ * in parallel on the GPU, exactsum.h).  n == 0 gives (0, 0, 0, 1). */
+int fccf_stage_centroid(fccf_ctx* ctx, const float* xyz, int64_t n, float out[4]);
+/* Stage export: s = ((0 + x0) + x1) + ... + x(n-1) in float, the accumulation
+ * order of fine_verify's similar_num (FCCF.cpp:830-835); bit-exact. */
+int fccf_stage_seqsum(fccf_ctx* ctx, const float* x, int64_t n, float* out);
+
 /* Named intermediate of the last fccf_register call with debug on (see DESIGN.md
  * "Debug names").  Copies min(cap_bytes, size) bytes; *n_bytes = full size. */
 int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes,
