@@ -139,6 +139,7 @@ def main():
             "e2e_ms_median": statistics.median(per) * 1e3,
             "K_per_registration": int(st.K),
             "K_pass": int(st.K_pass),
+            "graph_captures_last_step": int(st.graph_captures),
             "stage_ms": {k: round(v, 4) for k, v in st.as_dict()["ms"].items()},
             "rot_err_deg_vs_gt": rot_err,
             "trans_err_m_vs_gt": float(np.linalg.norm(T[:3, 3] - T_gt[:3, 3])),

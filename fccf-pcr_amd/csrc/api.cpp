@@ -68,6 +68,9 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
 extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   if (!c) return FCCF_E_ARG;
   (void)hipSetDevice(c->device);
+  for (auto& gk : c->g_seg)
+    for (auto& g : gk) g.reset();
+  c->g_fine.reset();
   for (auto& s : c->st)
     if (s) (void)hipStreamDestroy(s);
   for (auto& e : c->ev)

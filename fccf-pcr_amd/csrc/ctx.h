@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -70,12 +71,64 @@ struct PinnedBuf {
   }
 };
 
+// One captured hipGraph, re-captured whenever its key (the workspace layout and
+// every launch argument that is not read from device memory) changes.  The
+// pipeline's sizes live in device memory, so a graph replays for any input that
+// fits the captured capacities.  FCCF_GRAPHS=0 launches eagerly instead.
+struct CachedGraph {
+  std::vector<uint8_t> key;
+  hipGraphExec_t exec = nullptr;
+  int captures = 0;  // since the owner last cleared it
+  void reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = nullptr;
+    key.clear();
+  }
+  ~CachedGraph() { reset(); }
+  template <class F>
+  void run(const void* k, size_t kn, hipStream_t st, F body) {
+    static const bool enabled = [] {
+      const char* e = std::getenv("FCCF_GRAPHS");
+      return !(e && e[0] == '0');
+    }();
+    if (!enabled) {
+      body();
+      return;
+    }
+    const uint8_t* kb = (const uint8_t*)k;
+    if (!exec || key.size() != kn || std::memcmp(key.data(), kb, kn) != 0) {
+      reset();
+      hipGraph_t g = nullptr;
+      HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      try {
+        body();
+      } catch (...) {
+        (void)hipStreamEndCapture(st, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      HIP_CHECK(hipStreamEndCapture(st, &g));
+      const hipError_t e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (e != hipSuccess) {
+        exec = nullptr;
+        throw Error(FCCF_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+      }
+      key.assign(kb, kb + kn);
+      ++captures;
+    }
+    HIP_CHECK(hipGraphLaunch(exec, st));
+  }
+};
+
 }  // namespace fccf
 
 struct fccf_ctx {
   int device = 0;
   hipStream_t st[4] = {nullptr, nullptr, nullptr, nullptr};  // [0,1] per-cloud main, [2,3] side
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[8] = {};  // [0..3] per-cloud side-stream joins, [4..7] graph fork/join
+  fccf::CachedGraph g_seg[2][3];  // per cloud: downsample, centroid, faces (pipeline.cpp)
+  fccf::CachedGraph g_fine;    // fine-verify batch (K7)
   fccf::Arena arena;   // per-cloud buffers
   fccf::Arena arena2;  // matching
   fccf::Arena arena3;  // fine verify

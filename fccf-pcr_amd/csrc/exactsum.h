@@ -30,12 +30,16 @@ namespace fccf {
 constexpr int XS_L = 256;   // inputs per chunk (one wave x 4)
 constexpr int XS_G = 64;    // chunks per group
 constexpr int XS_NE = 3;    // binade hypotheses per table: Ebase, Ebase+1, Ebase+2
-constexpr int64_t XS_INF = (int64_t)1 << 62;   // empty-envelope sentinel
+constexpr int32_t XS_INF = 1 << 30;             // empty-envelope sentinel
+constexpr int32_t XS_LIM = 1 << 26;             // |Q|, |lo|, |hi| of any applicable summary stay below
 constexpr double XS_YMAX = 33554432.0;          // 2^25: a step this large always leaves binade E
 constexpr int XS_NOE = -100000;                 // "no prediction" Ebase
 
-struct XsSum {          // summary of a run under one binade E, for start parity 0 / 1
-  int64_t Q[2], lo[2], hi[2];
+// Summary of a run under one binade E, for start parity 0 / 1.  A summary can only
+// validate at a start |M| < 2^24 if every envelope bound and Q is below 2^26 in
+// magnitude, so anything larger is recorded as "bad" and int32 suffices.
+struct XsSum {
+  int32_t Q[2], lo[2], hi[2];
   int32_t ok, pad;
 };
 
@@ -59,14 +63,14 @@ FH XsSum xs_elem(float x, double inv_u) {
   const double y = (double)x * inv_u;
   if (!(fabs(y) < XS_YMAX)) return xs_bad();
   const double fl = floor(y);
-  const int64_t f = (int64_t)fl;
+  const int32_t f = (int32_t)fl;
   const double fr = y - fl;  // exact
   XsSum s;
   for (int p = 0; p < 2; ++p) {
-    int64_t q;
+    int32_t q;
     if (fr < 0.5) q = f;
     else if (fr > 0.5) q = f + 1;
-    else q = (((int64_t)p + f) & 1) ? f + 1 : f;  // tie: the new s/u is even
+    else q = ((p + f) & 1) ? f + 1 : f;  // tie: the new s/u is even
     s.Q[p] = q;
     s.lo[p] = f;
     s.hi[p] = f;
@@ -76,22 +80,63 @@ FH XsSum xs_elem(float x, double inv_u) {
   return s;
 }
 
+// a[p & 1] as a mask blend (a `p ? a[1] : a[0]` select is folded back into an
+// indexed load, which sends the whole struct to scratch memory)
+FH int32_t xs_sel(const int32_t a[2], int64_t p) {
+  const int32_t a0 = a[0], a1 = a[1], m = -(int32_t)(p & 1);
+  return a0 ^ ((a0 ^ a1) & m);
+}
+
 // run a then run b
 FH XsSum xs_compose(const XsSum& a, const XsSum& b) {
   XsSum r;
-  r.ok = a.ok & b.ok;
   r.pad = 0;
-  if (!r.ok) return xs_bad();
+  int ok = a.ok & b.ok;
   for (int p = 0; p < 2; ++p) {
-    const int64_t qa = a.Q[p];
-    const int pb = (int)((p + qa) & 1);
-    r.Q[p] = qa + b.Q[pb];
-    const int64_t bl = b.lo[pb] == XS_INF ? XS_INF : qa + b.lo[pb];
-    const int64_t bh = b.hi[pb] == -XS_INF ? -XS_INF : qa + b.hi[pb];
-    r.lo[p] = a.lo[p] < bl ? a.lo[p] : bl;
-    r.hi[p] = a.hi[p] > bh ? a.hi[p] : bh;
+    const int32_t qa = a.Q[p];
+    const int32_t pb = p + qa;
+    const int32_t q = qa + xs_sel(b.Q, pb);
+    const int32_t blo = xs_sel(b.lo, pb), bhi = xs_sel(b.hi, pb);
+    const int32_t bl = blo == XS_INF ? XS_INF : qa + blo;
+    const int32_t bh = bhi == -XS_INF ? -XS_INF : qa + bhi;
+    const int32_t lo = a.lo[p] < bl ? a.lo[p] : bl;
+    const int32_t hi = a.hi[p] > bh ? a.hi[p] : bh;
+    // inputs are within +-2^26 (or sentinels), so nothing above overflows int32
+    ok &= (q > -XS_LIM && q < XS_LIM) & (lo == XS_INF || lo > -XS_LIM) & (hi == -XS_INF || hi < XS_LIM);
+    r.Q[p] = q;
+    r.lo[p] = lo;
+    r.hi[p] = hi;
   }
+  if (!ok) return xs_bad();
+  r.ok = 1;
   return r;
+}
+
+// c ? b : a field by field, as mask blends (keeps tables in registers)
+FH XsSum xs_blend(const XsSum& a, const XsSum& b, bool c) {
+  const int32_t m = -(int32_t)c;
+  XsSum r;
+  for (int p = 0; p < 2; ++p) {
+    r.Q[p] = a.Q[p] ^ ((a.Q[p] ^ b.Q[p]) & m);
+    r.lo[p] = a.lo[p] ^ ((a.lo[p] ^ b.lo[p]) & m);
+    r.hi[p] = a.hi[p] ^ ((a.hi[p] ^ b.hi[p]) & m);
+  }
+  r.ok = a.ok ^ ((a.ok ^ b.ok) & m);
+  r.pad = 0;
+  return r;
+}
+
+// Tables of one unit (chunk or group): summaries under Eb, Eb+1, Eb+2.
+struct XsTab3 {
+  XsSum t0, t1, t2;
+  int32_t Eb;
+};
+
+// the summary of unit T under binade E (bad if E is not covered)
+FH XsSum xs_pick(const XsTab3& T, int E) {
+  const int h = E - T.Eb;
+  if (T.Eb == XS_NOE || h < 0 || h > 2) return xs_bad();
+  return xs_blend(xs_blend(T.t0, T.t1, h == 1), T.t2, h == 2);
 }
 
 // binade exponent and signed integer mantissa M (s = M * 2^(E-23)) of a normal float
@@ -110,16 +155,16 @@ FH bool xs_decompose(float s, int* E, int64_t* M) {
 // [M + lo, M + hi + 1) stays inside binade E on M's side of zero?
 FH bool xs_valid(const XsSum& h, int64_t M) {
   if (!h.ok) return false;
-  const int p = (int)(M & 1);
-  if (h.lo[p] == XS_INF) return true;  // empty run
-  const int64_t lo = M + h.lo[p], hi = M + h.hi[p];
+  const int32_t hl = xs_sel(h.lo, M), hh = xs_sel(h.hi, M);
+  if (hl == XS_INF) return true;  // empty run
+  const int64_t lo = M + hl, hi = M + hh;
   if (M > 0) return lo >= ((int64_t)1 << 23) && hi + 1 <= ((int64_t)1 << 24);
   return hi + 1 <= -((int64_t)1 << 23) && lo >= -((int64_t)1 << 24) + 1;
 }
 
 // end of the run: (M + Q) u, exact (it is the float the last rounding produced)
 FH float xs_apply(const XsSum& h, int64_t M, int E) {
-  return (float)ldexp((double)(M + h.Q[M & 1]), E - 23);
+  return (float)ldexp((double)(M + xs_sel(h.Q, M)), E - 23);
 }
 
 // Ebase (= predicted binade - 1) of a run starting at prefix value pre;

@@ -5,9 +5,10 @@
 //   k_xs_prefix  one block per row (problem x component): exclusive double prefix
 //   k_xs_chunk   one wave per chunk: 3 binade hypotheses x 2 parities, wave-composed
 //   k_xs_group   one wave per (row, 64-chunk group): compose chunk tables per binade
-//   k_xs_chain   one wave per row: serial apply, group -> chunk -> replay
+//   k_xs_chain   one wave per row: scan-jump over groups, then over the chunks of
+//                a group that crosses a binade, then a plain replay of the chunk
 // The first four are bandwidth-bound streaming passes over the inputs; the chain
-// touches one table per 16384 inputs except around binade crossings.
+// costs one wave scan per binade crossing (plus one 256-add replay).
 #include "devprim.h"
 #include "exactsum.h"
 #include "ctx.h"
@@ -15,27 +16,40 @@
 namespace fccf {
 namespace {
 
-__device__ __forceinline__ XsSum shfl_down_sum(const XsSum& a, int d) {
+// XsSum moved across lanes by one DPP control (row_shr:n / row_bcast:15 / :31);
+// lanes the control does not address keep their own value.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ XsSum dpp_sum(const XsSum& a) {
   XsSum o;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    o.Q[p] = __shfl_down(a.Q[p], d);
-    o.lo[p] = __shfl_down(a.lo[p], d);
-    o.hi[p] = __shfl_down(a.hi[p], d);
+    o.Q[p] = __builtin_amdgcn_update_dpp(a.Q[p], a.Q[p], CTRL, ROWS, 0xf, false);
+    o.lo[p] = __builtin_amdgcn_update_dpp(a.lo[p], a.lo[p], CTRL, ROWS, 0xf, false);
+    o.hi[p] = __builtin_amdgcn_update_dpp(a.hi[p], a.hi[p], CTRL, ROWS, 0xf, false);
   }
-  o.ok = __shfl_down(a.ok, d);
+  o.ok = __builtin_amdgcn_update_dpp(a.ok, a.ok, CTRL, ROWS, 0xf, false);
   o.pad = 0;
   return o;
 }
 
-// ordered reduction over the 64 lanes (lane 0 = first run); result in lane 0
-__device__ __forceinline__ XsSum wave_compose(XsSum a) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const XsSum o = shfl_down_sum(a, d);
-    if ((lane & (2 * d - 1)) == 0) a = xs_compose(a, o);
-  }
+// Inclusive ordered scan over the wave: lane l ends with units 0..l composed
+// (earlier lanes first).  Four row_shr steps scan each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry row totals forward.  No LDS traffic.
+__device__ __forceinline__ XsSum wave_scan(XsSum a) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  XsSum o;
+  o = dpp_sum<0x111, 0xf>(a);
+  if (r >= 1) a = xs_compose(o, a);
+  o = dpp_sum<0x112, 0xf>(a);
+  if (r >= 2) a = xs_compose(o, a);
+  o = dpp_sum<0x114, 0xf>(a);
+  if (r >= 4) a = xs_compose(o, a);
+  o = dpp_sum<0x118, 0xf>(a);
+  if (r >= 8) a = xs_compose(o, a);
+  o = dpp_sum<0x142, 0xa>(a);
+  if (lane & 16) a = xs_compose(o, a);
+  o = dpp_sum<0x143, 0xc>(a);
+  if (lane >= 32) a = xs_compose(o, a);
   return a;
 }
 
@@ -142,8 +156,8 @@ __global__ void __launch_bounds__(256) k_xs_chunk(const float* __restrict__ data
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (ok[j]) a = xs_compose(a, xs_elem(v[j][k], inv_u));
-        a = wave_compose(a);
-        if (lane == 0) ctab[(row * NC + c) * XS_NE + h] = a;
+        a = wave_scan(a);
+        if (lane == 63) ctab[(row * NC + c) * XS_NE + h] = a;
       }
     }
   }
@@ -169,79 +183,136 @@ __global__ void __launch_bounds__(256) k_xs_group(const uint32_t* __restrict__ c
         const int hc = Eg + h - Ec;
         a = (Ec != XS_NOE && hc >= 0 && hc < XS_NE) ? ctab[(row * NC + c) * XS_NE + hc] : xs_bad();
       }
-      a = wave_compose(a);
-      if (lane == 0) gtab[(row * NG + g) * XS_NE + h] = a;
+      a = wave_scan(a);
+      if (lane == 63) gtab[(row * NG + g) * XS_NE + h] = a;
     }
   }
 }
 
-__device__ __forceinline__ bool xs_try(float& s, const XsSum* tab, int Eb) {
-  int E;
-  int64_t M;
-  if (Eb == XS_NOE || !xs_decompose(s, &E, &M)) return false;
-  const int h = E - Eb;
-  if (h < 0 || h >= XS_NE) return false;
-  const XsSum t = tab[h];
-  if (!xs_valid(t, M)) return false;
-  s = xs_apply(t, M, E);
-  return true;
+
+__device__ __forceinline__ XsTab3 load_tab3(const XsSum* tab, const int32_t* eb, size_t u, bool have) {
+  XsTab3 T;
+  if (have) {
+    T.t0 = tab[u * XS_NE];
+    T.t1 = tab[u * XS_NE + 1];
+    T.t2 = tab[u * XS_NE + 2];
+    T.Eb = eb[u];
+  } else {
+    T.t0 = T.t1 = T.t2 = xs_identity();
+    T.Eb = XS_NOE;
+  }
+  return T;
 }
 
-// One wave per row.  s is identical in every lane, so control flow is uniform.
+// Apply units cur..cnt-1 (lane l holds unit l's tables) to s.  One ordered scan
+// composes every prefix under s's binade; validity is monotone in the prefix
+// length (envelopes only widen), so the first invalid lane f is found by a
+// ballot, prefix f-1 is applied in one step and unit f goes to `descend`.
+#ifdef XS_PROBE
+__device__ unsigned long long xs_probe[8];  // scans, replays, decompose misses, replay cycles, scan cycles
+#define XS_COUNT(i, v) (threadIdx.x == 0 ? (void)atomicAdd(&xs_probe[i], (unsigned long long)(v)) : (void)0)
+#else
+#define XS_COUNT(i, v) ((void)0)
+#endif
+
+template <class Descend>
+__device__ __forceinline__ void scan_jump(float& s, const XsTab3& T, int cnt, Descend descend) {
+  const int lane = threadIdx.x & 63;
+  int cur = 0;
+  while (cur < cnt) {
+    int E;
+    int64_t M;
+    if (!xs_decompose(s, &E, &M)) {  // zero / subnormal / non-finite start
+      XS_COUNT(2, 1);
+      descend(cur);
+      ++cur;
+      continue;
+    }
+#ifdef XS_PROBE
+    const long long t0 = wall_clock64();
+#endif
+    const bool mine = lane >= cur && lane < cnt;
+    XsSum a = mine ? xs_pick(T, E) : xs_identity();
+    a = wave_scan(a);
+    const uint64_t bad = __ballot(mine && !xs_valid(a, M));
+    const int f = bad ? (int)__builtin_ctzll(bad) : cnt;
+    if (f > cur) {
+      const int64_t Q = __builtin_amdgcn_readlane(xs_sel(a.Q, M), f - 1);
+      s = (float)ldexp((double)(M + Q), E - 23);
+    }
+    XS_COUNT(0, 1);
+#ifdef XS_PROBE
+    XS_COUNT(4, wall_clock64() - t0);
+#endif
+    if (f >= cnt) break;
+    descend(f);
+    cur = f + 1;
+  }
+}
+
+// One wave per row: groups (scan-jump) -> chunks (scan-jump) -> plain replay.
+// s is identical in every lane, so all control flow is uniform.
 template <int S>
 __global__ void __launch_bounds__(64) k_xs_chain(const float* __restrict__ data, int K, const uint32_t* __restrict__ off,
                                                  const uint32_t* __restrict__ cnt, const XsSum* __restrict__ ctab,
                                                  const int32_t* __restrict__ cE, const XsSum* __restrict__ gtab,
                                                  const int32_t* __restrict__ gE, uint32_t NC, uint32_t NG,
                                                  float* __restrict__ out, int divide) {
-  __shared__ XsSum tg[XS_G * XS_NE], tc[XS_G * XS_NE];
-  __shared__ int32_t eg[XS_G], ec[XS_G];
   const int row = blockIdx.x, lane = threadIdx.x;
   const int b = row / K, k = row % K;
   const Prob P = prob_of(data, S, off, cnt, b);
   const float* x = P.base + k;
   const uint32_t ng = (P.nch + XS_G - 1) / XS_G;
   float s = 0.f;
+  // Replay: the chunk is staged in LDS and summed with broadcast reads into a
+  // VGPR accumulator (a uniform SGPR chain would cost a readlane/readfirstlane
+  // round trip per add); reads of group g+1 overlap the adds of group g.
+  __shared__ __attribute__((aligned(16))) float rb[XS_L + 16];
+  auto replay = [&](uint32_t c) {
+    XS_COUNT(1, 1);
+#ifdef XS_PROBE
+    const long long t0 = wall_clock64();
+#endif
+    const uint32_t m = min((uint32_t)XS_L, P.n - c * XS_L);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = c * XS_L + lane * 4 + j;
+      rb[lane * 4 + j] = i < P.n ? x[(size_t)i * S] : 0.f;
+    }
+    __syncthreads();
+    float acc = s;
+    constexpr int GR = 16;
+    const uint32_t ng16 = m / GR;
+    float cur[GR];
+#pragma unroll
+    for (int q = 0; q < GR; ++q) cur[q] = rb[q];
+    for (uint32_t g = 0; g < ng16; ++g) {
+      float nxt[GR];
+      const float* src = rb + GR * ((g + 1) & 15);  // wraps harmlessly on the last group
+#pragma unroll
+      for (int q = 0; q < GR; ++q) nxt[q] = src[q];
+#pragma unroll
+      for (int q = 0; q < GR; ++q) acc += cur[q];
+#pragma unroll
+      for (int q = 0; q < GR; ++q) cur[q] = nxt[q];
+    }
+    for (uint32_t j = GR * ng16; j < m; ++j) acc += rb[j];
+    s = acc;
+    __syncthreads();
+#ifdef XS_PROBE
+    XS_COUNT(3, wall_clock64() - t0);
+#endif
+  };
+  auto group = [&](uint32_t g) {
+    const uint32_t c0 = g * XS_G;
+    const int nc = (int)min((uint32_t)XS_G, P.nch - c0);
+    const XsTab3 C = load_tab3(ctab, cE, (size_t)row * NC + c0 + lane, lane < nc);
+    scan_jump(s, C, nc, [&](int f) { replay(c0 + (uint32_t)f); });
+  };
   for (uint32_t gb = 0; gb < ng; gb += 64) {
-    __syncthreads();
-    if (gb + lane < ng) {
-      const size_t gi = (size_t)row * NG + gb + lane;
-      for (int h = 0; h < XS_NE; ++h) tg[lane * XS_NE + h] = gtab[gi * XS_NE + h];
-      eg[lane] = gE[gi];
-    }
-    __syncthreads();
-    for (uint32_t gi = 0; gi < 64 && gb + gi < ng; ++gi) {
-      if (xs_try(s, &tg[gi * XS_NE], eg[gi])) continue;
-      const uint32_t g = gb + gi;
-      __syncthreads();
-      {
-        const uint32_t c = g * XS_G + lane;
-        if (c < P.nch) {
-          const size_t ci = (size_t)row * NC + c;
-          for (int h = 0; h < XS_NE; ++h) tc[lane * XS_NE + h] = ctab[ci * XS_NE + h];
-          ec[lane] = cE[ci];
-        }
-      }
-      __syncthreads();
-      for (uint32_t cj = 0; cj < XS_G; ++cj) {
-        const uint32_t c = g * XS_G + cj;
-        if (c >= P.nch) break;
-        if (xs_try(s, &tc[cj * XS_NE], ec[cj])) continue;
-        // replay the chunk with plain float adds in input order
-        const uint32_t m = min((uint32_t)XS_L, P.n - c * XS_L);
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t i = c * XS_L + lane * 4 + j;
-          v[j] = i < P.n ? x[(size_t)i * S] : 0.f;
-        }
-        for (uint32_t l = 0; l * 4 < m; ++l) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (l * 4 + j < m) s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[j]), (int)l));
-        }
-      }
-    }
+    const int na = (int)min(64u, ng - gb);
+    const XsTab3 G = load_tab3(gtab, gE, (size_t)row * NG + gb + lane, lane < na);
+    scan_jump(s, G, na, [&](int f) { group(gb + (uint32_t)f); });
   }
   if (lane == 0) out[row] = divide ? (P.n ? s / (float)P.n : 0.f) : s;
 }

@@ -355,15 +355,17 @@ void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, do
   k_gather<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, d_n, b.sp);
 }
 
-void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, VoxRec* planar_out,
-                     float* resid_out, FaceBufs b, hipStream_t st, hipEvent_t centroid_ready) {
+void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, float* resid_out,
+                     FaceBufs b, hipStream_t st) {
   (void)xyz;
   k_voxel_fit<<<grid_for(cap, 4, 4096), 256, 0, st>>>(b.sp, b.starts, b.nleaf, vpt, cthr, b.recs, b.flag_planar,
                                                       b.resid_cnt);
   exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
   exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
   k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);
-  if (centroid_ready) (void)hipStreamWaitEvent(st, centroid_ready, 0);
+}
+
+void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_t st) {
   k_compact_planar<<<grid_for(cap), 256, 0, st>>>(b.nleaf, b.recs, b.flag_planar, b.planar_off, b.centroid,
                                                   planar_out);
 }

@@ -174,101 +174,120 @@ m44 T_from_qt(const QT& t) {
 }
 
 void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
-                       int64_t* ncl) {
+                       int64_t* nclp) {
   const int n = (int)in.size();
-  if (ncl) *ncl = 0;
+  if (nclp) *nclp = 0;
   if ((float)n <= P.cluster_number_threshold) {
     if (n == 0) fine.push_back({1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1u});
     else fine.insert(fine.end(), in.begin(), in.end());
     return;
   }
-  // KdTreeFLANN::radiusSearch(q, r): every j with L2_Simple d2 < float(r*r), sorted by (d2, j)
+  // KdTreeFLANN::radiusSearch(q, r): every j with L2_Simple d2 < float(r*r), sorted by (d2, j).
+  // d2 = ((0 + ex^2) + ey^2) + ez^2 adds non-negative terms, so d2 < r2 implies
+  // fl(ex)^2 < r2; that predicate is monotone along candidates sorted by tx, so two
+  // binary searches give a window that contains every neighbour, and the exact d2
+  // test inside it decides.  Candidates with non-finite tx have no neighbours
+  // (d2 is NaN or inf, even against themselves).
   const float r2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
-  const double cell = std::max(1.0, (double)P.cluster_distance_threshold * 1.25);
-  struct KH {
-    size_t operator()(const int64_t k) const { return std::hash<int64_t>()(k); }
-  };
-  auto key = [&](const QT& t) {
-    const int64_t x = (int64_t)std::floor(t.tx / cell), y = (int64_t)std::floor(t.ty / cell),
-                  z = (int64_t)std::floor(t.tz / cell);
-    return (x * 73856093) ^ (y * 19349663) ^ (z * 83492791);
-  };
-  auto cell_of = [&](const QT& t, int64_t* c) {
-    c[0] = (int64_t)std::floor(t.tx / cell);
-    c[1] = (int64_t)std::floor(t.ty / cell);
-    c[2] = (int64_t)std::floor(t.tz / cell);
-  };
-  std::unordered_map<int64_t, std::vector<int>, KH> grid;
-  for (int i = 0; i < n; ++i) grid[key(in[i])].push_back(i);
+  std::vector<int> byx;
+  byx.reserve(n);
+  for (int i = 0; i < n; ++i)
+    if (std::isfinite(in[i].tx)) byx.push_back(i);
+  std::sort(byx.begin(), byx.end(), [&](int a, int b) { return in[a].tx < in[b].tx || (in[a].tx == in[b].tx && a < b); });
+  const size_t nx = byx.size();
+  std::vector<float> sx(nx), sy(nx), sz3(nx);
+  for (size_t p = 0; p < nx; ++p) {
+    sx[p] = in[byx[p]].tx;
+    sy[p] = in[byx[p]].ty;
+    sz3[p] = in[byx[p]].tz;
+  }
   const AngleCut ccut = make_cut(P.cluster_angel_threshold);
   std::vector<f3> xaxis(n);
   for (int i = 0; i < n; ++i) xaxis[i] = quat_rotate(quatf{in[i].qw, in[i].qx, in[i].qy, in[i].qz}, f3{1.f, 0.f, 0.f});
-  std::vector<std::vector<int>> clusters;
+  // clusters as ranges of one flat member list, in creation order
+  std::vector<int> mem;
+  std::vector<int> cbeg;
   std::vector<std::pair<float, int>> nb;
+  std::vector<float> d2w;
   for (int i = 0; i + 1 < n; ++i) {  // the last candidate never seeds (:1084)
     if (in[i].alloc) continue;
     nb.clear();
-    int64_t c[3];
-    cell_of(in[i], c);
-    for (int64_t dx = -1; dx <= 1; ++dx)
-      for (int64_t dy = -1; dy <= 1; ++dy)
-        for (int64_t dz = -1; dz <= 1; ++dz) {
-          const int64_t k = ((c[0] + dx) * 73856093) ^ ((c[1] + dy) * 19349663) ^ ((c[2] + dz) * 83492791);
-          auto it = grid.find(k);
-          if (it == grid.end()) continue;
-          for (int j : it->second) {
-            int64_t cj[3];
-            cell_of(in[j], cj);
-            if (cj[0] != c[0] + dx || cj[1] != c[1] + dy || cj[2] != c[2] + dz) continue;  // hash collision
-            const float ex = in[i].tx - in[j].tx, ey = in[i].ty - in[j].ty, ez = in[i].tz - in[j].tz;
-            float d2 = 0.0f;
-            d2 += ex * ex;
-            d2 += ey * ey;
-            d2 += ez * ez;
-            if (d2 < r2) nb.push_back({d2, j});
-          }
-        }
-    std::sort(nb.begin(), nb.end());
-    std::vector<int> cl;
-    for (auto& e : nb) {
-      const f3 a = xaxis[i], b = xaxis[e.second];
-      if (angle_lt(normal_cos(a.x, a.y, a.z, b.x, b.y, b.z), ccut)) {
-        in[e.second].alloc = 1u;
-        cl.push_back(e.second);
+    const float xi = in[i].tx, yi = in[i].ty, zi = in[i].tz;
+    if (std::isfinite(xi)) {
+      const size_t lo = std::partition_point(sx.begin(), sx.end(), [&](float x) {
+                          const float ex = xi - x;
+                          return ex > 0.f && ex * ex >= r2;
+                        }) - sx.begin();
+      const size_t hi = std::partition_point(sx.begin() + lo, sx.end(), [&](float x) {
+                          const float ex = xi - x;
+                          return !(ex < 0.f && ex * ex >= r2);
+                        }) - sx.begin();
+      d2w.resize(hi - lo);
+      for (size_t p = lo; p < hi; ++p) {  // contiguous SoA: vectorises
+        const float ex = xi - sx[p], ey = yi - sy[p], ez = zi - sz3[p];
+        float d2 = 0.0f;
+        d2 += ex * ex;
+        d2 += ey * ey;
+        d2 += ez * ez;
+        d2w[p - lo] = d2;
       }
+      // neighbours passing the angle test, then ordered by (d2, j): the same
+      // sequence as testing the (d2, j)-sorted radius-search result in order
+      const f3 a = xaxis[i];
+      for (size_t p = lo; p < hi; ++p) {
+        if (!(d2w[p - lo] < r2)) continue;
+        const int j = byx[p];
+        const f3 b = xaxis[j];
+        if (angle_lt(normal_cos(a.x, a.y, a.z, b.x, b.y, b.z), ccut)) nb.push_back({d2w[p - lo], j});
+      }
+      std::sort(nb.begin(), nb.end());
     }
-    clusters.push_back(std::move(cl));
+    cbeg.push_back((int)mem.size());
+    for (auto& e : nb) {
+      in[e.second].alloc = 1u;
+      mem.push_back(e.second);
+    }
   }
-  if (ncl) *ncl = (int64_t)clusters.size();
-  // range_cluster (:1020-1038): exchange sort by size, emulated on indices
-  std::vector<int> ord(clusters.size());
-  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
-  auto sz = [&](int k) { return clusters[k].size(); };
-  // Only the first positions are consumed below; run passes lazily.
-  size_t sorted_upto = 0;
-  auto ensure_sorted = [&](size_t pos) {
-    while (sorted_upto <= pos && sorted_upto + 1 < ord.size()) {
-      const size_t i = sorted_upto;
-      for (size_t j = i + 1; j < ord.size(); ++j)
-        if (sz(ord[i]) < sz(ord[j])) std::swap(ord[i], ord[j]);
-      ++sorted_upto;
-    }
-  };
-  ensure_sorted(0);
-  int clusternum = (int)sz(ord[0]);
-  bool stop = false;
-  for (size_t r = 0; r < ord.size(); ++r) {
-    if (stop) break;  // nothing else happens once stop is set
-    ensure_sorted(r);
-    const std::vector<int>& cl = clusters[ord[r]];
-    if ((int)cl.size() >= clusternum) {
+  const int ncl = (int)cbeg.size();
+  cbeg.push_back((int)mem.size());
+  if (nclp) *nclp = (int64_t)ncl;
+  if (ncl == 0) return;
+  auto sz = [&](int k) { return cbeg[k + 1] - cbeg[k]; };
+  // range_cluster (:1020-1038), an exchange sort by size (swap when strictly
+  // smaller).  Elements below a threshold never change the relative order of the
+  // elements at or above it, and the sorted prefix holds exactly those.  With
+  // t = min(max size, 2), only clusters of size >= t can be emitted below
+  // (clusternum starts at the max size and the loop breaks before it drops under
+  // 2), so the exchange sort is run on those alone; past them only the (smaller)
+  // sizes drive the loop.  Equal sizes keep creation order.
+  int mx = 0;
+  for (int k = 0; k < ncl; ++k) mx = std::max(mx, sz(k));
+  const int thr = std::min(mx, 2);
+  std::vector<int> big;
+  std::vector<int> rest_sizes;
+  for (int k = 0; k < ncl; ++k) {
+    if (sz(k) >= thr) big.push_back(k);
+    else rest_sizes.push_back(sz(k));
+  }
+  for (size_t a = 0; a < big.size(); ++a)
+    for (size_t b = a + 1; b < big.size(); ++b)
+      if (sz(big[a]) < sz(big[b])) std::swap(big[a], big[b]);
+  std::sort(rest_sizes.begin(), rest_sizes.end(), std::greater<int>());
+  int clusternum = mx;
+  for (size_t r = 0; r < (size_t)ncl; ++r) {
+    const bool is_big = r < big.size();
+    const int size_r = is_big ? sz(big[r]) : rest_sizes[r - big.size()];
+    if (size_r >= clusternum) {
+      const int kk = big[r];  // size_r >= clusternum >= thr: r is in the big prefix
+      const int b0 = cbeg[kk], b1 = cbeg[kk + 1];
       float ax = 0, ay = 0, az = 0;
-      for (int k : cl) { ax = ax + in[k].tx; ay = ay + in[k].ty; az = az + in[k].tz; }
-      const float cs = (float)cl.size();
+      for (int m = b0; m < b1; ++m) { ax = ax + in[mem[m]].tx; ay = ay + in[mem[m]].ty; az = az + in[mem[m]].tz; }
+      const float cs = (float)(b1 - b0);
       ax = ax / cs; ay = ay / cs; az = az / cs;
       float s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
-      for (int k : cl) {
-        const quatf q = {in[k].qw, in[k].qx, in[k].qy, in[k].qz};
+      for (int m = b0; m < b1; ++m) {
+        const QT& t = in[mem[m]];
+        const quatf q = {t.qw, t.qx, t.qy, t.qz};
         const f3 u = quat_rotate(q, f3{1.f, 0.f, 0.f}), v = quat_rotate(q, f3{0.f, 1.f, 0.f});
         s1[0] = s1[0] + u.x; s1[1] = s1[1] + u.y; s1[2] = s1[2] + u.z;
         s2[0] = s2[0] + v.x; s2[1] = s2[1] + v.y; s2[2] = s2[2] + v.z;
@@ -283,7 +302,7 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
         clusternum--;
         if (clusternum < 2) break;
       } else {
-        stop = true;
+        break;  // stop: nothing else happens once it is set
       }
     }
   }

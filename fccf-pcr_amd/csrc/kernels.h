@@ -73,10 +73,11 @@ void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs x
 // before the fit kernel runs (the caller orders the streams).
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
                          hipStream_t st);
-// centroid_ready (may be null): event after which b.centroid holds the cloud centroid.
+// Per-leaf fit, planar/residual flags and the residual cloud.
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float voxel_point_threshold,
-                     float curvature_threshold, VoxRec* planar_out, float* resid_out, FaceBufs b, hipStream_t st,
-                     hipEvent_t centroid_ready);
+                     float curvature_threshold, float* resid_out, FaceBufs b, hipStream_t st);
+// Planar records, oriented towards b.centroid (must be ready: the caller orders streams).
+void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_t st);
 
 // Octree bound simulation over xyz[0..*d_n) starting from *state (one workgroup per
 // sequence; `batch` sequences at xyz + e*xyz_stride with state[e]).

@@ -177,23 +177,22 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.resid = a.take_n<float>(3 * (size_t)cap);
 }
 
-// Device part of one cloud: both VoxelGrid passes, remove-NaN, face voxels.  The
-// sequential cloud-centroid sum runs on a side stream beside the octree/sort/fit
-// work and only gates the final normal orientation.
-void enqueue_cloud(CloudWS& w, float leaf, const fccf_params& P, hipStream_t st, hipStream_t side, hipEvent_t ev_ds,
-                   hipEvent_t ev_cent) {
+// Device part of one cloud, in three stream segments (each replayed as a graph):
+//   A  (main)  both VoxelGrid passes with remove-NaN between them
+//   C  (side)  the sequential cloud-centroid sum, after A
+//   F  (main)  octree leaves, per-leaf fit, residual cloud, after A
+// and the planar compaction, which orients normals towards the centroid, after C and F.
+void seg_downsample(CloudWS& w, float leaf, hipStream_t st) {
   voxel_grid(w.in, w.sc, w.cap, leaf, w.ds1, w.sc + 1, w.vg, st);  // main :1668-1678
   k_finite_flags<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag);  // driver :1374-1375
   exclusive_scan_u32(w.fflag, w.foff, w.sc + 1, w.cap, w.sc + 2, w.vg.ss, st);
   k_finite_scatter<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag, w.foff, w.ds1f);
   voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st);  // driver :1377-1387
-  HIP_CHECK(hipEventRecord(ev_ds, st));
-  HIP_CHECK(hipStreamWaitEvent(side, ev_ds, 0));
-  cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, w.fb.xs, side);
-  HIP_CHECK(hipEventRecord(ev_cent, side));
+}
+void seg_centroid(CloudWS& w, hipStream_t side) { cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, w.fb.xs, side); }
+void seg_faces(CloudWS& w, const fccf_params& P, hipStream_t st) {
   face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
-  face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.planar, w.resid, w.fb,
-                  st, ev_cent);
+  face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.resid, w.fb, st);
 }
 
 template <class T>
@@ -224,6 +223,9 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   S.n_src = n_src;
   S.n_tar = n_tar;
   if (c->debug) c->dbg.clear();
+  c->g_fine.captures = 0;
+  for (auto& gk : c->g_seg)
+    for (auto& g : gk) g.captures = 0;
   const auto t_all = clk::now();
   auto t0 = clk::now();
   hipStream_t st0 = c->st[0], st1 = c->st[1];
@@ -232,29 +234,50 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   const int64_t nin[2] = {n_tar, n_src};
   const float* hin[2] = {tar, src};
   const uint32_t cap[2] = {(uint32_t)std::max<int64_t>(nin[0], 1), (uint32_t)std::max<int64_t>(nin[1], 1)};
-  c->arena.ensure(cloud_bytes(cap[0], !on_device) + cloud_bytes(cap[1], !on_device) + (1 << 20));
+  c->arena.ensure(cloud_bytes(cap[0], true) + cloud_bytes(cap[1], true) + (1 << 20));
   c->arena.reset();
+  // Inputs are staged into the workspace (H2D, or D2D for device-resident
+  // clouds) so the captured graph never depends on caller pointers.
+  uint32_t* hn = (uint32_t*)c->pinned.get(64);
   for (int k = 0; k < 2; ++k) {
-    carve_cloud(c->arena, w[k], cap[k], !on_device);
-    hipStream_t st = c->st[k];
+    carve_cloud(c->arena, w[k], cap[k], true);
     const uint32_t n = (uint32_t)nin[k];
-    if (on_device) {
-      w[k].in = hin[k];
-    } else {
-      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n, hipMemcpyHostToDevice, st));
-      w[k].in = w[k].in_copy;
-    }
-    uint32_t* hn = (uint32_t*)c->pinned.get(64) + k;
-    *hn = n;
-    HIP_CHECK(hipMemcpyAsync(w[k].sc, hn, 4, hipMemcpyHostToDevice, st));
-    enqueue_cloud(w[k], leaf, P, st, c->st[2 + k], c->ev[2 * k], c->ev[2 * k + 1]);
-    HIP_CHECK(hipGetLastError());
+    if (n)
+      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n,
+                               on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st0));
+    w[k].in = w[k].in_copy;
+    hn[k] = n;
+    HIP_CHECK(hipMemcpyAsync(w[k].sc, hn + k, 4, hipMemcpyHostToDevice, st0));
   }
+  struct {
+    const void* base;
+    size_t acap;
+    uint32_t cap0, cap1;
+    float leaf, fvs, vpt, ct;
+  } key = {c->arena.base, c->arena.cap, cap[0], cap[1], leaf, P.face_voxel_size, P.voxel_point_threshold,
+           P.curvature_threshold};
+  // st0 -> st1 fork (the staging copies above are on st0)
+  HIP_CHECK(hipEventRecord(c->ev[4], st0));
+  HIP_CHECK(hipStreamWaitEvent(st1, c->ev[4], 0));
+  for (int k = 0; k < 2; ++k) {
+    hipStream_t sm = c->st[k], ss = c->st[2 + k];
+    c->g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
+    HIP_CHECK(hipEventRecord(c->ev[2 * k], sm));
+    HIP_CHECK(hipStreamWaitEvent(ss, c->ev[2 * k], 0));
+    c->g_seg[k][1].run(&key, sizeof key, ss, [&] { seg_centroid(w[k], ss); });
+    HIP_CHECK(hipEventRecord(c->ev[2 * k + 1], ss));
+    c->g_seg[k][2].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm); });
+    HIP_CHECK(hipStreamWaitEvent(sm, c->ev[2 * k + 1], 0));
+    face_voxels_orient(w[k].cap, w[k].planar, w[k].fb, sm);
+  }
+  HIP_CHECK(hipEventRecord(c->ev[5], st1));  // join
+  HIP_CHECK(hipStreamWaitEvent(st0, c->ev[5], 0));
+  HIP_CHECK(hipGetLastError());
   // counts of both clouds
   uint32_t sc[2][4], fsc[2][4];
   for (int k = 0; k < 2; ++k) {
-    HIP_CHECK(hipMemcpyAsync(sc[k], w[k].sc, 16, hipMemcpyDeviceToHost, c->st[k]));
-    HIP_CHECK(hipMemcpyAsync(fsc[k], w[k].fb.nleaf, 16, hipMemcpyDeviceToHost, c->st[k]));
+    HIP_CHECK(hipMemcpyAsync(sc[k], w[k].sc, 16, hipMemcpyDeviceToHost, st0));
+    HIP_CHECK(hipMemcpyAsync(fsc[k], w[k].fb.nleaf, 16, hipMemcpyDeviceToHost, st0));
   }
   HIP_CHECK(hipStreamSynchronize(st0));
   HIP_CHECK(hipStreamSynchronize(st1));
@@ -263,9 +286,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   S.m_tar = sc[0][3];
   S.m_src = sc[1][3];
   std::vector<VoxRec> vox[2];
-  for (int k = 0; k < 2; ++k) vox[k] = d2h(w[k].planar, fsc[k][2], c->st[k]);
+  for (int k = 0; k < 2; ++k) vox[k] = d2h(w[k].planar, fsc[k][2], st0);
   HIP_CHECK(hipStreamSynchronize(st0));
-  HIP_CHECK(hipStreamSynchronize(st1));
   S.vox1 = fsc[0][2]; S.vox2 = fsc[1][2];
   S.res1 = fsc[0][3]; S.res2 = fsc[1][3];
   if (c->debug) {
@@ -509,7 +531,17 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
                                (uint32_t)std::max<size_t>(nk, 1));
     fb.xs = exact_sum_carve(c->arena3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
     HIP_CHECK(hipMemcpyAsync(fb.T, evals.data(), sizeof(m44) * E, hipMemcpyHostToDevice, st0));
-    fine_verify_batch(w[0].resid, n1, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
+    struct {
+      const void* base;
+      size_t acap;
+      const void *r1, *r2;
+      uint32_t n1, n2;
+      int32_t E;
+      float res;
+    } fkey = {c->arena3.base, c->arena3.cap, w[0].resid, w[1].resid, n1, n2, E, P.fine_verify_voxel_size};
+    c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
+      fine_verify_batch(w[0].resid, n1, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
+    });
     HIP_CHECK(hipGetLastError());
     uint32_t ferr = 0;
     HIP_CHECK(hipMemcpyAsync(scores.data(), fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st0));
@@ -562,6 +594,9 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     for (int j = 0; j < 4; ++j) T_out[4 * i + j] = T.m[i][j];
   S.ms[FCCF_T_FUSE] = ms_since(t0);
   S.ms_total = ms_since(t_all);
+  S.graph_captures = c->g_fine.captures;
+  for (auto& gk : c->g_seg)
+    for (auto& g : gk) S.graph_captures += g.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
   if (c->debug) {

@@ -45,11 +45,11 @@ class Stats(ctypes.Structure):
         "n_src", "n_tar", "m_src", "m_tar", "vox1", "vox2", "res1", "res2", "groups1", "groups2",
         "planes1", "planes2", "bases1", "bases2", "K", "K_pass")] + [
         ("cand", ctypes.c_int64 * 3), ("fine", ctypes.c_int64 * 3), ("lm_solves", ctypes.c_int64),
-        ("overflow_passthrough", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("overflow_passthrough", ctypes.c_int32), ("graph_captures", ctypes.c_int32),
         ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double)]
 
     def as_dict(self):
-        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "reserved")}
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms")}
         d["cand"] = list(self.cand)
         d["fine"] = list(self.fine)
         d["ms"] = dict(zip(T_NAMES, list(self.ms)))

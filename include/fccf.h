@@ -78,7 +78,7 @@ typedef struct fccf_stats {
   int64_t fine[3];               /* cluster-fused candidates per type             */
   int64_t lm_solves;             /* quick_verify refinements run                  */
   int32_t overflow_passthrough;  /* VoxelGrid int32 guard tripped (any pass)      */
-  int32_t reserved;
+  int32_t graph_captures;        /* device-stage graphs (re)captured by this call */
   double ms[FCCF_T_COUNT];       /* stage wall times                              */
   double ms_total;               /* host arrays (or resident device arrays) -> T  */
 } fccf_stats;

@@ -98,3 +98,17 @@ def test_other_room(ctx, oracle, fccf):
     run = oracle.Run(src, tar, 0.08)
     ctx.register(src, tar, 0.08)
     compare_all(ctx, run)
+
+
+def test_graph_replay_with_new_data_and_sizes(ctx, oracle, fccf):
+    """The device stages run as captured hipGraphs keyed by workspace layout: a
+    second call with different points of the same size replays the graph, a call
+    with a different size re-captures.  Each must match the oracle bitwise."""
+    src, tar, _ = fccf.synth_pair(80_000)
+    rng = np.random.default_rng(3)
+    src2 = (src + rng.normal(0, 0.002, src.shape)).astype(np.float32)  # same n: replay
+    for s, t in ((src, tar), (src2, tar), (src2[:70_001], tar)):  # last: new capacity, re-capture
+        run = oracle.Run(s, t, 0.1, oracle.STABLE)
+        T, _ = ctx.register(s, t, 0.1)
+        compare_all(ctx, run)
+        np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))

@@ -10,7 +10,7 @@
 #include "../fccf-pcr_amd/csrc/exactsum.h"
 using namespace fccf;
 
-struct Stats { long groups = 0, gfail = 0, chunks = 0, cfail = 0; };
+struct Stats { long scans = 0, replays = 0; };
 
 static float naive(const std::vector<float>& x) {
   float s = 0.f;
@@ -18,14 +18,33 @@ static float naive(const std::vector<float>& x) {
   return s;
 }
 
-static bool try_apply(float& s, const XsSum* tab, int Eb) {
-  int E;
-  int64_t M;
-  if (Eb == XS_NOE || !xs_decompose(s, &E, &M)) return false;
-  const int h = E - Eb;
-  if (h < 0 || h >= XS_NE || !xs_valid(tab[h], M)) return false;
-  s = xs_apply(tab[h], M, E);
-  return true;
+// Serial restatement of exactsum.hip's scan_jump: compose units cur.. under s's
+// binade until the first prefix that does not validate, apply the prefix before
+// it, hand that unit to `descend`, continue after it.
+template <class Descend>
+static void scan_jump(float& s, const std::vector<XsTab3>& T, int cnt, Stats& st, Descend descend) {
+  int cur = 0;
+  while (cur < cnt) {
+    int E;
+    int64_t M;
+    if (!xs_decompose(s, &E, &M)) {
+      descend(cur);
+      ++cur;
+      continue;
+    }
+    ++st.scans;
+    XsSum a = xs_identity(), last = a;
+    int f = cnt;
+    for (int l = cur; l < cnt; ++l) {
+      a = xs_compose(a, xs_pick(T[l], E));
+      if (!xs_valid(a, M)) { f = l; break; }
+      last = a;
+    }
+    if (f > cur) s = xs_apply(last, M, E);
+    if (f >= cnt) break;
+    descend(f);
+    cur = f + 1;
+  }
 }
 
 static float exact(const std::vector<float>& x, Stats& st) {
@@ -36,40 +55,34 @@ static float exact(const std::vector<float>& x, Stats& st) {
     for (int k = c * XS_L; k < std::min(n, (c + 1) * XS_L); ++k) a += x[k];
     pre[c + 1] = pre[c] + a;
   }
-  std::vector<XsSum> ct((size_t)nch * XS_NE);
-  std::vector<int> cE(nch);
+  std::vector<XsTab3> ct(nch);
   for (int c = 0; c < nch; ++c) {
-    cE[c] = xs_predict(pre[c]);
     const int b = c * XS_L, m = std::min(XS_L, n - b);
-    for (int h = 0; h < XS_NE; ++h)
-      ct[(size_t)c * XS_NE + h] = cE[c] == XS_NOE ? xs_bad() : xs_run(&x[b], 1, m, cE[c] + h);
+    ct[c].Eb = xs_predict(pre[c]);
+    XsSum* t[3] = {&ct[c].t0, &ct[c].t1, &ct[c].t2};
+    for (int h = 0; h < XS_NE; ++h) *t[h] = ct[c].Eb == XS_NOE ? xs_bad() : xs_run(&x[b], 1, m, ct[c].Eb + h);
   }
-  std::vector<XsSum> gt((size_t)ng * XS_NE);
-  std::vector<int> gE(ng);
+  std::vector<XsTab3> gt(ng);
   for (int g = 0; g < ng; ++g) {
-    gE[g] = xs_predict(pre[(size_t)g * XS_G]);
+    gt[g].Eb = xs_predict(pre[(size_t)g * XS_G]);
+    XsSum* t[3] = {&gt[g].t0, &gt[g].t1, &gt[g].t2};
     for (int h = 0; h < XS_NE; ++h) {
       XsSum a = xs_identity();
-      for (int c = g * XS_G; c < std::min(nch, (g + 1) * XS_G); ++c) {
-        const int hc = gE[g] + h - cE[c];
-        const bool have = gE[g] != XS_NOE && cE[c] != XS_NOE && hc >= 0 && hc < XS_NE;
-        a = xs_compose(a, have ? ct[(size_t)c * XS_NE + hc] : xs_bad());
-      }
-      gt[(size_t)g * XS_NE + h] = a;
+      for (int c = g * XS_G; c < std::min(nch, (g + 1) * XS_G); ++c)
+        a = xs_compose(a, gt[g].Eb == XS_NOE ? xs_bad() : xs_pick(ct[c], gt[g].Eb + h));
+      *t[h] = a;
     }
   }
   float s = 0.f;
-  for (int g = 0; g < ng; ++g) {
-    ++st.groups;
-    if (try_apply(s, &gt[(size_t)g * XS_NE], gE[g])) continue;
-    ++st.gfail;
-    for (int c = g * XS_G; c < std::min(nch, (g + 1) * XS_G); ++c) {
-      ++st.chunks;
-      if (try_apply(s, &ct[(size_t)c * XS_NE], cE[c])) continue;
-      ++st.cfail;
+  scan_jump(s, gt, ng, st, [&](int g) {
+    const int c0 = g * XS_G, nc = std::min(XS_G, nch - c0);
+    std::vector<XsTab3> sub(ct.begin() + c0, ct.begin() + c0 + nc);
+    scan_jump(s, sub, nc, st, [&](int f) {
+      ++st.replays;
+      const int c = c0 + f;
       for (int k = c * XS_L; k < std::min(n, (c + 1) * XS_L); ++k) s += x[k];
-    }
-  }
+    });
+  });
   return s;
 }
 
@@ -107,7 +120,6 @@ int main(int argc, char** argv) {
       if (bad < 5) printf("MISMATCH kind %d n %d: %.9g vs %.9g\n", kind, n, a, b);
     }
   }
-  printf("trials %d mismatches %d groups %ld gfail %ld chunks %ld cfail %ld\n", trials, bad, st.groups, st.gfail,
-         st.chunks, st.cfail);
+  printf("trials %d mismatches %d scans %ld replays %ld\n", trials, bad, st.scans, st.replays);
   return bad ? 1 : 0;
 }
