@@ -80,6 +80,27 @@ def cpu_baseline(src, tar, leaf, budget_s):
                       f"introsort summation order, 1 thread"}
 
 
+class _SelftestCtx:
+    """--selftest: stands in for fccf_amd.Ctx so the distributed/JSON logic can be
+    exercised on CPU (tests/test_dist.py).  Computes nothing; never used for numbers."""
+
+    class _St:
+        K, K_pass, graph_captures = 100, 10, 0
+
+        def as_dict(self):
+            return {"ms": {"stub": 0.0}}
+
+    def upload(self, a):
+        return 0
+
+    def free(self, d):
+        pass
+
+    def register_device(self, ds, ns, dt, nt, leaf):
+        time.sleep(0.002)
+        return np.eye(4, dtype=np.float32), self._St()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,14 +109,21 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--selftest", action="store_true", help="CPU stub registration (tests only)")
     args = ap.parse_args()
 
     rank, ws, local, dist = dist_setup()
     import fccf_amd as F
     cfg = F.CONFIGS[args.config]
-    src, tar, T_gt = F.synth_pair(cfg["n"], cfg["room"])
+    if args.selftest:
+        src = tar = np.zeros((cfg["n"], 3), np.float32)
+        T_gt = np.eye(4, dtype=np.float32)
+        ctx = _SelftestCtx()
+        args.no_cpu_baseline = True
+    else:
+        src, tar, T_gt = F.synth_pair(cfg["n"], cfg["room"])
+        ctx = F.Ctx(local)
     leaf = cfg["leaf"]
-    ctx = F.Ctx(local)
     d_src, d_tar = ctx.upload(src), ctx.upload(tar)
 
     for _ in range(args.warmup):
@@ -131,7 +159,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic",
+            "data": "selftest-stub" if args.selftest else "synthetic",
             "config": {"workload": f"{args.config}: synthetic {cfg['n']:,}/{cfg['n']:,}-point room pair "
                                    f"R{tuple(cfg['room'])}, voxel {leaf} m, one registration per step per GPU",
                        "n_points": cfg["n"], "leaf": leaf, "room": list(cfg["room"]),

@@ -1,0 +1,24 @@
+"""bench.py's multi-rank path (one process per GPU, gloo barrier + max-over-ranks)
+exercised on CPU with world_size 2 and a stub registration (--selftest)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_gloo(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29531", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "5", "--warmup", "1", "--config", "c2", "--selftest"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 5 and d["warmup"] == 1 and d["scaling"] == "weak"
+    # value = K summed over both ranks / the slowest rank's wall time
+    assert abs(d["value"] - 2 * 5 * 100 / (d["ms_per_step"] * 5 / 1e3)) / d["value"] < 1e-6
+    assert d["data"] == "selftest-stub" and "cpu_baseline" not in d
