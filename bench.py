@@ -27,6 +27,11 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 
 METRIC = "coplane-pair correspondences/sec + end-to-end registration ms, 1M-pt pair"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM"); every kernel here is HBM/latency bound
+# Kernels with a probe site (fccf-pcr_amd/csrc, FCCF_PROBED) and their algorithmic bytes per launch
+# ("Measurement").  The roofline reports the one with the most GPU time per step.
+PROBE_KERNELS = ["k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter", "k_vg_keys", "k_vg_centroid",
+                 "k_gather", "k_voxel_fit", "k_fv_counts", "k_match_count", "k_match_emit"]
 
 
 def dist_setup():
@@ -101,6 +106,31 @@ class _SelftestCtx:
         return np.eye(4, dtype=np.float32), self._St()
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py), else None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    return None
+
+
+def probe_pass(ctx, reg, kernel, steps):
+    ctx.set_probe(kernel)
+    reg()  # one untimed eager warm-up step
+    ctx.set_probe(kernel)  # resets the totals
+    for _ in range(steps):
+        reg()
+    ms, n, b = ctx.probe_read()
+    return ms, n, b
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +140,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--selftest", action="store_true", help="CPU stub registration (tests only)")
+    ap.add_argument("--probe-kernel", default="auto", help="kernel for the roofline object (auto = dominant)")
     args = ap.parse_args()
 
     rank, ws, local, dist = dist_setup()
@@ -126,8 +157,25 @@ def main():
     leaf = cfg["leaf"]
     d_src, d_tar = ctx.upload(src), ctx.upload(tar)
 
+    def reg():
+        return ctx.register_device(d_src, src.shape[0], d_tar, tar.shape[0], leaf)
+
+    # Untimed pre-pass: GPU time per step of every probed kernel (HIP events around
+    # each launch; probed calls launch eagerly, see csrc/probe.h).  The roofline
+    # kernel is the one with the most GPU time per step (or --probe-kernel).
+    table, probe = {}, None
+    if not args.selftest:
+        for k in PROBE_KERNELS:
+            ms, n, b = probe_pass(ctx, reg, k, 3)
+            if n:
+                table[k] = {"ms_per_step": ms / 3, "launches_per_step": n / 3, "avg_launch_us": ms * 1e3 / n,
+                            "algorithmic_bytes_per_launch": b / n,
+                            "achieved_GBps": (b / n) / (ms * 1e-3 / n) / 1e9 if ms > 0 else None}
+        ctx.set_probe(None)
+        probe = max(table, key=lambda k: table[k]["ms_per_step"]) if args.probe_kernel == "auto" else args.probe_kernel
+
     for _ in range(args.warmup):
-        T, st = ctx.register_device(d_src, src.shape[0], d_tar, tar.shape[0], leaf)
+        T, st = reg()
     barrier(dist)
     t0 = time.perf_counter()
     Ks = 0
@@ -139,6 +187,19 @@ def main():
         Ks += st.K
     elapsed = time.perf_counter() - t0
     barrier(dist)
+    roofline = None
+    if probe:
+        # Probe window right after the timed region, same inputs: every launch of
+        # the roofline kernel timed with HIP events on its own stream.
+        pms, pn, pb = probe_pass(ctx, reg, probe, args.steps)
+        ctx.set_probe(None)
+        if pn:
+            avg_s = pms * 1e-3 / pn
+            achieved = (pb / pn) / avg_s / 1e9
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe), "kernel": probe,
+                        "avg_launch_us": avg_s * 1e6, "algorithmic_bytes_per_launch": pb / pn,
+                        "launches_per_step": pn / args.steps}
     elapsed = allmax(dist, elapsed)
     Ks_all = allsum(dist, float(Ks))
     ctx.free(d_src)
@@ -172,6 +233,10 @@ def main():
             "rot_err_deg_vs_gt": rot_err,
             "trans_err_m_vs_gt": float(np.linalg.norm(T[:3, 3] - T_gt[:3, 3])),
         }
+        if roofline is not None:
+            out["roofline"] = roofline
+            out["kernel_table"] = {k: {a: (round(b, 4) if isinstance(b, float) else b) for a, b in v.items()}
+                                   for k, v in table.items()}
         if ws == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(src, tar, leaf, args.cpu_budget)
         print(json.dumps(out), flush=True)

@@ -86,6 +86,23 @@ extern "C" int fccf_ctx_set_debug(fccf_ctx* c, int on) {
   return FCCF_OK;
 }
 
+extern "C" int fccf_ctx_set_probe(fccf_ctx* c, const char* kernel) {
+  if (!c) return FCCF_E_ARG;
+  c->probe.target = kernel ? kernel : "";
+  c->probe.total_ms = c->probe.total_bytes = 0.0;
+  c->probe.launches = 0;
+  c->probe.armed.clear();
+  return FCCF_OK;
+}
+
+extern "C" int fccf_probe_read(fccf_ctx* c, double* total_ms, int64_t* launches, double* total_bytes) {
+  if (!c || !total_ms || !launches || !total_bytes) return FCCF_E_ARG;
+  *total_ms = c->probe.total_ms;
+  *launches = c->probe.launches;
+  *total_bytes = c->probe.total_bytes;
+  return FCCF_OK;
+}
+
 extern "C" int fccf_debug_get(fccf_ctx* c, const char* name, void* buf, int64_t cap, int64_t* nbytes) {
   if (!c || !name) return FCCF_E_ARG;
   auto it = c->dbg.find(name);

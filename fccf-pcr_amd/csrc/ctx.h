@@ -12,6 +12,7 @@
 
 #include "../../include/fccf.h"
 #include "pool.h"
+#include "probe.h"
 
 namespace fccf {
 
@@ -91,7 +92,7 @@ struct CachedGraph {
       const char* e = std::getenv("FCCF_GRAPHS");
       return !(e && e[0] == '0');
     }();
-    if (!enabled) {
+    if (!enabled || (g_probe && g_probe->on())) {  // probed calls launch eagerly (probe.h)
       body();
       return;
     }
@@ -134,6 +135,7 @@ struct fccf_ctx {
   fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
   fccf::Pool pool;
+  fccf::Probe probe;
   bool debug = false;
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;

@@ -1,6 +1,7 @@
 // devprim.hip — stable LSD radix sort, run-length segmentation and exclusive scan
 // for gfx950.  Wave64-native: per-digit ranks come from 8 ballots per 64-key
 // chunk (no 32-lane warp idioms), block = 4 waves, tile = 2048 keys.
+#include "probe.h"
 #include "devprim.h"
 
 namespace fccf {
@@ -161,8 +162,9 @@ void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, u
     const int src = p & 1, dst = src ^ 1;
     k_rs_hist<K><<<nb, T, 0, st>>>(kb[src], d_n, d_nbits, shift, s.hist, nb);
     k_rs_rowscan<<<256, T, 0, st>>>(s.hist, nb, s.tot, d_nbits, shift);
-    k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb,
-                                      (iota && p == 0) ? 1 : 0);
+    FCCF_PROBED("k_rs_scatter", st, (d_n, 2.0 * (sizeof(K) + 4)),
+                k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb,
+                                                  (iota && p == 0) ? 1 : 0));
   }
   const uint32_t g = min(nb * 8u, 2048u);
   k_rs_copyback<K><<<g, 256, 0, st>>>(k1, v1, k0, v0, d_n, d_nbits, max_passes);

@@ -9,6 +9,7 @@
 //                a group that crosses a binade, then a plain replay of the chunk
 // The first four are bandwidth-bound streaming passes over the inputs; the chain
 // costs one wave scan per binade crossing (plus one 256-add replay).
+#include "probe.h"
 #include "devprim.h"
 #include "exactsum.h"
 #include "ctx.h"
@@ -358,15 +359,19 @@ void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint3
   if (S == 3) {
     k_xs_csum<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    k_xs_chunk<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
+    FCCF_PROBED("k_xs_chunk", st, (cnt, 4.0 * 3),
+                k_xs_chunk<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC));
     k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    k_xs_chain<3><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    FCCF_PROBED("k_xs_chain", st, (cnt, 4.0 * 3),
+                k_xs_chain<3><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide));
   } else {
     k_xs_csum<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    k_xs_chunk<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
+    FCCF_PROBED("k_xs_chunk", st, (cnt, 4.0 * 1),
+                k_xs_chunk<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC));
     k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    k_xs_chain<1><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    FCCF_PROBED("k_xs_chain", st, (cnt, 4.0 * 1),
+                k_xs_chain<1><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide));
   }
 }
 

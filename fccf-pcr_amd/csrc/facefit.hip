@@ -12,6 +12,7 @@
 //  * compaction: planar leaves (Morton order) and the residual cloud cloud_sub
 //    (points of non-planar leaves, Morton then index order, :527-530).
 // Sums run over each leaf's points in ascending index, the reference's order.
+#include "probe.h"
 #include "kernels.h"
 
 namespace fccf {
@@ -341,7 +342,8 @@ void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
                 hipStream_t st, int batch, size_t xyz_stride, size_t aggr_stride) {
   (void)cap;
-  k_oct_sim<<<batch, 1024, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride);
+  FCCF_PROBED("k_oct_sim", st, (d_n, 24.0 * batch / AGGR_BLOCK),
+              k_oct_sim<<<batch, 1024, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride));
 }
 
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
@@ -352,14 +354,16 @@ void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, do
   k_oct_codes<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.oct, res, b.c0, b.nbits);
   radix_sort_u64(b.c0, b.v0, b.c1, b.v1, d_n, cap, b.nbits, 64, true, b.ss, st);
   segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st, b.seg_of);
-  k_gather<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, d_n, b.sp);
+  FCCF_PROBED("k_gather", st, (d_n, 28.0),
+              k_gather<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, d_n, b.sp));
 }
 
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, float* resid_out,
                      FaceBufs b, hipStream_t st) {
   (void)xyz;
-  k_voxel_fit<<<grid_for(cap, 4, 4096), 256, 0, st>>>(b.sp, b.starts, b.nleaf, vpt, cthr, b.recs, b.flag_planar,
-                                                      b.resid_cnt);
+  FCCF_PROBED("k_voxel_fit", st, (d_n, 12.0, b.nleaf, (double)sizeof(VoxRec) + 12.0),
+              k_voxel_fit<<<grid_for(cap, 4, 4096), 256, 0, st>>>(b.sp, b.starts, b.nleaf, vpt, cthr, b.recs,
+                                                                  b.flag_planar, b.resid_cnt));
   exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
   exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
   k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);

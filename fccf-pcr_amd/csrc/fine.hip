@@ -8,6 +8,7 @@
 // score = similar / allinvec.  The S1 half of the octree bound replay is shared by
 // all evaluations.  Sort key = (e | morton | is_target); counts are exact integers,
 // the two float sums run in the reference's leaf order (one lane per evaluation).
+#include "probe.h"
 #include "kernels.h"
 #include "match.h"
 
@@ -100,8 +101,15 @@ __global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ 
   const uint32_t ns = scal[2], sh = scal[3] - 1u;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
     const uint32_t b = starts[s], e = starts[s + 1];
-    uint32_t src = 0;
-    for (uint32_t k = b; k < e; ++k) src += (keys[k] & 1ull) ? 0u : 1u;
+    // keys of one leaf differ only in the is_target bit and are sorted, so the
+    // source points come first: the split is found by binary search
+    uint32_t lo = b, hi = e;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (keys[mid] & 1ull) hi = mid;
+      else lo = mid + 1;
+    }
+    const uint32_t src = lo - b;
     const float sn = (float)src, tn = (float)((e - b) - src);
     float t = 0.f;
     if (sn >= 1.f && tn >= 1.f) {
@@ -164,7 +172,8 @@ void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
   (void)hipMemsetAsync(b.range, 0, sizeof(uint32_t) * 2 * MAX_EVAL, st);
-  k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.k1, b.starts, b.scal, b.term, b.range);
+  FCCF_PROBED("k_fv_counts", st, (b.scal, 16.0, b.scal + 2, 12.0),
+              k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.k1, b.starts, b.scal, b.term, b.range));
   k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
   k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E);

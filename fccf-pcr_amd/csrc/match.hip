@@ -1,13 +1,14 @@
 // match.hip — K5: all-pairs coplane-pair correspondence search (FCCF.cpp:1410-1428)
 // fused with the closed-form transform of each match (computer_transform, :841-1018).
 //
-// One lane per test k = i1 * B2 + i2 (b1-major, the reference loop order).  A test
+// One wave per test k = i1 * B2 + i2 (b1-major, the reference loop order).  A test
 // passes when |angle1 - angle2| < 5 deg and the roughness types agree; it then emits
 // one transform per (third source plane, matching target plane) in loop order, or
 // the weighted-centroid fallback (:1000-1017).  Emission is two-pass: counts ->
 // per-type exclusive scan -> write, so each type's list is in exactly the order
 // transformation_vecter[type] receives push_backs.  The plane/pair tables (<= 16
 // planes, <= 120 pairs per cloud) live in LDS.
+#include "probe.h"
 #include "kernels.h"
 #include "match.h"
 
@@ -71,8 +72,13 @@ __device__ f3 ls3(f3 n1, f3 m1, f3 k1, f3 D) {
   return mul3v(mul33(Mi, AT), D);
 }
 
-// Returns the number of transforms the test emits; writes them when out != null.
-__device__ int match_test(const MatchIn& M, int k, MCand* out) {
+// One wave per test k = i1 * B2 + i2.  Its candidate (third source plane k3,
+// target plane q) pairs, p = k3 * nF2 + q in the reference's loop order, are spread
+// over the lanes; ballot + mbcnt give every accepted pair its rank, so emission
+// keeps loop order.  Returns the number of transforms the test emits (>= 1 when
+// the test passes: the weighted-centroid fallback); writes them when out != null.
+__device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
+  const int lane = threadIdx.x & 63;
   const int i1 = k / M.nB2, i2 = k % M.nB2;
   const MBase& b1 = M.B1[i1];
   const MBase& b2 = M.B2[i2];
@@ -80,38 +86,46 @@ __device__ int match_test(const MatchIn& M, int k, MCand* out) {
   Ctx c;
   prep(M, b1.i1, b1.i2, b2.i1, b2.i2, c);
   const m44 T0 = rot_only(c.rot);
+  const quatf qr = quat_from_rot(c.rot);  // fused R -> quaternion (FCCF.cpp:1437-1462)
   const MPlane *A = M.F1, *B = M.F2;
+  const int np = M.nF1 * M.nF2;
   int cnt = 0;
-  for (int k3 = 0; k3 < M.nF1; ++k3) {
-    if (k3 == b1.i1 || k3 == b1.i2) continue;
-    const f3 kn = {A[k3].n[0], A[k3].n[1], A[k3].n[2]};
-    if (!(fabsf(dot3(c.n1cm1, kn)) > M.third_thr)) continue;
-    for (int q = 0; q < M.nF2; ++q) {
-      if (q == b2.i1 || q == b2.i2) continue;
-      const f3 pn = tf_so3(T0, B[q].n[0], B[q].n[1], B[q].n[2]);
-      const float cs = normal_cos(kn, pn);
-      if (angle_lt(cs, M.third_cut) && fabsf(dot3(c.n2cm2, pn)) > M.third_thr) {
-        if (out) {
-          const f3 pc = tf_se3(T0, B[q].c[0], B[q].c[1], B[q].c[2]);
-          const f3 c11 = {A[b1.i1].c[0], A[b1.i1].c[1], A[b1.i1].c[2]};
-          const f3 c12 = {A[b1.i2].c[0], A[b1.i2].c[1], A[b1.i2].c[2]};
-          const f3 c13 = {A[k3].c[0], A[k3].c[1], A[k3].c[2]};
-          const f3 c21 = {B[b2.i1].c[0], B[b2.i1].c[1], B[b2.i1].c[2]};
-          const f3 c22 = {B[b2.i2].c[0], B[b2.i2].c[1], B[b2.i2].c[2]};
-          const f3 D = {dot3(c11, c.n1) - dot3(c21, c.n2), dot3(c12, c.m1) - dot3(c22, c.m2r),
-                        dot3(c13, kn) - dot3(pc, pn)};
-          const f3 t = ls3(c.n1, c.m1, kn, D);
-          MCand& o = out[cnt];
-          for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) o.R[3 * i + j] = c.rot.m[i][j];
-          o.t[0] = t.x; o.t[1] = t.y; o.t[2] = t.z;
-        }
-        ++cnt;
+  for (int p0 = 0; p0 < np; p0 += 64) {
+    const int p = p0 + lane;
+    bool ok = false;
+    int k3 = 0, q = 0;
+    f3 kn = {0.f, 0.f, 0.f}, pn = {0.f, 0.f, 0.f};
+    if (p < np) {
+      k3 = p / M.nF2;
+      q = p % M.nF2;
+      kn = {A[k3].n[0], A[k3].n[1], A[k3].n[2]};
+      if (k3 != b1.i1 && k3 != b1.i2 && q != b2.i1 && q != b2.i2 && fabsf(dot3(c.n1cm1, kn)) > M.third_thr) {
+        pn = tf_so3(T0, B[q].n[0], B[q].n[1], B[q].n[2]);
+        ok = angle_lt(normal_cos(kn, pn), M.third_cut) && fabsf(dot3(c.n2cm2, pn)) > M.third_thr;
       }
     }
+    const uint64_t m = __ballot(ok);
+    if (out && ok) {
+      const int r = cnt + (int)__popcll(m & ((1ull << lane) - 1ull));
+      const f3 pc = tf_se3(T0, B[q].c[0], B[q].c[1], B[q].c[2]);
+      const f3 c11 = {A[b1.i1].c[0], A[b1.i1].c[1], A[b1.i1].c[2]};
+      const f3 c12 = {A[b1.i2].c[0], A[b1.i2].c[1], A[b1.i2].c[2]};
+      const f3 c13 = {A[k3].c[0], A[k3].c[1], A[k3].c[2]};
+      const f3 c21 = {B[b2.i1].c[0], B[b2.i1].c[1], B[b2.i1].c[2]};
+      const f3 c22 = {B[b2.i2].c[0], B[b2.i2].c[1], B[b2.i2].c[2]};
+      const f3 D = {dot3(c11, c.n1) - dot3(c21, c.n2), dot3(c12, c.m1) - dot3(c22, c.m2r),
+                    dot3(c13, kn) - dot3(pc, pn)};
+      const f3 t = ls3(c.n1, c.m1, kn, D);
+      MCand& o = out[r];
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) o.R[3 * a + b] = c.rot.m[a][b];
+      o.t[0] = t.x; o.t[1] = t.y; o.t[2] = t.z;
+      qout[r] = {qr.w, qr.x, qr.y, qr.z, t.x, t.y, t.z, 0u};
+    }
+    cnt += (int)__popcll(m);
   }
   if (cnt == 0) {
-    if (out) {
+    if (out && lane == 0) {
       const MPlane &a = A[b1.i1], &b = A[b1.i2], &d = B[b2.i1], &e = B[b2.i2];
       const float sx = (a.c[0] * a.fps + b.c[0] * b.fps) / (a.fps + b.fps);
       const float sy = (a.c[1] * a.fps + b.c[1] * b.fps) / (a.fps + b.fps);
@@ -121,9 +135,10 @@ __device__ int match_test(const MatchIn& M, int k, MCand* out) {
       const float tz = (d.c[2] * d.fps + e.c[2] * e.fps) / (d.fps + e.fps);
       const f3 tc = mul3v(c.rot, f3{tx, ty, tz});
       MCand& o = out[0];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) o.R[3 * i + j] = c.rot.m[i][j];
+      for (int a2 = 0; a2 < 3; ++a2)
+        for (int b2i = 0; b2i < 3; ++b2i) o.R[3 * a2 + b2i] = c.rot.m[a2][b2i];
       o.t[0] = sx - tc.x; o.t[1] = sy - tc.y; o.t[2] = sz - tc.z;
+      qout[0] = {qr.w, qr.x, qr.y, qr.z, o.t[0], o.t[1], o.t[2], 0u};
     }
     cnt = 1;
   }
@@ -136,10 +151,12 @@ __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__
   if (threadIdx.x == 0) M = *Mp;
   __syncthreads();
   const int K = M.nB1 * M.nB2;
-  for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
-    const int n = match_test(M, k, nullptr);
-    cnt[k] = (uint32_t)n;
-    type[k] = n ? M.B1[k / M.nB2].type : -1;
+  for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < K; k += gridDim.x * 4) {
+    const int n = match_test_wave(M, k, nullptr, nullptr);
+    if ((threadIdx.x & 63) == 0) {
+      cnt[k] = (uint32_t)n;
+      type[k] = n ? M.B1[k / M.nB2].type : -1;
+    }
   }
 }
 
@@ -186,21 +203,13 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
   if (threadIdx.x == 0) M = *Mp;
   __syncthreads();
   const int K = M.nB1 * M.nB2;
-  for (int k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
+  for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < K; k += gridDim.x * 4) {
     if (!cnt[k]) continue;
     const int t = type[k];
     MCand* cb = t == 0 ? c0 : (t == 1 ? c1 : c2);
     QTd* qb = t == 0 ? q0 : (t == 1 ? q1 : q2);
     const uint32_t o = off[k];
-    const int n = match_test(M, k, cb + o);
-    for (int j = 0; j < n; ++j) {  // fused R -> quaternion (FCCF.cpp:1437-1462)
-      const MCand& c = cb[o + j];
-      m33 R;
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) R.m[a][b] = c.R[3 * a + b];
-      const quatf q = quat_from_rot(R);
-      qb[o + j] = {q.w, q.x, q.y, q.z, c.t[0], c.t[1], c.t[2], 0u};
-    }
+    match_test_wave(M, k, cb + o, qb + o);
   }
 }
 
@@ -209,10 +218,12 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
                       MCand* c[3], QTd* q[3], hipStream_t st) {
   if (K <= 0) return;
-  const int g = (K + 255) / 256;
-  k_match_count<<<g, 256, 0, st>>>(d_in, cnt, type);
+  const int g = (K + 3) / 4;  // one wave per test
+  FCCF_PROBED("k_match_count", st, (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)),
+              k_match_count<<<g, 256, 0, st>>>(d_in, cnt, type));
   k_match_scan<<<1, 256, 0, st>>>(d_in, cnt, type, off, totals);
-  k_match_emit<<<g, 256, 0, st>>>(d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]);
+  FCCF_PROBED("k_match_emit", st, (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)),
+              k_match_emit<<<g, 256, 0, st>>>(d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]));
 }
 
 }  // namespace fccf

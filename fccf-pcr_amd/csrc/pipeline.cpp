@@ -223,6 +223,10 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   S.n_src = n_src;
   S.n_tar = n_tar;
   if (c->debug) c->dbg.clear();
+  struct ProbeGuard {
+    explicit ProbeGuard(Probe* p) { g_probe = p; p->armed.clear(); }
+    ~ProbeGuard() { g_probe = nullptr; }
+  } probe_guard(&c->probe);
   c->g_fine.captures = 0;
   for (auto& gk : c->g_seg)
     for (auto& g : gk) g.captures = 0;
@@ -333,10 +337,10 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   // ---------------- host: growing + selection + select_base
   GrowOut g[2];
   std::vector<Base> base[2];
-  for (int k = 0; k < 2; ++k) {
+  c->pool.parallel_for(2, [&](int k) {  // the two clouds are independent
     g[k] = grow_and_select(vox[k].data(), (int)vox[k].size(), P);
     base[k] = select_base(g[k].planes, g[k].theta, P, k + 1);
-  }
+  });
   S.groups1 = (int64_t)g[0].groups.size();
   S.groups2 = (int64_t)g[1].groups.size();
   S.planes1 = (int64_t)g[0].planes.size();
@@ -594,6 +598,10 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     for (int j = 0; j < 4; ++j) T_out[4 * i + j] = T.m[i][j];
   S.ms[FCCF_T_FUSE] = ms_since(t0);
   S.ms_total = ms_since(t_all);
+  if (c->probe.on()) {
+    HIP_CHECK(hipDeviceSynchronize());
+    probe_collect(c->probe);
+  }
   S.graph_captures = c->g_fine.captures;
   for (auto& gk : c->g_seg)
     for (auto& g : gk) S.graph_captures += g.captures;

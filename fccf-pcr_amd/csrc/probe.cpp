@@ -1,0 +1,61 @@
+// probe.cpp — see probe.h.
+#include "probe.h"
+
+#include "ctx.h"
+
+namespace fccf {
+
+thread_local Probe* g_probe = nullptr;
+
+namespace {
+// Parks the stream until the host sets *flag (bounded: gives up after ~0.2 s so a
+// host-side failure can never hang the queue).
+__global__ void k_probe_gate(int* flag) {
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+    if (wall_clock64() - t0 > 20000000LL) break;  // 100 MHz wall clock
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+}  // namespace
+
+ProbeScope::ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_count, double per_unit,
+                       const uint32_t* d_count2, double per_unit2, double fixed) {
+  Probe* pr = g_probe;
+  if (!pr || !pr->on() || pr->target != kernel) return;
+  p = std::make_shared<ProbePair>();
+  HIP_CHECK(hipEventCreate(&p->a));
+  HIP_CHECK(hipEventCreate(&p->b));
+  HIP_CHECK(hipHostMalloc((void**)&p->gate, 64, hipHostMallocCoherent));
+  __atomic_store_n(p->gate, 0, __ATOMIC_RELEASE);
+  k_probe_gate<<<1, 1, 0, st>>>(p->gate);
+  p->d_count = d_count;
+  p->d_count2 = d_count2;
+  p->per_unit = per_unit;
+  p->per_unit2 = per_unit2;
+  p->fixed = fixed;
+  HIP_CHECK(hipEventRecord(p->a, st));
+}
+
+void ProbeScope::end(hipStream_t st) {
+  if (!p) return;
+  HIP_CHECK(hipEventRecord(p->b, st));
+  __atomic_store_n(p->gate, 1, __ATOMIC_RELEASE);  // release the stream
+  g_probe->armed.push_back(p);
+}
+
+void probe_collect(Probe& pr) {
+  for (auto& p : pr.armed) {
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, p->a, p->b));
+    uint32_t u1 = 0, u2 = 0;
+    if (p->d_count) HIP_CHECK(hipMemcpy(&u1, p->d_count, 4, hipMemcpyDeviceToHost));
+    if (p->d_count2) HIP_CHECK(hipMemcpy(&u2, p->d_count2, 4, hipMemcpyDeviceToHost));
+    pr.total_ms += ms;
+    pr.total_bytes += p->per_unit * u1 + p->per_unit2 * u2 + p->fixed;
+    ++pr.launches;
+  }
+  pr.armed.clear();
+}
+
+}  // namespace fccf

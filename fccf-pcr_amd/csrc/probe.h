@@ -1,0 +1,66 @@
+// probe.h — per-kernel HIP-event timing for the roofline report (bench.py).
+//
+// A ctx may name one kernel to probe (fccf_ctx_set_probe).  Launch sites of the
+// candidate kernels wrap their launch in FCCF_PROBED(...): when the name matches,
+// a pair of timing events is recorded on the launch stream around it.  HIP cannot
+// time events recorded inside a captured graph, so while a probe is on the device
+// stages launch eagerly (CachedGraph::run).  To keep host launch latency out of the
+// measurement, the stream is first parked on a gate kernel that spins on a pinned
+// host flag; the host releases it only after the opening event, the kernel and the
+// closing event are all enqueued.  After the call's streams are synchronised, each
+// pair adds (elapsed time, algorithmic bytes) to the ctx totals.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace fccf {
+
+struct ProbePair {
+  hipEvent_t a = nullptr, b = nullptr;
+  int* gate = nullptr;                  // pinned host flag the gate kernel waits on
+  const uint32_t* d_count = nullptr;   // device-resident unit counts (may be null)
+  const uint32_t* d_count2 = nullptr;
+  double per_unit = 0.0, per_unit2 = 0.0, fixed = 0.0;
+  ~ProbePair() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    if (gate) (void)hipHostFree(gate);
+  }
+};
+
+struct Probe {
+  std::string target;                              // kernel name; empty = off
+  std::vector<std::shared_ptr<ProbePair>> armed;   // pairs executed by the current call
+  double total_ms = 0.0, total_bytes = 0.0;
+  int64_t launches = 0;
+  bool on() const { return !target.empty(); }
+};
+
+// The probe of the ctx whose call is running on this thread (null outside calls).
+extern thread_local Probe* g_probe;
+
+struct ProbeScope {
+  std::shared_ptr<ProbePair> p;
+  ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_count, double per_unit,
+             const uint32_t* d_count2 = nullptr, double per_unit2 = 0.0, double fixed = 0.0);
+  void end(hipStream_t st);
+};
+
+// algorithmic bytes of one launch = per_unit * *d_count + per_unit2 * *d_count2 + fixed
+// Resolve armed pairs into totals (call after the streams are synchronised).
+void probe_collect(Probe& pr);
+
+}  // namespace fccf
+
+// FCCF_PROBED(name, stream, (d_count, per_unit[, d_count2, per_unit2, fixed]), launch)
+#define FCCF_PROBED(name, st, bytes, ...)                  \
+  do {                                                    \
+    ::fccf::ProbeScope _probe_scope(name, st, FCCF_UNPACK bytes); \
+    __VA_ARGS__;                                          \
+    _probe_scope.end(st);                                 \
+  } while (0)
+#define FCCF_UNPACK(...) __VA_ARGS__

@@ -77,6 +77,9 @@ _sig("fccf_device_free", ctypes.c_int, _P, _P)
 _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
 _sig("fccf_stage_centroid", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_stage_seqsum", ctypes.c_int, _P, _P, _I64, _P)
+_sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
+_sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
+     ctypes.POINTER(ctypes.c_double))
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
@@ -174,6 +177,16 @@ class Ctx:
         _check(_lib.fccf_stage_downsample(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data,
                                           ctypes.byref(m)), "fccf_stage_downsample")
         return out[: m.value].copy()
+
+    def set_probe(self, kernel):
+        """Time every launch of `kernel` with HIP events (None = off); resets totals."""
+        _check(_lib.fccf_ctx_set_probe(self._h, kernel.encode() if kernel else None), "fccf_ctx_set_probe")
+
+    def probe_read(self):
+        """(total_ms, launches, total_algorithmic_bytes) since set_probe."""
+        ms, n, b = ctypes.c_double(), _I64(), ctypes.c_double()
+        _check(_lib.fccf_probe_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "fccf_probe_read")
+        return ms.value, n.value, b.value
 
     def centroid(self, xyz):
         """compute3DCentroid (FCCF.cpp:473) of a dense cloud: float32[4] (x, y, z, 1)."""

@@ -126,6 +126,13 @@ int fccf_stage_centroid(fccf_ctx* ctx, const float* xyz, int64_t n, float out[4]
  * order of fine_verify's similar_num (FCCF.cpp:830-835); bit-exact. */
 int fccf_stage_seqsum(fccf_ctx* ctx, const float* x, int64_t n, float* out);
 
+/* Roofline probe (bench.py): time every launch of one kernel (by name, e.g.
+ * "k_vg_centroid") with HIP events on its own stream, also inside the captured
+ * graphs, and accumulate its algorithmic bytes ("Measurement").
+ * kernel NULL or "" switches the probe off.  Setting it resets the totals. */
+int fccf_ctx_set_probe(fccf_ctx* ctx, const char* kernel);
+int fccf_probe_read(fccf_ctx* ctx, double* total_ms, int64_t* launches, double* total_bytes);
+
 /* Named intermediate of the last fccf_register call with debug on (see DESIGN.md
  * "Debug names").  Copies min(cap_bytes, size) bytes; *n_bytes = full size. */
 int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes,
