@@ -48,7 +48,21 @@ __global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const
   const uint32_t n = *d_n;
   const uint32_t base = blockIdx.x * RS_TILE;
   const uint32_t end = min(base + (uint32_t)RS_TILE, n);
-  for (uint32_t i = base + threadIdx.x; i < end; i += T) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+  // one LDS atomic per distinct digit per 64 keys (ballot match), not per key:
+  // neighbouring keys share their high digits
+  for (uint32_t c0 = base; c0 < end; c0 += T) {
+    const uint32_t i = c0 + threadIdx.x;
+    const bool ok = i < end;
+    const uint32_t d = ok ? (uint32_t)(keys[i] >> shift) & 255u : 0u;
+    uint64_t m = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
+  }
   __syncthreads();
   hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }

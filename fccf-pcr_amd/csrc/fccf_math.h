@@ -85,6 +85,15 @@ FH float normal_cos(float x1, float y1, float z1, float x2, float y2, float z2) 
   return (float)((double)dp / (na * nb));
 }
 FH float normal_cos(f3 a, f3 b) { return normal_cos(a.x, a.y, a.z, b.x, b.y, b.z); }
+// normal_cos with both double norms precomputed (same bits: na = sqrt(a.a), nb = sqrt(b.b))
+FH double norm3d(float x, float y, float z) {
+  const double a0 = x, a1 = y, a2 = z;
+  return sqrt(dot3d(a0, a1, a2, a0, a1, a2));
+}
+FH float normal_cos_pre(float x1, float y1, float z1, double na, float x2, float y2, float z2, double nb) {
+  const float dp = (float)dot3d((double)x1, (double)y1, (double)z1, (double)x2, (double)y2, (double)z2);
+  return (float)((double)dp / (na * nb));
+}
 
 // theta(c) = float(double(acosf(c) * 180.f) / M_PI); acosf(c) := float(acos(double c)).
 // Host-only by policy: the device never evaluates acos, it compares c against the

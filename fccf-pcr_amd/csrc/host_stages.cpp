@@ -22,6 +22,7 @@ struct Group {
   std::vector<int> mem;             // voxel indices in voxelgrothnode order
   float s = 0, sc[3] = {0, 0, 0}, sn[3] = {0, 0, 0};  // running recompute sums
   float ac[3], an[3], fps;
+  double nan_ = 0;                  // norm3d(an), refreshed with the averages
   bool alloc = false;
 };
 
@@ -38,6 +39,7 @@ inline void set_avg(Group& g) {  // the recompute's averages (:580-586)
     g.ac[a] = g.sc[a] / g.s;
     g.an[a] = g.sn[a] / g.s;
   }
+  g.nan_ = norm3d(g.an[0], g.an[1], g.an[2]);
 }
 }  // namespace
 
@@ -47,6 +49,10 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
   std::vector<char> va(nv, 0);
   std::vector<Group> G;
   // stage 1 (:536-593): recompute-from-scratch == running sums in member order (App. B Q7)
+  // The predicate is `same && cop` with no side effects, so `cop` is evaluated only
+  // when `same` holds; voxel normal norms are computed once.
+  std::vector<double> vn(nv);
+  for (int j = 0; j < nv; ++j) vn[j] = norm3d(vox[j].n[0], vox[j].n[1], vox[j].n[2]);
   for (int i = 0; i < nv; ++i) {
     if (va[i]) continue;
     Group g;
@@ -55,14 +61,13 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
     add_member(g, vox[i]);
     g.fps = (float)vox[i].count;
     for (int a = 0; a < 3; ++a) { g.an[a] = vox[i].n[a]; g.ac[a] = vox[i].c[a]; }
+    g.nan_ = vn[i];
     for (int j = 0; j < nv; ++j) {
       if (va[j]) continue;
       const VoxRec& v = vox[j];
-      const bool same = !angle_gt(normal_cos(g.an[0], g.an[1], g.an[2], v.n[0], v.n[1], v.n[2]), cut1);
-      const bool cop = compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]},
-                                     f3{v.n[0], v.n[1], v.n[2]}, f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1,
-                                     P.parameter_k1);
-      if (same && cop) {
+      if (angle_gt(normal_cos_pre(g.an[0], g.an[1], g.an[2], g.nan_, v.n[0], v.n[1], v.n[2], vn[j]), cut1)) continue;
+      if (compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]}, f3{v.n[0], v.n[1], v.n[2]},
+                        f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1, P.parameter_k1)) {
         g.mem.push_back(j);
         va[j] = 1;
         add_member(g, v);
@@ -81,11 +86,10 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
         if (j == i || G[j].alloc) continue;
         Group& a = G[i];
         Group& b = G[j];
-        const bool same = !angle_gt(normal_cos(a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2]), cut2);
-        const bool cop = compare_plane(f3{a.an[0], a.an[1], a.an[2]}, f3{a.ac[0], a.ac[1], a.ac[2]},
-                                       f3{b.an[0], b.an[1], b.an[2]}, f3{b.ac[0], b.ac[1], b.ac[2]}, P.parameter_l2,
-                                       P.parameter_k2);
-        if (same && cop) {
+        if (angle_gt(normal_cos_pre(a.an[0], a.an[1], a.an[2], a.nan_, b.an[0], b.an[1], b.an[2], b.nan_), cut2))
+          continue;
+        if (compare_plane(f3{a.an[0], a.an[1], a.an[2]}, f3{a.ac[0], a.ac[1], a.ac[2]}, f3{b.an[0], b.an[1], b.an[2]},
+                          f3{b.ac[0], b.ac[1], b.ac[2]}, P.parameter_l2, P.parameter_k2)) {
           newadd = true;
           b.alloc = true;
           for (int m : b.mem) {

@@ -18,7 +18,7 @@ class Pool {
   explicit Pool(int n = 0) {
     if (n <= 0) {
       const char* e = std::getenv("FCCF_HOST_THREADS");
-      n = e ? std::atoi(e) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+      n = e ? std::atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     }
     for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
   }
