@@ -15,6 +15,11 @@ constexpr int RS_TILE = RS_THREADS * RS_CHUNKS;  // 2048 keys per block
 
 inline uint32_t rs_blocks(uint32_t cap) { return (cap + RS_TILE - 1) / RS_TILE; }
 
+// Radix sort tiles: 4096 keys per block (hist and scatter).
+constexpr int SORT_CHUNKS = 16;
+constexpr int SORT_TILE = RS_THREADS * SORT_CHUNKS;
+inline uint32_t sort_blocks(uint32_t cap) { return (cap + SORT_TILE - 1) / SORT_TILE; }
+
 // Scratch for radix_sort_pairs / segment_heads: hist needs 256*blocks u32,
 // tot 256 u32, blk blocks+1 u32.
 struct SortScratch {

@@ -46,8 +46,8 @@ __global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *d_n;
-  const uint32_t base = blockIdx.x * RS_TILE;
-  const uint32_t end = min(base + (uint32_t)RS_TILE, n);
+  const uint32_t base = blockIdx.x * SORT_TILE;
+  const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
   // one LDS atomic per distinct digit per 64 keys (ballot match), not per key:
   // neighbouring keys share their high digits
   for (uint32_t c0 = base; c0 < end; c0 += T) {
@@ -86,39 +86,47 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(uint32_t* __restrict__ hist, u
   if (threadIdx.x == 0) tot[d] = carry;
 }
 
+// Ranks a 4096-key tile (wave ballots), stages it in LDS in digit order, then
+// writes each digit run to its global slot with consecutive lanes on consecutive
+// addresses.  *active (probe, may be null) is cleared when the pass is skipped.
 template <class K>
 __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                   K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                   const uint32_t* __restrict__ d_n,
                                                   const uint32_t* __restrict__ d_nbits, int shift,
                                                   const uint32_t* __restrict__ hist,
-                                                  const uint32_t* __restrict__ tot, uint32_t nblocks, int iota) {
-  if ((uint32_t)shift >= *d_nbits) return;
-  __shared__ uint32_t dbase[256];
+                                                  const uint32_t* __restrict__ tot, uint32_t nblocks, int iota,
+                                                  uint32_t* __restrict__ active) {
+  const bool run = (uint32_t)shift < *d_nbits;
+  if (active && blockIdx.x == 0 && threadIdx.x == 0) *active = run ? 1u : 0u;
+  const uint32_t n = *d_n;
+  const uint32_t tile0 = blockIdx.x * SORT_TILE;
+  if (!run || tile0 >= n) return;  // grids are sized for the capacity; tiles past n are empty
+  __shared__ uint32_t gofs[256];     // global slot of the tile's first key of each digit
+  __shared__ uint32_t tex[256];      // exclusive digit offsets inside the tile
   __shared__ uint32_t wcnt[4][256];
   __shared__ uint32_t sh[4];
+  __shared__ K sk[SORT_TILE];
+  __shared__ uint32_t sv[SORT_TILE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   {
     uint32_t t;
-    dbase[tid] = block_scan_256(tot[tid], sh, &t);
+    gofs[tid] = block_scan_256(tot[tid], sh, &t) + hist[tid * nblocks + blockIdx.x];
   }
   for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
   __syncthreads();
-  const uint32_t n = *d_n;
-  const uint32_t base = blockIdx.x * RS_TILE + wave * (RS_CHUNKS * 64);
-  K kk[RS_CHUNKS];
-  uint32_t vv[RS_CHUNKS], rk[RS_CHUNKS], dg[RS_CHUNKS];
-  bool ok[RS_CHUNKS];
+  const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
+  K kk[SORT_CHUNKS];
+  uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
 #pragma unroll
-  for (int c = 0; c < RS_CHUNKS; ++c) {
+  for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t i = base + c * 64 + lane;
-    ok[c] = i < n;
-    kk[c] = ok[c] ? kin[i] : (K)0;
-    vv[c] = ok[c] ? (iota ? i : vin[i]) : 0u;
+    const bool ok = i < n;
+    kk[c] = ok ? kin[i] : (K)0;
+    vv[c] = ok ? (iota ? i : vin[i]) : 0u;
     const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
-    dg[c] = d;
-    const uint64_t valid = __ballot(ok[c]);
-    uint64_t m = valid;
+    dg[c] = ok ? d : 256u;
+    uint64_t m = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const bool bit = (d >> b) & 1u;
@@ -126,27 +134,38 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
       m &= bit ? bb : ~bb;
     }
     const uint32_t r = mbcnt(m);
-    const uint32_t pre = wcnt[wave][d];
+    const uint32_t pre = ok ? wcnt[wave][d] : 0u;
     rk[c] = pre + r;
-    if (ok[c] && r == 0) wcnt[wave][d] = pre + (uint32_t)__popcll(m);
+    if (ok && r == 0) wcnt[wave][d] = pre + (uint32_t)__popcll(m);
   }
   __syncthreads();
-  {
-    uint32_t s = 0;
+  {  // per-wave offsets within a digit, tile digit totals, their exclusive scan
+    uint32_t acc = 0;
     for (int w = 0; w < 4; ++w) {
       const uint32_t t = wcnt[w][tid];
-      wcnt[w][tid] = s;
-      s += t;
+      wcnt[w][tid] = acc;
+      acc += t;
     }
+    uint32_t t;
+    tex[tid] = block_scan_256(acc, sh, &t);
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < RS_CHUNKS; ++c) {
-    if (!ok[c]) continue;
+  for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t d = dg[c];
-    const uint32_t pos = dbase[d] + hist[d * nblocks + blockIdx.x] + wcnt[wave][d] + rk[c];
-    kout[pos] = kk[c];
-    vout[pos] = vv[c];
+    if (d > 255u) continue;
+    const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
+    sk[lp] = kk[c];
+    sv[lp] = vv[c];
+  }
+  __syncthreads();
+  const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
+  for (uint32_t j = tid; j < m; j += T) {
+    const K k = sk[j];
+    const uint32_t d = (uint32_t)(k >> shift) & 255u;
+    const uint32_t pos = gofs[d] + (j - tex[d]);
+    kout[pos] = k;
+    vout[pos] = sv[j];
   }
 }
 
@@ -166,7 +185,7 @@ __global__ void k_rs_copyback(const K* __restrict__ k1, const uint32_t* __restri
 template <class K>
 void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
                 const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
-  const uint32_t nb = rs_blocks(cap);
+  const uint32_t nb = sort_blocks(cap);
   if (nb == 0) return;
   const int max_passes = (max_bits + 7) / 8;
   K* kb[2] = {k0, k1};
@@ -177,8 +196,8 @@ void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, u
     k_rs_hist<K><<<nb, T, 0, st>>>(kb[src], d_n, d_nbits, shift, s.hist, nb);
     k_rs_rowscan<<<256, T, 0, st>>>(s.hist, nb, s.tot, d_nbits, shift);
     FCCF_PROBED("k_rs_scatter", st, (d_n, 2.0 * (sizeof(K) + 4)),
-                k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb,
-                                                  (iota && p == 0) ? 1 : 0));
+                k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist,
+                                                  s.tot, nb, (iota && p == 0) ? 1 : 0, _probe_scope.active()));
   }
   const uint32_t g = min(nb * 8u, 2048u);
   k_rs_copyback<K><<<g, 256, 0, st>>>(k1, v1, k0, v0, d_n, d_nbits, max_passes);

@@ -18,33 +18,45 @@
 namespace fccf {
 namespace {
 
-constexpr uint32_t INV_U32 = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------- octree bounds
+// Two-level aggregates of the finite points: per 4096-point block and per 64-point
+// sub-block.  One workgroup per block; wave w reduces sub-blocks w, w+4, ...
 // Batched over blockIdx.y = sequence e.
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
-                                                    float* __restrict__ aggr0, size_t xyz_stride,
-                                                    size_t aggr_stride) {
+                                                    float* __restrict__ aggr0, size_t xyz_stride, size_t aggr_stride,
+                                                    uint32_t nbc) {
   __shared__ float sh[4][6];
   const uint32_t n = *d_n;
   const float* xyz = xyz0 + blockIdx.y * xyz_stride;
   float* aggr = aggr0 + blockIdx.y * aggr_stride;
-  const uint32_t b0 = blockIdx.x * AGGR_BLOCK, b1 = min(b0 + AGGR_BLOCK, n);
-  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += 256) {
-    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    if (!finite3(x, y, z)) continue;
-    mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
-    mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
-  }
-  for (int a = 0; a < 3; ++a)
-    for (int o = 32; o > 0; o >>= 1) {
-      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
-      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+  float* sub = aggr + 6 * (size_t)nbc;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (uint32_t sb = w; sb < AGGR_BLOCK / AGGR_SUB; sb += 4) {
+    const uint32_t i = blockIdx.x * AGGR_BLOCK + sb * AGGR_SUB + lane;
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (i < n) {
+      const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+      if (finite3(x, y, z)) {
+        mn[0] = mx[0] = x;
+        mn[1] = mx[1] = y;
+        mn[2] = mx[2] = z;
+      }
     }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0)
-    for (int a = 0; a < 3; ++a) { sh[w][a] = mn[a]; sh[w][3 + a] = mx[a]; }
+    for (int a = 0; a < 3; ++a)
+      for (int o = 32; o > 0; o >>= 1) {
+        mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+        mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+      }
+    if (lane < 6) sub[6 * ((size_t)blockIdx.x * (AGGR_BLOCK / AGGR_SUB) + sb) + lane] = lane < 3 ? mn[lane] : mx[lane - 3];
+    for (int a = 0; a < 3; ++a) {
+      bmn[a] = fminf(bmn[a], mn[a]);
+      bmx[a] = fmaxf(bmx[a], mx[a]);
+    }
+  }
+  if (lane == 0)
+    for (int a = 0; a < 3; ++a) { sh[w][a] = bmn[a]; sh[w][3 + a] = bmx[a]; }
   __syncthreads();
   if (threadIdx.x < 6) {
     const int a = threadIdx.x;
@@ -54,57 +66,81 @@ __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xy
   }
 }
 
+struct Box6 {
+  float v[6];
+};
+
+__device__ __forceinline__ Box6 load_box(const float* a, bool ok) {
+  Box6 b;
+  for (int k = 0; k < 6; ++k) b.v[k] = ok ? a[k] : (k < 3 ? INFINITY : -INFINITY);
+  return b;
+}
+
+// a non-empty record some point of which may lie outside the current bounds
+__device__ __forceinline__ bool may_violate(const OctState& S, const Box6& b) {
+  if (!(b.v[0] <= b.v[3])) return false;  // no finite point
+  return !S.defined || !oct_inside(S, b.v[0], b.v[1], b.v[2]) || !oct_inside(S, b.v[3], b.v[4], b.v[5]);
+}
+
 // Replays adoptBoundingBoxToPoint over xyz[0..n) in order, starting from *state.
-// Batched over blockIdx.x = sequence e: xyz + e*xyz_stride, aggr + e*aggr_stride, state[e].
-__global__ void __launch_bounds__(1024) k_oct_sim(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
-                                                  const float* __restrict__ aggr0, double res,
-                                                  OctState* __restrict__ state0, size_t xyz_stride,
-                                                  size_t aggr_stride) {
-  __shared__ OctState S;
-  __shared__ uint32_t first_pt, first_blk;
-  const uint32_t tid = threadIdx.x;
+// One wave per sequence (blockIdx.x = e): block records, then the 64 sub-records of
+// a candidate block, then the 64 points of a candidate sub-block sit one per lane;
+// after each adoption the lanes re-test what they hold with one ballot, so memory is
+// touched only when the wave moves to a new block or sub-block, and every lane
+// replays the adoption itself (the state stays uniform without broadcasts).
+__global__ void __launch_bounds__(64) k_oct_sim(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
+                                                const float* __restrict__ aggr0, double res,
+                                                OctState* __restrict__ state0, size_t xyz_stride,
+                                                size_t aggr_stride, uint32_t nbc) {
+  const uint32_t lane = threadIdx.x;
   const uint32_t n = *d_n;
   const float* xyz = xyz0 + blockIdx.x * xyz_stride;
   const float* aggr = aggr0 + blockIdx.x * aggr_stride;
+  const float* sub = aggr + 6 * (size_t)nbc;
   OctState* state = state0 + blockIdx.x;
+  OctState S = *state;
   const uint32_t nblk = (n + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  if (tid == 0) S = *state;
-  __syncthreads();
-  uint32_t cur = 0;
-  while (cur < n) {
-    if (tid == 0) { first_pt = INV_U32; first_blk = INV_U32; }
-    __syncthreads();
-    const uint32_t blk = cur / AGGR_BLOCK;
-    const uint32_t bend = min((blk + 1) * AGGR_BLOCK, n);
-    for (uint32_t i = cur + tid; i < bend; i += 1024) {
-      const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-      if (finite3(x, y, z) && (!S.defined || !oct_inside(S, x, y, z))) atomicMin(&first_pt, i);
-    }
-    __syncthreads();
-    uint32_t fp = first_pt;
-    if (fp == INV_U32) {
-      for (uint32_t b = blk + 1 + tid; b < nblk; b += 1024) {
-        const float* a = aggr + 6 * b;
-        const bool nonempty = a[0] <= a[3];
-        if (nonempty && (!S.defined || !oct_inside(S, a[0], a[1], a[2]) || !oct_inside(S, a[3], a[4], a[5])))
-          atomicMin(&first_blk, b);
+  uint32_t pos = 0;  // points before pos are done
+  for (uint32_t bb = 0; bb < nblk; bb += 64) {
+    const uint32_t myb = bb + lane;
+    const Box6 A = load_box(aggr + 6 * (size_t)myb, myb < nblk);
+    while (true) {
+      const bool cb = myb < nblk && (myb + 1) * AGGR_BLOCK > pos && may_violate(S, A);
+      const uint64_t mb = __ballot(cb);
+      if (!mb) break;
+      const uint32_t fb = bb + (uint32_t)__builtin_ctzll(mb);
+      const uint32_t mys = fb * (AGGR_BLOCK / AGGR_SUB) + lane;
+      const Box6 B = load_box(sub + 6 * (size_t)mys, true);
+      while (true) {
+        const bool cs = (mys + 1) * AGGR_SUB > pos && may_violate(S, B);
+        const uint64_t ms = __ballot(cs);
+        if (!ms) break;
+        const uint32_t s0 = (fb * (AGGR_BLOCK / AGGR_SUB) + (uint32_t)__builtin_ctzll(ms)) * AGGR_SUB;
+        const uint32_t i = s0 + lane;
+        float p[3] = {0.f, 0.f, 0.f};
+        if (i < n) {
+          p[0] = xyz[3 * (size_t)i];
+          p[1] = xyz[3 * (size_t)i + 1];
+          p[2] = xyz[3 * (size_t)i + 2];
+        }
+        while (true) {
+          const bool cp = i >= pos && i < n && finite3(p[0], p[1], p[2]) && (!S.defined || !oct_inside(S, p[0], p[1], p[2]));
+          const uint64_t mp = __ballot(cp);
+          if (!mp) {
+            pos = s0 + AGGR_SUB;
+            break;
+          }
+          const int f = __builtin_ctzll(mp);
+          float q[3];
+          for (int a = 0; a < 3; ++a) q[a] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[a]), f));
+          oct_adopt(S, res, q);
+          pos = s0 + (uint32_t)f + 1;
+        }
       }
-      __syncthreads();
-      const uint32_t fb = first_blk;
-      __syncthreads();
-      if (fb == INV_U32) break;
-      cur = fb * AGGR_BLOCK;
-      continue;
+      pos = max(pos, (fb + 1) * AGGR_BLOCK);
     }
-    if (tid == 0) {
-      const float p[3] = {xyz[3 * fp], xyz[3 * fp + 1], xyz[3 * fp + 2]};
-      oct_adopt(S, res, p);
-    }
-    __syncthreads();
-    cur = fp + 1;
   }
-  __syncthreads();
-  if (tid == 0) *state = S;
+  if (lane == 0) *state = S;
 }
 
 __global__ void __launch_bounds__(256) k_oct_codes(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
@@ -336,14 +372,13 @@ void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs x
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
                 size_t xyz_stride, size_t aggr_stride) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, xyz_stride, aggr_stride);
+  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, xyz_stride, aggr_stride, aggr_blocks(cap));
 }
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
                 hipStream_t st, int batch, size_t xyz_stride, size_t aggr_stride) {
-  (void)cap;
   FCCF_PROBED("k_oct_sim", st, (d_n, 24.0 * batch / AGGR_BLOCK),
-              k_oct_sim<<<batch, 1024, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride));
+              k_oct_sim<<<batch, 64, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride, aggr_blocks(cap)));
 }
 
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,

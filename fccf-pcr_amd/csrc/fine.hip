@@ -153,8 +153,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
                        hipStream_t st) {
   if (E <= 0) return;
-  const uint32_t nb2 = (n2 + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  const size_t astride = 6 * (size_t)(nb2 ? nb2 : 1);
+  const size_t astride = aggr_floats(n2);
   k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t);
   k_fv_init<<<1, 64, 0, st>>>(b.state, E, b.scal, n1, n2);
   // scal[4], scal[5] hold n1, n2 for the device-count interfaces

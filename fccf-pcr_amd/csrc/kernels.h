@@ -49,7 +49,7 @@ struct FaceBufs {
   uint64_t *c0, *c1;       // codes, cap each
   uint32_t *v0, *v1;       // cap each
   uint32_t* starts;        // cap + 1
-  float* aggr;             // per 1024-point block: min xyz, max xyz (6 floats)
+  float* aggr;             // octree-bounds aggregates, aggr_floats(cap) (see block_aggr)
   OctState* oct;
   float* centroid;         // 4 floats
   XsBufs xs;               // centroid sum scratch (3 rows)
@@ -85,6 +85,11 @@ void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res,
                 OctState* state, hipStream_t st, int batch = 1, size_t xyz_stride = 0, size_t aggr_stride = 0);
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
                 size_t xyz_stride = 0, size_t aggr_stride = 0);
-constexpr uint32_t AGGR_BLOCK = 4096;
+constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
+constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
+// aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per
+// block; a record is the finite points' min xyz, max xyz (empty: min > max)
+inline uint32_t aggr_blocks(uint32_t cap) { return (cap + AGGR_BLOCK - 1) / AGGR_BLOCK + 1; }
+inline size_t aggr_floats(uint32_t cap) { return 6 * (size_t)aggr_blocks(cap) * (1 + AGGR_BLOCK / AGGR_SUB); }
 
 }  // namespace fccf

@@ -131,7 +131,7 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   b += 12 * N * 3 + 8 * N + 64;                                // ds1, ds1f, ds2, flags, offsets
   b += voxel_grid_bytes(cap);                                  // K1
   b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
-  b += 6 * 4 * ((N + AGGR_BLOCK - 1) / AGGR_BLOCK + 1) + 256;  // aggregates, state, centroid
+  b += 4 * aggr_floats(cap) + 256;                             // aggregates, state, centroid
   b += sizeof(VoxRec) * N + 4 * 4 * N + 64;                    // leaf records, flags, offsets
   b += 12 * N + 4 * N;                                         // sorted points, leaf of point
   b += sizeof(VoxRec) * N + 12 * N;                            // planar out, residual out
@@ -156,7 +156,7 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   f.v0 = a.take_n<uint32_t>(cap);
   f.v1 = a.take_n<uint32_t>(cap);
   f.starts = a.take_n<uint32_t>((size_t)cap + 1);
-  f.aggr = a.take_n<float>(6 * ((size_t)(cap + AGGR_BLOCK - 1) / AGGR_BLOCK + 1));
+  f.aggr = a.take_n<float>(aggr_floats(cap));
   f.oct = a.take_n<OctState>(1);
   f.centroid = a.take_n<float>(4);
   f.xs = exact_sum_carve(a.take(exact_sum_bytes(3, cap)), 3, cap);
@@ -506,8 +506,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   if (E > 0) {
     const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
     const size_t nk = (size_t)E * (n1 + n2);
-    const size_t nb2 = (n2 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1, nb1 = (n1 + AGGR_BLOCK - 1) / AGGR_BLOCK + 1;
-    const size_t need = 12 * (size_t)E * n2 + 24 * (nb1 + E * nb2) + sizeof(OctState) * (E + 1) +
+    const size_t af1 = aggr_floats(n1), af2 = aggr_floats(n2);
+    const size_t need = 12 * (size_t)E * n2 + 4 * (af1 + E * af2) + sizeof(OctState) * (E + 1) +
                         (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
                         sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256 +
                         exact_sum_bytes(E, n1 + n2) + 256;
@@ -515,8 +515,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     c->arena3.reset();
     FineBufs fb;
     fb.s2t = c->arena3.take_n<float>(3 * (size_t)E * n2);
-    fb.aggr1 = c->arena3.take_n<float>(6 * nb1);
-    fb.aggr2 = c->arena3.take_n<float>(6 * (size_t)E * nb2);
+    fb.aggr1 = c->arena3.take_n<float>(af1);
+    fb.aggr2 = c->arena3.take_n<float>((size_t)E * af2);
     fb.state = c->arena3.take_n<OctState>(E + 1);
     fb.k0 = c->arena3.take_n<uint64_t>(nk);
     fb.k1 = c->arena3.take_n<uint64_t>(nk);

@@ -23,10 +23,17 @@ ProbeScope::ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_cou
                        const uint32_t* d_count2, double per_unit2, double fixed) {
   Probe* pr = g_probe;
   if (!pr || !pr->on() || pr->target != kernel) return;
-  p = std::make_shared<ProbePair>();
-  HIP_CHECK(hipEventCreate(&p->a));
-  HIP_CHECK(hipEventCreate(&p->b));
-  HIP_CHECK(hipHostMalloc((void**)&p->gate, 64, hipHostMallocCoherent));
+  if (!pr->spare.empty()) {
+    p = pr->spare.back();
+    pr->spare.pop_back();
+  } else {
+    p = std::make_shared<ProbePair>();
+    HIP_CHECK(hipEventCreate(&p->a));
+    HIP_CHECK(hipEventCreate(&p->b));
+    HIP_CHECK(hipHostMalloc((void**)&p->gate, 64, hipHostMallocCoherent));
+    HIP_CHECK(hipMalloc((void**)&p->d_active, 4));
+  }
+  HIP_CHECK(hipMemsetAsync(p->d_active, 0xFF, 4, st));  // active unless the kernel says otherwise
   __atomic_store_n(p->gate, 0, __ATOMIC_RELEASE);
   k_probe_gate<<<1, 1, 0, st>>>(p->gate);
   p->d_count = d_count;
@@ -48,7 +55,10 @@ void probe_collect(Probe& pr) {
   for (auto& p : pr.armed) {
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, p->a, p->b));
-    uint32_t u1 = 0, u2 = 0;
+    uint32_t act = 1, u1 = 0, u2 = 0;
+    HIP_CHECK(hipMemcpy(&act, p->d_active, 4, hipMemcpyDeviceToHost));
+    pr.spare.push_back(p);
+    if (!act) continue;  // the kernel skipped its work (e.g. a radix pass past the key width)
     if (p->d_count) HIP_CHECK(hipMemcpy(&u1, p->d_count, 4, hipMemcpyDeviceToHost));
     if (p->d_count2) HIP_CHECK(hipMemcpy(&u2, p->d_count2, 4, hipMemcpyDeviceToHost));
     pr.total_ms += ms;

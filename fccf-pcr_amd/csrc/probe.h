@@ -22,6 +22,7 @@ namespace fccf {
 struct ProbePair {
   hipEvent_t a = nullptr, b = nullptr;
   int* gate = nullptr;                  // pinned host flag the gate kernel waits on
+  uint32_t* d_active = nullptr;         // device word: a kernel may clear it when it skipped its work
   const uint32_t* d_count = nullptr;   // device-resident unit counts (may be null)
   const uint32_t* d_count2 = nullptr;
   double per_unit = 0.0, per_unit2 = 0.0, fixed = 0.0;
@@ -29,12 +30,14 @@ struct ProbePair {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
     if (gate) (void)hipHostFree(gate);
+    if (d_active) (void)hipFree(d_active);
   }
 };
 
 struct Probe {
   std::string target;                              // kernel name; empty = off
   std::vector<std::shared_ptr<ProbePair>> armed;   // pairs executed by the current call
+  std::vector<std::shared_ptr<ProbePair>> spare;   // reusable pairs
   double total_ms = 0.0, total_bytes = 0.0;
   int64_t launches = 0;
   bool on() const { return !target.empty(); }
@@ -48,6 +51,9 @@ struct ProbeScope {
   ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_count, double per_unit,
              const uint32_t* d_count2 = nullptr, double per_unit2 = 0.0, double fixed = 0.0);
   void end(hipStream_t st);
+  // device word the probed kernel may set to 0 when it had nothing to do (the
+  // launch is then left out of the totals); null when this launch is not probed
+  uint32_t* active() const { return p ? p->d_active : nullptr; }
 };
 
 // algorithmic bytes of one launch = per_unit * *d_count + per_unit2 * *d_count2 + fixed
