@@ -48,12 +48,17 @@ __global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const
   const uint32_t n = *d_n;
   const uint32_t base = blockIdx.x * SORT_TILE;
   const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
-  // one LDS atomic per distinct digit per 64 keys (ballot match), not per key:
-  // neighbouring keys share their high digits
-  for (uint32_t c0 = base; c0 < end; c0 += T) {
-    const uint32_t i = c0 + threadIdx.x;
-    const bool ok = i < end;
-    const uint32_t d = ok ? (uint32_t)(keys[i] >> shift) & 255u : 0u;
+  // all 16 loads of the tile are issued before any is consumed (clamped indices,
+  // no branches), then one LDS atomic per distinct digit per 64 keys (ballot
+  // match): neighbouring keys share their high digits
+  K kk[SORT_CHUNKS];
+  const uint32_t last = n ? n - 1u : 0u;
+#pragma unroll
+  for (int c = 0; c < SORT_CHUNKS; ++c) kk[c] = keys[min(base + c * T + threadIdx.x, last)];
+#pragma unroll
+  for (int c = 0; c < SORT_CHUNKS; ++c) {
+    const bool ok = base + c * T + threadIdx.x < end;
+    const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
     uint64_t m = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -118,12 +123,17 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
   const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
   K kk[SORT_CHUNKS];
   uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
+  const uint32_t last = n - 1u;  // n > tile0 >= 0
+#pragma unroll
+  for (int c = 0; c < SORT_CHUNKS; ++c) {  // all loads in flight before the ranking
+    const uint32_t i = min(base + c * 64 + lane, last);
+    kk[c] = kin[i];
+    vv[c] = iota ? i : vin[i];
+  }
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t i = base + c * 64 + lane;
     const bool ok = i < n;
-    kk[c] = ok ? kin[i] : (K)0;
-    vv[c] = ok ? (iota ? i : vin[i]) : 0u;
     const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
     dg[c] = ok ? d : 256u;
     uint64_t m = __ballot(ok);
@@ -195,21 +205,32 @@ void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, u
     const int src = p & 1, dst = src ^ 1;
     k_rs_hist<K><<<nb, T, 0, st>>>(kb[src], d_n, d_nbits, shift, s.hist, nb);
     k_rs_rowscan<<<256, T, 0, st>>>(s.hist, nb, s.tot, d_nbits, shift);
-    FCCF_PROBED("k_rs_scatter", st, (d_n, 2.0 * (sizeof(K) + 4)),
-                k_rs_scatter<K><<<nb, T, 0, st>>>(kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist,
-                                                  s.tot, nb, (iota && p == 0) ? 1 : 0, _probe_scope.active()));
+    FCCF_LAUNCH("k_rs_scatter", (d_n, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, nb, T, 0, st, kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb, (iota && p == 0) ? 1 : 0, _probe.active());
   }
   const uint32_t g = min(nb * 8u, 2048u);
   k_rs_copyback<K><<<g, 256, 0, st>>>(k1, v1, k0, v0, d_n, d_nbits, max_passes);
 }
 
 // ---------------------------------------------------------------- segments / scan
+// keys[i0-1 .. i0+RS_CHUNKS] into registers, all loads issued before use
+// (clamped indices; positions outside [0, n) are masked by the callers)
+template <class K>
+__device__ __forceinline__ void load_run(const K* keys, uint32_t i0, uint32_t n, K kk[RS_CHUNKS + 2]) {
+  const uint32_t last = n ? n - 1u : 0u;
+#pragma unroll
+  for (int j = 0; j < RS_CHUNKS + 2; ++j) {
+    // kk[j] = keys[i0 - 1 + j]; for i0 == 0 the wrapped index clamps to `last`, and
+    // kk[0] is then never read (position 0 is always a head)
+    kk[j] = keys[min(i0 + (uint32_t)j - 1u, last)];
+  }
+}
+
 template <class K, bool HasInvalid>
-__device__ __forceinline__ bool is_head(const K* keys, uint32_t i, uint32_t n, K invalid) {
+__device__ __forceinline__ bool head_at(const K kk[RS_CHUNKS + 2], int j, uint32_t i, uint32_t n, K invalid) {
   if (i >= n) return false;
-  const K k = keys[i];
+  const K k = kk[j + 1];
   if (HasInvalid && k == invalid) return false;
-  return i == 0 || keys[i - 1] != k;
+  return i == 0 || kk[j] != k;
 }
 
 template <class K, bool HasInvalid>
@@ -218,8 +239,11 @@ __global__ void __launch_bounds__(T) k_seg_count(const K* __restrict__ keys, con
   __shared__ uint32_t sh[4];
   const uint32_t n = *d_n;
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  K kk[RS_CHUNKS + 2];
+  load_run<K>(keys, i0, n, kk);
   uint32_t c = 0;
-  for (int j = 0; j < RS_CHUNKS; ++j) c += is_head<K, HasInvalid>(keys, i0 + j, n, invalid) ? 1u : 0u;
+#pragma unroll
+  for (int j = 0; j < RS_CHUNKS; ++j) c += head_at<K, HasInvalid>(kk, j, i0 + j, n, invalid) ? 1u : 0u;
   uint32_t t;
   block_scan_256(c, sh, &t);
   if (threadIdx.x == 0) blk[blockIdx.x] = t;
@@ -250,22 +274,26 @@ __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, con
   __shared__ uint32_t sh[4];
   const uint32_t n = *d_n;
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  K kk[RS_CHUNKS + 2];
+  load_run<K>(keys, i0, n, kk);
   bool h[RS_CHUNKS];
   uint32_t c = 0;
+#pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
-    h[j] = is_head<K, HasInvalid>(keys, i0 + j, n, invalid);
+    h[j] = head_at<K, HasInvalid>(kk, j, i0 + j, n, invalid);
     c += h[j] ? 1u : 0u;
   }
   uint32_t t;
   uint32_t pos = blk[blockIdx.x] + block_scan_256(c, sh, &t);
+#pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
     const uint32_t i = i0 + j;
     if (h[j]) starts[pos++] = i;
     // end of the valid prefix: close the last segment
     if (i < n) {
-      const bool valid = !HasInvalid || keys[i] != invalid;
+      const bool valid = !HasInvalid || kk[j + 1] != invalid;
       if (seg_of && valid) seg_of[i] = pos - 1;
-      const bool next_valid = (i + 1 < n) && (!HasInvalid || keys[i + 1] != invalid);
+      const bool next_valid = (i + 1 < n) && (!HasInvalid || kk[j + 2] != invalid);
       if (valid && !next_valid) starts[pos] = i + 1;  // pos == segment count here
     }
   }

@@ -76,13 +76,20 @@ __device__ __forceinline__ Prob prob_of(const float* data, int S, const uint32_t
 // lane's 4 consecutive inputs of chunk c, components k < K (non-finite allowed)
 template <int S>
 __device__ __forceinline__ void load4(const Prob& P, uint32_t c, int lane, int K, float v[4][S], bool ok[4]) {
+  // all loads issued before use: clamped indices (P.n >= 1 whenever a chunk exists)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t i = c * XS_L + lane * 4 + j;
     ok[j] = i < P.n;
+    const size_t ic = min(i, P.n - 1u);
 #pragma unroll
-    for (int k = 0; k < S; ++k) v[j][k] = (ok[j] && k < K) ? P.base[(size_t)i * S + k] : 0.f;
+    for (int k = 0; k < S; ++k) v[j][k] = P.base[ic * S + k];
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < S; ++k)
+      if (!ok[j] || k >= K) v[j][k] = 0.f;
 }
 
 template <int S>
@@ -359,19 +366,15 @@ void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint3
   if (S == 3) {
     k_xs_csum<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    FCCF_PROBED("k_xs_chunk", st, (cnt, 4.0 * 3),
-                k_xs_chunk<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC));
+    FCCF_LAUNCH("k_xs_chunk", (cnt, 4.0 * 3), k_xs_chunk<3>, gc, 256, 0, st, data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
     k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_PROBED("k_xs_chain", st, (cnt, 4.0 * 3),
-                k_xs_chain<3><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide));
+    FCCF_LAUNCH("k_xs_chain", (cnt, 4.0 * 3), k_xs_chain<3>, rows, 64, 0, st, data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
   } else {
     k_xs_csum<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    FCCF_PROBED("k_xs_chunk", st, (cnt, 4.0 * 1),
-                k_xs_chunk<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC));
+    FCCF_LAUNCH("k_xs_chunk", (cnt, 4.0 * 1), k_xs_chunk<1>, gc, 256, 0, st, data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
     k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_PROBED("k_xs_chain", st, (cnt, 4.0 * 1),
-                k_xs_chain<1><<<rows, 64, 0, st>>>(data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide));
+    FCCF_LAUNCH("k_xs_chain", (cnt, 4.0 * 1), k_xs_chain<1>, rows, 64, 0, st, data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
   }
 }
 

@@ -21,7 +21,9 @@ namespace {
 
 // ---------------------------------------------------------------- octree bounds
 // Two-level aggregates of the finite points: per 4096-point block and per 64-point
-// sub-block.  One workgroup per block; wave w reduces sub-blocks w, w+4, ...
+// sub-block.  One workgroup per block; four threads per sub-block, 16 consecutive
+// points each (all loads issued before use), quad shuffles for the sub-record,
+// then the wave / block reduction for the block record.
 // Batched over blockIdx.y = sequence e.
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
                                                     float* __restrict__ aggr0, size_t xyz_stride, size_t aggr_stride,
@@ -31,35 +33,45 @@ __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xy
   const float* xyz = xyz0 + blockIdx.y * xyz_stride;
   float* aggr = aggr0 + blockIdx.y * aggr_stride;
   float* sub = aggr + 6 * (size_t)nbc;
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (uint32_t sb = w; sb < AGGR_BLOCK / AGGR_SUB; sb += 4) {
-    const uint32_t i = blockIdx.x * AGGR_BLOCK + sb * AGGR_SUB + lane;
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    if (i < n) {
-      const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-      if (finite3(x, y, z)) {
-        mn[0] = mx[0] = x;
-        mn[1] = mx[1] = y;
-        mn[2] = mx[2] = z;
-      }
-    }
-    for (int a = 0; a < 3; ++a)
-      for (int o = 32; o > 0; o >>= 1) {
-        mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
-        mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
-      }
-    if (lane < 6) sub[6 * ((size_t)blockIdx.x * (AGGR_BLOCK / AGGR_SUB) + sb) + lane] = lane < 3 ? mn[lane] : mx[lane - 3];
+  const uint32_t t = threadIdx.x, sb = t >> 2, q = t & 3, lane = t & 63, w = t >> 6;
+  const uint32_t p0 = blockIdx.x * AGGR_BLOCK + sb * AGGR_SUB + q * 16;
+  const uint32_t last = n ? n - 1u : 0u;
+  float v[16][3];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const size_t i = min(p0 + k, last);
+    v[k][0] = xyz[3 * i];
+    v[k][1] = xyz[3 * i + 1];
+    v[k][2] = xyz[3 * i + 2];
+  }
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (p0 + k >= n || !finite3(v[k][0], v[k][1], v[k][2])) continue;
     for (int a = 0; a < 3; ++a) {
-      bmn[a] = fminf(bmn[a], mn[a]);
-      bmx[a] = fmaxf(bmx[a], mx[a]);
+      mn[a] = fminf(mn[a], v[k][a]);
+      mx[a] = fmaxf(mx[a], v[k][a]);
     }
   }
+  for (int o = 1; o < 4; o <<= 1)  // the four threads of a sub-block
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
+  if (q == 0) {
+    float* r = sub + 6 * ((size_t)blockIdx.x * (AGGR_BLOCK / AGGR_SUB) + sb);
+    for (int a = 0; a < 3; ++a) { r[a] = mn[a]; r[3 + a] = mx[a]; }
+  }
+  for (int o = 4; o < 64; o <<= 1)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+    }
   if (lane == 0)
-    for (int a = 0; a < 3; ++a) { sh[w][a] = bmn[a]; sh[w][3 + a] = bmx[a]; }
+    for (int a = 0; a < 3; ++a) { sh[w][a] = mn[a]; sh[w][3 + a] = mx[a]; }
   __syncthreads();
-  if (threadIdx.x < 6) {
-    const int a = threadIdx.x;
+  if (t < 6) {
+    const int a = t;
     float r = sh[0][a];
     for (int ww = 1; ww < 4; ++ww) r = a < 3 ? fminf(r, sh[ww][a]) : fmaxf(r, sh[ww][a]);
     aggr[6 * blockIdx.x + a] = r;
@@ -377,8 +389,7 @@ void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
                 hipStream_t st, int batch, size_t xyz_stride, size_t aggr_stride) {
-  FCCF_PROBED("k_oct_sim", st, (d_n, 24.0 * batch / AGGR_BLOCK),
-              k_oct_sim<<<batch, 64, 0, st>>>(xyz, d_n, aggr, res, state, xyz_stride, aggr_stride, aggr_blocks(cap)));
+  FCCF_LAUNCH("k_oct_sim", (d_n, 24.0 * batch / AGGR_BLOCK), k_oct_sim, batch, 64, 0, st, xyz, d_n, aggr, res, state, xyz_stride, aggr_stride, aggr_blocks(cap));
 }
 
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
@@ -389,16 +400,13 @@ void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, do
   k_oct_codes<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.oct, res, b.c0, b.nbits);
   radix_sort_u64(b.c0, b.v0, b.c1, b.v1, d_n, cap, b.nbits, 64, true, b.ss, st);
   segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st, b.seg_of);
-  FCCF_PROBED("k_gather", st, (d_n, 28.0),
-              k_gather<<<grid_for(cap), 256, 0, st>>>(xyz, b.v0, d_n, b.sp));
+  FCCF_LAUNCH("k_gather", (d_n, 28.0), k_gather, grid_for(cap), 256, 0, st, xyz, b.v0, d_n, b.sp);
 }
 
 void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, float* resid_out,
                      FaceBufs b, hipStream_t st) {
   (void)xyz;
-  FCCF_PROBED("k_voxel_fit", st, (d_n, 12.0, b.nleaf, (double)sizeof(VoxRec) + 12.0),
-              k_voxel_fit<<<grid_for(cap, 4, 4096), 256, 0, st>>>(b.sp, b.starts, b.nleaf, vpt, cthr, b.recs,
-                                                                  b.flag_planar, b.resid_cnt));
+  FCCF_LAUNCH("k_voxel_fit", (d_n, 12.0, b.nleaf, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, grid_for(cap, 4, 4096), 256, 0, st, b.sp, b.starts, b.nleaf, vpt, cthr, b.recs, b.flag_planar, b.resid_cnt);
   exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
   exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
   k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);

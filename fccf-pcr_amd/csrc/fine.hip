@@ -171,8 +171,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
   (void)hipMemsetAsync(b.range, 0, sizeof(uint32_t) * 2 * MAX_EVAL, st);
-  FCCF_PROBED("k_fv_counts", st, (b.scal, 16.0, b.scal + 2, 12.0),
-              k_fv_counts<<<grid_for(n), 256, 0, st>>>(b.k0, b.k1, b.starts, b.scal, b.term, b.range));
+  FCCF_LAUNCH("k_fv_counts", (b.scal, 16.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.k1, b.starts, b.scal, b.term, b.range);
   k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
   k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E);

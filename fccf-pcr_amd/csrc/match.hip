@@ -219,11 +219,9 @@ void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, 
                       MCand* c[3], QTd* q[3], hipStream_t st) {
   if (K <= 0) return;
   const int g = (K + 3) / 4;  // one wave per test
-  FCCF_PROBED("k_match_count", st, (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)),
-              k_match_count<<<g, 256, 0, st>>>(d_in, cnt, type));
+  FCCF_LAUNCH("k_match_count", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_count, g, 256, 0, st, d_in, cnt, type);
   k_match_scan<<<1, 256, 0, st>>>(d_in, cnt, type, off, totals);
-  FCCF_PROBED("k_match_emit", st, (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)),
-              k_match_emit<<<g, 256, 0, st>>>(d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]));
+  FCCF_LAUNCH("k_match_emit", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_emit, g, 256, 0, st, d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]);
 }
 
 }  // namespace fccf

@@ -7,17 +7,6 @@ namespace fccf {
 
 thread_local Probe* g_probe = nullptr;
 
-namespace {
-// Parks the stream until the host sets *flag (bounded: gives up after ~0.2 s so a
-// host-side failure can never hang the queue).
-__global__ void k_probe_gate(int* flag) {
-  const long long t0 = wall_clock64();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
-    if (wall_clock64() - t0 > 20000000LL) break;  // 100 MHz wall clock
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-}  // namespace
 
 ProbeScope::ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_count, double per_unit,
                        const uint32_t* d_count2, double per_unit2, double fixed) {
@@ -30,24 +19,19 @@ ProbeScope::ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_cou
     p = std::make_shared<ProbePair>();
     HIP_CHECK(hipEventCreate(&p->a));
     HIP_CHECK(hipEventCreate(&p->b));
-    HIP_CHECK(hipHostMalloc((void**)&p->gate, 64, hipHostMallocCoherent));
     HIP_CHECK(hipMalloc((void**)&p->d_active, 4));
   }
   HIP_CHECK(hipMemsetAsync(p->d_active, 0xFF, 4, st));  // active unless the kernel says otherwise
-  __atomic_store_n(p->gate, 0, __ATOMIC_RELEASE);
-  k_probe_gate<<<1, 1, 0, st>>>(p->gate);
   p->d_count = d_count;
   p->d_count2 = d_count2;
   p->per_unit = per_unit;
   p->per_unit2 = per_unit2;
   p->fixed = fixed;
-  HIP_CHECK(hipEventRecord(p->a, st));
 }
 
 void ProbeScope::end(hipStream_t st) {
   if (!p) return;
-  HIP_CHECK(hipEventRecord(p->b, st));
-  __atomic_store_n(p->gate, 1, __ATOMIC_RELEASE);  // release the stream
+  (void)st;
   g_probe->armed.push_back(p);
 }
 

@@ -1,15 +1,15 @@
 // probe.h — per-kernel HIP-event timing for the roofline report (bench.py).
 //
-// A ctx may name one kernel to probe (fccf_ctx_set_probe).  Launch sites of the
-// candidate kernels wrap their launch in FCCF_PROBED(...): when the name matches,
-// a pair of timing events is recorded on the launch stream around it.  HIP cannot
-// time events recorded inside a captured graph, so while a probe is on the device
-// stages launch eagerly (CachedGraph::run).  To keep host launch latency out of the
-// measurement, the stream is first parked on a gate kernel that spins on a pinned
-// host flag; the host releases it only after the opening event, the kernel and the
-// closing event are all enqueued.  After the call's streams are synchronised, each
-// pair adds (elapsed time, algorithmic bytes) to the ctx totals.
+// A ctx may name one kernel to probe (fccf_ctx_set_probe).  Candidate kernels are
+// launched through FCCF_LAUNCH(...): when the name matches, the launch goes through
+// hipExtLaunchKernelGGL with a start and a stop event, which the runtime stamps
+// from the kernel's own dispatch (the interval the profiler reports, without the
+// queue latency that separate hipEventRecord markers would add).  HIP cannot time
+// events inside a captured graph, so while a probe is on the device stages launch
+// eagerly (CachedGraph::run).  After the call's streams are synchronised, each pair
+// adds (elapsed time, algorithmic bytes) to the ctx totals.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -20,8 +20,7 @@
 namespace fccf {
 
 struct ProbePair {
-  hipEvent_t a = nullptr, b = nullptr;
-  int* gate = nullptr;                  // pinned host flag the gate kernel waits on
+  hipEvent_t a = nullptr, b = nullptr;  // start / stop of the kernel's dispatch
   uint32_t* d_active = nullptr;         // device word: a kernel may clear it when it skipped its work
   const uint32_t* d_count = nullptr;   // device-resident unit counts (may be null)
   const uint32_t* d_count2 = nullptr;
@@ -29,7 +28,6 @@ struct ProbePair {
   ~ProbePair() {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
-    if (gate) (void)hipHostFree(gate);
     if (d_active) (void)hipFree(d_active);
   }
 };
@@ -62,11 +60,16 @@ void probe_collect(Probe& pr);
 
 }  // namespace fccf
 
-// FCCF_PROBED(name, stream, (d_count, per_unit[, d_count2, per_unit2, fixed]), launch)
-#define FCCF_PROBED(name, st, bytes, ...)                  \
-  do {                                                    \
-    ::fccf::ProbeScope _probe_scope(name, st, FCCF_UNPACK bytes); \
-    __VA_ARGS__;                                          \
-    _probe_scope.end(st);                                 \
+// FCCF_LAUNCH(name, (d_count, per_unit[, d_count2, per_unit2, fixed]), kernel, grid, block, shmem, stream,
+//             args...)  -- kernel<<<grid, block, shmem, stream>>>(args...), timed when probed.
+// Arguments may use _probe.active() (null unless this launch is probed).
+#define FCCF_LAUNCH(name, bytes, kernel, grid, block, shmem, st, ...)                               \
+  do {                                                                                             \
+    ::fccf::ProbeScope _probe(name, st, FCCF_UNPACK bytes);                                        \
+    if (_probe.p)                                                                                  \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, _probe.p->a, _probe.p->b, 0, __VA_ARGS__); \
+    else                                                                                           \
+      kernel<<<grid, block, shmem, st>>>(__VA_ARGS__);                                             \
+    _probe.end(st);                                                                                \
   } while (0)
 #define FCCF_UNPACK(...) __VA_ARGS__

@@ -169,12 +169,10 @@ void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf,
                 hipStream_t st) {
   k_vg_bbox<<<VG_BBOX_BLOCKS, 256, 0, st>>>(xyz, d_n, b.part);
   k_vg_params<<<1, 64, 0, st>>>(b.part, VG_BBOX_BLOCKS, leaf, b.params);
-  FCCF_PROBED("k_vg_keys", st, (d_n, 16.0),
-              k_vg_keys<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.params, b.k0));
+  FCCF_LAUNCH("k_vg_keys", (d_n, 16.0), k_vg_keys, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.k0);
   radix_sort_u32(b.k0, b.v0, b.k1, b.v1, d_n, cap, &b.params->nbits, 32, true, b.ss, st);
   segment_heads_u32(b.k0, d_n, cap, 0xFFFFFFFFu, b.starts, b.nseg, b.ss, st);
-  FCCF_PROBED("k_vg_centroid", st, (d_n, 16.0, d_m, 12.0),
-              k_vg_centroid<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.params, b.v0, b.starts, b.nseg, out, d_m));
+  FCCF_LAUNCH("k_vg_centroid", (d_n, 16.0, d_m, 12.0), k_vg_centroid, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.v0, b.starts, b.nseg, out, d_m);
 }
 
 }  // namespace fccf
