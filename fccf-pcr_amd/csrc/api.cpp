@@ -57,10 +57,15 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   fccf_ctx* c = new fccf_ctx();
   c->device = device;
   if (hipSetDevice(device) != hipSuccess) { delete c; return FCCF_E_HIP; }
-  for (auto& s : c->st)
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { delete c; return FCCF_E_HIP; }
-  for (auto& e : c->ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { delete c; return FCCF_E_HIP; }
+  bool ok = hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
+  for (auto& cs : c->cs) {
+    for (auto& s : cs.st) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) {
+    fccf_ctx_destroy(c);
+    return FCCF_E_HIP;
+  }
   *out = c;
   return FCCF_OK;
 }
@@ -68,13 +73,18 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
 extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   if (!c) return FCCF_E_ARG;
   (void)hipSetDevice(c->device);
-  for (auto& gk : c->g_seg)
-    for (auto& g : gk) g.reset();
+  (void)hipDeviceSynchronize();
+  pipeline_release(c);
   c->g_fine.reset();
-  for (auto& s : c->st)
-    if (s) (void)hipStreamDestroy(s);
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& cs : c->cs) {
+    for (auto& gk : cs.g_seg)
+      for (auto& g : gk) g.reset();
+    for (auto& s : cs.st)
+      if (s) (void)hipStreamDestroy(s);
+    for (auto& e : cs.ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  if (c->sb) (void)hipStreamDestroy(c->sb);
   delete c;
   return FCCF_OK;
 }
@@ -132,14 +142,14 @@ static int guarded(fccf_ctx* c, F&& f) {
 extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out, int64_t* m) {
   if (!c || (!xyz && n) || !out || !m || n < 0 || n > (int64_t)0x7FFFFFFF || !(leaf > 0.f)) return FCCF_E_ARG;
   return guarded(c, [&] {
-    hipStream_t st = c->st[0];
+    hipStream_t st = c->sb;
     const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
-    c->arena.ensure(voxel_grid_bytes(cap) + 12 * (size_t)cap * 2 + (1 << 20));
-    c->arena.reset();
-    float* d_in = c->arena.take_n<float>(3 * (size_t)cap);
-    float* d_out = c->arena.take_n<float>(3 * (size_t)cap);
-    uint32_t* d_sc = c->arena.take_n<uint32_t>(64);
-    VGBufs b = voxel_grid_carve(c->arena, cap);
+    c->arena2.ensure(voxel_grid_bytes(cap) + 12 * (size_t)cap * 2 + (1 << 20));
+    c->arena2.reset();
+    float* d_in = c->arena2.take_n<float>(3 * (size_t)cap);
+    float* d_out = c->arena2.take_n<float>(3 * (size_t)cap);
+    uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
+    VGBufs b = voxel_grid_carve(c->arena2, cap);
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
@@ -159,14 +169,14 @@ namespace {
 int stage_sum(fccf_ctx* c, const float* x, int64_t n, int S, bool divide, float* out) {
   if (!c || (!x && n) || !out || n < 0 || n > (int64_t)0x7FFFFFFF) return FCCF_E_ARG;
   return guarded(c, [&] {
-    hipStream_t st = c->st[0];
+    hipStream_t st = c->sb;
     const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
-    c->arena.ensure(4 * (size_t)S * cap + exact_sum_bytes(S, cap) + (1 << 16));
-    c->arena.reset();
-    float* d_in = c->arena.take_n<float>((size_t)S * cap);
-    uint32_t* d_sc = c->arena.take_n<uint32_t>(64);
-    float* d_out = c->arena.take_n<float>(4);
-    XsBufs xs = exact_sum_carve(c->arena.take(exact_sum_bytes(S, cap)), S, cap);
+    c->arena2.ensure(4 * (size_t)S * cap + exact_sum_bytes(S, cap) + (1 << 16));
+    c->arena2.reset();
+    float* d_in = c->arena2.take_n<float>((size_t)S * cap);
+    uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
+    float* d_out = c->arena2.take_n<float>(4);
+    XsBufs xs = exact_sum_carve(c->arena2.take(exact_sum_bytes(S, cap)), S, cap);
     uint32_t hn = (uint32_t)n;
     if (n) HIP_CHECK(hipMemcpyAsync(d_in, x, 4 * (size_t)S * n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));

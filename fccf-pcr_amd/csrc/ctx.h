@@ -126,12 +126,18 @@ struct CachedGraph {
 
 struct fccf_ctx {
   int device = 0;
-  hipStream_t st[4] = {nullptr, nullptr, nullptr, nullptr};  // [0,1] per-cloud main, [2,3] side
-  hipEvent_t ev[8] = {};  // [0..3] per-cloud side-stream joins, [4..7] graph fork/join
-  fccf::CachedGraph g_seg[2][3];  // per cloud: downsample, centroid, faces (pipeline.cpp)
-  fccf::CachedGraph g_fine;    // fine-verify batch (K7)
-  fccf::Arena arena;   // per-cloud buffers
-  fccf::Arena arena2;  // matching
+  // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
+  // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
+  struct CloudSet {
+    fccf::Arena arena;
+    hipStream_t st[4] = {};          // [0,1] per-cloud main, [2,3] side
+    hipEvent_t ev[6] = {};           // [0..3] per-cloud side joins, [4] fork / clouds done, [5] join
+    fccf::CachedGraph g_seg[2][3];   // per cloud: downsample, centroid, faces (pipeline.cpp)
+    void* ws = nullptr;              // pipeline.cpp state of the registration in flight
+  } cs[2];
+  hipStream_t sb = nullptr;          // matching, fine verification, copies, stage exports
+  fccf::CachedGraph g_fine;          // fine-verify batch (K7)
+  fccf::Arena arena2;  // matching (and the stage exports)
   fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
   fccf::Pool pool;

@@ -412,6 +412,13 @@ void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float 
   k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);
 }
 
+void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
+                   hipStream_t st) {
+  k_oct_reset<<<1, 1, 0, st>>>(state);
+  block_aggr(xyz, d_n, cap, aggr, st);
+  octree_sim(xyz, d_n, cap, res, aggr, state, st);
+}
+
 void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_t st) {
   k_compact_planar<<<grid_for(cap), 256, 0, st>>>(b.nleaf, b.recs, b.flag_planar, b.planar_off, b.centroid,
                                                   planar_out);

@@ -26,28 +26,21 @@ __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ 
   }
 }
 
-__global__ void k_fv_init(OctState* st, int E, uint32_t* scal, uint32_t n1, uint32_t n2) {
-  // st[E] := undefined; after the S1 replay it is copied to st[0..E)
-  if (threadIdx.x == 0) {
+// every evaluation's octree starts from the bounds after S1 (the fused cloud is S1 ++ T_e S2)
+__global__ void k_fv_init(const OctState* __restrict__ s1_state, OctState* st, int E, uint32_t* scal, uint32_t n1,
+                          uint32_t n2) {
+  const int e = threadIdx.x;
+  if (e < E) st[e] = *s1_state;
+  if (e == 0) {
     scal[4] = n1;
     scal[5] = n2;
     scal[7] = 0u;
-    OctState z;
-    for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
-    z.depth = 0;
-    z.defined = 0;
-    st[E] = z;
   }
 }
 
-__global__ void k_fv_fork(OctState* st, int E) {
-  const int e = threadIdx.x;
-  if (e < E) st[e] = st[E];
-}
-
 // scal: [0] total keys, [1] nbits, [3] shift = 3*Dmax+1, [4] n1, [5] n2, [6] E
-__global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict__ scal, uint32_t n1, uint32_t n2,
-                          int E) {
+__global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict__ scal, uint32_t* __restrict__ range,
+                          uint32_t n1, uint32_t n2, int E) {
   if (threadIdx.x != 0) return;
   uint32_t D = 0;
   for (int e = 0; e < E; ++e)
@@ -56,6 +49,7 @@ __global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict_
   while ((1u << eb) <= (uint32_t)E) ++eb;
   scal[0] = (uint32_t)E * (n1 + n2);
   scal[2] = 0u;  // segment count (stays 0 when there are no keys)
+  for (int i = 0; i < 2 * MAX_EVAL; ++i) range[i] = 0u;
   scal[3] = 3u * D + 1u;
   scal[1] = 3u * D + 1u + eb;
   scal[4] = n1;
@@ -150,27 +144,22 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
-                       hipStream_t st) {
+void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
+                       double res, FineBufs b, hipStream_t st) {
   if (E <= 0) return;
   const size_t astride = aggr_floats(n2);
   k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t);
-  k_fv_init<<<1, 64, 0, st>>>(b.state, E, b.scal, n1, n2);
-  // scal[4], scal[5] hold n1, n2 for the device-count interfaces
-  uint32_t* d_n1 = b.scal + 4;
+  k_fv_init<<<1, 64, 0, st>>>(s1_state, b.state, E, b.scal, n1, n2);
+  // scal[5] holds n2 for the device-count interfaces
   uint32_t* d_n2 = b.scal + 5;
-  block_aggr(s1, d_n1, n1, b.aggr1, st);
-  octree_sim(s1, d_n1, n1, res, b.aggr1, b.state + E, st);
-  k_fv_fork<<<1, 64, 0, st>>>(b.state, E);
   block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, 3 * (size_t)n2, astride);
   octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, 3 * (size_t)n2, astride);
-  k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, n1, n2, E);
+  k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, n1, n2, E);
   const uint32_t n = (uint32_t)E * (n1 + n2);
   k_fv_keys<<<dim3(grid_for(n1 + n2, 256, 1024), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0);
   radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 64, true, b.ss, st);
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
-  (void)hipMemsetAsync(b.range, 0, sizeof(uint32_t) * 2 * MAX_EVAL, st);
   FCCF_LAUNCH("k_fv_counts", (b.scal, 16.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.k1, b.starts, b.scal, b.term, b.range);
   k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order

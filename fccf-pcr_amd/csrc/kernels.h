@@ -83,6 +83,9 @@ void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_
 // sequence; `batch` sequences at xyz + e*xyz_stride with state[e]).
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr,
                 OctState* state, hipStream_t st, int batch = 1, size_t xyz_stride = 0, size_t aggr_stride = 0);
+// Fresh octree bounds replayed over xyz[0..*d_n) (aggr: aggr_floats(cap) floats).
+void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
+                   hipStream_t st);
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
                 size_t xyz_stride = 0, size_t aggr_stride = 0);
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate

@@ -33,7 +33,6 @@ void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, 
 constexpr int MAX_EVAL = 16;
 struct FineBufs {
   float* s2t;          // E * n2 * 3
-  float* aggr1;        // aggregates of S1
   float* aggr2;        // E * blocks(n2) * 6
   OctState* state;     // E + 1 (slot E = after S1)
   uint64_t *k0, *k1;   // E * (n1 + n2)
@@ -50,7 +49,9 @@ struct FineBufs {
   SortScratch ss;
   XsBufs xs;           // similar_num sum scratch (E rows, cap n1 + n2)
 };
-void fine_verify_batch(const float* s1, uint32_t n1, const float* s2, uint32_t n2, int E, double res, FineBufs b,
+// s1_state: octree bounds after inserting S1 alone (octree_replay, run ahead of time).
+void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
+                       double res, FineBufs b,
                        hipStream_t st);
 
 }  // namespace fccf

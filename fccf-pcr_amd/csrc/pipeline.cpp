@@ -122,6 +122,8 @@ struct CloudWS {
   FaceBufs fb;
   VoxRec* planar = nullptr;
   float* resid = nullptr;
+  float* faggr = nullptr;        // fine_verify S1 bounds replay (cloud 0 only)
+  OctState* fstate = nullptr;
 };
 
 size_t cloud_bytes(uint32_t cap, bool host_input) {
@@ -135,6 +137,7 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   b += sizeof(VoxRec) * N + 4 * 4 * N + 64;                    // leaf records, flags, offsets
   b += 12 * N + 4 * N;                                         // sorted points, leaf of point
   b += sizeof(VoxRec) * N + 12 * N;                            // planar out, residual out
+  b += 4 * aggr_floats(cap) + 512;                             // fine-verify S1 bounds replay
   b += sort_scratch_bytes(cap) + 64 * 256;                     // sort scratch + alignment slack
   b += exact_sum_bytes(3, cap) + 256;                          // centroid sum tables
   return b;
@@ -175,6 +178,8 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
   w.planar = a.take_n<VoxRec>(cap);
   w.resid = a.take_n<float>(3 * (size_t)cap);
+  w.faggr = a.take_n<float>(aggr_floats(cap));
+  w.fstate = a.take_n<OctState>(1);
 }
 
 // Device part of one cloud, in three stream segments (each replayed as a graph):
@@ -190,9 +195,13 @@ void seg_downsample(CloudWS& w, float leaf, hipStream_t st) {
   voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st);  // driver :1377-1387
 }
 void seg_centroid(CloudWS& w, hipStream_t side) { cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, w.fb.xs, side); }
-void seg_faces(CloudWS& w, const fccf_params& P, hipStream_t st) {
+void seg_faces(CloudWS& w, const fccf_params& P, hipStream_t st, bool s1) {
   face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
   face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.resid, w.fb, st);
+  // the residual cloud of the driver source is fine_verify's S1 (:788-805): its
+  // octree bounds do not depend on any candidate, so they are replayed here,
+  // overlapping the host stages that produce the candidates
+  if (s1) octree_replay(w.resid, w.fb.nresid, w.cap, (double)P.fine_verify_voxel_size, w.faggr, w.fstate, st);
 }
 
 template <class T>
@@ -216,36 +225,44 @@ void dump_planes(fccf_ctx* c, const std::string& k, const std::vector<Plane>& F)
 
 }  // namespace
 
-void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
-                  float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
-  fccf_stats S;
-  std::memset(&S, 0, sizeof S);
-  S.n_src = n_src;
-  S.n_tar = n_tar;
-  if (c->debug) c->dbg.clear();
-  struct ProbeGuard {
-    explicit ProbeGuard(Probe* p) { g_probe = p; p->armed.clear(); }
-    ~ProbeGuard() { g_probe = nullptr; }
-  } probe_guard(&c->probe);
-  c->g_fine.captures = 0;
-  for (auto& gk : c->g_seg)
-    for (auto& g : gk) g.captures = 0;
-  const auto t_all = clk::now();
-  auto t0 = clk::now();
-  hipStream_t st0 = c->st[0], st1 = c->st[1];
-  // cloud 0 = driver source = TAR file; cloud 1 = driver target = SRC file (:1683)
+namespace {
+
+// State of the registration whose clouds occupy CloudSet s.
+struct PipeSet {
   CloudWS w[2];
-  const int64_t nin[2] = {n_tar, n_src};
+  int64_t nin[2] = {0, 0};
+  uint32_t cap[2] = {1, 1};
+  clk::time_point t_enq;
+};
+
+PipeSet& pset(fccf_ctx* c, int s) {
+  if (!c->cs[s].ws) c->cs[s].ws = new PipeSet();
+  return *(PipeSet*)c->cs[s].ws;
+}
+
+// Phase A: stage the inputs and enqueue the cloud device stage of one pair on
+// CloudSet s (returns at once).  cloud 0 = driver source = TAR file; cloud 1 =
+// driver target = SRC file (:1683).
+void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
+                    bool on_device, float leaf, const fccf_params& P) {
+  auto& cs = c->cs[s];
+  PipeSet& ps = pset(c, s);
+  ps.t_enq = clk::now();
+  CloudWS* w = ps.w;
+  ps.nin[0] = n_tar;
+  ps.nin[1] = n_src;
   const float* hin[2] = {tar, src};
-  const uint32_t cap[2] = {(uint32_t)std::max<int64_t>(nin[0], 1), (uint32_t)std::max<int64_t>(nin[1], 1)};
-  c->arena.ensure(cloud_bytes(cap[0], true) + cloud_bytes(cap[1], true) + (1 << 20));
-  c->arena.reset();
+  for (int k = 0; k < 2; ++k) ps.cap[k] = (uint32_t)std::max<int64_t>(ps.nin[k], 1);
+  hipStream_t st0 = cs.st[0], st1 = cs.st[1];
+  cs.arena.ensure(cloud_bytes(ps.cap[0], true) + cloud_bytes(ps.cap[1], true) + (1 << 20));
+  cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
-  // clouds) so the captured graph never depends on caller pointers.
-  uint32_t* hn = (uint32_t*)c->pinned.get(64);
+  // clouds) so the captured graphs never depend on caller pointers.
+  uint32_t* hn = (uint32_t*)c->pinned.get(64) + 8 * s;
   for (int k = 0; k < 2; ++k) {
-    carve_cloud(c->arena, w[k], cap[k], true);
-    const uint32_t n = (uint32_t)nin[k];
+    w[k] = CloudWS();
+    carve_cloud(cs.arena, w[k], ps.cap[k], true);
+    const uint32_t n = (uint32_t)ps.nin[k];
     if (n)
       HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n,
                                on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st0));
@@ -257,26 +274,46 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     const void* base;
     size_t acap;
     uint32_t cap0, cap1;
-    float leaf, fvs, vpt, ct;
-  } key = {c->arena.base, c->arena.cap, cap[0], cap[1], leaf, P.face_voxel_size, P.voxel_point_threshold,
-           P.curvature_threshold};
+    float leaf, fvs, vpt, ct, fine_res;
+  } key = {cs.arena.base, cs.arena.cap, ps.cap[0], ps.cap[1], leaf, P.face_voxel_size, P.voxel_point_threshold,
+           P.curvature_threshold, P.fine_verify_voxel_size};
   // st0 -> st1 fork (the staging copies above are on st0)
-  HIP_CHECK(hipEventRecord(c->ev[4], st0));
-  HIP_CHECK(hipStreamWaitEvent(st1, c->ev[4], 0));
+  HIP_CHECK(hipEventRecord(cs.ev[4], st0));
+  HIP_CHECK(hipStreamWaitEvent(st1, cs.ev[4], 0));
   for (int k = 0; k < 2; ++k) {
-    hipStream_t sm = c->st[k], ss = c->st[2 + k];
-    c->g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
-    HIP_CHECK(hipEventRecord(c->ev[2 * k], sm));
-    HIP_CHECK(hipStreamWaitEvent(ss, c->ev[2 * k], 0));
-    c->g_seg[k][1].run(&key, sizeof key, ss, [&] { seg_centroid(w[k], ss); });
-    HIP_CHECK(hipEventRecord(c->ev[2 * k + 1], ss));
-    c->g_seg[k][2].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm); });
-    HIP_CHECK(hipStreamWaitEvent(sm, c->ev[2 * k + 1], 0));
+    hipStream_t sm = cs.st[k], ss = cs.st[2 + k];
+    cs.g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
+    HIP_CHECK(hipEventRecord(cs.ev[2 * k], sm));
+    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[2 * k], 0));
+    cs.g_seg[k][1].run(&key, sizeof key, ss, [&] { seg_centroid(w[k], ss); });
+    HIP_CHECK(hipEventRecord(cs.ev[2 * k + 1], ss));
+    cs.g_seg[k][2].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm, k == 0); });
+    HIP_CHECK(hipStreamWaitEvent(sm, cs.ev[2 * k + 1], 0));
     face_voxels_orient(w[k].cap, w[k].planar, w[k].fb, sm);
   }
-  HIP_CHECK(hipEventRecord(c->ev[5], st1));  // join
-  HIP_CHECK(hipStreamWaitEvent(st0, c->ev[5], 0));
+  HIP_CHECK(hipEventRecord(cs.ev[5], st1));  // join
+  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[5], 0));
+  HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
   HIP_CHECK(hipGetLastError());
+}
+
+// Phase B: everything after the cloud stage of the pair on CloudSet s, on c->sb.
+// after_clouds() runs as soon as the cloud stage has completed (the batch driver
+// enqueues the next pair's clouds there).
+template <class AfterClouds>
+void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_stats* stats,
+                     AfterClouds&& after_clouds) {
+  fccf_stats S;
+  std::memset(&S, 0, sizeof S);
+  PipeSet& ps = pset(c, s);
+  CloudWS* w = ps.w;
+  S.n_src = ps.nin[1];
+  S.n_tar = ps.nin[0];
+  if (c->debug) c->dbg.clear();
+  const auto t_all = ps.t_enq;
+  auto t0 = ps.t_enq;
+  hipStream_t st0 = c->sb;
+  HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[4], 0));
   // counts of both clouds
   uint32_t sc[2][4], fsc[2][4];
   for (int k = 0; k < 2; ++k) {
@@ -284,8 +321,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     HIP_CHECK(hipMemcpyAsync(fsc[k], w[k].fb.nleaf, 16, hipMemcpyDeviceToHost, st0));
   }
   HIP_CHECK(hipStreamSynchronize(st0));
-  HIP_CHECK(hipStreamSynchronize(st1));
   S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
+  after_clouds();
   t0 = clk::now();
   S.m_tar = sc[0][3];
   S.m_src = sc[1][3];
@@ -298,15 +335,15 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     const char* dsn[2] = {"ds_tar", "ds_src"};
     for (int k = 0; k < 2; ++k) {
       const std::string s = std::to_string(k + 1);
-      auto a = d2h(w[k].ds1, 3 * (size_t)sc[k][1], c->st[k]);
-      auto b = d2h(w[k].ds2, 3 * (size_t)sc[k][3], c->st[k]);
-      auto ce = d2h(w[k].fb.centroid, 4, c->st[k]);
-      auto oc = d2h(w[k].fb.oct, 1, c->st[k]);
-      auto recs = d2h(w[k].fb.recs, fsc[k][0], c->st[k]);
-      auto pl = d2h(w[k].fb.flag_planar, fsc[k][0], c->st[k]);
-      auto rc = d2h(w[k].fb.resid_cnt, fsc[k][0], c->st[k]);
-      auto res = d2h(w[k].resid, 3 * (size_t)fsc[k][3], c->st[k]);
-      HIP_CHECK(hipStreamSynchronize(c->st[k]));
+      auto a = d2h(w[k].ds1, 3 * (size_t)sc[k][1], st0);
+      auto b = d2h(w[k].ds2, 3 * (size_t)sc[k][3], st0);
+      auto ce = d2h(w[k].fb.centroid, 4, st0);
+      auto oc = d2h(w[k].fb.oct, 1, st0);
+      auto recs = d2h(w[k].fb.recs, fsc[k][0], st0);
+      auto pl = d2h(w[k].fb.flag_planar, fsc[k][0], st0);
+      auto rc = d2h(w[k].fb.resid_cnt, fsc[k][0], st0);
+      auto res = d2h(w[k].resid, 3 * (size_t)fsc[k][3], st0);
+      HIP_CHECK(hipStreamSynchronize(st0));
       c->dbg_put(dsn[k], a);
       c->dbg_put("ds" + s, b);
       ce[3] = 1.f;  // Eigen::Vector4f centroid[3] (unused by the algorithm)
@@ -506,8 +543,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   if (E > 0) {
     const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
     const size_t nk = (size_t)E * (n1 + n2);
-    const size_t af1 = aggr_floats(n1), af2 = aggr_floats(n2);
-    const size_t need = 12 * (size_t)E * n2 + 4 * (af1 + E * af2) + sizeof(OctState) * (E + 1) +
+    const size_t af2 = aggr_floats(n2);
+    const size_t need = 12 * (size_t)E * n2 + 4 * E * af2 + sizeof(OctState) * (E + 1) +
                         (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
                         sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256 +
                         exact_sum_bytes(E, n1 + n2) + 256;
@@ -515,7 +552,6 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     c->arena3.reset();
     FineBufs fb;
     fb.s2t = c->arena3.take_n<float>(3 * (size_t)E * n2);
-    fb.aggr1 = c->arena3.take_n<float>(af1);
     fb.aggr2 = c->arena3.take_n<float>((size_t)E * af2);
     fb.state = c->arena3.take_n<OctState>(E + 1);
     fb.k0 = c->arena3.take_n<uint64_t>(nk);
@@ -538,13 +574,14 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     struct {
       const void* base;
       size_t acap;
-      const void *r1, *r2;
+      const void *r1, *r2, *s1state;
       uint32_t n1, n2;
       int32_t E;
       float res;
-    } fkey = {c->arena3.base, c->arena3.cap, w[0].resid, w[1].resid, n1, n2, E, P.fine_verify_voxel_size};
+    } fkey = {c->arena3.base, c->arena3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E,
+              P.fine_verify_voxel_size};
     c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
-      fine_verify_batch(w[0].resid, n1, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
+      fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
     });
     HIP_CHECK(hipGetLastError());
     uint32_t ferr = 0;
@@ -603,7 +640,7 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     probe_collect(c->probe);
   }
   S.graph_captures = c->g_fine.captures;
-  for (auto& gk : c->g_seg)
+  for (auto& gk : c->cs[s].g_seg)
     for (auto& g : gk) S.graph_captures += g.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
@@ -618,6 +655,54 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     c->dbg_put("counts", counts);
   }
   if (stats) *stats = S;
+}
+
+void reset_capture_counts(fccf_ctx* c) {
+  c->g_fine.captures = 0;
+  for (auto& cs : c->cs)
+    for (auto& gk : cs.g_seg)
+      for (auto& g : gk) g.captures = 0;
+}
+
+struct ProbeGuard {
+  explicit ProbeGuard(Probe* p) {
+    g_probe = p;
+    p->armed.clear();
+  }
+  ~ProbeGuard() { g_probe = nullptr; }
+};
+
+}  // namespace
+
+void pipeline_release(fccf_ctx* c) {
+  for (auto& cs : c->cs) {
+    delete (PipeSet*)cs.ws;
+    cs.ws = nullptr;
+  }
+}
+
+void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
+                  float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
+  ProbeGuard probe_guard(&c->probe);
+  reset_capture_counts(c);
+  clouds_enqueue(c, 0, src, n_src, tar, n_tar, on_device, leaf, P);
+  register_finish(c, 0, P, T_out, stats, [] {});
+}
+
+void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src, const float* const* tar,
+                        const int64_t* n_tar, bool on_device, float leaf, const fccf_params& P, float* T_out,
+                        fccf_stats* stats) {
+  if (n <= 0) return;
+  ProbeGuard probe_guard(&c->probe);
+  reset_capture_counts(c);
+  clouds_enqueue(c, 0, src[0], n_src[0], tar[0], n_tar[0], on_device, leaf, P);
+  for (int i = 0; i < n; ++i) {
+    const int s = i & 1;
+    register_finish(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
+      // the next pair's cloud stage overlaps this pair's later stages
+      if (i + 1 < n) clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+    });
+  }
 }
 
 }  // namespace fccf
@@ -663,4 +748,16 @@ extern "C" int fccf_register_device(fccf_ctx* c, const float* d_src, int64_t ns,
   if (params) P = *params;
   else fccf_params_default(&P);
   return guarded2(c, [&] { run_register(c, d_src, ns, d_tar, nt, true, leaf, P, T, stats); });
+}
+
+extern "C" int fccf_register_batch(fccf_ctx* c, int n, const float* const* src, const int64_t* ns,
+                                   const float* const* tar, const int64_t* nt, int on_device, float leaf,
+                                   const fccf_params* params, float* T, fccf_stats* stats) {
+  if (!c || n < 0 || (n && (!src || !ns || !tar || !nt || !T))) return FCCF_E_ARG;
+  for (int i = 0; i < n; ++i)
+    if (int rc = check_args(c, src[i], ns[i], tar[i], nt[i], leaf, T + 16 * (size_t)i)) return rc;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded2(c, [&] { run_register_batch(c, n, src, ns, tar, nt, on_device != 0, leaf, P, T, stats); });
 }

@@ -24,4 +24,7 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
   return b;
 }
 
+// Releases the per-CloudSet pipeline state (fccf_ctx_destroy).
+void pipeline_release(fccf_ctx* c);
+
 }  // namespace fccf

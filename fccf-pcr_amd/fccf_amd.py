@@ -72,6 +72,8 @@ _sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctyp
      ctypes.POINTER(Stats))
 _sig("fccf_register_device", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
      ctypes.POINTER(Stats))
+_sig("fccf_register_batch", ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, ctypes.c_int, ctypes.c_float,
+     ctypes.POINTER(Params), _P, _P)
 _sig("fccf_device_upload", ctypes.c_int, _P, _P, _I64, ctypes.POINTER(_P))
 _sig("fccf_device_free", ctypes.c_int, _P, _P)
 _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
@@ -159,6 +161,28 @@ class Ctx:
                                        ctypes.byref(st))
         _check(rc, "fccf_register_device")
         return T.reshape(4, 4), st
+
+    def register_batch(self, pairs, leaf: float, params=None, on_device=False):
+        """Pipelined registration of [(src, tar), ...] (host arrays, or (ptr, n) device
+        pairs when on_device).  Returns (T[n,4,4], [Stats])."""
+        n = len(pairs)
+        keep, sp, tp, sn, tn = [], [], [], [], []
+        for s, t in pairs:
+            if on_device:
+                (ps, ns_), (pt, nt_) = s, t
+            else:
+                a, b = _f32(s), _f32(t)
+                keep += [a, b]
+                ps, ns_, pt, nt_ = a.ctypes.data, a.shape[0], b.ctypes.data, b.shape[0]
+            sp.append(ps); tp.append(pt); sn.append(ns_); tn.append(nt_)
+        arr_p = (_P * max(n, 1))
+        arr_i = (_I64 * max(n, 1))
+        T = np.zeros((max(n, 1), 4, 4), np.float32)
+        stats = (Stats * max(n, 1))()
+        p = params if params is not None else default_params()
+        _check(_lib.fccf_register_batch(self._h, n, arr_p(*sp), arr_i(*sn), arr_p(*tp), arr_i(*tn), int(on_device),
+                                        float(leaf), ctypes.byref(p), T.ctypes.data, stats), "fccf_register_batch")
+        return T[:n], list(stats)[:n]
 
     def upload(self, xyz) -> int:
         """Copy xyz into a new HBM buffer of this ctx's device; returns the device pointer."""

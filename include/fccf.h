@@ -106,6 +106,15 @@ int fccf_register_device(fccf_ctx* ctx, const float* d_src_xyz, int64_t n_src,
                          const float* d_tar_xyz, int64_t n_tar, float leaf,
                          const fccf_params* params, float T_rowmajor[16], fccf_stats* stats);
 
+/* Batch / throughput mode: n independent pairs, pipelined so
+ * that pair i+1's cloud stage (VoxelGrid passes, face voxels) runs on the GPU while
+ * pair i's later stages run.  Every pair's T and stats equal what fccf_register
+ * (fccf_register_device when on_device != 0) returns for it alone.
+ * T_rowmajor: 16*n floats; stats: n entries or NULL. */
+int fccf_register_batch(fccf_ctx* ctx, int n, const float* const* src_xyz, const int64_t* n_src,
+                        const float* const* tar_xyz, const int64_t* n_tar, int on_device, float leaf,
+                        const fccf_params* params, float* T_rowmajor, fccf_stats* stats);
+
 /* Device-resident inputs for fccf_register_device (bench / batch users): copy n
  * xyz points to a new HBM buffer on ctx's device; release with fccf_device_free. */
 int fccf_device_upload(fccf_ctx* ctx, const float* xyz, int64_t n, float** d_xyz);

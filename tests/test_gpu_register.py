@@ -112,3 +112,44 @@ def test_graph_replay_with_new_data_and_sizes(ctx, oracle, fccf):
         T, _ = ctx.register(s, t, 0.1)
         compare_all(ctx, run)
         np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
+
+
+def test_probe_path_is_exact_and_counts_launches(ctx, oracle, fccf):
+    """With a kernel probe on, the device stages launch eagerly (no graphs) and the
+    probed launches go through hipExtLaunchKernelGGL; results must not change."""
+    src, tar, _ = fccf.synth_pair(80_000)
+    run = oracle.Run(src, tar, 0.1, oracle.STABLE)
+    for k in ("k_rs_scatter", "k_oct_sim", "k_xs_chain"):
+        ctx.set_probe(k)
+        T, _ = ctx.register(src, tar, 0.1)
+        ms, n, b = ctx.probe_read()
+        ctx.set_probe(None)
+        np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
+        assert n > 0 and ms > 0 and b > 0, (k, ms, n, b)
+    compare_all(ctx, run)
+
+
+def test_batch_pipeline_equals_single_registrations(ctx, oracle, fccf):
+    """fccf_register_batch overlaps pair i+1's cloud stage with pair i's later
+    stages (double-buffered cloud workspaces); every result must equal the
+    single-pair registration and the oracle, for host and device inputs."""
+    base_src, base_tar, _ = fccf.synth_pair(70_000)
+    rng = np.random.default_rng(9)
+    pairs = [(base_src, base_tar)]
+    for k in range(3):
+        jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
+        pairs.append(((base_src + jit).astype(np.float32), base_tar[: 60_000 + 5000 * k]))
+    Tb, stb = ctx.register_batch(pairs, 0.1)
+    for (s, t), T in zip(pairs, Tb):
+        ref = oracle.Run(s, t, 0.1, oracle.STABLE).T
+        np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    assert all(st.K > 0 for st in stb)
+    dev = [(ctx.upload(s), ctx.upload(t)) for s, t in pairs]
+    try:
+        Td, _ = ctx.register_batch([((ds, s.shape[0]), (dt, t.shape[0])) for (ds, dt), (s, t) in zip(dev, pairs)], 0.1,
+                                   on_device=True)
+    finally:
+        for ds, dt in dev:
+            ctx.free(ds)
+            ctx.free(dt)
+    np.testing.assert_array_equal(Td.view(np.uint32), Tb.view(np.uint32))
