@@ -181,6 +181,7 @@ def main():
         return ctx.register_batch([pair] * k, leaf, on_device=True)
 
     pipelined = not args.no_pipeline and not args.selftest
+    batch_ms = None
     for _ in range(args.warmup):
         T, st = reg()
     if pipelined and args.warmup:
@@ -193,6 +194,7 @@ def main():
         Tb, sts = batch(args.steps)
         T, st = Tb[-1], sts[-1]
         Ks = sum(x.K for x in sts)
+        batch_ms = {k: statistics.mean(x.as_dict()["ms"][k] for x in sts) for k in sts[0].as_dict()["ms"]}
     else:
         for _ in range(args.steps):
             T, st = reg()  # returns after T is on host
@@ -251,6 +253,7 @@ def main():
             "K_pass": int(st.K_pass),
             "graph_captures_last_step": int(st.graph_captures),
             "stage_ms": {k: round(v, 4) for k, v in st.as_dict()["ms"].items()},
+            "stage_ms_in_batch": {k: round(v, 4) for k, v in batch_ms.items()} if batch_ms else None,
             "rot_err_deg_vs_gt": rot_err,
             "trans_err_m_vs_gt": float(np.linalg.norm(T[:3, 3] - T_gt[:3, 3])),
         }

@@ -57,11 +57,11 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   fccf_ctx* c = new fccf_ctx();
   c->device = device;
   if (hipSetDevice(device) != hipSuccess) { delete c; return FCCF_E_HIP; }
-  bool ok = hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
-  for (auto& cs : c->cs) {
-    for (auto& s : cs.st) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  bool ok = true;
+  for (auto& s : c->sa) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
+  for (auto& cs : c->cs)
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  }
   if (!ok) {
     fccf_ctx_destroy(c);
     return FCCF_E_HIP;
@@ -79,11 +79,11 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& gk : cs.g_seg)
       for (auto& g : gk) g.reset();
-    for (auto& s : cs.st)
-      if (s) (void)hipStreamDestroy(s);
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
   }
+  for (auto& s : c->sa)
+    if (s) (void)hipStreamDestroy(s);
   if (c->sb) (void)hipStreamDestroy(c->sb);
   delete c;
   return FCCF_OK;

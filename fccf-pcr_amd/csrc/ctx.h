@@ -128,13 +128,16 @@ struct fccf_ctx {
   int device = 0;
   // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
   // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
+  // Two sets never run their cloud stages at the same time, so they share streams:
+  // sa[0], sa[1] per-cloud main, sa[2] both centroid sums, and sb for everything
+  // else -- four streams for the four hardware queues a process gets by default.
   struct CloudSet {
     fccf::Arena arena;
-    hipStream_t st[4] = {};          // [0,1] per-cloud main, [2,3] side
     hipEvent_t ev[6] = {};           // [0..3] per-cloud side joins, [4] fork / clouds done, [5] join
     fccf::CachedGraph g_seg[2][3];   // per cloud: downsample, centroid, faces (pipeline.cpp)
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];
+  hipStream_t sa[3] = {};            // cloud stage streams (shared by both sets)
   hipStream_t sb = nullptr;          // matching, fine verification, copies, stage exports
   fccf::CachedGraph g_fine;          // fine-verify batch (K7)
   fccf::Arena arena2;  // matching (and the stage exports)

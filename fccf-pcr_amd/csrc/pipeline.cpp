@@ -253,7 +253,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   ps.nin[1] = n_src;
   const float* hin[2] = {tar, src};
   for (int k = 0; k < 2; ++k) ps.cap[k] = (uint32_t)std::max<int64_t>(ps.nin[k], 1);
-  hipStream_t st0 = cs.st[0], st1 = cs.st[1];
+  hipStream_t st0 = c->sa[0], st1 = c->sa[1];
   cs.arena.ensure(cloud_bytes(ps.cap[0], true) + cloud_bytes(ps.cap[1], true) + (1 << 20));
   cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
@@ -281,7 +281,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));
   HIP_CHECK(hipStreamWaitEvent(st1, cs.ev[4], 0));
   for (int k = 0; k < 2; ++k) {
-    hipStream_t sm = cs.st[k], ss = cs.st[2 + k];
+    hipStream_t sm = c->sa[k], ss = c->sa[2];  // both centroid sums share the side stream
     cs.g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
     HIP_CHECK(hipEventRecord(cs.ev[2 * k], sm));
     HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[2 * k], 0));
@@ -302,7 +302,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
 // enqueues the next pair's clouds there).
 template <class AfterClouds>
 void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_stats* stats,
-                     AfterClouds&& after_clouds) {
+                     AfterClouds&& after_clouds, hipEvent_t fine_after = nullptr) {
   fccf_stats S;
   std::memset(&S, 0, sizeof S);
   PipeSet& ps = pset(c, s);
@@ -580,6 +580,9 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
       float res;
     } fkey = {c->arena3.base, c->arena3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E,
               P.fine_verify_voxel_size};
+    // in a batch, fine verification waits for the next pair's cloud stage: chains of
+    // small kernels from the two stages interleave badly, run back to back they don't
+    if (fine_after) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
     c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
     });
@@ -698,10 +701,13 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   clouds_enqueue(c, 0, src[0], n_src[0], tar[0], n_tar[0], on_device, leaf, P);
   for (int i = 0; i < n; ++i) {
     const int s = i & 1;
-    register_finish(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
-      // the next pair's cloud stage overlaps this pair's later stages
-      if (i + 1 < n) clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
-    });
+    register_finish(
+        c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr,
+        [&] {  // the next pair's cloud stage overlaps this pair's host stages
+          if (i + 1 < n)
+            clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+        },
+        i + 1 < n ? c->cs[s ^ 1].ev[4] : nullptr);
   }
 }
 
