@@ -79,6 +79,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& gk : cs.g_seg)
       for (auto& g : gk) g.reset();
+    cs.g_cen.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -153,7 +154,8 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
-    voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st);
+    // presorted check on: sorted inputs take the identity path, others the full sort
+    voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st, true);
     HIP_CHECK(hipGetLastError());
     uint32_t hm = 0;
     HIP_CHECK(hipMemcpyAsync(&hm, d_sc + 1, 4, hipMemcpyDeviceToHost, st));

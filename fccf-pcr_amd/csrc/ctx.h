@@ -2,7 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -118,7 +120,12 @@ struct CachedGraph {
       key.assign(kb, kb + kn);
       ++captures;
     }
+    static const bool trace = std::getenv("FCCF_HOST_TRACE") != nullptr;
+    const auto h0 = std::chrono::steady_clock::now();
     HIP_CHECK(hipGraphLaunch(exec, st));
+    if (trace)
+      std::fprintf(stderr, "graph launch host %.1f us\n",
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count());
   }
 };
 
@@ -129,12 +136,13 @@ struct fccf_ctx {
   // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
   // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
   // Two sets never run their cloud stages at the same time, so they share streams:
-  // sa[0], sa[1] per-cloud main, sa[2] both centroid sums, and sb for everything
+  // sa[0], sa[1] per-cloud main, sa[2] the centroid sums, and sb for everything
   // else -- four streams for the four hardware queues a process gets by default.
   struct CloudSet {
     fccf::Arena arena;
-    hipEvent_t ev[6] = {};           // [0..3] per-cloud side joins, [4] fork / clouds done, [5] join
-    fccf::CachedGraph g_seg[2][3];   // per cloud: downsample, centroid, faces (pipeline.cpp)
+    hipEvent_t ev[6] = {};           // [0,1] per-cloud downsample done, [2] centroids done, [4] fork / clouds done, [5] join
+    fccf::CachedGraph g_seg[2][2];   // per cloud: downsample, faces (pipeline.cpp)
+    fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];
   hipStream_t sa[3] = {};            // cloud stage streams (shared by both sets)

@@ -61,6 +61,11 @@ XsBufs exact_sum_carve(void* base, int rows, uint32_t cap);
 void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint32_t* cnt, int nprob, float* out,
                bool divide, XsBufs x, hipStream_t st);
 
+// The same for two separate arrays: problem 0 = a[0..*na), problem 1 = b[0..*nb);
+// out[0..K) and out[K..2K).  Scratch: rows = 2*K, cap = max of both counts.
+void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32_t* nb, int S, int K, float* out,
+                bool divide, XsBufs x, hipStream_t st);
+
 // Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap,
                         uint32_t* d_total, SortScratch s, hipStream_t st);

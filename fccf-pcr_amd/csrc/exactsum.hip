@@ -65,10 +65,25 @@ struct Prob {
   uint32_t n, nch;
 };
 
-__device__ __forceinline__ Prob prob_of(const float* data, int S, const uint32_t* off, const uint32_t* cnt, int b) {
+// Where the problems live: either one array with per-problem offsets/counts
+// (off may be null), or (data2 != null) two separate arrays, problem 0 = data with
+// count *cnt and problem 1 = data2 with count *cnt2 (both clouds' centroids).
+struct XsIn {
+  const float* data;
+  const uint32_t* off;
+  const uint32_t* cnt;
+  const float* data2;
+  const uint32_t* cnt2;
+};
+
+__device__ __forceinline__ uint32_t prob_n(const XsIn& in, int b) {
+  return (in.data2 && b == 1) ? *in.cnt2 : in.cnt[b];
+}
+
+__device__ __forceinline__ Prob prob_of(const XsIn& in, int S, int b) {
   Prob p;
-  p.n = cnt[b];
-  p.base = data + (size_t)(off ? off[b] : 0u) * S;
+  p.n = prob_n(in, b);
+  p.base = (in.data2 && b == 1) ? in.data2 : in.data + (size_t)(in.off ? in.off[b] : 0u) * S;
   p.nch = (p.n + XS_L - 1) / XS_L;
   return p;
 }
@@ -93,11 +108,9 @@ __device__ __forceinline__ void load4(const Prob& P, uint32_t c, int lane, int K
 }
 
 template <int S>
-__global__ void __launch_bounds__(256) k_xs_csum(const float* __restrict__ data, int K, const uint32_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ cnt, double* __restrict__ pre,
-                                                 uint32_t NC) {
+__global__ void __launch_bounds__(256) k_xs_csum(XsIn in, int K, double* __restrict__ pre, uint32_t NC) {
   const int b = blockIdx.y, lane = threadIdx.x & 63;
-  const Prob P = prob_of(data, S, off, cnt, b);
+  const Prob P = prob_of(in, S, b);
   for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < P.nch; c += gridDim.x * 4) {
     float v[4][S];
     bool ok[4];
@@ -115,11 +128,10 @@ __global__ void __launch_bounds__(256) k_xs_csum(const float* __restrict__ data,
 }
 
 // in-place: pre[row][1..nch] chunk sums -> pre[row][0..nch] exclusive prefix
-__global__ void __launch_bounds__(256) k_xs_prefix(const uint32_t* __restrict__ cnt, int K, double* __restrict__ pre,
-                                                   uint32_t NC) {
+__global__ void __launch_bounds__(256) k_xs_prefix(XsIn in, int K, double* __restrict__ pre, uint32_t NC) {
   __shared__ double sh[256];
   const int row = blockIdx.x, t = threadIdx.x;
-  const uint32_t nch = (cnt[row / K] + XS_L - 1) / XS_L;
+  const uint32_t nch = (prob_n(in, row / K) + XS_L - 1) / XS_L;
   double* p = pre + (size_t)row * (NC + 1);
   double carry = 0.0;
   if (t == 0) p[0] = 0.0;
@@ -142,11 +154,10 @@ __global__ void __launch_bounds__(256) k_xs_prefix(const uint32_t* __restrict__ 
 }
 
 template <int S>
-__global__ void __launch_bounds__(256) k_xs_chunk(const float* __restrict__ data, int K, const uint32_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ cnt, const double* __restrict__ pre,
+__global__ void __launch_bounds__(256) k_xs_chunk(XsIn in, int K, const double* __restrict__ pre,
                                                   XsSum* __restrict__ ctab, int32_t* __restrict__ cE, uint32_t NC) {
   const int b = blockIdx.y, lane = threadIdx.x & 63;
-  const Prob P = prob_of(data, S, off, cnt, b);
+  const Prob P = prob_of(in, S, b);
   for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < P.nch; c += gridDim.x * 4) {
     float v[4][S];
     bool ok[4];
@@ -171,13 +182,13 @@ __global__ void __launch_bounds__(256) k_xs_chunk(const float* __restrict__ data
   }
 }
 
-__global__ void __launch_bounds__(256) k_xs_group(const uint32_t* __restrict__ cnt, int K, const double* __restrict__ pre,
+__global__ void __launch_bounds__(256) k_xs_group(XsIn in, int K, const double* __restrict__ pre,
                                                   const XsSum* __restrict__ ctab, const int32_t* __restrict__ cE,
                                                   XsSum* __restrict__ gtab, int32_t* __restrict__ gE, uint32_t NC,
                                                   uint32_t NG) {
   const size_t row = blockIdx.y;
   const int lane = threadIdx.x & 63;
-  const uint32_t nch = (cnt[row / K] + XS_L - 1) / XS_L;
+  const uint32_t nch = (prob_n(in, (int)(row / K)) + XS_L - 1) / XS_L;
   const uint32_t ng = (nch + XS_G - 1) / XS_G;
   for (uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6); g < ng; g += gridDim.x * 4) {
     const int Eg = xs_predict(pre[row * (NC + 1) + (size_t)g * XS_G]);
@@ -261,14 +272,13 @@ __device__ __forceinline__ void scan_jump(float& s, const XsTab3& T, int cnt, De
 // One wave per row: groups (scan-jump) -> chunks (scan-jump) -> plain replay.
 // s is identical in every lane, so all control flow is uniform.
 template <int S>
-__global__ void __launch_bounds__(64) k_xs_chain(const float* __restrict__ data, int K, const uint32_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ cnt, const XsSum* __restrict__ ctab,
+__global__ void __launch_bounds__(64) k_xs_chain(XsIn in, int K, const XsSum* __restrict__ ctab,
                                                  const int32_t* __restrict__ cE, const XsSum* __restrict__ gtab,
                                                  const int32_t* __restrict__ gE, uint32_t NC, uint32_t NG,
                                                  float* __restrict__ out, int divide) {
   const int row = blockIdx.x, lane = threadIdx.x;
   const int b = row / K, k = row % K;
-  const Prob P = prob_of(data, S, off, cnt, b);
+  const Prob P = prob_of(in, S, b);
   const float* x = P.base + k;
   const uint32_t ng = (P.nch + XS_G - 1) / XS_G;
   float s = 0.f;
@@ -357,25 +367,38 @@ XsBufs exact_sum_carve(void* base, int rows, uint32_t cap) {
   return x;
 }
 
-void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint32_t* cnt, int nprob, float* out,
-               bool divide, XsBufs x, hipStream_t st) {
+namespace {
+void exact_sum_in(const XsIn& in, int S, int K, int nprob, float* out, bool divide, XsBufs x, hipStream_t st) {
   if (nprob <= 0) return;
   const int rows = nprob * K;
   if (rows > x.rows) throw Error(FCCF_E_INTERNAL, "exact_sum: scratch carved for fewer rows");
   const dim3 gc(clampg((x.NC + 3) / 4, 1024), nprob), gg(clampg((x.NG + 3) / 4, 256), rows);
   if (S == 3) {
-    k_xs_csum<3><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
-    k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    FCCF_LAUNCH("k_xs_chunk", (cnt, 4.0 * 3), k_xs_chunk<3>, gc, 256, 0, st, data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
-    k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_LAUNCH("k_xs_chain", (cnt, 4.0 * 3), k_xs_chain<3>, rows, 64, 0, st, data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    k_xs_csum<3><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
+    k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
+    // probe bytes: 12 B per element of every problem (two-array form: both counts)
+    const uint32_t* c2 = in.data2 ? in.cnt2 : nullptr;
+    FCCF_LAUNCH("k_xs_chunk", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
+    k_xs_group<<<gg, 256, 0, st>>>(in, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
+    FCCF_LAUNCH("k_xs_chain", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
   } else {
-    k_xs_csum<1><<<gc, 256, 0, st>>>(data, K, off, cnt, x.pre, x.NC);
-    k_xs_prefix<<<rows, 256, 0, st>>>(cnt, K, x.pre, x.NC);
-    FCCF_LAUNCH("k_xs_chunk", (cnt, 4.0 * 1), k_xs_chunk<1>, gc, 256, 0, st, data, K, off, cnt, x.pre, x.ctab, x.cE, x.NC);
-    k_xs_group<<<gg, 256, 0, st>>>(cnt, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_LAUNCH("k_xs_chain", (cnt, 4.0 * 1), k_xs_chain<1>, rows, 64, 0, st, data, K, off, cnt, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    k_xs_csum<1><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
+    k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
+    FCCF_LAUNCH("k_xs_chunk", (in.cnt, 4.0 * 1), k_xs_chunk<1>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
+    k_xs_group<<<gg, 256, 0, st>>>(in, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
+    FCCF_LAUNCH("k_xs_chain", (in.cnt, 4.0 * 1), k_xs_chain<1>, rows, 64, 0, st, in, K, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
   }
+}
+}  // namespace
+
+void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint32_t* cnt, int nprob, float* out,
+               bool divide, XsBufs x, hipStream_t st) {
+  exact_sum_in(XsIn{data, off, cnt, nullptr, nullptr}, S, K, nprob, out, divide, x, st);
+}
+
+void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32_t* nb, int S, int K, float* out,
+                bool divide, XsBufs x, hipStream_t st) {
+  exact_sum_in(XsIn{a, nullptr, na, b, nb}, S, K, 2, out, divide, x, st);
 }
 
 }  // namespace fccf

@@ -377,9 +377,6 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs xs, hipStream_t st) {
-  exact_sum(xyz, 3, 3, nullptr, d_n, 1, out4, true, xs, st);  // compute3DCentroid (:473)
-}
 
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
                 size_t xyz_stride, size_t aggr_stride) {

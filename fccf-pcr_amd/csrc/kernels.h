@@ -17,8 +17,9 @@ struct VGParams {
   int32_t div_b[3];
   int64_t mul1, mul2;
   uint32_t overflow;  // int32 index guard tripped: output = input
-  uint32_t nbits;     // radix bits (0 when overflow / empty)
-  uint32_t pad[2];
+  uint32_t nbits;     // radix bits (0 when overflow / empty, or when the keys are already sorted)
+  uint32_t unsorted;  // presorted check: some key is not strictly above its predecessor
+  uint32_t chk_done;  // presorted check: blocks finished
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
@@ -34,8 +35,12 @@ struct VGBufs {
 
 // xyz[0..*d_n) -> out[0..*d_m), PCL VoxelGrid<PointXYZ> semantics with stable
 // (ascending input index) accumulation inside a leaf.
+// presorted: the input is expected to be in (nearly) ascending leaf order -- the
+// driver's second pass over main's output (:1377-1387 after :1668-1678).  A check
+// kernel then skips the radix passes when the keys are already strictly increasing
+// (every leaf holds one point), which leaves the result unchanged.
 void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf, float* out, uint32_t* d_m,
-                VGBufs b, hipStream_t st);
+                VGBufs b, hipStream_t st, bool presorted = false);
 
 // ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
 struct VoxRec {  // one occupied octree leaf, Morton order
@@ -51,8 +56,7 @@ struct FaceBufs {
   uint32_t* starts;        // cap + 1
   float* aggr;             // octree-bounds aggregates, aggr_floats(cap) (see block_aggr)
   OctState* oct;
-  float* centroid;         // 4 floats
-  XsBufs xs;               // centroid sum scratch (3 rows)
+  float* centroid;         // 3 floats (the cloud centroid, exact_sum2 in pipeline.cpp)
   VoxRec* recs;            // cap (all leaves)
   uint32_t* flag_planar;   // cap
   uint32_t* resid_cnt;     // cap
@@ -67,8 +71,6 @@ struct FaceBufs {
   SortScratch ss;
 };
 
-// Launch the sequential cloud-centroid reduction (PCL compute3DCentroid order).
-void cloud_centroid(const float* xyz, const uint32_t* d_n, float* out4, XsBufs xs, hipStream_t st);
 // Octree leaves + per-leaf plane fit + compaction.  `centroid` must be ready
 // before the fit kernel runs (the caller orders the streams).
 void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -139,7 +141,6 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   b += sizeof(VoxRec) * N + 12 * N;                            // planar out, residual out
   b += 4 * aggr_floats(cap) + 512;                             // fine-verify S1 bounds replay
   b += sort_scratch_bytes(cap) + 64 * 256;                     // sort scratch + alignment slack
-  b += exact_sum_bytes(3, cap) + 256;                          // centroid sum tables
   return b;
 }
 
@@ -161,8 +162,7 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   f.starts = a.take_n<uint32_t>((size_t)cap + 1);
   f.aggr = a.take_n<float>(aggr_floats(cap));
   f.oct = a.take_n<OctState>(1);
-  f.centroid = a.take_n<float>(4);
-  f.xs = exact_sum_carve(a.take(exact_sum_bytes(3, cap)), 3, cap);
+  f.centroid = nullptr;  // set by clouds_enqueue: both centroids share one buffer
   f.recs = a.take_n<VoxRec>(cap);
   f.flag_planar = a.take_n<uint32_t>(cap);
   f.resid_cnt = a.take_n<uint32_t>(cap);
@@ -182,19 +182,19 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.fstate = a.take_n<OctState>(1);
 }
 
-// Device part of one cloud, in three stream segments (each replayed as a graph):
+// Device part of one cloud, in two stream segments (each replayed as a graph):
 //   A  (main)  both VoxelGrid passes with remove-NaN between them
-//   C  (side)  the sequential cloud-centroid sum, after A
 //   F  (main)  octree leaves, per-leaf fit, residual cloud, after A
-// and the planar compaction, which orients normals towards the centroid, after C and F.
+// plus, on the side stream after both clouds' A, one graph summing both cloud
+// centroids (the sequential compute3DCentroid sums, six rows in one launch set),
+// and the planar compaction, which orients normals towards the centroid.
 void seg_downsample(CloudWS& w, float leaf, hipStream_t st) {
   voxel_grid(w.in, w.sc, w.cap, leaf, w.ds1, w.sc + 1, w.vg, st);  // main :1668-1678
   k_finite_flags<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag);  // driver :1374-1375
   exclusive_scan_u32(w.fflag, w.foff, w.sc + 1, w.cap, w.sc + 2, w.vg.ss, st);
   k_finite_scatter<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag, w.foff, w.ds1f);
-  voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st);  // driver :1377-1387
+  voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st, true);  // driver :1377-1387
 }
-void seg_centroid(CloudWS& w, hipStream_t side) { cloud_centroid(w.ds2, w.sc + 3, w.fb.centroid, w.fb.xs, side); }
 void seg_faces(CloudWS& w, const fccf_params& P, hipStream_t st, bool s1) {
   face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
   face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.resid, w.fb, st);
@@ -227,11 +227,36 @@ void dump_planes(fccf_ctx* c, const std::string& k, const std::vector<Plane>& F)
 
 namespace {
 
+// Development timing of the cloud-stage segments (FCCF_SEG_TIMING).
+struct SegTimer {
+  hipEvent_t ev[11] = {};
+  bool armed = false;
+};
+SegTimer& seg_timer(int s) {
+  static SegTimer t[2];
+  if (!t[s].ev[0])
+    for (auto& e : t[s].ev) HIP_CHECK(hipEventCreate(&e));
+  return t[s];
+}
+void seg_timer_print(int s) {
+  SegTimer& t = seg_timer(s);
+  if (!t.armed) return;
+  t.armed = false;
+  HIP_CHECK(hipEventSynchronize(t.ev[10]));
+  HIP_CHECK(hipEventSynchronize(t.ev[5]));
+  float v[11];
+  for (int i = 1; i < 11; ++i) HIP_CHECK(hipEventElapsedTime(&v[i], t.ev[0], t.ev[i]));
+  std::fprintf(stderr, "seg us (from fork): c0 ds %.0f-%.0f faces ->%.0f orient ->%.0f | c1 ds %.0f-%.0f faces ->%.0f orient ->%.0f | centroids ->%.0f\n",
+               v[1] * 1e3, v[2] * 1e3, v[4] * 1e3, v[5] * 1e3, v[6] * 1e3, v[7] * 1e3, v[9] * 1e3, v[10] * 1e3, v[3] * 1e3);
+}
+
 // State of the registration whose clouds occupy CloudSet s.
 struct PipeSet {
   CloudWS w[2];
   int64_t nin[2] = {0, 0};
   uint32_t cap[2] = {1, 1};
+  float* cen = nullptr;  // both cloud centroids: cloud k at cen[3k .. 3k+2]
+  XsBufs xs;             // their exact-sum scratch (6 rows)
   clk::time_point t_enq;
 };
 
@@ -254,14 +279,19 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   const float* hin[2] = {tar, src};
   for (int k = 0; k < 2; ++k) ps.cap[k] = (uint32_t)std::max<int64_t>(ps.nin[k], 1);
   hipStream_t st0 = c->sa[0], st1 = c->sa[1];
-  cs.arena.ensure(cloud_bytes(ps.cap[0], true) + cloud_bytes(ps.cap[1], true) + (1 << 20));
+  cs.arena.ensure(cloud_bytes(ps.cap[0], true) + cloud_bytes(ps.cap[1], true) +
+                  exact_sum_bytes(6, std::max(ps.cap[0], ps.cap[1])) + (1 << 20));
   cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
   // clouds) so the captured graphs never depend on caller pointers.
   uint32_t* hn = (uint32_t*)c->pinned.get(64) + 8 * s;
+  const uint32_t capmax = std::max(ps.cap[0], ps.cap[1]);
+  ps.cen = cs.arena.take_n<float>(8);
+  ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
     carve_cloud(cs.arena, w[k], ps.cap[k], true);
+    w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
     const uint32_t n = (uint32_t)ps.nin[k];
     if (n)
       HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n,
@@ -280,17 +310,37 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   // st0 -> st1 fork (the staging copies above are on st0)
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));
   HIP_CHECK(hipStreamWaitEvent(st1, cs.ev[4], 0));
+  // FCCF_SEG_TIMING=1 (development): timing events between the segment graphs,
+  // printed to stderr by register_finish.
+  static const bool seg_timing = std::getenv("FCCF_SEG_TIMING") != nullptr;
+  SegTimer& tm = seg_timer(s);
+  auto mark = [&](int i, hipStream_t q) {
+    if (seg_timing) HIP_CHECK(hipEventRecord(tm.ev[i], q));
+  };
+  mark(0, st0);
+  hipStream_t ss = c->sa[2];
   for (int k = 0; k < 2; ++k) {
-    hipStream_t sm = c->sa[k], ss = c->sa[2];  // both centroid sums share the side stream
+    hipStream_t sm = c->sa[k];
+    mark(1 + 5 * k, sm);
     cs.g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
-    HIP_CHECK(hipEventRecord(cs.ev[2 * k], sm));
-    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[2 * k], 0));
-    cs.g_seg[k][1].run(&key, sizeof key, ss, [&] { seg_centroid(w[k], ss); });
-    HIP_CHECK(hipEventRecord(cs.ev[2 * k + 1], ss));
-    cs.g_seg[k][2].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm, k == 0); });
-    HIP_CHECK(hipStreamWaitEvent(sm, cs.ev[2 * k + 1], 0));
-    face_voxels_orient(w[k].cap, w[k].planar, w[k].fb, sm);
+    mark(2 + 5 * k, sm);
+    HIP_CHECK(hipEventRecord(cs.ev[k], sm));
+    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[k], 0));
   }
+  cs.g_cen.run(&key, sizeof key, ss, [&] {
+    exact_sum2(w[0].ds2, w[0].sc + 3, w[1].ds2, w[1].sc + 3, 3, 3, ps.cen, true, ps.xs, ss);  // compute3DCentroid (:473)
+  });
+  mark(3, ss);
+  HIP_CHECK(hipEventRecord(cs.ev[2], ss));
+  for (int k = 0; k < 2; ++k) {
+    hipStream_t sm = c->sa[k];
+    cs.g_seg[k][1].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm, k == 0); });
+    mark(4 + 5 * k, sm);
+    HIP_CHECK(hipStreamWaitEvent(sm, cs.ev[2], 0));
+    face_voxels_orient(w[k].cap, w[k].planar, w[k].fb, sm);
+    mark(5 + 5 * k, sm);
+  }
+  tm.armed = seg_timing;
   HIP_CHECK(hipEventRecord(cs.ev[5], st1));  // join
   HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[5], 0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
@@ -322,6 +372,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   }
   HIP_CHECK(hipStreamSynchronize(st0));
   S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
+  seg_timer_print(s);
   after_clouds();
   t0 = clk::now();
   S.m_tar = sc[0][3];
@@ -645,6 +696,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   S.graph_captures = c->g_fine.captures;
   for (auto& gk : c->cs[s].g_seg)
     for (auto& g : gk) S.graph_captures += g.captures;
+  S.graph_captures += c->cs[s].g_cen.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
   if (c->debug) {
@@ -662,9 +714,11 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
 
 void reset_capture_counts(fccf_ctx* c) {
   c->g_fine.captures = 0;
-  for (auto& cs : c->cs)
+  for (auto& cs : c->cs) {
     for (auto& gk : cs.g_seg)
       for (auto& g : gk) g.captures = 0;
+    cs.g_cen.captures = 0;
+  }
 }
 
 struct ProbeGuard {

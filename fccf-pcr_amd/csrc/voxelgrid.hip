@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(64) k_vg_params(const float* __restrict__ part
   q.nbits = 0;
   q.mul1 = q.mul2 = 0;
   for (int a = 0; a < 3; ++a) q.min_b[a] = q.div_b[a] = 0;
-  q.pad[0] = q.pad[1] = 0;
+  q.unsorted = 0;
+  q.chk_done = 0;
   if (cnt > 0) {
     const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
     const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
@@ -128,6 +129,33 @@ __global__ void __launch_bounds__(256) k_vg_keys(const float* __restrict__ xyz, 
   }
 }
 
+// Presorted check (second pass): vals = identity, and if every key is strictly above
+// its predecessor the last block to finish sets nbits = 0, so the radix passes exit
+// at once and the identity permutation stands -- the stable sort of sorted keys.
+__global__ void __launch_bounds__(256) k_vg_sorted(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ d_n,
+                                                   VGParams* __restrict__ P, uint32_t* __restrict__ vals) {
+  __shared__ uint32_t bad_sh;
+  if (threadIdx.x == 0) bad_sh = 0;
+  __syncthreads();
+  const bool live = !P->overflow && P->nfinite != 0;
+  const uint32_t n = *d_n;
+  uint32_t bad = 0;
+  if (live)
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+      vals[i] = i;
+      if (i + 1 < n && !(keys[i] < keys[i + 1])) bad = 1;
+    }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&bad_sh, 1u);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  if (bad_sh) atomicOr(&P->unsorted, 1u);
+  __threadfence();
+  if (atomicAdd(&P->chk_done, 1u) == gridDim.x - 1) {
+    __threadfence();
+    if (live && atomicOr(&P->unsorted, 0u) == 0) P->nbits = 0;
+  }
+}
+
 // One thread per leaf: Vector3f accumulation in ascending input index, then / n.
 __global__ void __launch_bounds__(256) k_vg_centroid(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
                                                      const VGParams* __restrict__ P, const uint32_t* __restrict__ vals,
@@ -166,11 +194,13 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 }  // namespace
 
 void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf, float* out, uint32_t* d_m, VGBufs b,
-                hipStream_t st) {
+                hipStream_t st, bool presorted) {
   k_vg_bbox<<<VG_BBOX_BLOCKS, 256, 0, st>>>(xyz, d_n, b.part);
   k_vg_params<<<1, 64, 0, st>>>(b.part, VG_BBOX_BLOCKS, leaf, b.params);
   FCCF_LAUNCH("k_vg_keys", (d_n, 16.0), k_vg_keys, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.k0);
-  radix_sort_u32(b.k0, b.v0, b.k1, b.v1, d_n, cap, &b.params->nbits, 32, true, b.ss, st);
+  if (presorted) k_vg_sorted<<<grid_for(cap, 1024, 1024), 256, 0, st>>>(b.k0, d_n, b.params, b.v0);
+  // with nbits = 0 every pass exits and v0 keeps the identity written above
+  radix_sort_u32(b.k0, b.v0, b.k1, b.v1, d_n, cap, &b.params->nbits, 32, !presorted, b.ss, st);
   segment_heads_u32(b.k0, d_n, cap, 0xFFFFFFFFu, b.starts, b.nseg, b.ss, st);
   FCCF_LAUNCH("k_vg_centroid", (d_n, 16.0, d_m, 12.0), k_vg_centroid, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.v0, b.starts, b.nseg, out, d_m);
 }

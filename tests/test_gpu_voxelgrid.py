@@ -59,3 +59,17 @@ def test_many_leaves_random(ctx, oracle):
     rng = np.random.default_rng(2)
     x = rng.uniform(-30, 30, size=(2_000_000, 3)).astype(np.float32)
     check(ctx, oracle, x, 0.5)
+
+
+def test_presorted_check_paths(ctx, oracle, fccf):
+    """The stage export runs the presorted check (voxel_grid(presorted=true)): sorted
+    input takes the identity path (radix passes skipped), anything else the full
+    sort.  Both must equal the oracle on inputs near the boundary of the check."""
+    m1 = check(ctx, oracle, fccf.synth_scene(120_000, seed=5), 0.1)
+    check(ctx, oracle, m1, 0.1)                                   # strictly increasing: identity
+    sw = m1.copy()
+    sw[[1000, 1001]] = sw[[1001, 1000]]
+    check(ctx, oracle, sw, 0.1)                                   # one descent: full sort
+    check(ctx, oracle, np.concatenate([m1, m1[-1:]]), 0.1)        # equal last keys: full sort
+    check(ctx, oracle, np.concatenate([m1, np.full((1, 3), np.nan, np.float32)]), 0.1)  # invalid key last
+    check(ctx, oracle, m1[::-1].copy(), 0.1)                      # descending
