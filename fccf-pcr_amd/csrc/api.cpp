@@ -77,8 +77,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   pipeline_release(c);
   c->g_fine.reset();
   for (auto& cs : c->cs) {
-    for (auto& gk : cs.g_seg)
-      for (auto& g : gk) g.reset();
+    for (auto& g : cs.g_seg) g.reset();
     cs.g_cen.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
@@ -140,7 +139,10 @@ static int guarded(fccf_ctx* c, F&& f) {
   }
 }
 
-extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out, int64_t* m) {
+extern "C" const char* fccf_ctx_last_error(fccf_ctx* c) { return c ? c->last_error.c_str() : ""; }
+
+namespace {
+int stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out, int64_t* m, bool presorted) {
   if (!c || (!xyz && n) || !out || !m || n < 0 || n > (int64_t)0x7FFFFFFF || !(leaf > 0.f)) return FCCF_E_ARG;
   return guarded(c, [&] {
     hipStream_t st = c->sb;
@@ -154,8 +156,7 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
-    // presorted check on: sorted inputs take the identity path, others the full sort
-    voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st, true);
+    voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st, presorted);
     HIP_CHECK(hipGetLastError());
     uint32_t hm = 0;
     HIP_CHECK(hipMemcpyAsync(&hm, d_sc + 1, 4, hipMemcpyDeviceToHost, st));
@@ -164,6 +165,17 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
     HIP_CHECK(hipStreamSynchronize(st));
     *m = hm;
   });
+}
+
+}  // namespace
+
+extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out, int64_t* m) {
+  return stage_downsample(c, xyz, n, leaf, out, m, false);
+}
+
+extern "C" int fccf_stage_downsample_presorted(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out,
+                                               int64_t* m) {
+  return stage_downsample(c, xyz, n, leaf, out, m, true);
 }
 
 namespace {
@@ -218,3 +230,22 @@ extern "C" int fccf_device_free(fccf_ctx* c, float* d) {
     if (d) HIP_CHECK(hipFree(d));
   });
 }
+
+#ifdef FCCF_KTRACE
+// ---------------------------------------------------------------- ktrace (development)
+namespace fccf {
+static std::vector<void (*)(unsigned long long*)>& kt_setters() {
+  static std::vector<void (*)(unsigned long long*)> v;
+  return v;
+}
+void ktrace_register(void (*setter)(unsigned long long*)) { kt_setters().push_back(setter); }
+}  // namespace fccf
+
+// Point every instrumented translation unit at buf (device, 16384 u64; word 0 =
+// record count, reset here), or detach with NULL.
+extern "C" int fccf_ktrace_arm(void* buf) {
+  if (buf) (void)hipMemset(buf, 0, 8);
+  for (auto f : fccf::kt_setters()) f((unsigned long long*)buf);
+  return hipDeviceSynchronize() == hipSuccess ? FCCF_OK : FCCF_E_HIP;
+}
+#endif

@@ -136,12 +136,12 @@ struct fccf_ctx {
   // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
   // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
   // Two sets never run their cloud stages at the same time, so they share streams:
-  // sa[0], sa[1] per-cloud main, sa[2] the centroid sums, and sb for everything
-  // else -- four streams for the four hardware queues a process gets by default.
+  // sa[0] the batched cloud stage, sa[2] the centroid sums, and sb for everything
+  // else (sa[1] is spare) -- within the four hardware queues a process gets.
   struct CloudSet {
     fccf::Arena arena;
-    hipEvent_t ev[6] = {};           // [0,1] per-cloud downsample done, [2] centroids done, [4] fork / clouds done, [5] join
-    fccf::CachedGraph g_seg[2][2];   // per cloud: downsample, faces (pipeline.cpp)
+    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [4] clouds done
+    fccf::CachedGraph g_seg[2];      // both clouds batched: downsample, faces (pipeline.cpp)
     fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "exactsum.h"
+#include "ktrace.h"
 
 namespace fccf {
 
@@ -15,9 +16,10 @@ constexpr int RS_TILE = RS_THREADS * RS_CHUNKS;  // 2048 keys per block
 
 inline uint32_t rs_blocks(uint32_t cap) { return (cap + RS_TILE - 1) / RS_TILE; }
 
-// Radix sort tiles: 4096 keys per block (hist and scatter).
-constexpr int SORT_CHUNKS = 16;
-constexpr int SORT_TILE = RS_THREADS * SORT_CHUNKS;
+// Radix sort tiles: 4096 keys per block of 1024 threads (hist and scatter).
+constexpr int SORT_THREADS = 1024;
+constexpr int SORT_CHUNKS = 4;
+constexpr int SORT_TILE = SORT_THREADS * SORT_CHUNKS;
 inline uint32_t sort_blocks(uint32_t cap) { return (cap + SORT_TILE - 1) / SORT_TILE; }
 
 // Scratch for radix_sort_pairs / segment_heads: hist needs 256*blocks u32,
@@ -30,25 +32,50 @@ struct SortScratch {
 size_t sort_scratch_bytes(uint32_t cap);
 SortScratch sort_scratch_carve(void* base, uint32_t cap);
 
+// Per-problem arguments of a batched launch: problem e = blockIdx.y uses v[e].
+// The primitives below run `nbatch` (1 or 2) independent problems -- the two
+// clouds of a registration -- in the same launches (a kernel boundary costs
+// ~1.7 us on gfx950 and two streams of dependent kernels interfere, so one
+// stream of batched launches is the fast shape).  A single value converts to a
+// batch of one.
+template <class T>
+struct B2 {
+  T v[2];
+  B2() = default;
+  __host__ __device__ B2(T a) : v{a, a} {}
+  __host__ __device__ B2(T a, T b) : v{a, b} {}
+  template <class U>
+  __host__ __device__ B2(const B2<U>& o) : v{o.v[0], o.v[1]} {}
+  __host__ __device__ T operator[](int i) const { return v[i]; }
+};
+
 // Stable LSD radix sort of (key, val) by the low *d_nbits bits of key (8-bit
 // digits).  The sorted result is always left in (k0, v0); (k1, v1) are temporaries.
 // If vals_iota, v0 is ignored on input and the values are the input positions.
-void radix_sort_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* d_n,
-                    uint32_t cap, const uint32_t* d_nbits, int max_bits, bool vals_iota,
-                    SortScratch s, hipStream_t st);
-void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, const uint32_t* d_n,
-                    uint32_t cap, const uint32_t* d_nbits, int max_bits, bool vals_iota,
-                    SortScratch s, hipStream_t st);
+// cap bounds every problem's count.  The first fast_bits (a multiple of 8) run as
+// device-wide passes (3 launches each, a pass past *d_nbits exits at once); any
+// higher bits run in one single-workgroup tail launch (k_rs_tail), which also
+// exits at once unless needed.  tail_need (optional): the tail runs only where
+// *tail_need != 0 (fast_bits == 0: a sort of keys usually already in order).
+void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
+                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));
+void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
+                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));
 
 // Run-length segmentation of sorted keys[0..*d_n): starts[s] = first index of
 // segment s, starts[S] = *d_n, *d_nseg = S.  Keys equal to `invalid` (which sort
 // last) are excluded: the valid prefix ends at the first invalid key.
 // seg_of (optional): segment index of every valid element.
-void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid,
-                       uint32_t* starts, uint32_t* d_nseg, SortScratch s, hipStream_t st,
-                       uint32_t* seg_of = nullptr);
-void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts,
-                       uint32_t* d_nseg, SortScratch s, hipStream_t st, uint32_t* seg_of = nullptr);
+// run (optional): skip problems whose *run == 0 (their outputs are left untouched).
+void segment_heads_u32(B2<const uint32_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
+                       B2<uint32_t*> starts, B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
+                       B2<uint32_t*> seg_of = B2<uint32_t*>(nullptr), int nbatch = 1,
+                       B2<const uint32_t*> run = B2<const uint32_t*>(nullptr));
+void segment_heads_u64(B2<const uint64_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, B2<uint32_t*> starts,
+                       B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
+                       B2<uint32_t*> seg_of = B2<uint32_t*>(nullptr), int nbatch = 1);
 
 // Sequential float sums in the reference's left-to-right order, s = ((0 + v0) + v1) + ...
 // bit-exact, computed in parallel (exactsum.h).  Problem b sums elements
@@ -67,7 +94,7 @@ void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32
                 bool divide, XsBufs x, hipStream_t st);
 
 // Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
-void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap,
-                        uint32_t* d_total, SortScratch s, hipStream_t st);
+void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
+                        B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch = 1);
 
 }  // namespace fccf

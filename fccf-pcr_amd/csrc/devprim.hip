@@ -1,8 +1,10 @@
 // devprim.hip — stable LSD radix sort, run-length segmentation and exclusive scan
 // for gfx950.  Wave64-native: per-digit ranks come from 8 ballots per 64-key
 // chunk (no 32-lane warp idioms), block = 4 waves, tile = 2048 keys.
+#define KT_TU 1  // ktrace.h source tag
 #include "probe.h"
 #include "devprim.h"
+#include "ctx.h"
 
 namespace fccf {
 
@@ -37,27 +39,58 @@ __device__ __forceinline__ uint32_t block_scan_256(uint32_t v, uint32_t* sh, uin
 
 __device__ __forceinline__ uint32_t passes_of(uint32_t nbits) { return (nbits + 7u) / 8u; }
 
-template <class K>
-__global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
-                                               const uint32_t* __restrict__ d_nbits, int shift,
-                                               uint32_t* __restrict__ hist, uint32_t nblocks) {
-  if ((uint32_t)shift >= *d_nbits) return;
-  __shared__ uint32_t cnt[256];
-  cnt[threadIdx.x] = 0;
+// Radix-sort tiles: 4096 keys per block of ST = 1024 threads (16 waves x 4 chunks of
+// 64 keys).  A fat block keeps the per-tile ranking short (each wave ranks 256
+// keys) while the tile count, and with it the digit x tile histogram, stays small.
+constexpr int ST = SORT_THREADS;
+constexpr int SW = ST / 64;  // waves per sort block
+
+// Exclusive scan of v over the first 256 threads of an ST-thread block (threads
+// >= 256 pass 0 and get garbage); sh needs SW u32.  Every thread must call it.
+__device__ __forceinline__ uint32_t scan_256_of(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  if (threadIdx.x >= 256) v = 0;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63 && wave < 4) sh[wave] = x;
   __syncthreads();
-  const uint32_t n = *d_n;
+  uint32_t wp = 0;
+  for (uint32_t w = 0; w < wave && w < 4; ++w) wp += sh[w];
+  const uint32_t tot = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
+template <class K>
+__global__ void __launch_bounds__(ST) k_rs_hist(B2<const K*> keys2, B2<const uint32_t*> d_n2,
+                                                B2<const uint32_t*> d_nbits2, int shift, B2<SortScratch> ss,
+                                                uint32_t nblocks) {
+  KT();
+  const int e = blockIdx.y;
+  const K* __restrict__ keys = keys2[e];
+  uint32_t* __restrict__ hist = ss[e].hist;
+  if ((uint32_t)shift >= *d_nbits2[e]) return;
+  __shared__ uint32_t cnt[256];
+  if (threadIdx.x < 256) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t n = *d_n2[e];
   const uint32_t base = blockIdx.x * SORT_TILE;
   const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
-  // all 16 loads of the tile are issued before any is consumed (clamped indices,
-  // no branches), then one LDS atomic per distinct digit per 64 keys (ballot
-  // match): neighbouring keys share their high digits
+  // all loads of the tile are issued before any is consumed (clamped indices, no
+  // branches), then one LDS atomic per distinct digit per 64 keys (ballot match):
+  // neighbouring keys share their high digits
   K kk[SORT_CHUNKS];
   const uint32_t last = n ? n - 1u : 0u;
 #pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) kk[c] = keys[min(base + c * T + threadIdx.x, last)];
+  for (int c = 0; c < SORT_CHUNKS; ++c) kk[c] = keys[min(base + c * ST + threadIdx.x, last)];
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
-    const bool ok = base + c * T + threadIdx.x < end;
+    const bool ok = base + c * ST + threadIdx.x < end;
     const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
     uint64_t m = __ballot(ok);
 #pragma unroll
@@ -69,14 +102,17 @@ __global__ void __launch_bounds__(T) k_rs_hist(const K* __restrict__ keys, const
     if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
   }
   __syncthreads();
-  hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < 256) hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
 // One block per digit: exclusive scan of that digit's per-block counts in place.
-__global__ void __launch_bounds__(T) k_rs_rowscan(uint32_t* __restrict__ hist, uint32_t nblocks,
-                                                  uint32_t* __restrict__ tot, const uint32_t* __restrict__ d_nbits,
+__global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t nblocks, B2<const uint32_t*> d_nbits2,
                                                   int shift) {
-  if ((uint32_t)shift >= *d_nbits) return;
+  KT();
+  const int e = blockIdx.y;
+  uint32_t* __restrict__ hist = ss[e].hist;
+  uint32_t* __restrict__ tot = ss[e].tot;
+  if ((uint32_t)shift >= *d_nbits2[e]) return;
   __shared__ uint32_t sh[4];
   const uint32_t d = blockIdx.x;
   uint32_t carry = 0;
@@ -95,31 +131,31 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(uint32_t* __restrict__ hist, u
 // writes each digit run to its global slot with consecutive lanes on consecutive
 // addresses.  *active (probe, may be null) is cleared when the pass is skipped.
 template <class K>
-__global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                  const uint32_t* __restrict__ d_n,
-                                                  const uint32_t* __restrict__ d_nbits, int shift,
-                                                  const uint32_t* __restrict__ hist,
-                                                  const uint32_t* __restrict__ tot, uint32_t nblocks, int iota,
-                                                  uint32_t* __restrict__ active) {
-  const bool run = (uint32_t)shift < *d_nbits;
-  if (active && blockIdx.x == 0 && threadIdx.x == 0) *active = run ? 1u : 0u;
-  const uint32_t n = *d_n;
+__global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const uint32_t*> vin2, B2<K*> kout2,
+                                                   B2<uint32_t*> vout2, B2<const uint32_t*> d_n2,
+                                                   B2<const uint32_t*> d_nbits2, int shift, B2<SortScratch> ss,
+                                                   uint32_t nblocks, int iota, uint32_t* __restrict__ active) {
+  KT();
+  const int e = blockIdx.y;
+  const K* __restrict__ kin = kin2[e];
+  const uint32_t* __restrict__ vin = vin2[e];
+  K* __restrict__ kout = kout2[e];
+  uint32_t* __restrict__ vout = vout2[e];
+  const uint32_t* __restrict__ hist = ss[e].hist;
+  const uint32_t* __restrict__ tot = ss[e].tot;
+  const bool run = (uint32_t)shift < *d_nbits2[e];
+  if (active && e == 0 && blockIdx.x == 0 && threadIdx.x == 0)  // probe: any problem of the batch active
+    *active = (run || (gridDim.y > 1 && (uint32_t)shift < *d_nbits2[1])) ? 1u : 0u;
+  const uint32_t n = *d_n2[e];
   const uint32_t tile0 = blockIdx.x * SORT_TILE;
   if (!run || tile0 >= n) return;  // grids are sized for the capacity; tiles past n are empty
   __shared__ uint32_t gofs[256];     // global slot of the tile's first key of each digit
   __shared__ uint32_t tex[256];      // exclusive digit offsets inside the tile
-  __shared__ uint32_t wcnt[4][256];
-  __shared__ uint32_t sh[4];
+  __shared__ uint32_t wcnt[SW][256];
+  __shared__ uint32_t sh[SW];
   __shared__ K sk[SORT_TILE];
   __shared__ uint32_t sv[SORT_TILE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  {
-    uint32_t t;
-    gofs[tid] = block_scan_256(tot[tid], sh, &t) + hist[tid * nblocks + blockIdx.x];
-  }
-  for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
-  __syncthreads();
   const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
   K kk[SORT_CHUNKS];
   uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
@@ -130,6 +166,15 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
     kk[c] = kin[i];
     vv[c] = iota ? i : vin[i];
   }
+  {
+    uint32_t t;
+    const uint32_t g = tid < 256 ? tot[tid] : 0u;
+    const uint32_t h = tid < 256 ? hist[tid * nblocks + blockIdx.x] : 0u;
+    const uint32_t ex = scan_256_of(g, sh, &t);
+    if (tid < 256) gofs[tid] = ex + h;
+  }
+  for (uint32_t j = tid; j < SW * 256; j += ST) (&wcnt[0][0])[j] = 0;
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t i = base + c * 64 + lane;
@@ -151,13 +196,15 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
   __syncthreads();
   {  // per-wave offsets within a digit, tile digit totals, their exclusive scan
     uint32_t acc = 0;
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t t = wcnt[w][tid];
-      wcnt[w][tid] = acc;
-      acc += t;
-    }
+    if (tid < 256)
+      for (int w = 0; w < SW; ++w) {
+        const uint32_t t = wcnt[w][tid];
+        wcnt[w][tid] = acc;
+        acc += t;
+      }
     uint32_t t;
-    tex[tid] = block_scan_256(acc, sh, &t);
+    const uint32_t ex = scan_256_of(acc, sh, &t);
+    if (tid < 256) tex[tid] = ex;
   }
   __syncthreads();
 #pragma unroll
@@ -170,7 +217,7 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
   }
   __syncthreads();
   const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
-  for (uint32_t j = tid; j < m; j += T) {
+  for (uint32_t j = tid; j < m; j += ST) {
     const K k = sk[j];
     const uint32_t d = (uint32_t)(k >> shift) & 255u;
     const uint32_t pos = gofs[d] + (j - tex[d]);
@@ -179,13 +226,144 @@ __global__ void __launch_bounds__(T) k_rs_scatter(const K* __restrict__ kin, con
   }
 }
 
+// The high passes of a sort, for keys wider than the fast passes cover (octree
+// codes of very large extents), or the whole sort of keys that are normally already
+// in order (VoxelGrid's second pass; `need` = its "unsorted" flag): one workgroup per
+// problem runs the stable 8-bit LSD passes [lo_bit, nbits) over all tiles in order.
+// Slow (one CU) but a single launch that exits at once in the common case, where
+// the launches of never-needed fast passes would each cost a kernel boundary.
 template <class K>
-__global__ void k_rs_copyback(const K* __restrict__ k1, const uint32_t* __restrict__ v1, K* __restrict__ k0,
-                              uint32_t* __restrict__ v0, const uint32_t* __restrict__ d_n,
-                              const uint32_t* __restrict__ d_nbits, int max_passes) {
-  const uint32_t p = min(passes_of(*d_nbits), (uint32_t)max_passes);
+__global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B2<K*> k12, B2<uint32_t*> v12,
+                                                B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2, int lo_bit,
+                                                B2<const uint32_t*> need2) {
+  KT();
+  const int e = blockIdx.y;
+  const uint32_t nbits = *d_nbits2[e], n = *d_n2[e];
+  if ((uint32_t)lo_bit >= nbits || n < 2) return;
+  if (need2[e] && *need2[e] == 0u) return;
+  K* kb[2] = {k02[e], k12[e]};
+  uint32_t* vb[2] = {v02[e], v12[e]};
+  __shared__ uint32_t run_ofs[256], cnt[256], tex[256], tcnt[256];
+  __shared__ uint32_t wcnt[SW][256];
+  __shared__ uint32_t sh[SW];
+  __shared__ K sk[SORT_TILE];
+  __shared__ uint32_t sv[SORT_TILE];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  int src = 0;
+  for (uint32_t shift = (uint32_t)lo_bit; shift < nbits; shift += 8) {
+    const K* __restrict__ kin = kb[src];
+    const uint32_t* __restrict__ vin = vb[src];
+    K* __restrict__ kout = kb[src ^ 1];
+    uint32_t* __restrict__ vout = vb[src ^ 1];
+    if (tid < 256) cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < n; b0 += ST) {  // digit histogram of the whole array
+      const uint32_t i = b0 + tid;
+      const bool ok = i < n;
+      const uint32_t d = ok ? (uint32_t)(kin[i] >> shift) & 255u : 0u;
+      uint64_t m = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+      }
+      if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
+    }
+    __syncthreads();
+    {
+      uint32_t t;
+      const uint32_t ex = scan_256_of(tid < 256 ? cnt[tid] : 0u, sh, &t);
+      if (tid < 256) run_ofs[tid] = ex;
+    }
+    __syncthreads();
+    for (uint32_t tile0 = 0; tile0 < n; tile0 += SORT_TILE) {  // stable scatter, tile by tile
+      const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
+      K kk[SORT_CHUNKS];
+      uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
+#pragma unroll
+      for (int c = 0; c < SORT_CHUNKS; ++c) {
+        const uint32_t i = min(base + c * 64 + lane, n - 1u);
+        kk[c] = kin[i];
+        vv[c] = vin[i];
+      }
+      for (uint32_t j = tid; j < SW * 256; j += ST) (&wcnt[0][0])[j] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < SORT_CHUNKS; ++c) {
+        const uint32_t i = base + c * 64 + lane;
+        const bool ok = i < n;
+        const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
+        dg[c] = ok ? d : 256u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const bool bit = (d >> b) & 1u;
+          const uint64_t bb = __ballot(bit);
+          m &= bit ? bb : ~bb;
+        }
+        const uint32_t r = mbcnt(m);
+        const uint32_t pre = ok ? wcnt[wave][d] : 0u;
+        rk[c] = pre + r;
+        if (ok && r == 0) wcnt[wave][d] = pre + (uint32_t)__popcll(m);
+      }
+      __syncthreads();
+      {
+        uint32_t acc = 0;
+        if (tid < 256)
+          for (int w = 0; w < SW; ++w) {
+            const uint32_t t = wcnt[w][tid];
+            wcnt[w][tid] = acc;
+            acc += t;
+          }
+        if (tid < 256) tcnt[tid] = acc;
+        uint32_t t;
+        const uint32_t ex = scan_256_of(acc, sh, &t);
+        if (tid < 256) tex[tid] = ex;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < SORT_CHUNKS; ++c) {
+        const uint32_t d = dg[c];
+        if (d > 255u) continue;
+        const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
+        sk[lp] = kk[c];
+        sv[lp] = vv[c];
+      }
+      __syncthreads();
+      const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
+      for (uint32_t j = tid; j < m; j += ST) {
+        const K k = sk[j];
+        const uint32_t d = (uint32_t)(k >> shift) & 255u;
+        const uint32_t pos = run_ofs[d] + (j - tex[d]);
+        kout[pos] = k;
+        vout[pos] = sv[j];
+      }
+      __syncthreads();
+      if (tid < 256) run_ofs[tid] += tcnt[tid];
+      __syncthreads();
+    }
+    src ^= 1;
+  }
+  if (src)
+    for (uint32_t i = tid; i < n; i += ST) {
+      kb[0][i] = kb[1][i];
+      vb[0][i] = vb[1][i];
+    }
+}
+
+template <class K>
+__global__ void k_rs_copyback(B2<const K*> k12, B2<const uint32_t*> v12, B2<K*> k02, B2<uint32_t*> v02,
+                              B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2, int max_passes) {
+  KT();
+  const int e = blockIdx.y;
+  const uint32_t p = min(passes_of(*d_nbits2[e]), (uint32_t)max_passes);
   if ((p & 1u) == 0u) return;
-  const uint32_t n = *d_n;
+  const K* __restrict__ k1 = k12[e];
+  const uint32_t* __restrict__ v1 = v12[e];
+  K* __restrict__ k0 = k02[e];
+  uint32_t* __restrict__ v0 = v02[e];
+  const uint32_t n = *d_n2[e];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     k0[i] = k1[i];
     v0[i] = v1[i];
@@ -193,25 +371,36 @@ __global__ void k_rs_copyback(const K* __restrict__ k1, const uint32_t* __restri
 }
 
 template <class K>
-void radix_sort(K* k0, uint32_t* v0, K* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
-                const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
+void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n, uint32_t cap,
+                B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s, hipStream_t st,
+                int nbatch, B2<const uint32_t*> tail_need) {
   const uint32_t nb = sort_blocks(cap);
   if (nb == 0) return;
-  const int max_passes = (max_bits + 7) / 8;
-  K* kb[2] = {k0, k1};
-  uint32_t* vb[2] = {v0, v1};
-  for (int p = 0; p < max_passes; ++p) {
+  if (fast_bits == 0 && iota) throw Error(FCCF_E_INTERNAL, "radix_sort: a tail-only sort takes its values as input");
+  const int fast_passes = fast_bits / 8;
+  B2<K*> kb[2] = {k0, k1};
+  B2<uint32_t*> vb[2] = {v0, v1};
+  for (int p = 0; p < fast_passes; ++p) {
     const int shift = 8 * p;
     const int src = p & 1, dst = src ^ 1;
-    k_rs_hist<K><<<nb, T, 0, st>>>(kb[src], d_n, d_nbits, shift, s.hist, nb);
-    k_rs_rowscan<<<256, T, 0, st>>>(s.hist, nb, s.tot, d_nbits, shift);
-    FCCF_LAUNCH("k_rs_scatter", (d_n, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, nb, T, 0, st, kb[src], vb[src], kb[dst], vb[dst], d_n, d_nbits, shift, s.hist, s.tot, nb, (iota && p == 0) ? 1 : 0, _probe.active());
+    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(kb[src], d_n, d_nbits, shift, s, nb);
+    k_rs_rowscan<<<dim3(256, nbatch), T, 0, st>>>(s, nb, d_nbits, shift);
+    FCCF_LAUNCH("k_rs_scatter", (d_n[0], 2.0 * (sizeof(K) + 4), nbatch > 1 ? d_n[1] : nullptr, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, shift, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
   }
-  const uint32_t g = min(nb * 8u, 2048u);
-  k_rs_copyback<K><<<g, 256, 0, st>>>(k1, v1, k0, v0, d_n, d_nbits, max_passes);
+  if (fast_passes) {
+    const uint32_t g = min(nb * 8u, 2048u);
+    k_rs_copyback<K><<<dim3(g, nbatch), 256, 0, st>>>(B2<const K*>(k1), B2<const uint32_t*>(v1), k0, v0, d_n, d_nbits,
+                                                    fast_passes);
+  }
+  if (fast_bits < (int)(8 * sizeof(K)))
+    k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_bits, tail_need);
 }
 
 // ---------------------------------------------------------------- segments / scan
+// Two launches each: per-tile counts, then the writes.  Each write block forms its
+// tile's exclusive prefix itself from the counts of the tiles before it (a block
+// reduction over <= a few thousand words, all L2 hits), which saves the separate
+// scan-of-tile-counts launch; the block owning the last element writes the total.
 // keys[i0-1 .. i0+RS_CHUNKS] into registers, all loads issued before use
 // (clamped indices; positions outside [0, n) are masked by the callers)
 template <class K>
@@ -233,49 +422,54 @@ __device__ __forceinline__ bool head_at(const K kk[RS_CHUNKS + 2], int j, uint32
   return i == 0 || kk[j] != k;
 }
 
+// sum of blk[0 .. blockIdx.x) over the block (every thread gets it)
+__device__ __forceinline__ uint32_t tiles_before(const uint32_t* __restrict__ blk, uint32_t* sh) {
+  uint32_t v = 0;
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += T) v += blk[i];
+  uint32_t t;
+  block_scan_256(v, sh, &t);
+  return t;
+}
+
+// the block that owns the last element (block 0 when n == 0) reports the total
+__device__ __forceinline__ bool owns_last(uint32_t n) { return blockIdx.x == (n ? (n - 1u) / RS_TILE : 0u); }
+
 template <class K, bool HasInvalid>
-__global__ void __launch_bounds__(T) k_seg_count(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
-                                                 K invalid, uint32_t* __restrict__ blk) {
+__global__ void __launch_bounds__(T) k_seg_count(B2<const K*> keys2, B2<const uint32_t*> d_n2, K invalid,
+                                                 B2<SortScratch> ss, B2<const uint32_t*> run2) {
+  KT();
   __shared__ uint32_t sh[4];
-  const uint32_t n = *d_n;
+  const int e = blockIdx.y;
+  if (run2[e] && *run2[e] == 0u) return;
+  const uint32_t n = *d_n2[e];
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
   K kk[RS_CHUNKS + 2];
-  load_run<K>(keys, i0, n, kk);
+  load_run<K>(keys2[e], i0, n, kk);
   uint32_t c = 0;
 #pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) c += head_at<K, HasInvalid>(kk, j, i0 + j, n, invalid) ? 1u : 0u;
   uint32_t t;
   block_scan_256(c, sh, &t);
-  if (threadIdx.x == 0) blk[blockIdx.x] = t;
-}
-
-// single block: exclusive scan of blk[0..nb) in place, blk[nb] = total, *d_out = total
-__global__ void __launch_bounds__(T) k_scan_blocks(uint32_t* __restrict__ blk, uint32_t nb, uint32_t* __restrict__ d_out) {
-  __shared__ uint32_t sh[4];
-  uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nb; b0 += T) {
-    const uint32_t i = b0 + threadIdx.x;
-    const uint32_t v = i < nb ? blk[i] : 0u;
-    uint32_t t;
-    const uint32_t ex = block_scan_256(v, sh, &t);
-    if (i < nb) blk[i] = carry + ex;
-    carry += t;
-  }
-  if (threadIdx.x == 0) {
-    blk[nb] = carry;
-    if (d_out) *d_out = carry;
-  }
+  if (threadIdx.x == 0) ss[e].blk[blockIdx.x] = t;
 }
 
 template <class K, bool HasInvalid>
-__global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, const uint32_t* __restrict__ d_n,
-                                                 K invalid, const uint32_t* __restrict__ blk,
-                                                 uint32_t* __restrict__ starts, uint32_t* __restrict__ seg_of) {
+__global__ void __launch_bounds__(T) k_seg_write(B2<const K*> keys2, B2<const uint32_t*> d_n2, K invalid,
+                                                 B2<SortScratch> ss, B2<uint32_t*> starts2, B2<uint32_t*> d_nseg2,
+                                                 B2<uint32_t*> seg_of2, B2<const uint32_t*> run2) {
+  KT();
   __shared__ uint32_t sh[4];
-  const uint32_t n = *d_n;
+  const int e = blockIdx.y;
+  if (run2[e] && *run2[e] == 0u) return;
+  const uint32_t n = *d_n2[e];
+  if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
+  uint32_t* __restrict__ starts = starts2[e];
+  uint32_t* __restrict__ seg_of = seg_of2[e];
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
   K kk[RS_CHUNKS + 2];
-  load_run<K>(keys, i0, n, kk);
+  load_run<K>(keys2[e], i0, n, kk);
+  const uint32_t before = tiles_before(ss[e].blk, sh);
   bool h[RS_CHUNKS];
   uint32_t c = 0;
 #pragma unroll
@@ -284,7 +478,8 @@ __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, con
     c += h[j] ? 1u : 0u;
   }
   uint32_t t;
-  uint32_t pos = blk[blockIdx.x] + block_scan_256(c, sh, &t);
+  uint32_t pos = before + block_scan_256(c, sh, &t);
+  if (threadIdx.x == 0 && owns_last(n)) *d_nseg2[e] = before + t;
 #pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
     const uint32_t i = i0 + j;
@@ -300,39 +495,57 @@ __global__ void __launch_bounds__(T) k_seg_write(const K* __restrict__ keys, con
 }
 
 template <class K, bool HasInvalid>
-void segment_heads(const K* keys, const uint32_t* d_n, uint32_t cap, K invalid, uint32_t* starts, uint32_t* d_nseg,
-                   SortScratch s, hipStream_t st, uint32_t* seg_of) {
-  const uint32_t nb = rs_blocks(cap);
-  if (nb == 0) return;
-  k_seg_count<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk);
-  k_scan_blocks<<<1, T, 0, st>>>(s.blk, nb, d_nseg);
-  k_seg_write<K, HasInvalid><<<nb, T, 0, st>>>(keys, d_n, invalid, s.blk, starts, seg_of);
+void segment_heads(B2<const K*> keys, B2<const uint32_t*> d_n, uint32_t cap, K invalid, B2<uint32_t*> starts,
+                   B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st, B2<uint32_t*> seg_of, int nbatch,
+                   B2<const uint32_t*> run) {
+  const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
+  k_seg_count<K, HasInvalid><<<dim3(nb, nbatch), T, 0, st>>>(keys, d_n, invalid, s, run);
+  k_seg_write<K, HasInvalid><<<dim3(nb, nbatch), T, 0, st>>>(keys, d_n, invalid, s, starts, d_nseg, seg_of, run);
 }
 
-__global__ void __launch_bounds__(T) k_sum_tiles(const uint32_t* __restrict__ in, const uint32_t* __restrict__ d_n,
-                                                 uint32_t* __restrict__ blk) {
+__global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<const uint32_t*> d_n2,
+                                                 B2<SortScratch> ss) {
+  KT();
   __shared__ uint32_t sh[4];
-  const uint32_t n = *d_n;
-  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
-  uint32_t c = 0;
-  for (int j = 0; j < RS_CHUNKS; ++j) c += (i0 + j < n) ? in[i0 + j] : 0u;
-  uint32_t t;
-  block_scan_256(c, sh, &t);
-  if (threadIdx.x == 0) blk[blockIdx.x] = t;
-}
-
-__global__ void __launch_bounds__(T) k_scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                  const uint32_t* __restrict__ d_n, const uint32_t* __restrict__ blk) {
-  __shared__ uint32_t sh[4];
-  const uint32_t n = *d_n;
+  const int e = blockIdx.y;
+  const uint32_t n = *d_n2[e];
+  if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
+  const uint32_t* __restrict__ in = in2[e];
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
   uint32_t v[RS_CHUNKS], c = 0;
+#pragma unroll
+  for (int j = 0; j < RS_CHUNKS; ++j) v[j] = in[min(i0 + j, n ? n - 1u : 0u)];
+#pragma unroll
+  for (int j = 0; j < RS_CHUNKS; ++j) c += (i0 + j < n) ? v[j] : 0u;
+  uint32_t t;
+  block_scan_256(c, sh, &t);
+  if (threadIdx.x == 0) ss[e].blk[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<uint32_t*> out2,
+                                                  B2<const uint32_t*> d_n2, B2<SortScratch> ss,
+                                                  B2<uint32_t*> d_total2) {
+  KT();
+  __shared__ uint32_t sh[4];
+  const int e = blockIdx.y;
+  const uint32_t n = *d_n2[e];
+  if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
+  const uint32_t* __restrict__ in = in2[e];
+  uint32_t* __restrict__ out = out2[e];
+  const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
+  uint32_t v[RS_CHUNKS], c = 0;
+#pragma unroll
+  for (int j = 0; j < RS_CHUNKS; ++j) v[j] = in[min(i0 + j, n ? n - 1u : 0u)];
+#pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
-    v[j] = (i0 + j < n) ? in[i0 + j] : 0u;
+    v[j] = (i0 + j < n) ? v[j] : 0u;
     c += v[j];
   }
+  const uint32_t before = tiles_before(ss[e].blk, sh);
   uint32_t t;
-  uint32_t run = blk[blockIdx.x] + block_scan_256(c, sh, &t);
+  uint32_t run = before + block_scan_256(c, sh, &t);
+  if (threadIdx.x == 0 && owns_last(n) && d_total2[e]) *d_total2[e] = before + t;
+#pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
     if (i0 + j < n) out[i0 + j] = run;
     run += v[j];
@@ -356,29 +569,31 @@ SortScratch sort_scratch_carve(void* base, uint32_t cap) {
   return s;
 }
 
-void radix_sort_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
-                    const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
-  radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, max_bits, iota, s, st);
+void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
+                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need) {
+  radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need);
 }
-void radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, const uint32_t* d_n, uint32_t cap,
-                    const uint32_t* d_nbits, int max_bits, bool iota, SortScratch s, hipStream_t st) {
-  radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, max_bits, iota, s, st);
+void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
+                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need) {
+  radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need);
 }
-void segment_heads_u32(const uint32_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t invalid, uint32_t* starts,
-                       uint32_t* d_nseg, SortScratch s, hipStream_t st, uint32_t* seg_of) {
-  segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st, seg_of);
+void segment_heads_u32(B2<const uint32_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
+                       B2<uint32_t*> starts, B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
+                       B2<uint32_t*> seg_of, int nbatch, B2<const uint32_t*> run) {
+  segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st, seg_of, nbatch, run);
 }
-void segment_heads_u64(const uint64_t* keys, const uint32_t* d_n, uint32_t cap, uint32_t* starts, uint32_t* d_nseg,
-                       SortScratch s, hipStream_t st, uint32_t* seg_of) {
-  segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st, seg_of);
+void segment_heads_u64(B2<const uint64_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, B2<uint32_t*> starts,
+                       B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st, B2<uint32_t*> seg_of, int nbatch) {
+  segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st, seg_of, nbatch,
+                                B2<const uint32_t*>(nullptr));
 }
-void exclusive_scan_u32(const uint32_t* in, uint32_t* out, const uint32_t* d_n, uint32_t cap, uint32_t* d_total,
-                        SortScratch s, hipStream_t st) {
-  const uint32_t nb = rs_blocks(cap);
-  if (nb == 0) return;
-  k_sum_tiles<<<nb, T, 0, st>>>(in, d_n, s.blk);
-  k_scan_blocks<<<1, T, 0, st>>>(s.blk, nb, d_total);
-  k_scan_tiles<<<nb, T, 0, st>>>(in, out, d_n, s.blk);
+void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
+                        B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch) {
+  const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
+  k_sum_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, d_n, s);
+  k_scan_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, out, d_n, s, d_total);
 }
 
 }  // namespace fccf

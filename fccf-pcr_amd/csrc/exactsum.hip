@@ -9,6 +9,7 @@
 //                a group that crosses a binade, then a plain replay of the chunk
 // The first four are bandwidth-bound streaming passes over the inputs; the chain
 // costs one wave scan per binade crossing (plus one 256-add replay).
+#define KT_TU 4  // ktrace.h source tag
 #include "probe.h"
 #include "devprim.h"
 #include "exactsum.h"
@@ -109,6 +110,7 @@ __device__ __forceinline__ void load4(const Prob& P, uint32_t c, int lane, int K
 
 template <int S>
 __global__ void __launch_bounds__(256) k_xs_csum(XsIn in, int K, double* __restrict__ pre, uint32_t NC) {
+  KT();
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   const Prob P = prob_of(in, S, b);
   for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < P.nch; c += gridDim.x * 4) {
@@ -129,6 +131,7 @@ __global__ void __launch_bounds__(256) k_xs_csum(XsIn in, int K, double* __restr
 
 // in-place: pre[row][1..nch] chunk sums -> pre[row][0..nch] exclusive prefix
 __global__ void __launch_bounds__(256) k_xs_prefix(XsIn in, int K, double* __restrict__ pre, uint32_t NC) {
+  KT();
   __shared__ double sh[256];
   const int row = blockIdx.x, t = threadIdx.x;
   const uint32_t nch = (prob_n(in, row / K) + XS_L - 1) / XS_L;
@@ -156,6 +159,7 @@ __global__ void __launch_bounds__(256) k_xs_prefix(XsIn in, int K, double* __res
 template <int S>
 __global__ void __launch_bounds__(256) k_xs_chunk(XsIn in, int K, const double* __restrict__ pre,
                                                   XsSum* __restrict__ ctab, int32_t* __restrict__ cE, uint32_t NC) {
+  KT();
   const int b = blockIdx.y, lane = threadIdx.x & 63;
   const Prob P = prob_of(in, S, b);
   for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < P.nch; c += gridDim.x * 4) {
@@ -186,6 +190,7 @@ __global__ void __launch_bounds__(256) k_xs_group(XsIn in, int K, const double* 
                                                   const XsSum* __restrict__ ctab, const int32_t* __restrict__ cE,
                                                   XsSum* __restrict__ gtab, int32_t* __restrict__ gE, uint32_t NC,
                                                   uint32_t NG) {
+  KT();
   const size_t row = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const uint32_t nch = (prob_n(in, (int)(row / K)) + XS_L - 1) / XS_L;
@@ -276,6 +281,7 @@ __global__ void __launch_bounds__(64) k_xs_chain(XsIn in, int K, const XsSum* __
                                                  const int32_t* __restrict__ cE, const XsSum* __restrict__ gtab,
                                                  const int32_t* __restrict__ gE, uint32_t NC, uint32_t NG,
                                                  float* __restrict__ out, int divide) {
+  KT();
   const int row = blockIdx.x, lane = threadIdx.x;
   const int b = row / K, k = row % K;
   const Prob P = prob_of(in, S, b);

@@ -12,6 +12,7 @@
 //  * compaction: planar leaves (Morton order) and the residual cloud cloud_sub
 //    (points of non-planar leaves, Morton then index order, :527-530).
 // Sums run over each leaf's points in ascending index, the reference's order.
+#define KT_TU 3  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
 
@@ -25,13 +26,14 @@ namespace {
 // points each (all loads issued before use), quad shuffles for the sub-record,
 // then the wave / block reduction for the block record.
 // Batched over blockIdx.y = sequence e.
-__global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
-                                                    float* __restrict__ aggr0, size_t xyz_stride, size_t aggr_stride,
+__global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n0,
+                                                    float* __restrict__ aggr0, SeqStrides sd,
                                                     uint32_t nbc) {
+  KT();
   __shared__ float sh[4][6];
-  const uint32_t n = *d_n;
-  const float* xyz = xyz0 + blockIdx.y * xyz_stride;
-  float* aggr = aggr0 + blockIdx.y * aggr_stride;
+  const float* xyz = sd.at(xyz0, sd.xyz, blockIdx.y);
+  float* aggr = sd.at(aggr0, sd.aggr, blockIdx.y);
+  const uint32_t n = *sd.at(d_n0, sd.n, blockIdx.y);
   float* sub = aggr + 6 * (size_t)nbc;
   const uint32_t t = threadIdx.x, sb = t >> 2, q = t & 3, lane = t & 63, w = t >> 6;
   const uint32_t p0 = blockIdx.x * AGGR_BLOCK + sb * AGGR_SUB + q * 16;
@@ -100,16 +102,16 @@ __device__ __forceinline__ bool may_violate(const OctState& S, const Box6& b) {
 // after each adoption the lanes re-test what they hold with one ballot, so memory is
 // touched only when the wave moves to a new block or sub-block, and every lane
 // replays the adoption itself (the state stays uniform without broadcasts).
-__global__ void __launch_bounds__(64) k_oct_sim(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n,
+__global__ void __launch_bounds__(64) k_oct_sim(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n0,
                                                 const float* __restrict__ aggr0, double res,
-                                                OctState* __restrict__ state0, size_t xyz_stride,
-                                                size_t aggr_stride, uint32_t nbc) {
+                                                OctState* __restrict__ state0, SeqStrides sd, uint32_t nbc) {
+  KT();
   const uint32_t lane = threadIdx.x;
-  const uint32_t n = *d_n;
-  const float* xyz = xyz0 + blockIdx.x * xyz_stride;
-  const float* aggr = aggr0 + blockIdx.x * aggr_stride;
+  const float* xyz = sd.at(xyz0, sd.xyz, blockIdx.x);
+  const float* aggr = sd.at(aggr0, sd.aggr, blockIdx.x);
+  const uint32_t n = *sd.at(d_n0, sd.n, blockIdx.x);
   const float* sub = aggr + 6 * (size_t)nbc;
-  OctState* state = state0 + blockIdx.x;
+  OctState* state = sd.at(state0, sd.state, blockIdx.x);
   OctState S = *state;
   const uint32_t nblk = (n + AGGR_BLOCK - 1) / AGGR_BLOCK;
   uint32_t pos = 0;  // points before pos are done
@@ -155,11 +157,16 @@ __global__ void __launch_bounds__(64) k_oct_sim(const float* __restrict__ xyz0, 
   if (lane == 0) *state = S;
 }
 
-__global__ void __launch_bounds__(256) k_oct_codes(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                                   const OctState* __restrict__ state, double res,
-                                                   uint64_t* __restrict__ codes, uint32_t* __restrict__ d_nbits) {
-  const OctState S = *state;
-  const uint32_t n = *d_n;
+__global__ void __launch_bounds__(256) k_oct_codes(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
+                                                   B2<const OctState*> state2, double res, B2<uint64_t*> codes2,
+                                                   B2<uint32_t*> d_nbits2) {
+  KT();
+  const int e = blockIdx.y;
+  const OctState S = *state2[e];
+  const uint32_t n = *d_n2[e];
+  const float* __restrict__ xyz = xyz2[e];
+  uint64_t* __restrict__ codes = codes2[e];
+  uint32_t* __restrict__ d_nbits = d_nbits2[e];
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
   if (gid == 0) *d_nbits = S.defined ? 3u * S.depth + 1u : 1u;
   for (uint32_t i = gid; i < n; i += gridDim.x * 256) {
@@ -238,9 +245,14 @@ __device__ void eig_min(const float A[3][3], float& ev, f3& v) {
 
 // Points in leaf order (Morton, then index): the per-leaf loops below then read
 // contiguous memory instead of gathering through the sort permutation.
-__global__ void __launch_bounds__(256) k_gather(const float* __restrict__ xyz, const uint32_t* __restrict__ vals,
-                                                const uint32_t* __restrict__ d_n, float* __restrict__ sp) {
-  const uint32_t n = *d_n;
+__global__ void __launch_bounds__(256) k_gather(B2<const float*> xyz2, B2<const uint32_t*> vals2,
+                                                B2<const uint32_t*> d_n2, B2<float*> sp2) {
+  KT();
+  const int e = blockIdx.y;
+  const uint32_t n = *d_n2[e];
+  const float* __restrict__ xyz = xyz2[e];
+  const uint32_t* __restrict__ vals = vals2[e];
+  float* __restrict__ sp = sp2[e];
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
     const uint32_t j = vals[k];
     sp[3 * k] = xyz[3 * j]; sp[3 * k + 1] = xyz[3 * j + 1]; sp[3 * k + 2] = xyz[3 * j + 2];
@@ -253,13 +265,17 @@ __global__ void __launch_bounds__(256) k_gather(const float* __restrict__ xyz, c
 // LDS as (x, y, z, 1) so every lane computes term = p[i1] * p[i2] (the linear sums
 // use i2 = w = 1, and x * 1 == x exactly).  compute3DCentroid (:490) is the same
 // sequential x/y/z sum divided by n, i.e. accumulators 6..8 / n bit-for-bit.
-__global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ sp, const uint32_t* __restrict__ starts,
-                                                   const uint32_t* __restrict__ d_nleaf, float vpt, float cthr,
-                                                   VoxRec* __restrict__ recs, uint32_t* __restrict__ planar,
-                                                   uint32_t* __restrict__ resid) {
+__global__ void __launch_bounds__(256) k_voxel_fit(B2<FaceBufs> fb, float vpt, float cthr) {
+  KT();
   __shared__ __attribute__((aligned(16))) float pts[4][64 * 4];
+  const FaceBufs& B = fb.v[blockIdx.y];
+  const float* __restrict__ sp = B.sp;
+  const uint32_t* __restrict__ starts = B.starts;
+  VoxRec* __restrict__ recs = B.recs;
+  uint32_t* __restrict__ planar = B.flag_planar;
+  uint32_t* __restrict__ resid = B.resid_cnt;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t nl = *d_nleaf;
+  const uint32_t nl = *B.nleaf;
   const int i1t[16] = {0, 0, 0, 1, 1, 2, 0, 1, 2, 0, 0, 0, 0, 0, 0, 0};
   const int i2t[16] = {0, 1, 2, 1, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3};
   const int i1 = i1t[lane & 15], i2 = i2t[lane & 15];
@@ -331,12 +347,17 @@ __global__ void __launch_bounds__(256) k_voxel_fit(const float* __restrict__ sp,
 }
 
 // cloud_sub (:527-530): every point of a non-planar leaf, leaf order then index order.
-__global__ void __launch_bounds__(256) k_compact_resid(const float* __restrict__ sp, const uint32_t* __restrict__ d_n,
-                                                       const uint32_t* __restrict__ seg_of,
-                                                       const uint32_t* __restrict__ starts,
-                                                       const uint32_t* __restrict__ resid,
-                                                       const uint32_t* __restrict__ roff, float* __restrict__ rout) {
-  const uint32_t n = *d_n;
+__global__ void __launch_bounds__(256) k_compact_resid(B2<FaceBufs> fb, B2<const uint32_t*> d_n2, B2<float*> rout2) {
+  KT();
+  const int e = blockIdx.y;
+  const FaceBufs& B = fb.v[e];
+  const float* __restrict__ sp = B.sp;
+  const uint32_t* __restrict__ seg_of = B.seg_of;
+  const uint32_t* __restrict__ starts = B.starts;
+  const uint32_t* __restrict__ resid = B.resid_cnt;
+  const uint32_t* __restrict__ roff = B.resid_off;
+  float* __restrict__ rout = rout2[e];
+  const uint32_t n = *d_n2[e];
   for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
     const uint32_t s = seg_of[k];
     if (!resid[s]) continue;
@@ -346,12 +367,16 @@ __global__ void __launch_bounds__(256) k_compact_resid(const float* __restrict__
 }
 
 // Planar leaves with the normal oriented towards the cloud centroid (:504-516).
-__global__ void __launch_bounds__(256) k_compact_planar(const uint32_t* __restrict__ d_nleaf,
-                                                        const VoxRec* __restrict__ recs,
-                                                        const uint32_t* __restrict__ planar,
-                                                        const uint32_t* __restrict__ poff, const float* __restrict__ cc,
-                                                        VoxRec* __restrict__ pout) {
-  const uint32_t nl = *d_nleaf;
+__global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxRec*> pout2) {
+  KT();
+  const int e = blockIdx.y;
+  const FaceBufs& B = fb.v[e];
+  const VoxRec* __restrict__ recs = B.recs;
+  const uint32_t* __restrict__ planar = B.flag_planar;
+  const uint32_t* __restrict__ poff = B.planar_off;
+  const float* __restrict__ cc = B.centroid;
+  VoxRec* __restrict__ pout = pout2[e];
+  const uint32_t nl = *B.nleaf;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
     if (!planar[s]) continue;
     VoxRec r = recs[s];
@@ -362,12 +387,13 @@ __global__ void __launch_bounds__(256) k_compact_planar(const uint32_t* __restri
   }
 }
 
-__global__ void k_oct_reset(OctState* s) {
+__global__ void k_oct_reset(B2<OctState*> s) {
+  KT();
   OctState z;
   for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
   z.depth = 0;
   z.defined = 0;
-  *s = z;
+  *s[threadIdx.x] = z;
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -379,46 +405,79 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
-                size_t xyz_stride, size_t aggr_stride) {
+                SeqStrides sd) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, xyz_stride, aggr_stride, aggr_blocks(cap));
+  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap));
 }
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
-                hipStream_t st, int batch, size_t xyz_stride, size_t aggr_stride) {
-  FCCF_LAUNCH("k_oct_sim", (d_n, 24.0 * batch / AGGR_BLOCK), k_oct_sim, batch, 64, 0, st, xyz, d_n, aggr, res, state, xyz_stride, aggr_stride, aggr_blocks(cap));
+                hipStream_t st, int batch, SeqStrides sd) {
+  FCCF_LAUNCH("k_oct_sim", (d_n, 24.0 * batch / AGGR_BLOCK), k_oct_sim, batch, 64, 0, st, xyz, d_n, aggr, res, state, sd, aggr_blocks(cap));
 }
 
-void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
-                         hipStream_t st) {
-  k_oct_reset<<<1, 1, 0, st>>>(b.oct);
-  block_aggr(xyz, d_n, cap, b.aggr, st);
-  octree_sim(xyz, d_n, cap, res, b.aggr, b.oct, st);
-  k_oct_codes<<<grid_for(cap), 256, 0, st>>>(xyz, d_n, b.oct, res, b.c0, b.nbits);
-  radix_sort_u64(b.c0, b.v0, b.c1, b.v1, d_n, cap, b.nbits, 64, true, b.ss, st);
-  segment_heads_u64(b.c0, d_n, cap, b.starts, b.nleaf, b.ss, st, b.seg_of);
-  FCCF_LAUNCH("k_gather", (d_n, 28.0), k_gather, grid_for(cap), 256, 0, st, xyz, b.v0, d_n, b.sp);
+namespace {
+template <class T>
+size_t byte_stride(const B2<T*>& p, int nbatch) {
+  return nbatch > 1 ? (size_t)((const char*)p[1] - (const char*)p[0]) : 0;
+}
+template <class F>
+auto pick(const B2<FaceBufs>& b, F get) -> B2<decltype(get(b[0]))> {
+  return B2<decltype(get(b[0]))>(get(b[0]), get(b[1]));
+}
+}  // namespace
+
+void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, double res, B2<FaceBufs> b,
+                         hipStream_t st, int nbatch) {
+  const B2<OctState*> oct = pick(b, [](const FaceBufs& f) { return f.oct; });
+  const B2<float*> aggr = pick(b, [](const FaceBufs& f) { return f.aggr; });
+  SeqStrides sd;
+  sd.xyz = byte_stride(xyz, nbatch);
+  sd.aggr = byte_stride(aggr, nbatch);
+  sd.state = byte_stride(oct, nbatch);
+  sd.n = byte_stride(d_n, nbatch);
+  k_oct_reset<<<1, nbatch, 0, st>>>(oct);
+  block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd);
+  octree_sim(xyz[0], d_n[0], cap, res, aggr[0], oct[0], st, nbatch, sd);
+  const B2<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
+  const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
+  const B2<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
+  k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B2<const OctState*>(oct), res, c0, nbits);
+  // codes are 3 bits per octree level (+1): 4 fast passes cover depth <= 10, i.e.
+  // extents up to ~1000 x face_voxel_size; deeper trees finish in the tail launch
+  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 32, true,
+                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch);
+  segment_heads_u64(B2<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
+                    pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
+                    st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
+  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
+  FCCF_LAUNCH("k_gather", (d_n[0], 28.0, n2, 28.0), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B2<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
 }
 
-void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float vpt, float cthr, float* resid_out,
-                     FaceBufs b, hipStream_t st) {
-  (void)xyz;
-  FCCF_LAUNCH("k_voxel_fit", (d_n, 12.0, b.nleaf, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, grid_for(cap, 4, 4096), 256, 0, st, b.sp, b.starts, b.nleaf, vpt, cthr, b.recs, b.flag_planar, b.resid_cnt);
-  exclusive_scan_u32(b.flag_planar, b.planar_off, b.nleaf, cap, b.nplanar, b.ss, st);
-  exclusive_scan_u32(b.resid_cnt, b.resid_off, b.nleaf, cap, b.nresid, b.ss, st);
-  k_compact_resid<<<grid_for(cap), 256, 0, st>>>(b.sp, d_n, b.seg_of, b.starts, b.resid_cnt, b.resid_off, resid_out);
+void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float vpt, float cthr, B2<float*> resid_out,
+                     B2<FaceBufs> b, hipStream_t st, int nbatch) {
+  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
+  const uint32_t* l2 = nbatch > 1 ? b[1].nleaf : nullptr;
+  FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, 4096), nbatch), 256, 0, st, b, vpt, cthr);
+  const B2<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
+  const B2<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
+  exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
+                     pick(b, [](const FaceBufs& f) { return f.planar_off; }), nleaf, cap,
+                     pick(b, [](const FaceBufs& f) { return f.nplanar; }), ss, st, nbatch);
+  exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.resid_cnt; }),
+                     pick(b, [](const FaceBufs& f) { return f.resid_off; }), nleaf, cap,
+                     pick(b, [](const FaceBufs& f) { return f.nresid; }), ss, st, nbatch);
+  k_compact_resid<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, d_n, resid_out);
 }
 
 void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
                    hipStream_t st) {
-  k_oct_reset<<<1, 1, 0, st>>>(state);
+  k_oct_reset<<<1, 1, 0, st>>>(B2<OctState*>(state));
   block_aggr(xyz, d_n, cap, aggr, st);
   octree_sim(xyz, d_n, cap, res, aggr, state, st);
 }
 
-void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_t st) {
-  k_compact_planar<<<grid_for(cap), 256, 0, st>>>(b.nleaf, b.recs, b.flag_planar, b.planar_off, b.centroid,
-                                                  planar_out);
+void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch) {
+  k_compact_planar<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, planar_out);
 }
 
 }  // namespace fccf

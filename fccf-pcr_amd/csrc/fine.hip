@@ -8,6 +8,7 @@
 // score = similar / allinvec.  The S1 half of the octree bound replay is shared by
 // all evaluations.  Sort key = (e | morton | is_target); counts are exact integers,
 // the two float sums run in the reference's leaf order (one lane per evaluation).
+#define KT_TU 5  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
 #include "match.h"
@@ -17,6 +18,7 @@ namespace {
 
 __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ s2, uint32_t n2,
                                                       const m44* __restrict__ T, float* __restrict__ s2t) {
+  KT();
   const int e = blockIdx.y;
   const m44 M = T[e];
   float* o = s2t + (size_t)e * 3 * n2;
@@ -29,6 +31,7 @@ __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ 
 // every evaluation's octree starts from the bounds after S1 (the fused cloud is S1 ++ T_e S2)
 __global__ void k_fv_init(const OctState* __restrict__ s1_state, OctState* st, int E, uint32_t* scal, uint32_t n1,
                           uint32_t n2) {
+  KT();
   const int e = threadIdx.x;
   if (e < E) st[e] = *s1_state;
   if (e == 0) {
@@ -41,6 +44,7 @@ __global__ void k_fv_init(const OctState* __restrict__ s1_state, OctState* st, i
 // scal: [0] total keys, [1] nbits, [3] shift = 3*Dmax+1, [4] n1, [5] n2, [6] E
 __global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict__ scal, uint32_t* __restrict__ range,
                           uint32_t n1, uint32_t n2, int E) {
+  KT();
   if (threadIdx.x != 0) return;
   uint32_t D = 0;
   for (int e = 0; e < E; ++e)
@@ -60,6 +64,7 @@ __global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict_
 __global__ void __launch_bounds__(256) k_fv_keys(const float* __restrict__ s1, const float* __restrict__ s2t,
                                                  const OctState* __restrict__ st, const uint32_t* __restrict__ scal,
                                                  double res, uint64_t* __restrict__ keys) {
+  KT();
   const int e = blockIdx.y;
   const OctState S = st[e];
   const uint32_t n1 = scal[4], n2 = scal[5], shift = scal[3];
@@ -78,6 +83,7 @@ __global__ void __launch_bounds__(256) k_fv_keys(const float* __restrict__ s1, c
 
 __global__ void __launch_bounds__(256) k_fv_leafkeys(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ scal,
                                                      uint64_t* __restrict__ vk) {
+  KT();
   const uint32_t n = scal[0];
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint64_t k = keys[i];
@@ -92,6 +98,7 @@ __global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ starts,
                                                    const uint32_t* __restrict__ scal, float* __restrict__ term,
                                                    uint32_t* __restrict__ range) {
+  KT();
   const uint32_t ns = scal[2], sh = scal[3] - 1u;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
     const uint32_t b = starts[s], e = starts[s + 1];
@@ -121,6 +128,7 @@ __global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ 
 // integer counts is exact below 2^24, so it equals the integer point count.
 __global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __restrict__ range,
                             uint32_t* __restrict__ nseg_e, float* __restrict__ all, uint32_t* __restrict__ scal, int E) {
+  KT();
   const int e = threadIdx.x;
   if (e >= E) return;
   const uint32_t f = range[2 * e], l = range[2 * e + 1];
@@ -133,6 +141,7 @@ __global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __res
 
 __global__ void k_fv_score(const float* __restrict__ similar, const float* __restrict__ all, float* __restrict__ scores,
                            int E) {
+  KT();
   const int e = threadIdx.x;
   if (e < E) scores[e] = similar[e] / all[e];
 }
@@ -152,12 +161,17 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   k_fv_init<<<1, 64, 0, st>>>(s1_state, b.state, E, b.scal, n1, n2);
   // scal[5] holds n2 for the device-count interfaces
   uint32_t* d_n2 = b.scal + 5;
-  block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, 3 * (size_t)n2, astride);
-  octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, 3 * (size_t)n2, astride);
+  SeqStrides sd;  // evaluation e: its own transformed S2 copy, aggregates and state; shared count
+  sd.xyz = 12 * (size_t)n2;
+  sd.aggr = 4 * astride;
+  sd.state = sizeof(OctState);
+  block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
+  octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, sd);
   k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, n1, n2, E);
   const uint32_t n = (uint32_t)E * (n1 + n2);
   k_fv_keys<<<dim3(grid_for(n1 + n2, 256, 1024), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0);
-  radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 64, true, b.ss, st);
+  // (e | morton | is_target): 4 fast passes cover depth <= 9 with <= 15 evaluations
+  radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 32, true, b.ss, st);
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
   FCCF_LAUNCH("k_fv_counts", (b.scal, 16.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.k1, b.starts, b.scal, b.term, b.range);

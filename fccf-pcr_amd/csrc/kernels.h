@@ -39,8 +39,9 @@ struct VGBufs {
 // driver's second pass over main's output (:1377-1387 after :1668-1678).  A check
 // kernel then skips the radix passes when the keys are already strictly increasing
 // (every leaf holds one point), which leaves the result unchanged.
-void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf, float* out, uint32_t* d_m,
-                VGBufs b, hipStream_t st, bool presorted = false);
+// nbatch = 2 runs both clouds (argument pairs, blockIdx.y = cloud) in the same launches.
+void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted = false, int nbatch = 1);
 
 // ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
 struct VoxRec {  // one occupied octree leaf, Morton order
@@ -71,25 +72,38 @@ struct FaceBufs {
   SortScratch ss;
 };
 
-// Octree leaves + per-leaf plane fit + compaction.  `centroid` must be ready
-// before the fit kernel runs (the caller orders the streams).
-void face_voxels_prepare(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, FaceBufs b,
-                         hipStream_t st);
+// Octree leaves (Morton order) of each cloud of the batch.  Batched clouds must be
+// carved identically: every pointer of cloud 1 sits `stride` bytes after cloud 0's.
+void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, double res, B2<FaceBufs> b,
+                         hipStream_t st, int nbatch = 1);
 // Per-leaf fit, planar/residual flags and the residual cloud.
-void face_voxels_fit(const float* xyz, const uint32_t* d_n, uint32_t cap, float voxel_point_threshold,
-                     float curvature_threshold, float* resid_out, FaceBufs b, hipStream_t st);
+void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float voxel_point_threshold, float curvature_threshold, B2<float*> resid_out,
+                     B2<FaceBufs> b, hipStream_t st, int nbatch = 1);
 // Planar records, oriented towards b.centroid (must be ready: the caller orders streams).
-void face_voxels_orient(uint32_t cap, VoxRec* planar_out, FaceBufs b, hipStream_t st);
+void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch = 1);
 
+// Byte strides between the sequences of a batched octree launch: sequence e uses
+// xyz + e*xyz, aggr + e*aggr, state + e*state, d_n + e*n (bytes; 0 = shared).
+struct SeqStrides {
+  size_t xyz = 0, aggr = 0, state = 0, n = 0;
+  template <class T>
+  __host__ __device__ static T* at(T* p, size_t stride, uint32_t e) {
+    return (T*)((char*)p + stride * e);
+  }
+  template <class T>
+  __host__ __device__ static const T* at(const T* p, size_t stride, uint32_t e) {
+    return (const T*)((const char*)p + stride * e);
+  }
+};
 // Octree bound simulation over xyz[0..*d_n) starting from *state (one workgroup per
-// sequence; `batch` sequences at xyz + e*xyz_stride with state[e]).
+// sequence; `batch` sequences laid out by `sd`).
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr,
-                OctState* state, hipStream_t st, int batch = 1, size_t xyz_stride = 0, size_t aggr_stride = 0);
+                OctState* state, hipStream_t st, int batch = 1, SeqStrides sd = SeqStrides());
 // Fresh octree bounds replayed over xyz[0..*d_n) (aggr: aggr_floats(cap) floats).
 void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
                    hipStream_t st);
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
-                size_t xyz_stride = 0, size_t aggr_stride = 0);
+                SeqStrides sd = SeqStrides());
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
 constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
 // aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per

@@ -8,6 +8,7 @@
 // per-type exclusive scan -> write, so each type's list is in exactly the order
 // transformation_vecter[type] receives push_backs.  The plane/pair tables (<= 16
 // planes, <= 120 pairs per cloud) live in LDS.
+#define KT_TU 6  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
 #include "match.h"
@@ -147,6 +148,7 @@ __device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
 
 __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__ Mp, uint32_t* __restrict__ cnt,
                                                      int32_t* __restrict__ type) {
+  KT();
   __shared__ MatchIn M;
   if (threadIdx.x == 0) M = *Mp;
   __syncthreads();
@@ -164,6 +166,7 @@ __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__
 __global__ void __launch_bounds__(256) k_match_scan(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ type, uint32_t* __restrict__ off,
                                                     uint32_t* __restrict__ totals) {
+  KT();
   __shared__ uint32_t sh[4][3];
   const int K = Mp->nB1 * Mp->nB2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -199,6 +202,7 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
                                                     MCand* __restrict__ c0, MCand* __restrict__ c1,
                                                     MCand* __restrict__ c2, QTd* __restrict__ q0,
                                                     QTd* __restrict__ q1, QTd* __restrict__ q2) {
+  KT();
   __shared__ MatchIn M;
   if (threadIdx.x == 0) M = *Mp;
   __syncthreads();

@@ -10,6 +10,7 @@
 // Cloud roles follow the reference's swapped call (FCCF.cpp:1683): driver
 // "source" (index 0 here, F1/S1) is the TAR file, driver "target" (index 1, F2/S2)
 // is the SRC file; the output T maps src-file points into the tar frame.
+#define KT_TU 7  // ktrace.h source tag
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,16 +36,24 @@ using clk = std::chrono::steady_clock;
 double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); }
 
 // ------------------------------------------------------------ remove-NaN (:1374-1375)
-__global__ void k_finite_flags(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                               uint32_t* __restrict__ f) {
-  const uint32_t n = *d_n;
+__global__ void k_finite_flags(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<uint32_t*> f2) {
+  KT();
+  const int e = blockIdx.y;
+  const float* __restrict__ xyz = xyz2[e];
+  uint32_t* __restrict__ f = f2[e];
+  const uint32_t n = *d_n2[e];
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
     f[i] = finite3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]) ? 1u : 0u;
 }
-__global__ void k_finite_scatter(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                 const uint32_t* __restrict__ f, const uint32_t* __restrict__ off,
-                                 float* __restrict__ out) {
-  const uint32_t n = *d_n;
+__global__ void k_finite_scatter(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<const uint32_t*> f2,
+                                 B2<const uint32_t*> off2, B2<float*> out2) {
+  KT();
+  const int e = blockIdx.y;
+  const float* __restrict__ xyz = xyz2[e];
+  const uint32_t* __restrict__ f = f2[e];
+  const uint32_t* __restrict__ off = off2[e];
+  float* __restrict__ out = out2[e];
+  const uint32_t n = *d_n2[e];
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
     if (f[i]) {
       const uint32_t o = off[i];
@@ -182,26 +191,46 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.fstate = a.take_n<OctState>(1);
 }
 
-// Device part of one cloud, in two stream segments (each replayed as a graph):
-//   A  (main)  both VoxelGrid passes with remove-NaN between them
-//   F  (main)  octree leaves, per-leaf fit, residual cloud, after A
-// plus, on the side stream after both clouds' A, one graph summing both cloud
-// centroids (the sequential compute3DCentroid sums, six rows in one launch set),
-// and the planar compaction, which orients normals towards the centroid.
-void seg_downsample(CloudWS& w, float leaf, hipStream_t st) {
-  voxel_grid(w.in, w.sc, w.cap, leaf, w.ds1, w.sc + 1, w.vg, st);  // main :1668-1678
-  k_finite_flags<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag);  // driver :1374-1375
-  exclusive_scan_u32(w.fflag, w.foff, w.sc + 1, w.cap, w.sc + 2, w.vg.ss, st);
-  k_finite_scatter<<<grid_for(w.cap), 256, 0, st>>>(w.ds1, w.sc + 1, w.fflag, w.foff, w.ds1f);
-  voxel_grid(w.ds1f, w.sc + 2, w.cap, leaf, w.ds2, w.sc + 3, w.vg, st, true);  // driver :1377-1387
+// Device part of both clouds of a pair, batched (blockIdx.y = cloud, both clouds
+// carved identically) in two graph segments on one stream:
+//   A  both VoxelGrid passes with remove-NaN between them
+//   F  octree leaves, per-leaf fit, residual cloud, after A
+// plus, on the side stream after A, one graph summing both cloud centroids (the
+// sequential compute3DCentroid sums, six rows in one launch set), and the planar
+// compaction, which orients normals towards the centroid, after F and the sums.
+template <class T, class F>
+B2<T> both(const CloudWS* w, F get) { return B2<T>(get(w[0]), get(w[1])); }
+
+void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
+  const uint32_t cap = w[0].cap;
+  auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
+  const B2<VGBufs> vg(w[0].vg, w[1].vg);
+  const B2<float*> ds1 = both<float*>(w, [](const CloudWS& c) { return c.ds1; });
+  const B2<float*> ds1f = both<float*>(w, [](const CloudWS& c) { return c.ds1f; });
+  const B2<uint32_t*> fflag = both<uint32_t*>(w, [](const CloudWS& c) { return c.fflag; });
+  voxel_grid(both<const float*>(w, [](const CloudWS& c) { return c.in; }), sc(0), cap, leaf, ds1, sc(1), vg, st,
+             false, 2);  // main :1668-1678
+  k_finite_flags<<<dim3(grid_for(cap), 2), 256, 0, st>>>(B2<const float*>(ds1), sc(1), fflag);  // driver :1374-1375
+  exclusive_scan_u32(B2<const uint32_t*>(fflag), both<uint32_t*>(w, [](const CloudWS& c) { return c.foff; }), sc(1),
+                     cap, sc(2), B2<SortScratch>(w[0].vg.ss, w[1].vg.ss), st, 2);
+  k_finite_scatter<<<dim3(grid_for(cap), 2), 256, 0, st>>>(
+      B2<const float*>(ds1), sc(1), B2<const uint32_t*>(fflag),
+      both<const uint32_t*>(w, [](const CloudWS& c) { return (const uint32_t*)c.foff; }), ds1f);
+  voxel_grid(B2<const float*>(ds1f), sc(2), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds2; }), sc(3),
+             vg, st, true, 2);  // driver :1377-1387
 }
-void seg_faces(CloudWS& w, const fccf_params& P, hipStream_t st, bool s1) {
-  face_voxels_prepare(w.ds2, w.sc + 3, w.cap, (double)P.face_voxel_size, w.fb, st);
-  face_voxels_fit(w.ds2, w.sc + 3, w.cap, P.voxel_point_threshold, P.curvature_threshold, w.resid, w.fb, st);
+void seg_faces(CloudWS* w, const fccf_params& P, hipStream_t st) {
+  const uint32_t cap = w[0].cap;
+  const B2<FaceBufs> fb(w[0].fb, w[1].fb);
+  const B2<const uint32_t*> m2(w[0].sc + 3, w[1].sc + 3);
+  face_voxels_prepare(both<const float*>(w, [](const CloudWS& c) { return (const float*)c.ds2; }), m2, cap,
+                      (double)P.face_voxel_size, fb, st, 2);
+  face_voxels_fit(m2, cap, P.voxel_point_threshold, P.curvature_threshold,
+                  both<float*>(w, [](const CloudWS& c) { return c.resid; }), fb, st, 2);
   // the residual cloud of the driver source is fine_verify's S1 (:788-805): its
   // octree bounds do not depend on any candidate, so they are replayed here,
   // overlapping the host stages that produce the candidates
-  if (s1) octree_replay(w.resid, w.fb.nresid, w.cap, (double)P.fine_verify_voxel_size, w.faggr, w.fstate, st);
+  octree_replay(w[0].resid, w[0].fb.nresid, cap, (double)P.fine_verify_voxel_size, w[0].faggr, w[0].fstate, st);
 }
 
 template <class T>
@@ -229,7 +258,7 @@ namespace {
 
 // Development timing of the cloud-stage segments (FCCF_SEG_TIMING).
 struct SegTimer {
-  hipEvent_t ev[11] = {};
+  hipEvent_t ev[5] = {};
   bool armed = false;
 };
 SegTimer& seg_timer(int s) {
@@ -242,12 +271,13 @@ void seg_timer_print(int s) {
   SegTimer& t = seg_timer(s);
   if (!t.armed) return;
   t.armed = false;
-  HIP_CHECK(hipEventSynchronize(t.ev[10]));
-  HIP_CHECK(hipEventSynchronize(t.ev[5]));
-  float v[11];
-  for (int i = 1; i < 11; ++i) HIP_CHECK(hipEventElapsedTime(&v[i], t.ev[0], t.ev[i]));
-  std::fprintf(stderr, "seg us (from fork): c0 ds %.0f-%.0f faces ->%.0f orient ->%.0f | c1 ds %.0f-%.0f faces ->%.0f orient ->%.0f | centroids ->%.0f\n",
-               v[1] * 1e3, v[2] * 1e3, v[4] * 1e3, v[5] * 1e3, v[6] * 1e3, v[7] * 1e3, v[9] * 1e3, v[10] * 1e3, v[3] * 1e3);
+  float v[5] = {};
+  for (int i = 0; i < 5; ++i) {
+    HIP_CHECK(hipEventSynchronize(t.ev[i]));
+    if (i) HIP_CHECK(hipEventElapsedTime(&v[i], t.ev[0], t.ev[i]));
+  }
+  std::fprintf(stderr, "seg us (from start): downsample ->%.0f faces ->%.0f centroids ->%.0f orient ->%.0f\n",
+               v[1] * 1e3, v[2] * 1e3, v[3] * 1e3, v[4] * 1e3);
 }
 
 // State of the registration whose clouds occupy CloudSet s.
@@ -277,20 +307,21 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   ps.nin[0] = n_tar;
   ps.nin[1] = n_src;
   const float* hin[2] = {tar, src};
-  for (int k = 0; k < 2; ++k) ps.cap[k] = (uint32_t)std::max<int64_t>(ps.nin[k], 1);
-  hipStream_t st0 = c->sa[0], st1 = c->sa[1];
-  cs.arena.ensure(cloud_bytes(ps.cap[0], true) + cloud_bytes(ps.cap[1], true) +
-                  exact_sum_bytes(6, std::max(ps.cap[0], ps.cap[1])) + (1 << 20));
+  // both clouds get the larger capacity, so their workspaces are laid out alike
+  // (batched launches address cloud 1 at a fixed offset from cloud 0)
+  const uint32_t capmax = (uint32_t)std::max<int64_t>(std::max(ps.nin[0], ps.nin[1]), 1);
+  ps.cap[0] = ps.cap[1] = capmax;
+  hipStream_t st0 = c->sa[0], ss = c->sa[2];
+  cs.arena.ensure(2 * cloud_bytes(capmax, true) + exact_sum_bytes(6, capmax) + (1 << 20));
   cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
   // clouds) so the captured graphs never depend on caller pointers.
   uint32_t* hn = (uint32_t*)c->pinned.get(64) + 8 * s;
-  const uint32_t capmax = std::max(ps.cap[0], ps.cap[1]);
   ps.cen = cs.arena.take_n<float>(8);
   ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
-    carve_cloud(cs.arena, w[k], ps.cap[k], true);
+    carve_cloud(cs.arena, w[k], capmax, true);
     w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
     const uint32_t n = (uint32_t)ps.nin[k];
     if (n)
@@ -303,13 +334,10 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   struct {
     const void* base;
     size_t acap;
-    uint32_t cap0, cap1;
+    uint32_t cap;
     float leaf, fvs, vpt, ct, fine_res;
-  } key = {cs.arena.base, cs.arena.cap, ps.cap[0], ps.cap[1], leaf, P.face_voxel_size, P.voxel_point_threshold,
+  } key = {cs.arena.base, cs.arena.cap, capmax, leaf, P.face_voxel_size, P.voxel_point_threshold,
            P.curvature_threshold, P.fine_verify_voxel_size};
-  // st0 -> st1 fork (the staging copies above are on st0)
-  HIP_CHECK(hipEventRecord(cs.ev[4], st0));
-  HIP_CHECK(hipStreamWaitEvent(st1, cs.ev[4], 0));
   // FCCF_SEG_TIMING=1 (development): timing events between the segment graphs,
   // printed to stderr by register_finish.
   static const bool seg_timing = std::getenv("FCCF_SEG_TIMING") != nullptr;
@@ -318,31 +346,21 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     if (seg_timing) HIP_CHECK(hipEventRecord(tm.ev[i], q));
   };
   mark(0, st0);
-  hipStream_t ss = c->sa[2];
-  for (int k = 0; k < 2; ++k) {
-    hipStream_t sm = c->sa[k];
-    mark(1 + 5 * k, sm);
-    cs.g_seg[k][0].run(&key, sizeof key, sm, [&] { seg_downsample(w[k], leaf, sm); });
-    mark(2 + 5 * k, sm);
-    HIP_CHECK(hipEventRecord(cs.ev[k], sm));
-    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[k], 0));
-  }
+  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_downsample(w, leaf, st0); });
+  mark(1, st0);
+  HIP_CHECK(hipEventRecord(cs.ev[0], st0));
+  HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[0], 0));
   cs.g_cen.run(&key, sizeof key, ss, [&] {
     exact_sum2(w[0].ds2, w[0].sc + 3, w[1].ds2, w[1].sc + 3, 3, 3, ps.cen, true, ps.xs, ss);  // compute3DCentroid (:473)
   });
   mark(3, ss);
   HIP_CHECK(hipEventRecord(cs.ev[2], ss));
-  for (int k = 0; k < 2; ++k) {
-    hipStream_t sm = c->sa[k];
-    cs.g_seg[k][1].run(&key, sizeof key, sm, [&] { seg_faces(w[k], P, sm, k == 0); });
-    mark(4 + 5 * k, sm);
-    HIP_CHECK(hipStreamWaitEvent(sm, cs.ev[2], 0));
-    face_voxels_orient(w[k].cap, w[k].planar, w[k].fb, sm);
-    mark(5 + 5 * k, sm);
-  }
+  cs.g_seg[1].run(&key, sizeof key, st0, [&] { seg_faces(w, P, st0); });
+  mark(2, st0);
+  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[2], 0));
+  face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2);
+  mark(4, st0);
   tm.armed = seg_timing;
-  HIP_CHECK(hipEventRecord(cs.ev[5], st1));  // join
-  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[5], 0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
   HIP_CHECK(hipGetLastError());
 }
@@ -694,8 +712,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     probe_collect(c->probe);
   }
   S.graph_captures = c->g_fine.captures;
-  for (auto& gk : c->cs[s].g_seg)
-    for (auto& g : gk) S.graph_captures += g.captures;
+  for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
   S.graph_captures += c->cs[s].g_cen.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
@@ -715,8 +732,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
 void reset_capture_counts(fccf_ctx* c) {
   c->g_fine.captures = 0;
   for (auto& cs : c->cs) {
-    for (auto& gk : cs.g_seg)
-      for (auto& g : gk) g.captures = 0;
+    for (auto& g : cs.g_seg) g.captures = 0;
     cs.g_cen.captures = 0;
   }
 }

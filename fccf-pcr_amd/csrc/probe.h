@@ -24,7 +24,9 @@ struct ProbePair {
   uint32_t* d_active = nullptr;         // device word: a kernel may clear it when it skipped its work
   const uint32_t* d_count = nullptr;   // device-resident unit counts (may be null)
   const uint32_t* d_count2 = nullptr;
-  double per_unit = 0.0, per_unit2 = 0.0, fixed = 0.0;
+  const uint32_t* d_count3 = nullptr;
+  const uint32_t* d_count4 = nullptr;
+  double per_unit = 0.0, per_unit2 = 0.0, fixed = 0.0, per_unit3 = 0.0, per_unit4 = 0.0;
   ~ProbePair() {
     if (a) (void)hipEventDestroy(a);
     if (b) (void)hipEventDestroy(b);
@@ -47,7 +49,9 @@ extern thread_local Probe* g_probe;
 struct ProbeScope {
   std::shared_ptr<ProbePair> p;
   ProbeScope(const char* kernel, hipStream_t st, const uint32_t* d_count, double per_unit,
-             const uint32_t* d_count2 = nullptr, double per_unit2 = 0.0, double fixed = 0.0);
+             const uint32_t* d_count2 = nullptr, double per_unit2 = 0.0, double fixed = 0.0,
+             const uint32_t* d_count3 = nullptr, double per_unit3 = 0.0, const uint32_t* d_count4 = nullptr,
+             double per_unit4 = 0.0);
   void end(hipStream_t st);
   // device word the probed kernel may set to 0 when it had nothing to do (the
   // launch is then left out of the totals); null when this launch is not probed
@@ -55,6 +59,7 @@ struct ProbeScope {
 };
 
 // algorithmic bytes of one launch = per_unit * *d_count + per_unit2 * *d_count2 + fixed
+//   (+ per_unit3 * *d_count3 + per_unit4 * *d_count4: the second problem of a batched launch)
 // Resolve armed pairs into totals (call after the streams are synchronised).
 void probe_collect(Probe& pr);
 

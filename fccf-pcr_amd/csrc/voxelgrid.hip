@@ -10,6 +10,7 @@
 //
 // HBM traffic per pass (algorithmic): read 12 B/pt, write 12 B/leaf; the radix sort
 // adds 2 x (4+4) B/pt per 8-bit digit pass.
+#define KT_TU 2  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
 
@@ -26,10 +27,12 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Per-block partial bbox of finite points: part[b] = {min xyz, max xyz, count(bits), 0}.
-__global__ void __launch_bounds__(256) k_vg_bbox(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                                 float* __restrict__ part) {
+__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<float*> part2) {
+  KT();
   __shared__ float sh[4][7];
-  const uint32_t n = *d_n;
+  const int e = blockIdx.y;
+  const float* __restrict__ xyz = xyz2[e];
+  const uint32_t n = *d_n2[e];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t cnt = 0;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -58,15 +61,17 @@ __global__ void __launch_bounds__(256) k_vg_bbox(const float* __restrict__ xyz, 
       for (int a = 0; a < 3; ++a) { r[a] = fminf(r[a], sh[ww][a]); r[3 + a] = fmaxf(r[3 + a], sh[ww][3 + a]); }
       c += __float_as_uint(sh[ww][6]);
     }
-    float* p = part + 8 * blockIdx.x;
+    float* p = part2[e] + 8 * blockIdx.x;
     for (int a = 0; a < 6; ++a) p[a] = r[a];
     p[6] = __uint_as_float(c);
     p[7] = 0.f;
   }
 }
 
-__global__ void __launch_bounds__(64) k_vg_params(const float* __restrict__ part, int nparts, float leaf,
-                                                 VGParams* __restrict__ P) {
+__global__ void __launch_bounds__(64) k_vg_params(B2<const float*> part2, int nparts, float leaf, B2<VGParams*> P2) {
+  KT();
+  const float* __restrict__ part = part2[blockIdx.y];
+  VGParams* __restrict__ P = P2[blockIdx.y];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t cnt = 0;
   for (int b = threadIdx.x; b < nparts; b += 64) {
@@ -111,61 +116,65 @@ __global__ void __launch_bounds__(64) k_vg_params(const float* __restrict__ part
   *P = q;
 }
 
-__global__ void __launch_bounds__(256) k_vg_keys(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                                 const VGParams* __restrict__ P, uint32_t* __restrict__ keys) {
-  const VGParams q = *P;
-  if (q.overflow || q.nfinite == 0) return;
-  const uint32_t n = *d_n;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    uint32_t key = 0xFFFFFFFFu;
-    if (finite3(x, y, z)) {
-      const int i0 = (int)(floorf(x * q.inv) - (float)q.min_b[0]);
-      const int i1 = (int)(floorf(y * q.inv) - (float)q.min_b[1]);
-      const int i2 = (int)(floorf(z * q.inv) - (float)q.min_b[2]);
-      key = (uint32_t)((int64_t)i0 + (int64_t)i1 * q.mul1 + (int64_t)i2 * q.mul2);
-    }
-    keys[i] = key;
-  }
+__device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, float z) {
+  if (!finite3(x, y, z)) return 0xFFFFFFFFu;
+  const int i0 = (int)(floorf(x * q.inv) - (float)q.min_b[0]);
+  const int i1 = (int)(floorf(y * q.inv) - (float)q.min_b[1]);
+  const int i2 = (int)(floorf(z * q.inv) - (float)q.min_b[2]);
+  return (uint32_t)((int64_t)i0 + (int64_t)i1 * q.mul1 + (int64_t)i2 * q.mul2);
 }
 
-// Presorted check (second pass): vals = identity, and if every key is strictly above
-// its predecessor the last block to finish sets nbits = 0, so the radix passes exit
-// at once and the identity permutation stands -- the stable sort of sorted keys.
-__global__ void __launch_bounds__(256) k_vg_sorted(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ d_n,
-                                                   VGParams* __restrict__ P, uint32_t* __restrict__ vals) {
-  __shared__ uint32_t bad_sh;
-  if (threadIdx.x == 0) bad_sh = 0;
-  __syncthreads();
-  const bool live = !P->overflow && P->nfinite != 0;
-  const uint32_t n = *d_n;
-  uint32_t bad = 0;
-  if (live)
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-      vals[i] = i;
-      if (i + 1 < n && !(keys[i] < keys[i + 1])) bad = 1;
-    }
-  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&bad_sh, 1u);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  if (bad_sh) atomicOr(&P->unsorted, 1u);
-  __threadfence();
-  if (atomicAdd(&P->chk_done, 1u) == gridDim.x - 1) {
-    __threadfence();
-    if (live && atomicOr(&P->unsorted, 0u) == 0) P->nbits = 0;
+// Leaf keys.  presorted (the driver's second pass): vals = identity, and a key not
+// strictly above its predecessor -- or any non-finite point -- sets P->unsorted;
+// otherwise every leaf holds exactly one point and the pass is the identity (the
+// sort tail, segmentation and centroid kernels take their shortcut).
+__global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<VGParams*> P2,
+                                                 B2<uint32_t*> keys2, B2<uint32_t*> vals2, int presorted) {
+  KT();
+  const int e = blockIdx.y;
+  VGParams* P = P2[e];
+  const VGParams q = *P;
+  const uint32_t n = *d_n2[e];
+  if (q.overflow) return;
+  if (q.nfinite == 0) {
+    if (presorted && n && blockIdx.x == 0 && threadIdx.x == 0) P->unsorted = 1u;
+    return;
   }
+  const float* __restrict__ xyz = xyz2[e];
+  uint32_t* __restrict__ keys = keys2[e];
+  uint32_t* __restrict__ vals = vals2[e];
+  bool bad = false;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t key = vg_key(q, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+    keys[i] = key;
+    if (presorted) {
+      vals[i] = i;
+      if (key == 0xFFFFFFFFu) bad = true;
+      if (i + 1 < n && !(key < vg_key(q, xyz[3 * i + 3], xyz[3 * i + 4], xyz[3 * i + 5]))) bad = true;
+    }
+  }
+  if (presorted && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&P->unsorted, 1u);
 }
 
 // One thread per leaf: Vector3f accumulation in ascending input index, then / n.
-__global__ void __launch_bounds__(256) k_vg_centroid(const float* __restrict__ xyz, const uint32_t* __restrict__ d_n,
-                                                     const VGParams* __restrict__ P, const uint32_t* __restrict__ vals,
-                                                     const uint32_t* __restrict__ starts,
-                                                     const uint32_t* __restrict__ d_nseg, float* __restrict__ out,
-                                                     uint32_t* __restrict__ d_m) {
-  const VGParams q = *P;
-  const uint32_t n = *d_n;
+__global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
+                                                     B2<const VGParams*> P2, B2<const uint32_t*> vals2,
+                                                     B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
+                                                     B2<float*> out2, B2<uint32_t*> d_m2, int presorted) {
+  KT();
+  const int e = blockIdx.y;
+  const VGParams q = *P2[e];
+  const float* __restrict__ xyz = xyz2[e];
+  const uint32_t* __restrict__ vals = vals2[e];
+  const uint32_t* __restrict__ starts = starts2[e];
+  const uint32_t* __restrict__ d_nseg = d_nseg2[e];
+  float* __restrict__ out = out2[e];
+  uint32_t* __restrict__ d_m = d_m2[e];
+  const uint32_t n = *d_n2[e];
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
-  if (q.overflow) {  // "Integer indices would overflow": output = *input_
+  // "Integer indices would overflow": output = *input_; presorted with every leaf
+  // holding one finite point: the centroid of one point is the point (p / 1.f == p)
+  if (q.overflow || (presorted && q.unsorted == 0u && n && q.nfinite == n)) {
     for (uint32_t i = gid; i < n; i += gsz) {
       out[3 * i] = xyz[3 * i]; out[3 * i + 1] = xyz[3 * i + 1]; out[3 * i + 2] = xyz[3 * i + 2];
     }
@@ -193,16 +202,33 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-void voxel_grid(const float* xyz, const uint32_t* d_n, uint32_t cap, float leaf, float* out, uint32_t* d_m, VGBufs b,
-                hipStream_t st, bool presorted) {
-  k_vg_bbox<<<VG_BBOX_BLOCKS, 256, 0, st>>>(xyz, d_n, b.part);
-  k_vg_params<<<1, 64, 0, st>>>(b.part, VG_BBOX_BLOCKS, leaf, b.params);
-  FCCF_LAUNCH("k_vg_keys", (d_n, 16.0), k_vg_keys, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.k0);
-  if (presorted) k_vg_sorted<<<grid_for(cap, 1024, 1024), 256, 0, st>>>(b.k0, d_n, b.params, b.v0);
-  // with nbits = 0 every pass exits and v0 keeps the identity written above
-  radix_sort_u32(b.k0, b.v0, b.k1, b.v1, d_n, cap, &b.params->nbits, 32, !presorted, b.ss, st);
-  segment_heads_u32(b.k0, d_n, cap, 0xFFFFFFFFu, b.starts, b.nseg, b.ss, st);
-  FCCF_LAUNCH("k_vg_centroid", (d_n, 16.0, d_m, 12.0), k_vg_centroid, grid_for(cap), 256, 0, st, xyz, d_n, b.params, b.v0, b.starts, b.nseg, out, d_m);
+void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch) {
+  auto F = [&](auto get) { return B2<decltype(get(b[0]))>(get(b[0]), get(b[1])); };
+  const B2<VGParams*> P = F([](const VGBufs& v) { return v.params; });
+  const B2<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
+  const B2<uint32_t*> k1 = F([](const VGBufs& v) { return v.k1; }), v1 = F([](const VGBufs& v) { return v.v1; });
+  const B2<uint32_t*> starts = F([](const VGBufs& v) { return v.starts; }), nseg = F([](const VGBufs& v) { return v.nseg; });
+  const B2<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
+  const B2<const uint32_t*> nbits(&b[0].params->nbits, &b[1].params->nbits);
+  const dim3 g(grid_for(cap), nbatch);
+  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(xyz, d_n, F([](const VGBufs& v) { return v.part; }));
+  k_vg_params<<<dim3(1, nbatch), 64, 0, st>>>(F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS,
+                                               leaf, P);
+  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts
+  const uint32_t* m2 = nbatch > 1 ? d_m[1] : nullptr;
+  const B2<const uint32_t*> unsorted(&b[0].params->unsorted, &b[1].params->unsorted);
+  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, g, 256, 0, st, xyz, d_n, P, k0, v0, presorted ? 1 : 0);
+  if (!presorted) {
+    radix_sort_u32(k0, v0, k1, v1, d_n, cap, nbits, 32, true, ss, st, nbatch);
+    segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
+                      nbatch);
+  } else {  // usually already in leaf order: a tail-only sort and segmentation that run only if not
+    radix_sort_u32(k0, v0, k1, v1, d_n, cap, nbits, 0, false, ss, st, nbatch, unsorted);
+    segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
+                      nbatch, unsorted);
+  }
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, xyz, d_n, B2<const VGParams*>(P), B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0);
 }
 
 }  // namespace fccf

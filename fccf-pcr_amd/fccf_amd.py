@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfccf.so")
+LIB_PATH = os.environ.get("FCCF_LIB") or os.path.join(_HERE, "lib", "libfccf.so")  # FCCF_LIB: dev builds (lib_kt/)
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"libfccf not built: {LIB_PATH} missing (run `make -C fccf-pcr_amd` or __graft_entry__.build())")
@@ -68,6 +68,7 @@ _sig("fccf_strerror", ctypes.c_char_p, ctypes.c_int)
 _sig("fccf_ctx_create", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int)
 _sig("fccf_ctx_destroy", ctypes.c_int, _P)
 _sig("fccf_ctx_set_debug", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_ctx_last_error", ctypes.c_char_p, _P)
 _sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
      ctypes.POINTER(Stats))
 _sig("fccf_register_device", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
@@ -77,6 +78,7 @@ _sig("fccf_register_batch", ctypes.c_int, _P, ctypes.c_int, _P, _P, _P, _P, ctyp
 _sig("fccf_device_upload", ctypes.c_int, _P, _P, _I64, ctypes.POINTER(_P))
 _sig("fccf_device_free", ctypes.c_int, _P, _P)
 _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
+_sig("fccf_stage_downsample_presorted", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
 _sig("fccf_stage_centroid", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_stage_seqsum", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
@@ -93,14 +95,15 @@ _sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ct
 
 
 class FCCFError(RuntimeError):
-    def __init__(self, code, where=""):
+    def __init__(self, code, where="", detail=""):
         self.code = code
-        super().__init__(f"{where}: {_lib.fccf_strerror(code).decode()} ({code})")
+        super().__init__(f"{where}: {_lib.fccf_strerror(code).decode()} ({code})" + (f": {detail}" if detail else ""))
 
 
-def _check(rc, where):
+def _check(rc, where, h=None):
     if rc != FCCF_OK:
-        raise FCCFError(rc, where)
+        detail = (_lib.fccf_ctx_last_error(h) or b"").decode(errors="replace") if h else ""
+        raise FCCFError(rc, where, detail)
 
 
 def default_params() -> Params:
@@ -121,7 +124,7 @@ class Ctx:
         self._h = _P()
         _check(_lib.fccf_ctx_create(ctypes.byref(self._h), int(device)), "fccf_ctx_create")
         if debug:
-            _check(_lib.fccf_ctx_set_debug(self._h, 1), "fccf_ctx_set_debug")
+            _check(_lib.fccf_ctx_set_debug(self._h, 1), "fccf_ctx_set_debug", self._h)
 
     def close(self):
         if self._h:
@@ -148,7 +151,7 @@ class Ctx:
         rc = _lib.fccf_register(self._h, s.ctypes.data, s.shape[0], t.ctypes.data, t.shape[0], float(leaf),
                                 ctypes.byref(params) if params is not None else None, T.ctypes.data,
                                 ctypes.byref(st))
-        _check(rc, "fccf_register")
+        _check(rc, "fccf_register", self._h)
         return T.reshape(4, 4), st
 
     def register_device(self, d_src: int, n_src: int, d_tar: int, n_tar: int, leaf: float,
@@ -159,7 +162,7 @@ class Ctx:
         rc = _lib.fccf_register_device(self._h, _P(d_src), int(n_src), _P(d_tar), int(n_tar), float(leaf),
                                        ctypes.byref(params) if params is not None else None, T.ctypes.data,
                                        ctypes.byref(st))
-        _check(rc, "fccf_register_device")
+        _check(rc, "fccf_register_device", self._h)
         return T.reshape(4, 4), st
 
     def register_batch(self, pairs, leaf: float, params=None, on_device=False):
@@ -181,49 +184,51 @@ class Ctx:
         stats = (Stats * max(n, 1))()
         p = params if params is not None else default_params()
         _check(_lib.fccf_register_batch(self._h, n, arr_p(*sp), arr_i(*sn), arr_p(*tp), arr_i(*tn), int(on_device),
-                                        float(leaf), ctypes.byref(p), T.ctypes.data, stats), "fccf_register_batch")
+                                        float(leaf), ctypes.byref(p), T.ctypes.data, stats), "fccf_register_batch", self._h)
         return T[:n], list(stats)[:n]
 
     def upload(self, xyz) -> int:
         """Copy xyz into a new HBM buffer of this ctx's device; returns the device pointer."""
         a = _f32(xyz)
         d = _P()
-        _check(_lib.fccf_device_upload(self._h, a.ctypes.data, a.shape[0], ctypes.byref(d)), "fccf_device_upload")
+        _check(_lib.fccf_device_upload(self._h, a.ctypes.data, a.shape[0], ctypes.byref(d)), "fccf_device_upload", self._h)
         return int(d.value or 0)
 
     def free(self, dptr: int):
-        _check(_lib.fccf_device_free(self._h, _P(dptr)), "fccf_device_free")
+        _check(_lib.fccf_device_free(self._h, _P(dptr)), "fccf_device_free", self._h)
 
-    def downsample(self, xyz, leaf: float):
+    def downsample(self, xyz, leaf: float, presorted: bool = False):
+        """PCL VoxelGrid on the GPU; presorted=True runs it as the driver's second pass does."""
         a = _f32(xyz)
         out = np.zeros_like(a) if a.shape[0] else np.zeros((1, 3), np.float32)
         m = _I64()
-        _check(_lib.fccf_stage_downsample(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data,
-                                          ctypes.byref(m)), "fccf_stage_downsample")
+        f = _lib.fccf_stage_downsample_presorted if presorted else _lib.fccf_stage_downsample
+        _check(f(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data, ctypes.byref(m)),
+               "fccf_stage_downsample", self._h)
         return out[: m.value].copy()
 
     def set_probe(self, kernel):
         """Time every launch of `kernel` with HIP events (None = off); resets totals."""
-        _check(_lib.fccf_ctx_set_probe(self._h, kernel.encode() if kernel else None), "fccf_ctx_set_probe")
+        _check(_lib.fccf_ctx_set_probe(self._h, kernel.encode() if kernel else None), "fccf_ctx_set_probe", self._h)
 
     def probe_read(self):
         """(total_ms, launches, total_algorithmic_bytes) since set_probe."""
         ms, n, b = ctypes.c_double(), _I64(), ctypes.c_double()
-        _check(_lib.fccf_probe_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "fccf_probe_read")
+        _check(_lib.fccf_probe_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "fccf_probe_read", self._h)
         return ms.value, n.value, b.value
 
     def centroid(self, xyz):
         """compute3DCentroid (FCCF.cpp:473) of a dense cloud: float32[4] (x, y, z, 1)."""
         a = _f32(xyz)
         out = np.zeros(4, np.float32)
-        _check(_lib.fccf_stage_centroid(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_centroid")
+        _check(_lib.fccf_stage_centroid(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_centroid", self._h)
         return out
 
     def seqsum(self, x) -> np.float32:
         """Left-to-right float32 sum ((0 + x0) + x1) + ... (similar_num order, FCCF.cpp:830-835)."""
         a = np.ascontiguousarray(np.asarray(x, np.float32).reshape(-1))
         out = np.zeros(1, np.float32)
-        _check(_lib.fccf_stage_seqsum(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_seqsum")
+        _check(_lib.fccf_stage_seqsum(self._h, a.ctypes.data, a.shape[0], out.ctypes.data), "fccf_stage_seqsum", self._h)
         return out[0]
 
     def debug(self, name: str, dtype=np.float32):

@@ -91,6 +91,8 @@ const char* fccf_strerror(int code);
 /* device: HIP ordinal (the ctx creates its own non-blocking stream). */
 int fccf_ctx_create(fccf_ctx** ctx, int device);
 int fccf_ctx_destroy(fccf_ctx* ctx);
+/* Message of the last failing call on ctx ("" if none); valid until the next call. */
+const char* fccf_ctx_last_error(fccf_ctx* ctx);
 /* Keep per-stage intermediates for fccf_debug_get (tests). Off by default. */
 int fccf_ctx_set_debug(fccf_ctx* ctx, int on);
 
@@ -125,6 +127,11 @@ int fccf_device_free(fccf_ctx* ctx, float* d_xyz);
  * ascending leaf index; points of one leaf are summed in ascending input order. */
 int fccf_stage_downsample(fccf_ctx* ctx, const float* xyz, int64_t n, float leaf, float* out_xyz,
                           int64_t* m);
+/* The same, as the driver's second pass runs it (FCCF.cpp:1377-1387 over main's
+ * output): a check in the key kernel takes the identity shortcut when the keys are
+ * already strictly increasing, else a single-workgroup sort.  Same result for any input. */
+int fccf_stage_downsample_presorted(fccf_ctx* ctx, const float* xyz, int64_t n, float leaf, float* out_xyz,
+                                    int64_t* m);
 
 /* Stage export: pcl::compute3DCentroid of a dense cloud (FCCF.cpp:473 via
  * face_extrate): out = (sum x / n, sum y / n, sum z / n, 1) with each sum a

@@ -153,3 +153,19 @@ def test_batch_pipeline_equals_single_registrations(ctx, oracle, fccf):
             ctx.free(ds)
             ctx.free(dt)
     np.testing.assert_array_equal(Td.view(np.uint32), Tb.view(np.uint32))
+
+
+def test_deep_octree_tail_sort(ctx, oracle, fccf):
+    """A clump of points ~1.5 km away makes both octrees (1 m face voxels, 0.5 m
+    fine verify) deeper than the four fast radix passes cover (3 bits per level),
+    so the single-workgroup tail sort (k_rs_tail) finishes them; bitwise parity."""
+    src, tar, _ = fccf.synth_pair(60_000)
+    rng = np.random.default_rng(4)
+    far = (np.array([1500.0, 40.0, 2.0]) + rng.uniform(0, 0.9, size=(12, 3))).astype(np.float32)
+    src2 = np.concatenate([src, far])
+    tar2 = np.concatenate([far + np.float32(0.01), tar])
+    run = oracle.Run(src2, tar2, 0.1, oracle.STABLE)
+    assert run.get("oct1", np.float64)[3] > 10 and run.get("oct2", np.float64)[3] > 10  # depth
+    T, _ = ctx.register(src2, tar2, 0.1)
+    compare_all(ctx, run)
+    np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))

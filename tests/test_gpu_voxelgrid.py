@@ -12,9 +12,9 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def check(ctx, oracle, xyz, leaf):
+def check(ctx, oracle, xyz, leaf, presorted=False):
     ref, ovf = oracle.voxel_grid(xyz, leaf)
-    got = ctx.downsample(xyz, leaf)
+    got = ctx.downsample(xyz, leaf, presorted)
     assert got.shape == ref.shape, (got.shape, ref.shape, ovf)
     np.testing.assert_array_equal(bits(got), bits(ref))
     return ref
@@ -24,7 +24,7 @@ def check(ctx, oracle, xyz, leaf):
 def test_scene(ctx, oracle, fccf, n, leaf):
     xyz = fccf.synth_scene(n, seed=3)
     m1 = check(ctx, oracle, xyz, leaf)
-    check(ctx, oracle, m1, leaf)  # the driver's second pass on main's output
+    check(ctx, oracle, m1, leaf, presorted=True)  # the driver's second pass on main's output
 
 
 def test_transformed_negative_coords(ctx, oracle, fccf):
@@ -62,14 +62,19 @@ def test_many_leaves_random(ctx, oracle):
 
 
 def test_presorted_check_paths(ctx, oracle, fccf):
-    """The stage export runs the presorted check (voxel_grid(presorted=true)): sorted
-    input takes the identity path (radix passes skipped), anything else the full
-    sort.  Both must equal the oracle on inputs near the boundary of the check."""
+    """fccf_stage_downsample_presorted (the driver's second pass): sorted input takes
+    the identity path (no sort), anything else the single-workgroup tail sort.  Both
+    must equal the oracle on inputs near the boundary of the check."""
     m1 = check(ctx, oracle, fccf.synth_scene(120_000, seed=5), 0.1)
-    check(ctx, oracle, m1, 0.1)                                   # strictly increasing: identity
+    check(ctx, oracle, m1, 0.1, True)                                   # strictly increasing: identity
     sw = m1.copy()
     sw[[1000, 1001]] = sw[[1001, 1000]]
-    check(ctx, oracle, sw, 0.1)                                   # one descent: full sort
-    check(ctx, oracle, np.concatenate([m1, m1[-1:]]), 0.1)        # equal last keys: full sort
-    check(ctx, oracle, np.concatenate([m1, np.full((1, 3), np.nan, np.float32)]), 0.1)  # invalid key last
-    check(ctx, oracle, m1[::-1].copy(), 0.1)                      # descending
+    check(ctx, oracle, sw, 0.1, True)                                   # one descent: tail sort
+    check(ctx, oracle, np.concatenate([m1, m1[-1:]]), 0.1, True)        # equal last keys
+    check(ctx, oracle, np.concatenate([m1, np.full((1, 3), np.nan, np.float32)]), 0.1, True)  # non-finite last
+    check(ctx, oracle, m1[::-1].copy(), 0.1, True)                      # descending
+    check(ctx, oracle, fccf.synth_scene(60_000, seed=6), 0.05, True)    # random order: tail sort
+    check(ctx, oracle, np.zeros((0, 3), np.float32), 0.1, True)
+    check(ctx, oracle, np.full((3, 3), np.nan, np.float32), 0.1, True)  # no finite point
+    x = np.random.default_rng(1).uniform(-5000, 5000, size=(3000, 3)).astype(np.float32)
+    check(ctx, oracle, x, 0.01, True)                                   # overflow pass-through
