@@ -11,12 +11,13 @@
 // by Q = sum of q and the integer envelope [lo, hi] of Q_k + floor(x_k/u) (units
 // of u); "every partial of this run stays in binade E" is then a pure integer
 // test on the actual start M = s/u.  Summaries of consecutive runs compose
-// (xs_compose is associative), so a wave reduces a 256-input chunk, and 64 chunk
-// summaries reduce to a group summary, in O(log) depth.  Hypotheses cover the 3
-// binades around a double-precision prefix prediction.  A short serial chain then
-// applies one group (16384 inputs) per step, descends to chunks where a group does
-// not validate (binade crossings, zero/subnormal starts, non-finite inputs), and
-// replays a chunk with plain float adds where no chunk hypothesis validates.
+// (xs_compose is associative), so a wave reduces a 256-input chunk in O(log)
+// depth, and one ordered wave scan composes 64 chunk summaries.  Hypotheses cover
+// the 3 binades around a double-precision prefix prediction.  A short serial
+// chain then applies up to 64 chunks (16384 inputs) per scan and replays with
+// plain float adds a chunk that does not validate (binade crossings,
+// zero/subnormal starts, non-finite inputs).  XS_G (64-chunk groups) survives
+// only in the host fuzz model (tests/xs_fuzz.cpp): any grouping composes.
 // Result bits are identical to the naive loop (tests/test_exactsum.py fuzzes it).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -162,6 +163,19 @@ FH bool xs_valid(const XsSum& h, int64_t M) {
   return hi + 1 <= -((int64_t)1 << 23) && lo >= -((int64_t)1 << 24) + 1;
 }
 
+// The same test for one unit at its own start Me (int64, any sign; the side of
+// zero is M's, the start of the whole scan): the composed run is valid iff every
+// unit is valid at its own start, because a valid unit ends inside the binade
+// (Q lies in [lo, hi + 1]).  The device chain uses this form (k_xs_chain).
+FH bool xs_valid_unit(const XsSum& h, int64_t Me, bool pos) {
+  if (!h.ok) return false;
+  const int32_t hl = xs_sel(h.lo, Me), hh = xs_sel(h.hi, Me);
+  if (hl == XS_INF) return true;
+  const int64_t lo = Me + hl, hi = Me + hh;
+  if (pos) return lo >= ((int64_t)1 << 23) && hi + 1 <= ((int64_t)1 << 24);
+  return hi + 1 <= -((int64_t)1 << 23) && lo >= -((int64_t)1 << 24) + 1;
+}
+
 // end of the run: (M + Q) u, exact (it is the float the last rounding produced)
 FH float xs_apply(const XsSum& h, int64_t M, int E) {
   return (float)ldexp((double)(M + xs_sel(h.Q, M)), E - 23);
@@ -178,14 +192,12 @@ FH int xs_predict(double pre) {
 }
 
 // Device scratch of exact_sum (devprim.h): per row (problem x component) NC chunk
-// tables and NG group tables.
+// tables.
 struct XsBufs {
   double* pre;     // rows x (NC + 1): chunk sums, then exclusive prefix
   XsSum* ctab;     // rows x NC x XS_NE
   int32_t* cE;     // rows x NC: Ebase per chunk
-  XsSum* gtab;     // rows x NG x XS_NE
-  int32_t* gE;     // rows x NG
-  uint32_t NC, NG;
+  uint32_t NC;
   int rows;
 };
 

@@ -1,14 +1,14 @@
 // exactsum.hip — exact parallel left-to-right float32 sums (algorithm: exactsum.h).
 //
-// Five launches per call, all sized from device counts:
+// Four launches per call, all sized from device counts:
 //   k_xs_csum    one wave per (problem, 256-input chunk): double chunk sums (K comps)
 //   k_xs_prefix  one block per row (problem x component): exclusive double prefix
 //   k_xs_chunk   one wave per chunk: 3 binade hypotheses x 2 parities, wave-composed
-//   k_xs_group   one wave per (row, 64-chunk group): compose chunk tables per binade
-//   k_xs_chain   one wave per row: scan-jump over groups, then over the chunks of
-//                a group that crosses a binade, then a plain replay of the chunk
-// The first four are bandwidth-bound streaming passes over the inputs; the chain
-// costs one wave scan per binade crossing (plus one 256-add replay).
+//   k_xs_chain   one wave per row: one ordered scan per 64-chunk window, a plain
+//                replay of each chunk that crosses a binade
+// The first three are bandwidth-bound streaming passes over the inputs; the chain
+// costs one wave scan per window plus one scan and a 256-add replay per crossing,
+// with its loads issued one or two windows ahead.
 #define KT_TU 4  // ktrace.h source tag
 #include "probe.h"
 #include "devprim.h"
@@ -18,47 +18,107 @@
 namespace fccf {
 namespace {
 
-// XsSum moved across lanes by one DPP control (row_shr:n / row_bcast:15 / :31);
-// lanes the control does not address keep their own value.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ XsSum dpp_sum(const XsSum& a) {
-  XsSum o;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    o.Q[p] = __builtin_amdgcn_update_dpp(a.Q[p], a.Q[p], CTRL, ROWS, 0xf, false);
-    o.lo[p] = __builtin_amdgcn_update_dpp(a.lo[p], a.lo[p], CTRL, ROWS, 0xf, false);
-    o.hi[p] = __builtin_amdgcn_update_dpp(a.hi[p], a.hi[p], CTRL, ROWS, 0xf, false);
-  }
-  o.ok = __builtin_amdgcn_update_dpp(a.ok, a.ok, CTRL, ROWS, 0xf, false);
-  o.pad = 0;
-  return o;
-}
-
-// Inclusive ordered scan over the wave: lane l ends with units 0..l composed
-// (earlier lanes first).  Four row_shr steps scan each 16-lane row, then
-// row_bcast:15 / row_bcast:31 carry row totals forward.  No LDS traffic.
-__device__ __forceinline__ XsSum wave_scan(XsSum a) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
-  XsSum o;
-  o = dpp_sum<0x111, 0xf>(a);
-  if (r >= 1) a = xs_compose(o, a);
-  o = dpp_sum<0x112, 0xf>(a);
-  if (r >= 2) a = xs_compose(o, a);
-  o = dpp_sum<0x114, 0xf>(a);
-  if (r >= 4) a = xs_compose(o, a);
-  o = dpp_sum<0x118, 0xf>(a);
-  if (r >= 8) a = xs_compose(o, a);
-  o = dpp_sum<0x142, 0xa>(a);
-  if (lane & 16) a = xs_compose(o, a);
-  o = dpp_sum<0x143, 0xc>(a);
-  if (lane >= 32) a = xs_compose(o, a);
-  return a;
-}
-
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
   return v;
+}
+
+// Inclusive ordered scan of parity maps.  Unit l maps a start parity p to its
+// quantum count Q_l[p] (and so to the end parity p + Q_l[p]); lane l ends with
+// the count of units 0..l for each parity at unit 0.  Two int32 per lane per
+// step instead of a whole summary: this is the chain's critical path.
+// Wrap-around in lanes past the first invalid unit is harmless (never read).
+__device__ __forceinline__ void pmap_scan(uint32_t& q0, uint32_t& q1) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  auto step = [&](uint32_t o0, uint32_t o1, bool take) {
+    // earlier run o, then this run: Q[p] = o[p] + this[(p + o[p]) & 1]
+    const uint32_t m0 = 0u - (o0 & 1u), m1 = 0u - ((o1 + 1u) & 1u);
+    const uint32_t n0 = o0 + (q0 ^ ((q0 ^ q1) & m0));
+    const uint32_t n1 = o1 + (q0 ^ ((q0 ^ q1) & m1));
+    if (take) { q0 = n0; q1 = n1; }
+  };
+#define XS_PSTEP(CTRL, ROWS, COND)                                                        \
+  {                                                                                        \
+    const uint32_t o0 = __builtin_amdgcn_update_dpp(q0, q0, CTRL, ROWS, 0xf, false);       \
+    const uint32_t o1 = __builtin_amdgcn_update_dpp(q1, q1, CTRL, ROWS, 0xf, false);       \
+    step(o0, o1, COND);                                                                    \
+  }
+  XS_PSTEP(0x111, 0xf, r >= 1)
+  XS_PSTEP(0x112, 0xf, r >= 2)
+  XS_PSTEP(0x114, 0xf, r >= 4)
+  XS_PSTEP(0x118, 0xf, r >= 8)
+  XS_PSTEP(0x142, 0xa, (lane & 16) != 0)
+  XS_PSTEP(0x143, 0xc, lane >= 32)
+#undef XS_PSTEP
+}
+
+// parity-free form (no unit of the scan depends on the start parity)
+__device__ __forceinline__ uint32_t add_scan(uint32_t q) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  uint32_t o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x111, 0xf, 0xf, false); if (r >= 1) q += o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x112, 0xf, 0xf, false); if (r >= 2) q += o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x114, 0xf, 0xf, false); if (r >= 4) q += o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x118, 0xf, 0xf, false); if (r >= 8) q += o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x142, 0xa, 0xf, false); if (lane & 16) q += o;
+  o = __builtin_amdgcn_update_dpp(q, q, 0x143, 0xc, 0xf, false); if (lane >= 32) q += o;
+  return q;
+}
+
+// value of lane l-1 (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+// Inclusive ordered min / max over the wave (lane 63 ends with the total).
+template <bool MAX>
+__device__ __forceinline__ int32_t mm_scan(int32_t q) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  int32_t o;
+#define XS_MM(CTRL, ROWS, COND)                                          \
+  o = __builtin_amdgcn_update_dpp(q, q, CTRL, ROWS, 0xf, false);         \
+  if (COND) q = MAX ? (o > q ? o : q) : (o < q ? o : q);
+  XS_MM(0x111, 0xf, r >= 1)
+  XS_MM(0x112, 0xf, r >= 2)
+  XS_MM(0x114, 0xf, r >= 4)
+  XS_MM(0x118, 0xf, r >= 8)
+  XS_MM(0x142, 0xa, (lane & 16) != 0)
+  XS_MM(0x143, 0xc, lane >= 32)
+#undef XS_MM
+  return q;
+}
+
+// The composition of the 64 lanes' summaries (lane 0 first), valid in lane 63.
+// Instead of composing whole summaries along the scan, the quantum counts are
+// scanned as parity maps, every lane shifts its envelope by its exclusive count
+// (under its own start parity), and the envelopes reduce by min / max.  Same
+// summary as folding xs_compose over the lanes (the bounds check differs only in
+// where it rejects: any summary it accepts is exact, XS_LIM keeps int32 safe,
+// since consecutive counts differ by less than 2^26).
+__device__ __forceinline__ XsSum wave_total(const XsSum& a) {
+  uint32_t q0 = (uint32_t)a.Q[0], q1 = (uint32_t)a.Q[1];
+  pmap_scan(q0, q1);
+  const uint32_t e[2] = {wave_shr1(q0), wave_shr1(q1)};
+  XsSum t;
+  int ok = a.ok;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int32_t ep = (int32_t)e[p];
+    const int32_t alo = xs_sel(a.lo, p + ep), ahi = xs_sel(a.hi, p + ep);
+    const int32_t lo = alo == XS_INF ? XS_INF : ep + alo;
+    const int32_t hi = ahi == -XS_INF ? -XS_INF : ep + ahi;
+    const int32_t qi = (int32_t)(p ? q1 : q0);
+    ok &= (ep > -XS_LIM && ep < XS_LIM) & (qi > -XS_LIM && qi < XS_LIM) & (lo == XS_INF || lo > -XS_LIM) &
+          (hi == -XS_INF || hi < XS_LIM);
+    t.Q[p] = qi;
+    t.lo[p] = mm_scan<false>(lo);
+    t.hi[p] = mm_scan<true>(hi);
+  }
+  t.ok = __ballot(!ok) == 0;
+  t.pad = 0;
+  if (!t.ok) t = xs_bad();
+  return t;
 }
 
 struct Prob {
@@ -179,40 +239,12 @@ __global__ void __launch_bounds__(256) k_xs_chunk(XsIn in, int K, const double* 
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (ok[j]) a = xs_compose(a, xs_elem(v[j][k], inv_u));
-        a = wave_scan(a);
+        a = wave_total(a);
         if (lane == 63) ctab[(row * NC + c) * XS_NE + h] = a;
       }
     }
   }
 }
-
-__global__ void __launch_bounds__(256) k_xs_group(XsIn in, int K, const double* __restrict__ pre,
-                                                  const XsSum* __restrict__ ctab, const int32_t* __restrict__ cE,
-                                                  XsSum* __restrict__ gtab, int32_t* __restrict__ gE, uint32_t NC,
-                                                  uint32_t NG) {
-  KT();
-  const size_t row = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const uint32_t nch = (prob_n(in, (int)(row / K)) + XS_L - 1) / XS_L;
-  const uint32_t ng = (nch + XS_G - 1) / XS_G;
-  for (uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6); g < ng; g += gridDim.x * 4) {
-    const int Eg = xs_predict(pre[row * (NC + 1) + (size_t)g * XS_G]);
-    if (lane == 0) gE[row * NG + g] = Eg;
-    if (Eg == XS_NOE) continue;
-    const uint32_t c = g * XS_G + lane;
-    const int Ec = c < nch ? cE[row * NC + c] : XS_NOE;
-    for (int h = 0; h < XS_NE; ++h) {
-      XsSum a = xs_identity();
-      if (c < nch) {
-        const int hc = Eg + h - Ec;
-        a = (Ec != XS_NOE && hc >= 0 && hc < XS_NE) ? ctab[(row * NC + c) * XS_NE + hc] : xs_bad();
-      }
-      a = wave_scan(a);
-      if (lane == 63) gtab[(row * NG + g) * XS_NE + h] = a;
-    }
-  }
-}
-
 
 __device__ __forceinline__ XsTab3 load_tab3(const XsSum* tab, const int32_t* eb, size_t u, bool have) {
   XsTab3 T;
@@ -228,17 +260,18 @@ __device__ __forceinline__ XsTab3 load_tab3(const XsSum* tab, const int32_t* eb,
   return T;
 }
 
-// Apply units cur..cnt-1 (lane l holds unit l's tables) to s.  One ordered scan
-// composes every prefix under s's binade; validity is monotone in the prefix
-// length (envelopes only widen), so the first invalid lane f is found by a
-// ballot, prefix f-1 is applied in one step and unit f goes to `descend`.
 #ifdef XS_PROBE
-__device__ unsigned long long xs_probe[8];  // scans, replays, decompose misses, replay cycles, scan cycles
+__device__ unsigned long long xs_probe[8];  // scans, replays, decompose misses, replay cycles, scan cycles, prefetch misses
 #define XS_COUNT(i, v) (threadIdx.x == 0 ? (void)atomicAdd(&xs_probe[i], (unsigned long long)(v)) : (void)0)
 #else
 #define XS_COUNT(i, v) ((void)0)
 #endif
 
+// Apply units cur..cnt-1 (lane l holds unit l's tables) to s.  Each unit is
+// picked under s's binade E; an ordered scan of the units' quantum counts gives
+// every unit its own start M_l, each unit checks its envelope there
+// (xs_valid_unit), the first invalid lane f is found by a ballot, units cur..f-1
+// are applied in one step and unit f goes to `descend`.
 template <class Descend>
 __device__ __forceinline__ void scan_jump(float& s, const XsTab3& T, int cnt, Descend descend) {
   const int lane = threadIdx.x & 63;
@@ -256,12 +289,22 @@ __device__ __forceinline__ void scan_jump(float& s, const XsTab3& T, int cnt, De
     const long long t0 = wall_clock64();
 #endif
     const bool mine = lane >= cur && lane < cnt;
-    XsSum a = mine ? xs_pick(T, E) : xs_identity();
-    a = wave_scan(a);
-    const uint64_t bad = __ballot(mine && !xs_valid(a, M));
+    const XsSum h = mine ? xs_pick(T, E) : xs_identity();
+    uint32_t q0 = (uint32_t)h.Q[0], q1 = (uint32_t)h.Q[1];
+    const int P = (int)(M & 1);
+    uint32_t qi;  // inclusive count for the scan's start parity P
+    if (__ballot(q0 != q1) == 0) {
+      qi = add_scan(q0);
+    } else {
+      pmap_scan(q0, q1);
+      qi = P ? q1 : q0;
+    }
+    const uint32_t qe = wave_shr1(qi);
+    const int64_t Me = M + (int64_t)(int32_t)qe;
+    const uint64_t bad = __ballot(mine && !xs_valid_unit(h, Me, M > 0));
     const int f = bad ? (int)__builtin_ctzll(bad) : cnt;
     if (f > cur) {
-      const int64_t Q = __builtin_amdgcn_readlane(xs_sel(a.Q, M), f - 1);
+      const int64_t Q = (int32_t)__builtin_amdgcn_readlane(qi, f - 1);
       s = (float)ldexp((double)(M + Q), E - 23);
     }
     XS_COUNT(0, 1);
@@ -274,35 +317,94 @@ __device__ __forceinline__ void scan_jump(float& s, const XsTab3& T, int cnt, De
   }
 }
 
-// One wave per row: groups (scan-jump) -> chunks (scan-jump) -> plain replay.
-// s is identical in every lane, so all control flow is uniform.
+// A window of 64 consecutive chunks: lane l holds chunk w*64+l's tables and the
+// double prefix at its start and end (used only to predict binade crossings).
+struct XsWin {
+  XsTab3 T;
+  double p0, p1;
+};
+
+// Chunk data prefetched for one window: up to XS_PF predicted crossing chunks,
+// lane l holding inputs 4l..4l+3 of each.
+constexpr int XS_PF = 4;
+struct XsPf {
+  uint32_t c[XS_PF];  // chunk ids (uniform); UINT32_MAX = empty slot
+  float v[XS_PF][4];
+};
+
+// One wave per row: stream the row's chunk tables window by window (64 chunks per
+// ordered scan), with tables loaded two windows ahead and the data of the chunks
+// whose double prefix predicts a binade or sign change loaded one window ahead, so
+// the serial chain rarely waits on memory.  A chunk that does not validate under
+// the running sum's binade is replayed with plain float adds.  s is identical in
+// every lane, so all control flow is uniform.
 template <int S>
-__global__ void __launch_bounds__(64) k_xs_chain(XsIn in, int K, const XsSum* __restrict__ ctab,
-                                                 const int32_t* __restrict__ cE, const XsSum* __restrict__ gtab,
-                                                 const int32_t* __restrict__ gE, uint32_t NC, uint32_t NG,
-                                                 float* __restrict__ out, int divide) {
+__global__ void __launch_bounds__(64) k_xs_chain(XsIn in, int K, const double* __restrict__ pre,
+                                                 const XsSum* __restrict__ ctab, const int32_t* __restrict__ cE,
+                                                 uint32_t NC, float* __restrict__ out, int divide) {
   KT();
   const int row = blockIdx.x, lane = threadIdx.x;
   const int b = row / K, k = row % K;
   const Prob P = prob_of(in, S, b);
   const float* x = P.base + k;
-  const uint32_t ng = (P.nch + XS_G - 1) / XS_G;
+  const uint32_t nch = P.nch, nw = (nch + 63) / 64;
+  const size_t t0 = (size_t)row * NC;
+  const double* pr = pre + (size_t)row * (NC + 1);
   float s = 0.f;
-  // Replay: the chunk is staged in LDS and summed with broadcast reads into a
-  // VGPR accumulator (a uniform SGPR chain would cost a readlane/readfirstlane
-  // round trip per add); reads of group g+1 overlap the adds of group g.
   __shared__ __attribute__((aligned(16))) float rb[XS_L + 16];
-  auto replay = [&](uint32_t c) {
-    XS_COUNT(1, 1);
-#ifdef XS_PROBE
-    const long long t0 = wall_clock64();
-#endif
-    const uint32_t m = min((uint32_t)XS_L, P.n - c * XS_L);
+
+  auto load_win = [&](uint32_t w, XsWin& W) {
+    const uint32_t c = w * 64 + lane;
+    const bool have = w < nw && c < nch;
+    W.T = load_tab3(ctab, cE, t0 + c, have);
+    W.p0 = have ? pr[c] : 0.0;
+    W.p1 = have ? pr[c + 1] : 0.0;
+  };
+  auto load_chunk = [&](uint32_t c, float v[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t i = c * XS_L + lane * 4 + j;
-      rb[lane * 4 + j] = i < P.n ? x[(size_t)i * S] : 0.f;
+      v[j] = x[(size_t)min(i, P.n - 1u) * S];
     }
+  };
+  // issue the data loads of window w's predicted crossing chunks
+  auto prefetch = [&](uint32_t w, const XsWin& W, XsPf& D) {
+    const uint32_t c = w * 64 + lane;
+    bool p = false;
+    if (w < nw && c < nch)
+      p = W.T.Eb == XS_NOE || xs_predict(W.p1) != W.T.Eb || ((W.p0 < 0.0) != (W.p1 < 0.0));
+    uint64_t m = __ballot(p);
+#pragma unroll
+    for (int q = 0; q < XS_PF; ++q) {
+      D.c[q] = m ? w * 64 + (uint32_t)__builtin_ctzll(m) : 0xffffffffu;
+      m &= m - 1;
+      if (D.c[q] != 0xffffffffu) load_chunk(D.c[q], D.v[q]);
+    }
+  };
+  // Replay: the chunk is staged in LDS and summed with broadcast reads into a
+  // VGPR accumulator (a uniform SGPR chain would cost a readlane/readfirstlane
+  // round trip per add); reads of add group g+1 overlap the adds of group g.
+  auto replay = [&](uint32_t c, const XsPf& D) {
+    XS_COUNT(1, 1);
+#ifdef XS_PROBE
+    const long long tr = wall_clock64();
+#endif
+    float v[4];
+    bool hit = false;
+#pragma unroll
+    for (int q = 0; q < XS_PF; ++q)
+      if (D.c[q] == c) {
+        hit = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = D.v[q][j];
+      }
+    if (!hit) {
+      XS_COUNT(5, 1);
+      load_chunk(c, v);
+    }
+    const uint32_t m = min((uint32_t)XS_L, P.n - c * XS_L);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[lane * 4 + j] = v[j];
     __syncthreads();
     float acc = s;
     constexpr int GR = 16;
@@ -324,19 +426,29 @@ __global__ void __launch_bounds__(64) k_xs_chain(XsIn in, int K, const XsSum* __
     s = acc;
     __syncthreads();
 #ifdef XS_PROBE
-    XS_COUNT(3, wall_clock64() - t0);
+    XS_COUNT(3, wall_clock64() - tr);
 #endif
   };
-  auto group = [&](uint32_t g) {
-    const uint32_t c0 = g * XS_G;
-    const int nc = (int)min((uint32_t)XS_G, P.nch - c0);
-    const XsTab3 C = load_tab3(ctab, cE, (size_t)row * NC + c0 + lane, lane < nc);
-    scan_jump(s, C, nc, [&](int f) { replay(c0 + (uint32_t)f); });
+  // window w: tables in Wc (loaded two windows ago), data in Dc (one window ago);
+  // issues the tables of w+2 into Wl and the data of w+1 into Dn.  Three-way
+  // rotation by unrolling, so no register holding an in-flight load is copied.
+  auto step = [&](uint32_t w, const XsWin& Wc, const XsWin& Wn, XsWin& Wl, const XsPf& Dc, XsPf& Dn) {
+    load_win(w + 2, Wl);
+    prefetch(w + 1, Wn, Dn);
+    const int nc = (int)min(64u, nch - w * 64);
+    scan_jump(s, Wc.T, nc, [&](int f) { replay(w * 64 + (uint32_t)f, Dc); });
   };
-  for (uint32_t gb = 0; gb < ng; gb += 64) {
-    const int na = (int)min(64u, ng - gb);
-    const XsTab3 G = load_tab3(gtab, gE, (size_t)row * NG + gb + lane, lane < na);
-    scan_jump(s, G, na, [&](int f) { group(gb + (uint32_t)f); });
+  XsWin W0, W1, W2;
+  XsPf D0, D1, D2;
+  load_win(0, W0);
+  load_win(1, W1);
+  prefetch(0, W0, D0);
+  for (uint32_t w = 0; w < nw; w += 3) {
+    step(w, W0, W1, W2, D0, D1);
+    if (w + 1 >= nw) break;
+    step(w + 1, W1, W2, W0, D1, D2);
+    if (w + 2 >= nw) break;
+    step(w + 2, W2, W0, W1, D2, D0);
   }
   if (lane == 0) out[row] = divide ? (P.n ? s / (float)P.n : 0.f) : s;
 }
@@ -348,28 +460,22 @@ inline uint32_t clampg(uint32_t v, uint32_t mx) { return v < 1 ? 1 : (v > mx ? m
 static size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
 size_t exact_sum_bytes(int rows, uint32_t cap) {
-  const size_t NC = cap / XS_L + 1, NG = NC / XS_G + 1;
+  const size_t NC = cap / XS_L + 1;
   return up256(rows * (NC + 1) * sizeof(double)) + up256(rows * NC * XS_NE * sizeof(XsSum)) +
-         up256(rows * NC * sizeof(int32_t)) + up256(rows * NG * XS_NE * sizeof(XsSum)) +
-         up256(rows * NG * sizeof(int32_t)) + 256;
+         up256(rows * NC * sizeof(int32_t)) + 256;
 }
 
 XsBufs exact_sum_carve(void* base, int rows, uint32_t cap) {
   XsBufs x;
   x.NC = cap / XS_L + 1;
-  x.NG = x.NC / XS_G + 1;
   x.rows = rows;
   char* p = (char*)(((uintptr_t)base + 255) & ~(uintptr_t)255);
-  const size_t NC = x.NC, NG = x.NG;
+  const size_t NC = x.NC;
   x.pre = (double*)p;
   p += up256(rows * (NC + 1) * sizeof(double));
   x.ctab = (XsSum*)p;
   p += up256(rows * NC * XS_NE * sizeof(XsSum));
   x.cE = (int32_t*)p;
-  p += up256(rows * NC * sizeof(int32_t));
-  x.gtab = (XsSum*)p;
-  p += up256(rows * NG * XS_NE * sizeof(XsSum));
-  x.gE = (int32_t*)p;
   return x;
 }
 
@@ -378,21 +484,19 @@ void exact_sum_in(const XsIn& in, int S, int K, int nprob, float* out, bool divi
   if (nprob <= 0) return;
   const int rows = nprob * K;
   if (rows > x.rows) throw Error(FCCF_E_INTERNAL, "exact_sum: scratch carved for fewer rows");
-  const dim3 gc(clampg((x.NC + 3) / 4, 1024), nprob), gg(clampg((x.NG + 3) / 4, 256), rows);
+  const dim3 gc(clampg((x.NC + 3) / 4, 1024), nprob);
   if (S == 3) {
     k_xs_csum<3><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
     // probe bytes: 12 B per element of every problem (two-array form: both counts)
     const uint32_t* c2 = in.data2 ? in.cnt2 : nullptr;
     FCCF_LAUNCH("k_xs_chunk", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
-    k_xs_group<<<gg, 256, 0, st>>>(in, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_LAUNCH("k_xs_chain", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    FCCF_LAUNCH("k_xs_chain", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
   } else {
     k_xs_csum<1><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
     FCCF_LAUNCH("k_xs_chunk", (in.cnt, 4.0 * 1), k_xs_chunk<1>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
-    k_xs_group<<<gg, 256, 0, st>>>(in, K, x.pre, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG);
-    FCCF_LAUNCH("k_xs_chain", (in.cnt, 4.0 * 1), k_xs_chain<1>, rows, 64, 0, st, in, K, x.ctab, x.cE, x.gtab, x.gE, x.NC, x.NG, out, divide);
+    FCCF_LAUNCH("k_xs_chain", (in.cnt, 4.0 * 1), k_xs_chain<1>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
   }
 }
 }  // namespace

@@ -45,8 +45,8 @@ int main(int argc, char** argv) {
     float out[3];
     hipMemcpy(out, d_out, 12, hipMemcpyDeviceToHost);
     hipMemcpyFromSymbol(z, HIP_SYMBOL(xs_probe), sizeof(z));
-    printf("n %u total %.1f us exact %d%d%d scans %llu replays %llu dmiss %llu replay_clk %llu scan_clk %llu\n", n,
-           ms * 1e3, out[0] == ref[0], out[1] == ref[1], out[2] == ref[2], z[0], z[1], z[2], z[3], z[4]);
+    printf("n %u total %.1f us exact %d%d%d scans %llu replays %llu dmiss %llu replay_clk %llu scan_clk %llu pf_miss %llu\n", n,
+           ms * 1e3, out[0] == ref[0], out[1] == ref[1], out[2] == ref[2], z[0], z[1], z[2], z[3], z[4], z[5]);
   }
   return 0;
 }
