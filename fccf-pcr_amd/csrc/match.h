@@ -13,7 +13,7 @@ constexpr int MAX_BASES = 136;   // C(17, 2)
 struct MPlane { float c[3], n[3], fps; int32_t nvox; };
 struct MBase { int32_t i1, i2; float angle; int32_t type; };
 
-struct MatchIn {
+struct alignas(16) MatchIn {
   MPlane F1[MAX_PLANES], F2[MAX_PLANES];
   MBase B1[MAX_BASES], B2[MAX_BASES];
   int32_t nF1, nF2, nB1, nB2;

@@ -146,12 +146,20 @@ __device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
   return cnt;
 }
 
+// The plane/pair tables into LDS, all threads copying 16-byte words.
+__device__ __forceinline__ void load_tables(MatchIn& M, const MatchIn* __restrict__ Mp) {
+  static_assert(sizeof(MatchIn) % 16 == 0, "MatchIn is copied in 16-byte words");
+  const int4* src = reinterpret_cast<const int4*>(Mp);
+  int4* dst = reinterpret_cast<int4*>(&M);
+  for (int i = threadIdx.x; i < (int)(sizeof(MatchIn) / 16); i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__ Mp, uint32_t* __restrict__ cnt,
                                                      int32_t* __restrict__ type) {
   KT();
-  __shared__ MatchIn M;
-  if (threadIdx.x == 0) M = *Mp;
-  __syncthreads();
+  __shared__ __attribute__((aligned(16))) MatchIn M;
+  load_tables(M, Mp);
   const int K = M.nB1 * M.nB2;
   for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < K; k += gridDim.x * 4) {
     const int n = match_test_wave(M, k, nullptr, nullptr);
@@ -162,39 +170,62 @@ __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__
   }
 }
 
-// single block: per-type exclusive scan in test order
-__global__ void __launch_bounds__(256) k_match_scan(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
-                                                    const int32_t* __restrict__ type, uint32_t* __restrict__ off,
-                                                    uint32_t* __restrict__ totals) {
+// single block of 1024 threads: per-type exclusive scan in test order.  Thread t
+// owns a contiguous run of tests: local per-type sums, one block scan of the
+// three sums, then a second walk over its run writes the offsets.
+__global__ void __launch_bounds__(1024) k_match_scan(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
+                                                     const int32_t* __restrict__ type, uint32_t* __restrict__ off,
+                                                     uint32_t* __restrict__ totals) {
   KT();
-  __shared__ uint32_t sh[4][3];
+  __shared__ uint32_t sh[16][3];
   const int K = Mp->nB1 * Mp->nB2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t carry[3] = {0, 0, 0};
-  for (int b0 = 0; b0 < K; b0 += 256) {
-    const int k = b0 + threadIdx.x;
-    const uint32_t c = k < K ? cnt[k] : 0u;
-    const int t = k < K ? type[k] : -1;
-    uint32_t ex = 0;
-    for (int ty = 0; ty < 3; ++ty) {
-      uint32_t x = (t == ty) ? c : 0u;
-      const uint32_t v = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) sh[w][ty] = x;
-      __syncthreads();
-      uint32_t wp = 0;
-      for (int ww = 0; ww < w; ++ww) wp += sh[ww][ty];
-      const uint32_t tot = sh[0][ty] + sh[1][ty] + sh[2][ty] + sh[3][ty];
-      __syncthreads();
-      if (t == ty) ex = carry[ty] + wp + x - v;
-      carry[ty] += tot;
-    }
-    if (k < K) off[k] = ex;
+  const int per = (K + 1023) / 1024;
+  const int k0 = min(K, (int)threadIdx.x * per), k1 = min(K, k0 + per);
+  uint32_t loc[3] = {0, 0, 0};
+  for (int k = k0; k < k1; ++k) {
+    const int t = type[k];
+    const uint32_t c = cnt[k];
+    loc[0] += t == 0 ? c : 0u;
+    loc[1] += t == 1 ? c : 0u;
+    loc[2] += t == 2 ? c : 0u;
   }
-  if (threadIdx.x < 3) totals[threadIdx.x] = carry[threadIdx.x];
+  uint32_t inc[3];
+#pragma unroll
+  for (int ty = 0; ty < 3; ++ty) {
+    uint32_t x = loc[ty];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    inc[ty] = x;
+    if (lane == 63) sh[w][ty] = x;
+  }
+  __syncthreads();
+  uint32_t run[3];
+#pragma unroll
+  for (int ty = 0; ty < 3; ++ty) {
+    uint32_t wp = 0, tot = 0;
+    for (int ww = 0; ww < 16; ++ww) {
+      wp += ww < w ? sh[ww][ty] : 0u;
+      tot += sh[ww][ty];
+    }
+    run[ty] = wp + inc[ty] - loc[ty];
+    if (threadIdx.x == 0) totals[ty] = tot;
+  }
+  for (int k = k0; k < k1; ++k) {
+    const int t = type[k];
+    const uint32_t c = cnt[k];
+    uint32_t o = 0;
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty)
+      if (t == ty) {
+        o = run[ty];
+        run[ty] += c;
+      }
+    off[k] = o;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
@@ -203,9 +234,8 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
                                                     MCand* __restrict__ c2, QTd* __restrict__ q0,
                                                     QTd* __restrict__ q1, QTd* __restrict__ q2) {
   KT();
-  __shared__ MatchIn M;
-  if (threadIdx.x == 0) M = *Mp;
-  __syncthreads();
+  __shared__ __attribute__((aligned(16))) MatchIn M;
+  load_tables(M, Mp);
   const int K = M.nB1 * M.nB2;
   for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < K; k += gridDim.x * 4) {
     if (!cnt[k]) continue;
@@ -224,7 +254,7 @@ void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, 
   if (K <= 0) return;
   const int g = (K + 3) / 4;  // one wave per test
   FCCF_LAUNCH("k_match_count", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_count, g, 256, 0, st, d_in, cnt, type);
-  k_match_scan<<<1, 256, 0, st>>>(d_in, cnt, type, off, totals);
+  k_match_scan<<<1, 1024, 0, st>>>(d_in, cnt, type, off, totals);
   FCCF_LAUNCH("k_match_emit", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_emit, g, 256, 0, st, d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]);
 }
 
