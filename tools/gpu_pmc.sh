@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic per launch from two separate PMC passes over the bench command
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; MI355X_MICROARCH.md "HBM").
+# Usage (via gpurun): bash tools/gpu_pmc.sh <tag>
+set -e
+TAG=${1:-pmc}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/fetch -o run -- python3 -u bench.py --no-cpu-baseline --steps 5 --warmup 2 > $OUT/fetch.json 2> $OUT/fetch.err
+echo "fetch pass ok"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/write -o run -- python3 -u bench.py --no-cpu-baseline --steps 5 --warmup 2 > $OUT/write.json 2> $OUT/write.err
+echo "write pass ok"
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json
+cat $OUT/pmc_traffic.json
