@@ -74,6 +74,14 @@ struct PinnedBuf {
   }
 };
 
+// Pinned, host-mapped, coherent mailboxes (mail.h), allocated once per ctx.
+struct MailBuf {
+  void* p = nullptr;
+  ~MailBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 // One captured hipGraph, re-captured whenever its key (the workspace layout and
 // every launch argument that is not read from device memory) changes.  The
 // pipeline's sizes live in device memory, so a graph replays for any input that
@@ -151,6 +159,7 @@ struct fccf_ctx {
   fccf::Arena arena2;  // matching (and the stage exports)
   fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
+  fccf::MailBuf mail;  // pipeline.cpp host_mail()
   fccf::Pool pool;
   fccf::Probe probe;
   bool debug = false;

@@ -15,6 +15,7 @@
 #define KT_TU 3  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
+#include "mail.h"
 
 namespace fccf {
 namespace {
@@ -367,7 +368,10 @@ __global__ void __launch_bounds__(256) k_compact_resid(B2<FaceBufs> fb, B2<const
 }
 
 // Planar leaves with the normal oriented towards the cloud centroid (:504-516).
-__global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxRec*> pout2) {
+// With a mailbox, the records (up to its capacity) and both clouds' counts are
+// also written to pinned host memory: phase B reads them after one event sync.
+__global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxRec*> pout2, CloudMail* __restrict__ mail,
+                                                        B2<const uint32_t*> sc2) {
   KT();
   const int e = blockIdx.y;
   const FaceBufs& B = fb.v[e];
@@ -377,13 +381,20 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
   const float* __restrict__ cc = B.centroid;
   VoxRec* __restrict__ pout = pout2[e];
   const uint32_t nl = *B.nleaf;
+  if (mail && blockIdx.x == 0 && threadIdx.x < 8) {
+    const uint32_t i = threadIdx.x & 3u;
+    if (threadIdx.x < 4) mail->sc[e][i] = sc2[e][i];
+    else mail->fsc[e][i] = B.nleaf[i];
+  }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
     if (!planar[s]) continue;
     VoxRec r = recs[s];
     const f3 to = {r.c[0] - cc[0], r.c[1] - cc[1], r.c[2] - cc[2]};
     const f3 nv = {r.n[0], r.n[1], r.n[2]};
     if (!(dot3(to, nv) < 0.f)) { r.n[0] = -nv.x; r.n[1] = -nv.y; r.n[2] = -nv.z; }
-    pout[poff[s]] = r;
+    const uint32_t o = poff[s];
+    pout[o] = r;
+    if (mail && o < CloudMail::REC_CAP) mail->rec[e][o] = r;
   }
 }
 
@@ -476,8 +487,9 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
   octree_sim(xyz, d_n, cap, res, aggr, state, st);
 }
 
-void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch) {
-  k_compact_planar<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, planar_out);
+void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch,
+                        CloudMail* mail, B2<const uint32_t*> sc) {
+  k_compact_planar<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, planar_out, mail, sc);
 }
 
 }  // namespace fccf

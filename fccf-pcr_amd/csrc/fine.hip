@@ -12,6 +12,7 @@
 #include "probe.h"
 #include "kernels.h"
 #include "match.h"
+#include "mail.h"
 
 namespace fccf {
 namespace {
@@ -140,10 +141,15 @@ __global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __res
 }
 
 __global__ void k_fv_score(const float* __restrict__ similar, const float* __restrict__ all, float* __restrict__ scores,
-                           int E) {
+                           int E, const uint32_t* __restrict__ scal, FineMail* __restrict__ mail) {
   KT();
   const int e = threadIdx.x;
-  if (e < E) scores[e] = similar[e] / all[e];
+  if (e < E) {
+    const float sc = similar[e] / all[e];
+    scores[e] = sc;
+    if (mail) mail->scores[e] = sc;
+  }
+  if (mail && e == 0) mail->err = scal[7];
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -154,7 +160,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 }  // namespace
 
 void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
-                       double res, FineBufs b, hipStream_t st) {
+                       double res, FineBufs b, hipStream_t st, FineMail* mail) {
   if (E <= 0) return;
   const size_t astride = aggr_floats(n2);
   k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t);
@@ -177,7 +183,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   FCCF_LAUNCH("k_fv_counts", (b.scal, 16.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.k1, b.starts, b.scal, b.term, b.range);
   k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
-  k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E);
+  k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E, b.scal, mail);
 }
 
 }  // namespace fccf

@@ -80,7 +80,10 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
 void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float voxel_point_threshold, float curvature_threshold, B2<float*> resid_out,
                      B2<FaceBufs> b, hipStream_t st, int nbatch = 1);
 // Planar records, oriented towards b.centroid (must be ready: the caller orders streams).
-void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch = 1);
+struct CloudMail;
+// mail (may be null): pinned mailbox receiving the records and both clouds' counts (sc = scalars of each cloud)
+void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch = 1,
+                        CloudMail* mail = nullptr, B2<const uint32_t*> sc = B2<const uint32_t*>(nullptr));
 
 // Byte strides between the sequences of a batched octree launch: sequence e uses
 // xyz + e*xyz, aggr + e*aggr, state + e*state, d_n + e*n (bytes; 0 = shared).

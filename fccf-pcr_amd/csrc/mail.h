@@ -1,0 +1,44 @@
+// mail.h — pinned, host-mapped mailboxes that the device stages write their
+// phase-B outputs into, so the host reads them after ONE event/stream sync per
+// stage instead of a chain of count-then-data device-to-host copies (each
+// pageable copy is a blocking host round trip on ROCm).  Device kernels fill
+// them as a side effect of a launch they already make (k_compact_planar,
+// k_match_scan/k_match_emit, k_fv_score).  Anything past a mailbox capacity is
+// still in its device buffer; the host copies that rare overflow explicitly.
+#pragma once
+#include <stdint.h>
+
+#include "kernels.h"
+#include "match.h"
+
+namespace fccf {
+
+struct CloudMail {                     // one per cloud set (double-buffered pairs)
+  static constexpr uint32_t REC_CAP = 16384;   // planar 1 m voxels per cloud
+  uint32_t sc[2][4];                   // per cloud: n_in, M1, M1 finite, M2
+  uint32_t fsc[2][4];                  // per cloud: leaves, -, planar leaves, residual points
+  VoxRec rec[2][REC_CAP];              // oriented planar records, Morton order
+};
+
+struct MatchMail {
+  static constexpr uint32_t Q_CAP = 65536;     // candidate transforms per type
+  MatchIn M;                           // host staging of the matching tables (H2D source)
+  uint32_t tot[4];                     // candidates per type
+  uint32_t kpass;                      // tests with >= 1 candidate
+  uint32_t pad[3];
+  QTd q[3][Q_CAP];
+};
+
+struct FineMail {
+  m44 T[MAX_EVAL];                     // host staging of the evaluated transforms (H2D source)
+  float scores[MAX_EVAL];
+  uint32_t err;                        // fine_verify scal[7]
+};
+
+struct HostMail {
+  CloudMail clouds[2];
+  MatchMail match;
+  FineMail fine;
+};
+
+}  // namespace fccf

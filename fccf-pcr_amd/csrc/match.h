@@ -26,8 +26,10 @@ struct MCand { float R[9]; float t[3]; };
 struct QTd { float qw, qx, qy, qz, tx, ty, tz; uint32_t alloc; };
 
 // counts/types/offsets need K entries; totals 3; c[t]/q[t] sized by the caller.
+struct MatchMail;
+// mail (may be null): pinned mailbox receiving the totals, K_pass and the candidate lists (mail.h)
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
-                      MCand* c[3], QTd* q[3], hipStream_t st);
+                      MCand* c[3], QTd* q[3], hipStream_t st, MatchMail* mail = nullptr);
 
 // ------------------------------------------------ K7: fine_verify (FCCF.cpp:785-839)
 constexpr int MAX_EVAL = 16;
@@ -50,8 +52,10 @@ struct FineBufs {
   XsBufs xs;           // similar_num sum scratch (E rows, cap n1 + n2)
 };
 // s1_state: octree bounds after inserting S1 alone (octree_replay, run ahead of time).
+// mail (may be null): pinned mailbox receiving the E scores and the error word (mail.h)
+struct FineMail;
 void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
                        double res, FineBufs b,
-                       hipStream_t st);
+                       hipStream_t st, FineMail* mail = nullptr);
 
 }  // namespace fccf

@@ -12,6 +12,7 @@
 #include "probe.h"
 #include "kernels.h"
 #include "match.h"
+#include "mail.h"
 
 namespace fccf {
 namespace {
@@ -78,7 +79,8 @@ __device__ f3 ls3(f3 n1, f3 m1, f3 k1, f3 D) {
 // over the lanes; ballot + mbcnt give every accepted pair its rank, so emission
 // keeps loop order.  Returns the number of transforms the test emits (>= 1 when
 // the test passes: the weighted-centroid fallback); writes them when out != null.
-__device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
+// hq (may be null): host mailbox of this type; qout[r] goes to hq[hoff + r] too while in capacity.
+__device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout, QTd* hq = nullptr, uint32_t hoff = 0) {
   const int lane = threadIdx.x & 63;
   const int i1 = k / M.nB2, i2 = k % M.nB2;
   const MBase& b1 = M.B1[i1];
@@ -121,7 +123,9 @@ __device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
       for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) o.R[3 * a + b] = c.rot.m[a][b];
       o.t[0] = t.x; o.t[1] = t.y; o.t[2] = t.z;
-      qout[r] = {qr.w, qr.x, qr.y, qr.z, t.x, t.y, t.z, 0u};
+      const QTd qv = {qr.w, qr.x, qr.y, qr.z, t.x, t.y, t.z, 0u};
+      qout[r] = qv;
+      if (hq && hoff + (uint32_t)r < MatchMail::Q_CAP) hq[hoff + r] = qv;
     }
     cnt += (int)__popcll(m);
   }
@@ -139,7 +143,9 @@ __device__ int match_test_wave(const MatchIn& M, int k, MCand* out, QTd* qout) {
       for (int a2 = 0; a2 < 3; ++a2)
         for (int b2i = 0; b2i < 3; ++b2i) o.R[3 * a2 + b2i] = c.rot.m[a2][b2i];
       o.t[0] = sx - tc.x; o.t[1] = sy - tc.y; o.t[2] = sz - tc.z;
-      qout[0] = {qr.w, qr.x, qr.y, qr.z, o.t[0], o.t[1], o.t[2], 0u};
+      const QTd qv = {qr.w, qr.x, qr.y, qr.z, o.t[0], o.t[1], o.t[2], 0u};
+      qout[0] = qv;
+      if (hq && hoff < MatchMail::Q_CAP) hq[hoff] = qv;
     }
     cnt = 1;
   }
@@ -175,20 +181,23 @@ __global__ void __launch_bounds__(256) k_match_count(const MatchIn* __restrict__
 // three sums, then a second walk over its run writes the offsets.
 __global__ void __launch_bounds__(1024) k_match_scan(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
                                                      const int32_t* __restrict__ type, uint32_t* __restrict__ off,
-                                                     uint32_t* __restrict__ totals) {
+                                                     uint32_t* __restrict__ totals, MatchMail* __restrict__ mail) {
   KT();
   __shared__ uint32_t sh[16][3];
+  __shared__ uint32_t kp;
+  if (threadIdx.x == 0) kp = 0;
   const int K = Mp->nB1 * Mp->nB2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int per = (K + 1023) / 1024;
   const int k0 = min(K, (int)threadIdx.x * per), k1 = min(K, k0 + per);
-  uint32_t loc[3] = {0, 0, 0};
+  uint32_t loc[3] = {0, 0, 0}, pass = 0;
   for (int k = k0; k < k1; ++k) {
     const int t = type[k];
     const uint32_t c = cnt[k];
     loc[0] += t == 0 ? c : 0u;
     loc[1] += t == 1 ? c : 0u;
     loc[2] += t == 2 ? c : 0u;
+    pass += c ? 1u : 0u;
   }
   uint32_t inc[3];
 #pragma unroll
@@ -212,7 +221,15 @@ __global__ void __launch_bounds__(1024) k_match_scan(const MatchIn* __restrict__
       tot += sh[ww][ty];
     }
     run[ty] = wp + inc[ty] - loc[ty];
-    if (threadIdx.x == 0) totals[ty] = tot;
+    if (threadIdx.x == 0) {
+      totals[ty] = tot;
+      if (mail) mail->tot[ty] = tot;
+    }
+  }
+  if (mail) {  // K_pass for the stats (tests with >= 1 candidate)
+    if (pass) atomicAdd(&kp, pass);
+    __syncthreads();
+    if (threadIdx.x == 0) mail->kpass = kp;
   }
   for (int k = k0; k < k1; ++k) {
     const int t = type[k];
@@ -232,7 +249,8 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
                                                     const int32_t* __restrict__ type, const uint32_t* __restrict__ off,
                                                     MCand* __restrict__ c0, MCand* __restrict__ c1,
                                                     MCand* __restrict__ c2, QTd* __restrict__ q0,
-                                                    QTd* __restrict__ q1, QTd* __restrict__ q2) {
+                                                    QTd* __restrict__ q1, QTd* __restrict__ q2,
+                                                    MatchMail* __restrict__ mail) {
   KT();
   __shared__ __attribute__((aligned(16))) MatchIn M;
   load_tables(M, Mp);
@@ -243,19 +261,19 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
     MCand* cb = t == 0 ? c0 : (t == 1 ? c1 : c2);
     QTd* qb = t == 0 ? q0 : (t == 1 ? q1 : q2);
     const uint32_t o = off[k];
-    match_test_wave(M, k, cb + o, qb + o);
+    match_test_wave(M, k, cb + o, qb + o, mail ? mail->q[t] : nullptr, o);
   }
 }
 
 }  // namespace
 
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
-                      MCand* c[3], QTd* q[3], hipStream_t st) {
+                      MCand* c[3], QTd* q[3], hipStream_t st, MatchMail* mail) {
   if (K <= 0) return;
   const int g = (K + 3) / 4;  // one wave per test
   FCCF_LAUNCH("k_match_count", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_count, g, 256, 0, st, d_in, cnt, type);
-  k_match_scan<<<1, 1024, 0, st>>>(d_in, cnt, type, off, totals);
-  FCCF_LAUNCH("k_match_emit", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_emit, g, 256, 0, st, d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2]);
+  k_match_scan<<<1, 1024, 0, st>>>(d_in, cnt, type, off, totals, mail);
+  FCCF_LAUNCH("k_match_emit", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_emit, g, 256, 0, st, d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2], mail);
 }
 
 }  // namespace fccf

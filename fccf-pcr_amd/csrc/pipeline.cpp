@@ -26,6 +26,7 @@
 #include "host_stages.h"
 #include "kernels.h"
 #include "match.h"
+#include "mail.h"
 #include "pipeline.h"
 
 namespace fccf {
@@ -233,6 +234,17 @@ void seg_faces(CloudWS* w, const fccf_params& P, hipStream_t st) {
   octree_replay(w[0].resid, w[0].fb.nresid, cap, (double)P.fine_verify_voxel_size, w[0].faggr, w[0].fstate, st);
 }
 
+// The ctx's pinned mailboxes (mail.h): allocated once, so graph-captured kernels may hold the pointer.
+HostMail* host_mail(fccf_ctx* c) {
+  if (!c->mail.p) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(HostMail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      throw Error(FCCF_E_OOM, "hipHostMalloc mailbox");
+    c->mail.p = p;
+  }
+  return (HostMail*)c->mail.p;
+}
+
 template <class T>
 std::vector<T> d2h(const T* d, size_t n, hipStream_t st) {
   std::vector<T> v(n);
@@ -358,7 +370,8 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   cs.g_seg[1].run(&key, sizeof key, st0, [&] { seg_faces(w, P, st0); });
   mark(2, st0);
   HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[2], 0));
-  face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2);
+  face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
+                     &host_mail(c)->clouds[s], B2<const uint32_t*>(w[0].sc, w[1].sc));
   mark(4, st0);
   tm.armed = seg_timing;
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
@@ -381,23 +394,26 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   const auto t_all = ps.t_enq;
   auto t0 = ps.t_enq;
   hipStream_t st0 = c->sb;
+  // counts and planar records of both clouds: written by k_compact_planar into
+  // this set's pinned mailbox, visible once the clouds-done event has completed
+  CloudMail& cm = host_mail(c)->clouds[s];
+  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
   HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[4], 0));
-  // counts of both clouds
   uint32_t sc[2][4], fsc[2][4];
+  std::memcpy(sc, cm.sc, sizeof sc);
+  std::memcpy(fsc, cm.fsc, sizeof fsc);
+  std::vector<VoxRec> vox[2];
   for (int k = 0; k < 2; ++k) {
-    HIP_CHECK(hipMemcpyAsync(sc[k], w[k].sc, 16, hipMemcpyDeviceToHost, st0));
-    HIP_CHECK(hipMemcpyAsync(fsc[k], w[k].fb.nleaf, 16, hipMemcpyDeviceToHost, st0));
+    if (fsc[k][2] <= CloudMail::REC_CAP) vox[k].assign(cm.rec[k], cm.rec[k] + fsc[k][2]);
+    else vox[k] = d2h(w[k].planar, fsc[k][2], st0);  // past the mailbox: copy from HBM
   }
-  HIP_CHECK(hipStreamSynchronize(st0));
+  if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
   S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
   seg_timer_print(s);
   after_clouds();
   t0 = clk::now();
   S.m_tar = sc[0][3];
   S.m_src = sc[1][3];
-  std::vector<VoxRec> vox[2];
-  for (int k = 0; k < 2; ++k) vox[k] = d2h(w[k].planar, fsc[k][2], st0);
-  HIP_CHECK(hipStreamSynchronize(st0));
   S.vox1 = fsc[0][2]; S.vox2 = fsc[1][2];
   S.res1 = fsc[0][3]; S.res2 = fsc[1][3];
   if (c->debug) {
@@ -477,7 +493,8 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   if (g[0].planes.size() > (size_t)MAX_PLANES || g[1].planes.size() > (size_t)MAX_PLANES ||
       base[0].size() > (size_t)MAX_BASES || base[1].size() > (size_t)MAX_BASES)
     throw Error(FCCF_E_INTERNAL, "plane table capacity");
-  MatchIn M;
+  MatchMail& mm = host_mail(c)->match;
+  MatchIn& M = mm.M;  // built in pinned memory: the H2D below is a true async copy
   std::memset(&M, 0, sizeof M);
   for (int k = 0; k < 2; ++k) {
     MPlane* dst = k == 0 ? M.F1 : M.F2;
@@ -517,16 +534,21 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   uint32_t tot[4] = {0, 0, 0, 0};
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
   HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
-  match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st0);
+  match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipMemcpyAsync(tot, dtot, 12, hipMemcpyDeviceToHost, st0));
-  HIP_CHECK(hipStreamSynchronize(st0));
+  HIP_CHECK(hipStreamSynchronize(st0));  // totals, K_pass and candidate lists are in the mailbox
   std::vector<QTd> qraw[3];
-  for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
-  std::vector<uint32_t> hcnt = d2h(dcnt, (size_t)K, st0);
-  HIP_CHECK(hipStreamSynchronize(st0));
   int64_t kpass = 0;
-  for (int k = 0; k < K; ++k) kpass += hcnt[k] ? 1 : 0;
+  if (K > 0) {
+    std::memcpy(tot, mm.tot, 12);
+    kpass = mm.kpass;
+    bool over = false;
+    for (int t = 0; t < 3; ++t) {
+      if (tot[t] <= MatchMail::Q_CAP) qraw[t].assign(mm.q[t], mm.q[t] + tot[t]);
+      else { qraw[t] = d2h(dq[t], tot[t], st0); over = true; }  // past the mailbox: copy from HBM
+    }
+    if (over) HIP_CHECK(hipStreamSynchronize(st0));
+  }
   S.K_pass = kpass;
   for (int t = 0; t < 3; ++t) S.cand[t] = tot[t];
   S.ms[FCCF_T_MATCH] = ms_since(t0);
@@ -639,7 +661,9 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     fb.ss = sort_scratch_carve(c->arena3.take(sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1))),
                                (uint32_t)std::max<size_t>(nk, 1));
     fb.xs = exact_sum_carve(c->arena3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
-    HIP_CHECK(hipMemcpyAsync(fb.T, evals.data(), sizeof(m44) * E, hipMemcpyHostToDevice, st0));
+    FineMail& fm = host_mail(c)->fine;
+    std::memcpy(fm.T, evals.data(), sizeof(m44) * E);  // pinned staging: async H2D
+    HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, st0));
     struct {
       const void* base;
       size_t acap;
@@ -653,13 +677,13 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     // small kernels from the two stages interleave badly, run back to back they don't
     if (fine_after) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
     c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
-      fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0);
+      fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0,
+                        &fm);
     });
     HIP_CHECK(hipGetLastError());
-    uint32_t ferr = 0;
-    HIP_CHECK(hipMemcpyAsync(scores.data(), fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st0));
-    HIP_CHECK(hipMemcpyAsync(&ferr, fb.scal + 7, 4, hipMemcpyDeviceToHost, st0));
-    HIP_CHECK(hipStreamSynchronize(st0));
+    HIP_CHECK(hipStreamSynchronize(st0));  // scores and the error word are in the mailbox
+    std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
+    const uint32_t ferr = fm.err;
     if (ferr) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
   }
   S.ms[FCCF_T_FINE] = ms_since(t0);

@@ -50,7 +50,7 @@ def rot_err_rad(A, B):
     return float(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1)))
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c3"])
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "c5"])
 def test_register_bit_exact(ctx, oracle, fccf, cfg):
     c = fccf.CONFIGS[cfg]
     src, tar, T_gt = fccf.synth_pair(c["n"], c["room"])
