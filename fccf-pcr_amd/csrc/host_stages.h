@@ -8,6 +8,7 @@
 #include "../../include/fccf.h"
 #include "fccf_math.h"
 #include "kernels.h"
+#include "pool.h"
 
 namespace fccf {
 
@@ -44,9 +45,10 @@ struct QT {  // transform_q_t (FCCF.cpp:74-84)
   uint32_t alloc;
 };
 
-// transform_cluster (:1040-1231) incl. range_cluster and average_normal.
+// transform_cluster (:1040-1231) incl. range_cluster and average_normal.  pool (may be
+// null) builds the neighbour lists of consecutive seeds in parallel.
 void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
-                       int64_t* nclusters);
+                       int64_t* nclusters, Pool* pool = nullptr);
 
 // quick_verify (:680-783) with ceres_refine (:210-249): refines T in place, returns score.
 float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2, const fccf_params& P,

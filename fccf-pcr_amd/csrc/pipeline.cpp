@@ -584,7 +584,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     const int cluster_num =
         transformation_num ? (int)(P.seclct_cluster_number * (float)qv.size() / (float)transformation_num) : 0;
     int64_t ncl = 0;
-    transform_cluster(qv, fine, cluster_num, P, &ncl);
+    transform_cluster(qv, fine, cluster_num, P, &ncl, &c->pool);
     counts.push_back(ncl);
     S.fine[t] = (int64_t)fine.size();
     S.ms[FCCF_T_CLUSTER] += ms_since(tc);

@@ -1,10 +1,22 @@
 // pool.h — small persistent host thread pool for the independent per-candidate
-// host stages (quick_verify + LM).  parallel_for writes results into per-index
-// slots, so the outcome does not depend on scheduling.
+// host stages (quick_verify + LM, clustering neighbour lists).  parallel_for
+// writes results into per-index slots, so the outcome does not depend on
+// scheduling.
+//
+// Latency matters more than throughput here: a registration makes a few
+// parallel_for calls of ~10-100 items, each item 1-50 us.  So
+//  * idle workers spin on the job word for a while before sleeping on a condition
+//    variable (a futex wake-up costs tens of microseconds per thread);
+//  * items are claimed with a CAS on one 64-bit word holding (job id, next index),
+//    so a worker that wakes late can never claim an item of a finished job;
+//  * the caller returns as soon as every item is done, without waiting for
+//    workers that never woke up.
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdint>
 #include <cstdlib>
 #include <functional>
 #include <mutex>
@@ -20,65 +32,87 @@ class Pool {
       const char* e = std::getenv("FCCF_HOST_THREADS");
       n = e ? std::atoi(e) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     }
+    const char* s = std::getenv("FCCF_POOL_SPIN_US");
+    spin_us_ = s ? std::atoi(s) : 500;
     for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
   }
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(m_);
-      quit_ = true;
+      quit_.store(true);
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
   }
   int size() const { return (int)workers_.size() + 1; }
-  // Runs f(i) for i in [0, n); the caller participates.
+  // Runs f(i) for i in [0, n); the caller participates.  Not reentrant.
   void parallel_for(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
     if (workers_.empty() || n == 1) {
       for (int i = 0; i < n; ++i) f(i);
       return;
     }
+    const uint64_t job = (job_ + 1) & 0xffffffffu;
+    job_ = job;
+    fn_ = &f;
+    n_.store(n, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    word_.store(job << 32, std::memory_order_release);  // publishes fn_, n_, done_
     {
-      std::lock_guard<std::mutex> g(m_);
-      fn_ = &f;
-      n_ = n;
-      next_.store(0);
-      active_ = (int)workers_.size();
-      ++gen_;
+      std::lock_guard<std::mutex> g(m_);  // pairs with the sleepers' predicate check
     }
     cv_.notify_all();
-    run();
-    std::unique_lock<std::mutex> g(m_);
-    done_cv_.wait(g, [this] { return active_ == 0; });
-    fn_ = nullptr;
+    run(job);
+    while (done_.load(std::memory_order_acquire) != n) relax();
   }
 
  private:
-  void run() {
-    for (int i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+  static void relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+  // Claims and runs items of job `job` until none is left.
+  void run(uint64_t job) {
+    uint64_t w = word_.load(std::memory_order_acquire);
+    while ((w >> 32) == job) {
+      const int i = (int)(w & 0xffffffffu);
+      if (i >= n_.load(std::memory_order_relaxed)) return;
+      if (!word_.compare_exchange_weak(w, w + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+      (*fn_)(i);
+      done_.fetch_add(1, std::memory_order_acq_rel);
+      w = word_.load(std::memory_order_acquire);
+    }
   }
   void loop() {
     uint64_t seen = 0;
     while (true) {
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return quit_ || gen_ != seen; });
-        if (quit_) return;
-        seen = gen_;
+      const auto t0 = std::chrono::steady_clock::now();
+      uint64_t w;
+      int k = 0;
+      while (((w = word_.load(std::memory_order_acquire)) >> 32) == seen && !quit_.load()) {
+        relax();
+        if ((++k & 255) == 0 &&
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us_) {
+          std::unique_lock<std::mutex> g(m_);
+          cv_.wait(g, [&] { return quit_.load() || (word_.load() >> 32) != seen; });
+        }
       }
-      run();
-      std::lock_guard<std::mutex> g(m_);
-      if (--active_ == 0) done_cv_.notify_all();
+      if (quit_.load()) return;
+      seen = w >> 32;
+      run(seen);
     }
   }
   std::vector<std::thread> workers_;
   std::mutex m_;
-  std::condition_variable cv_, done_cv_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> word_{0};  // (job id << 32) | next item
+  std::atomic<int> done_{0};
+  std::atomic<bool> quit_{false};
   const std::function<void(int)>* fn_ = nullptr;
-  std::atomic<int> next_{0};
-  int n_ = 0, active_ = 0;
-  uint64_t gen_ = 0;
-  bool quit_ = false;
+  std::atomic<int> n_{0};
+  uint64_t job_ = 0;
+  int spin_us_ = 500;
 };
 
 }  // namespace fccf
