@@ -177,22 +177,11 @@ m44 T_from_qt(const QT& t) {
   return T;
 }
 
-void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
-                       int64_t* nclp, Pool* pool) {
+// The host radius search of transform_cluster (:1075-1103): clusters in creation
+// order (seed, size) with their members in (d2, j) order as ranges of `mem`.
+static void cpu_clusters(std::vector<QT>& in, const fccf_params& P, float r2, Pool* pool, std::vector<int>& cseed,
+                         std::vector<int>& csize, std::vector<int>& mem, std::vector<int>& cbeg) {
   const int n = (int)in.size();
-  if (nclp) *nclp = 0;
-  if ((float)n <= P.cluster_number_threshold) {
-    if (n == 0) fine.push_back({1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1u});
-    else fine.insert(fine.end(), in.begin(), in.end());
-    return;
-  }
-  // KdTreeFLANN::radiusSearch(q, r): every j with L2_Simple d2 < float(r*r), sorted by (d2, j).
-  // d2 = ((0 + ex^2) + ey^2) + ez^2 adds non-negative terms, so d2 < r2 implies
-  // fl(ex)^2 < r2; that predicate is monotone along candidates sorted by tx, so two
-  // binary searches give a window that contains every neighbour, and the exact d2
-  // test inside it decides.  Candidates with non-finite tx have no neighbours
-  // (d2 is NaN or inf, even against themselves).
-  const float r2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
   std::vector<int> byx;
   byx.reserve(n);
   for (int i = 0; i < n; ++i)
@@ -245,9 +234,6 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
     }
     std::sort(nb.begin(), nb.end());
   };
-  // clusters as ranges of one flat member list, in creation order
-  std::vector<int> mem;
-  std::vector<int> cbeg;
   // Per seed the list costs ~0.2 us at C ~ 1e3 (measured), below a parallel_for's
   // overhead, so the speculative batches only pay for large candidate sets.
   if (n < 16384) pool = nullptr;
@@ -267,6 +253,8 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
       for (size_t b = 0; b < seeds.size(); ++b) neighbours(seeds[b], nbs[b], d2ws[b]);
     for (size_t b = 0; b < seeds.size(); ++b) {
       if (in[seeds[b]].alloc) continue;  // taken by an earlier seed of this batch
+      cseed.push_back(seeds[b]);
+      csize.push_back((int)nbs[b].size());
       cbeg.push_back((int)mem.size());
       for (auto& e : nbs[b]) {
         in[e.second].alloc = 1u;
@@ -274,11 +262,79 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
       }
     }
   }
-  const int ncl = (int)cbeg.size();
   cbeg.push_back((int)mem.size());
+}
+
+void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
+                       int64_t* nclp, Pool* pool, const uint64_t* bits) {
+  const int n = (int)in.size();
+  if (nclp) *nclp = 0;
+  if ((float)n <= P.cluster_number_threshold) {
+    if (n == 0) fine.push_back({1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1u});
+    else fine.insert(fine.end(), in.begin(), in.end());
+    return;
+  }
+  // KdTreeFLANN::radiusSearch(q, r): every j with L2_Simple d2 < float(r*r), sorted by (d2, j).
+  // d2 = ((0 + ex^2) + ey^2) + ez^2 adds non-negative terms, so d2 < r2 implies
+  // fl(ex)^2 < r2; that predicate is monotone along candidates sorted by tx, so two
+  // binary searches give a window that contains every neighbour, and the exact d2
+  // test inside it decides.  Candidates with non-finite tx have no neighbours
+  // (d2 is NaN or inf, even against themselves).
+  const float r2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
+  // clusters in creation order: seed, size, and (CPU path) the members in
+  // (d2, j) order as ranges of one flat list
+  std::vector<int> cseed, csize, mem, cbeg;
+  if (bits) {
+    // Device rows (k_cluster_bits): row i = the neighbour set of seed i.  Seeds are
+    // applied in order; a seed already taken is skipped (:1084-1086).
+    const int W = (n + 63) / 64;
+    std::vector<uint64_t> A(W, 0);
+    for (int i = 0; i + 1 < n; ++i) {  // the last candidate never seeds (:1084)
+      if ((A[i >> 6] >> (i & 63)) & 1u) continue;
+      const uint64_t* row = bits + (size_t)i * W;
+      int c = 0;
+      for (int w = 0; w < W; ++w) {
+        A[w] |= row[w];
+        c += __builtin_popcountll(row[w]);
+      }
+      cseed.push_back(i);
+      csize.push_back(c);
+    }
+  } else {
+    cpu_clusters(in, P, r2, pool, cseed, csize, mem, cbeg);
+  }
+  const int ncl = (int)cseed.size();
   if (nclp) *nclp = (int64_t)ncl;
   if (ncl == 0) return;
-  auto sz = [&](int k) { return cbeg[k + 1] - cbeg[k]; };
+  auto sz = [&](int k) { return csize[k]; };
+  // members of cluster k in the radius search's (d2, j) order
+  std::vector<int> mk;
+  std::vector<std::pair<float, int>> mord;
+  auto members = [&](int k) -> const std::vector<int>& {
+    mk.clear();
+    if (!bits) {
+      mk.assign(mem.begin() + cbeg[k], mem.begin() + cbeg[k + 1]);
+      return mk;
+    }
+    const int W = (n + 63) / 64;
+    const int i = cseed[k];
+    const uint64_t* row = bits + (size_t)i * W;
+    const float xi = in[i].tx, yi = in[i].ty, zi = in[i].tz;
+    mord.clear();
+    for (int w = 0; w < W; ++w)
+      for (uint64_t m = row[w]; m; m &= m - 1) {
+        const int j = w * 64 + __builtin_ctzll(m);
+        const float ex = xi - in[j].tx, ey = yi - in[j].ty, ez = zi - in[j].tz;
+        float d2 = 0.0f;
+        d2 += ex * ex;
+        d2 += ey * ey;
+        d2 += ez * ez;
+        mord.push_back({d2, j});
+      }
+    std::sort(mord.begin(), mord.end());
+    for (auto& e : mord) mk.push_back(e.second);
+    return mk;
+  };
   // range_cluster (:1020-1038), an exchange sort by size (swap when strictly
   // smaller).  Elements below a threshold never change the relative order of the
   // elements at or above it, and the sorted prefix holds exactly those.  With
@@ -305,14 +361,14 @@ void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_n
     const int size_r = is_big ? sz(big[r]) : rest_sizes[r - big.size()];
     if (size_r >= clusternum) {
       const int kk = big[r];  // size_r >= clusternum >= thr: r is in the big prefix
-      const int b0 = cbeg[kk], b1 = cbeg[kk + 1];
+      const std::vector<int>& mm = members(kk);
       float ax = 0, ay = 0, az = 0;
-      for (int m = b0; m < b1; ++m) { ax = ax + in[mem[m]].tx; ay = ay + in[mem[m]].ty; az = az + in[mem[m]].tz; }
-      const float cs = (float)(b1 - b0);
+      for (int m : mm) { ax = ax + in[m].tx; ay = ay + in[m].ty; az = az + in[m].tz; }
+      const float cs = (float)mm.size();
       ax = ax / cs; ay = ay / cs; az = az / cs;
       float s1[3] = {0, 0, 0}, s2[3] = {0, 0, 0};
-      for (int m = b0; m < b1; ++m) {
-        const QT& t = in[mem[m]];
+      for (int m : mm) {
+        const QT& t = in[m];
         const quatf q = {t.qw, t.qx, t.qy, t.qz};
         const f3 u = quat_rotate(q, f3{1.f, 0.f, 0.f}), v = quat_rotate(q, f3{0.f, 1.f, 0.f});
         s1[0] = s1[0] + u.x; s1[1] = s1[1] + u.y; s1[2] = s1[2] + u.z;

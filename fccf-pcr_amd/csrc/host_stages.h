@@ -46,9 +46,11 @@ struct QT {  // transform_q_t (FCCF.cpp:74-84)
 };
 
 // transform_cluster (:1040-1231) incl. range_cluster and average_normal.  pool (may be
-// null) builds the neighbour lists of consecutive seeds in parallel.
+// null) builds the neighbour lists of consecutive seeds in parallel.  bits (may be
+// null): the device's neighbour rows of these candidates (k_cluster_bits, n rows of
+// ceil(n/64) words), which replace the host radius search.
 void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cluster_num, const fccf_params& P,
-                       int64_t* nclusters, Pool* pool = nullptr);
+                       int64_t* nclusters, Pool* pool = nullptr, const uint64_t* bits = nullptr);
 
 // quick_verify (:680-783) with ceres_refine (:210-249): refines T in place, returns score.
 float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2, const fccf_params& P,

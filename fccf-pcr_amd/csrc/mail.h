@@ -22,11 +22,16 @@ struct CloudMail {                     // one per cloud set (double-buffered pai
 
 struct MatchMail {
   static constexpr uint32_t Q_CAP = 65536;     // candidate transforms per type
+  static constexpr uint32_t CB_CAP = 1u << 19; // neighbour bitmask words, all types
   MatchIn M;                           // host staging of the matching tables (H2D source)
   uint32_t tot[4];                     // candidates per type
   uint32_t kpass;                      // tests with >= 1 candidate
   uint32_t pad[3];
   QTd q[3][Q_CAP];
+  // transform_cluster neighbour rows (k_cluster_bits): type t's n_t x W_t words
+  // (W_t = ceil(n_t / 64)) at word offset sum_{t' < t} n_t' W_t'; written only when
+  // all types fit CB_CAP and cbits_on.
+  uint64_t cbits[CB_CAP];
 };
 
 struct FineMail {

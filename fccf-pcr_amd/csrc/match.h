@@ -52,6 +52,11 @@ struct FineBufs {
   XsBufs xs;           // similar_num sum scratch (E rows, cap n1 + n2)
 };
 // s1_state: octree bounds after inserting S1 alone (octree_replay, run ahead of time).
+// transform_cluster neighbour bitmasks of the three candidate lists into mail->cbits
+// (layout in mail.h); types with <= min_n candidates are skipped (not clustered).
+void cluster_bits(QTd* const q[3], const uint32_t* totals, float r2, AngleCut ccut, float min_n, MatchMail* mail,
+                  hipStream_t st);
+
 // mail (may be null): pinned mailbox receiving the E scores and the error word (mail.h)
 struct FineMail;
 void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,

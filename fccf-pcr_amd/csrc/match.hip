@@ -265,6 +265,56 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
   }
 }
 
+// transform_cluster's radius search (FCCF.cpp:1075-1103) as a bitmask: bit j of
+// row i is set when candidate j is a neighbour of seed i, i.e. d2 < r^2 (the
+// FLANN L2_Simple sum ((0 + ex^2) + ey^2) + ez^2) and the x axes of the two
+// rotations are within the cluster angle.  Which candidates a seed takes does not
+// depend on earlier seeds (every neighbour is pushed), so all rows are
+// independent; the host applies them in seed order (host_stages.cpp).  One wave
+// per (row, 64-column word): lane = column, the ballot is the word, written
+// straight into the pinned mailbox.  Rows of candidates with a non-finite tx come
+// out empty (d2 is NaN or inf), as in the host path.
+__global__ void __launch_bounds__(256) k_cluster_bits(const QTd* __restrict__ q0, const QTd* __restrict__ q1,
+                                                      const QTd* __restrict__ q2, const uint32_t* __restrict__ totals,
+                                                      float r2, AngleCut ccut, float min_n, uint64_t* __restrict__ out) {
+  KT();
+  const int t = blockIdx.y;
+  const QTd* __restrict__ q = t == 0 ? q0 : (t == 1 ? q1 : q2);
+  uint64_t words = 0, off = 0;
+  for (int u = 0; u < 3; ++u) {
+    const uint64_t n = totals[u], w = ((n + 63) / 64) * n;
+    if (u < t) off += w;
+    words += w;
+  }
+  if (words > MatchMail::CB_CAP) return;  // the host falls back to its own search
+  const uint32_t n = totals[t];
+  if ((float)n <= min_n) return;  // cluster_number_threshold: not clustered
+  const uint32_t W = (n + 63) / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t ntask = (uint64_t)n * W;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ntask; g += (uint64_t)gridDim.x * 4) {
+    const uint32_t i = (uint32_t)(g / W), w = (uint32_t)(g % W);
+    const uint32_t j = w * 64 + lane;
+    const QTd a = q[i];
+    bool nb = false;
+    if (j < n) {
+      const QTd b = q[j];
+      const float ex = a.tx - b.tx, ey = a.ty - b.ty, ez = a.tz - b.tz;
+      float d2 = 0.0f;
+      d2 += ex * ex;
+      d2 += ey * ey;
+      d2 += ez * ez;
+      if (d2 < r2) {
+        const f3 xa = quat_rotate(quatf{a.qw, a.qx, a.qy, a.qz}, f3{1.f, 0.f, 0.f});
+        const f3 xb = quat_rotate(quatf{b.qw, b.qx, b.qy, b.qz}, f3{1.f, 0.f, 0.f});
+        nb = angle_lt(normal_cos(xa.x, xa.y, xa.z, xb.x, xb.y, xb.z), ccut);
+      }
+    }
+    const uint64_t m = __ballot(nb);
+    if (lane == 0) out[off + g] = m;
+  }
+}
+
 }  // namespace
 
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
@@ -274,6 +324,11 @@ void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, 
   FCCF_LAUNCH("k_match_count", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_count, g, 256, 0, st, d_in, cnt, type);
   k_match_scan<<<1, 1024, 0, st>>>(d_in, cnt, type, off, totals, mail);
   FCCF_LAUNCH("k_match_emit", (nullptr, 0.0, nullptr, 0.0, (double)sizeof(MatchIn)), k_match_emit, g, 256, 0, st, d_in, cnt, type, off, c[0], c[1], c[2], q[0], q[1], q[2], mail);
+}
+
+void cluster_bits(QTd* const q[3], const uint32_t* totals, float r2, AngleCut ccut, float min_n, MatchMail* mail,
+                  hipStream_t st) {
+  k_cluster_bits<<<dim3(512, 3), 256, 0, st>>>(q[0], q[1], q[2], totals, r2, ccut, min_n, mail->cbits);
 }
 
 }  // namespace fccf

@@ -535,6 +535,12 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
   HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
   match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
+  // transform_cluster's radius search for all three lists on the device (k_cluster_bits)
+  const char* cbe = std::getenv("FCCF_CLUSTER_BITS");  // "0": host radius search (tests both paths)
+  const bool cbits_on = !(cbe && cbe[0] == '0');
+  const float cr2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
+  if (cbits_on && K > 0)
+    cluster_bits(dq, dtot, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(st0));  // totals, K_pass and candidate lists are in the mailbox
   std::vector<QTd> qraw[3];
@@ -581,10 +587,20 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
       qv[i] = {a.qw, a.qx, a.qy, a.qz, a.tx, a.ty, a.tz, 0u};
     }
     std::vector<QT> fine;
+    const uint64_t* bits = nullptr;  // the device's neighbour rows, when they fit the mailbox
+    if (cbits_on && K > 0) {
+      uint64_t words = 0, off = 0;
+      for (int u = 0; u < 3; ++u) {
+        const uint64_t w = (uint64_t)tot[u] * ((tot[u] + 63) / 64);
+        if (u < t) off += w;
+        words += w;
+      }
+      if (words <= MatchMail::CB_CAP) bits = mm.cbits + off;
+    }
     const int cluster_num =
         transformation_num ? (int)(P.seclct_cluster_number * (float)qv.size() / (float)transformation_num) : 0;
     int64_t ncl = 0;
-    transform_cluster(qv, fine, cluster_num, P, &ncl, &c->pool);
+    transform_cluster(qv, fine, cluster_num, P, &ncl, &c->pool, bits);
     counts.push_back(ncl);
     S.fine[t] = (int64_t)fine.size();
     S.ms[FCCF_T_CLUSTER] += ms_since(tc);

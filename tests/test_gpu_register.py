@@ -169,3 +169,18 @@ def test_deep_octree_tail_sort(ctx, oracle, fccf):
     T, _ = ctx.register(src2, tar2, 0.1)
     compare_all(ctx, run)
     np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
+
+
+def test_host_radius_search_path_matches(ctx, oracle, fccf, monkeypatch):
+    """transform_cluster's neighbour sets come from the device bitmask rows
+    (k_cluster_bits) by default; FCCF_CLUSTER_BITS=0 selects the host radius search.
+    Both must reproduce the oracle bit for bit."""
+    src, tar, _ = fccf.synth_pair(120_000)
+    run = oracle.Run(src, tar, 0.1, oracle.STABLE)
+    monkeypatch.setenv("FCCF_CLUSTER_BITS", "0")
+    T0, _ = ctx.register(src, tar, 0.1)
+    compare_all(ctx, run)
+    monkeypatch.delenv("FCCF_CLUSTER_BITS")
+    T1, _ = ctx.register(src, tar, 0.1)
+    compare_all(ctx, run)
+    np.testing.assert_array_equal(T0.view(np.uint32), T1.view(np.uint32))
