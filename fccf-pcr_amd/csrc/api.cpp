@@ -79,6 +79,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.reset();
     cs.g_cen.reset();
+    cs.g_rep.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
   }

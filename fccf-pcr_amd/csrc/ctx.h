@@ -148,9 +148,10 @@ struct fccf_ctx {
   // else (sa[1] is spare) -- within the four hardware queues a process gets.
   struct CloudSet {
     fccf::Arena arena;
-    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [4] clouds done
+    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [4] clouds done, [5] S1 replay done
     fccf::CachedGraph g_seg[2];      // both clouds batched: downsample, faces (pipeline.cpp)
     fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
+    fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];
   hipStream_t sa[3] = {};            // cloud stage streams (shared by both sets)

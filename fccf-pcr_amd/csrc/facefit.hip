@@ -29,8 +29,15 @@ namespace {
 // Batched over blockIdx.y = sequence e.
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n0,
                                                     float* __restrict__ aggr0, SeqStrides sd,
-                                                    uint32_t nbc) {
+                                                    uint32_t nbc, OctState* __restrict__ reset0) {
   KT();
+  if (reset0 && blockIdx.x == 0 && threadIdx.x == 0) {  // empty octree for k_oct_sim (sequence blockIdx.y)
+    OctState z;
+    for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
+    z.depth = 0;
+    z.defined = 0;
+    *sd.at(reset0, sd.state, blockIdx.y) = z;
+  }
   __shared__ float sh[4][6];
   const float* xyz = sd.at(xyz0, sd.xyz, blockIdx.y);
   float* aggr = sd.at(aggr0, sd.aggr, blockIdx.y);
@@ -398,14 +405,6 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
   }
 }
 
-__global__ void k_oct_reset(B2<OctState*> s) {
-  KT();
-  OctState z;
-  for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
-  z.depth = 0;
-  z.defined = 0;
-  *s[threadIdx.x] = z;
-}
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
   uint32_t g = (cap + per - 1) / per;
@@ -416,9 +415,9 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
-                SeqStrides sd) {
+                SeqStrides sd, OctState* reset_state) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap));
+  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap), reset_state);
 }
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
@@ -446,8 +445,7 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   sd.aggr = byte_stride(aggr, nbatch);
   sd.state = byte_stride(oct, nbatch);
   sd.n = byte_stride(d_n, nbatch);
-  k_oct_reset<<<1, nbatch, 0, st>>>(oct);
-  block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd);
+  block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd, oct[0]);  // also resets the octree states
   octree_sim(xyz[0], d_n[0], cap, res, aggr[0], oct[0], st, nbatch, sd);
   const B2<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
   const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
@@ -482,8 +480,7 @@ void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float vpt, float cth
 
 void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
                    hipStream_t st) {
-  k_oct_reset<<<1, 1, 0, st>>>(B2<OctState*>(state));
-  block_aggr(xyz, d_n, cap, aggr, st);
+  block_aggr(xyz, d_n, cap, aggr, st, 1, SeqStrides(), state);  // also resets the octree state
   octree_sim(xyz, d_n, cap, res, aggr, state, st);
 }
 

@@ -494,43 +494,55 @@ bool lm_eval(const float* pf, int P, const double x[7], double* cost, double* r,
 // DENSE_QR: min || [A; diag(D)] y - [b; 0] || by Householder QR (HouseholderQR form).
 constexpr int LM_MAXM = 2 * 17;  // <= one pair per source plane
 bool qr_solve(const double* A, int m, const double D[6], const double* b, double y[6]) {
-  const int n = 6, M = m + n;
-  double Q[(LM_MAXM + 6) * 6], rhs[LM_MAXM + 6];
-  for (int i = 0; i < M * n; ++i) Q[i] = 0.0;
-  for (int i = 0; i < M; ++i) rhs[i] = 0.0;
+  // Column-major [A; diag(D) | b]: column 6 is the right-hand side.  Every output
+  // element is computed with the same operations in the same order as the
+  // row-major HouseholderQR form (per column j, dot products run over ascending
+  // rows i); the seven column dot products of a step are interleaved for ILP.
+  constexpr int n = 6;
+  constexpr int LD = LM_MAXM + 6;
+  const int M = m + n;
+  double C[n + 1][LD];
+  for (int j = 0; j <= n; ++j)
+    for (int i = 0; i < M; ++i) C[j][i] = 0.0;
   for (int i = 0; i < m; ++i)
-    for (int j = 0; j < n; ++j) Q[(size_t)i * n + j] = A[(size_t)i * n + j];
-  for (int j = 0; j < n; ++j) Q[(size_t)(m + j) * n + j] = D[j];
-  for (int i = 0; i < m; ++i) rhs[i] = b[i];
+    for (int j = 0; j < n; ++j) C[j][i] = A[(size_t)i * n + j];
+  for (int j = 0; j < n; ++j) C[j][m + j] = D[j];
+  for (int i = 0; i < m; ++i) C[n][i] = b[i];
   for (int k = 0; k < n; ++k) {
-    const double c0 = Q[(size_t)k * n + k];
+    double* ck = C[k];
+    const double c0 = ck[k];
     double tail = 0.0;
-    for (int i = k + 1; i < M; ++i) tail += Q[(size_t)i * n + k] * Q[(size_t)i * n + k];
+    for (int i = k + 1; i < M; ++i) tail += ck[i] * ck[i];
     double tau, beta;
     if (tail <= DBL_MIN) {
       tau = 0.0;
       beta = c0;
-      for (int i = k + 1; i < M; ++i) Q[(size_t)i * n + k] = 0.0;
+      for (int i = k + 1; i < M; ++i) ck[i] = 0.0;
     } else {
       beta = std::sqrt(c0 * c0 + tail);
       if (c0 >= 0.0) beta = -beta;
-      for (int i = k + 1; i < M; ++i) Q[(size_t)i * n + k] = Q[(size_t)i * n + k] / (c0 - beta);
+      const double den = c0 - beta;
+      for (int i = k + 1; i < M; ++i) ck[i] = ck[i] / den;
       tau = (beta - c0) / beta;
     }
-    Q[(size_t)k * n + k] = beta;
-    for (int j = k + 1; j <= n; ++j) {  // j == n: the right-hand side
-      auto at = [&](int i) -> double& { return j < n ? Q[(size_t)i * n + j] : rhs[i]; };
-      double tmp = 0.0;
-      for (int i = k + 1; i < M; ++i) tmp += Q[(size_t)i * n + k] * at(i);
-      tmp += at(k);
-      at(k) = at(k) - tau * tmp;
-      for (int i = k + 1; i < M; ++i) at(i) = at(i) - tau * Q[(size_t)i * n + k] * tmp;
+    ck[k] = beta;
+    double tmp[n + 1];
+    for (int j = k + 1; j <= n; ++j) tmp[j] = 0.0;
+    for (int i = k + 1; i < M; ++i) {
+      const double v = ck[i];
+      for (int j = k + 1; j <= n; ++j) tmp[j] += v * C[j][i];
+    }
+    for (int j = k + 1; j <= n; ++j) {
+      double* cj = C[j];
+      const double t = tmp[j] + cj[k];
+      cj[k] = cj[k] - tau * t;
+      for (int i = k + 1; i < M; ++i) cj[i] = cj[i] - tau * ck[i] * t;
     }
   }
-  for (int i = 0; i < n; ++i) y[i] = rhs[i];
+  for (int i = 0; i < n; ++i) y[i] = C[n][i];
   for (int k = n - 1; k >= 0; --k) {
-    y[k] = y[k] / Q[(size_t)k * n + k];
-    for (int i = 0; i < k; ++i) y[i] = y[i] - y[k] * Q[(size_t)i * n + k];
+    y[k] = y[k] / C[k][k];
+    for (int i = 0; i < k; ++i) y[i] = y[i] - y[k] * C[k][i];
   }
   for (int i = 0; i < n; ++i)
     if (!std::isfinite(y[i])) return false;

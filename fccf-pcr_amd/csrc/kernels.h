@@ -105,8 +105,10 @@ void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res,
 // Fresh octree bounds replayed over xyz[0..*d_n) (aggr: aggr_floats(cap) floats).
 void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
                    hipStream_t st);
+// reset_state (optional): block 0 of each sequence also writes an empty OctState
+// there (sequence e at reset_state + e * sd.state bytes) for the octree_sim that follows.
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
-                SeqStrides sd = SeqStrides());
+                SeqStrides sd = SeqStrides(), OctState* reset_state = nullptr);
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
 constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
 // aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per

@@ -228,10 +228,12 @@ void seg_faces(CloudWS* w, const fccf_params& P, hipStream_t st) {
                       (double)P.face_voxel_size, fb, st, 2);
   face_voxels_fit(m2, cap, P.voxel_point_threshold, P.curvature_threshold,
                   both<float*>(w, [](const CloudWS& c) { return c.resid; }), fb, st, 2);
-  // the residual cloud of the driver source is fine_verify's S1 (:788-805): its
-  // octree bounds do not depend on any candidate, so they are replayed here,
-  // overlapping the host stages that produce the candidates
-  octree_replay(w[0].resid, w[0].fb.nresid, cap, (double)P.fine_verify_voxel_size, w[0].faggr, w[0].fstate, st);
+}
+// The residual cloud of the driver source is fine_verify's S1 (:788-805): its
+// octree bounds do not depend on any candidate, so they are replayed after the
+// clouds-done event, overlapping the host stages that produce the candidates.
+void seg_s1_replay(CloudWS* w, const fccf_params& P, hipStream_t st) {
+  octree_replay(w[0].resid, w[0].fb.nresid, w[0].cap, (double)P.fine_verify_voxel_size, w[0].faggr, w[0].fstate, st);
 }
 
 // The ctx's pinned mailboxes (mail.h): allocated once, so graph-captured kernels may hold the pointer.
@@ -375,6 +377,8 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   mark(4, st0);
   tm.armed = seg_timing;
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
+  cs.g_rep.run(&key, sizeof key, st0, [&] { seg_s1_replay(w, P, st0); });
+  HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
   HIP_CHECK(hipGetLastError());
 }
 
@@ -397,6 +401,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   // counts and planar records of both clouds: written by k_compact_planar into
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
+  c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
   HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
   HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[4], 0));
   uint32_t sc[2][4], fsc[2][4];
@@ -691,6 +696,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
               P.fine_verify_voxel_size};
     // in a batch, fine verification waits for the next pair's cloud stage: chains of
     // small kernels from the two stages interleave badly, run back to back they don't
+    HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[5], 0));  // S1 octree bounds replayed
     if (fine_after) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
     c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0,
@@ -753,6 +759,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   }
   S.graph_captures = c->g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
+  S.graph_captures += c->cs[s].g_rep.captures;
   S.graph_captures += c->cs[s].g_cen.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
@@ -773,6 +780,7 @@ void reset_capture_counts(fccf_ctx* c) {
   c->g_fine.captures = 0;
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.captures = 0;
+    cs.g_rep.captures = 0;
     cs.g_cen.captures = 0;
   }
 }

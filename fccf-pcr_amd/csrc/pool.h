@@ -45,6 +45,18 @@ class Pool {
     for (auto& t : workers_) t.join();
   }
   int size() const { return (int)workers_.size() + 1; }
+  // Wakes sleeping workers and keeps every worker spinning for `us` microseconds,
+  // so a parallel_for issued within that window starts on all threads at once
+  // (call it before a wait whose end is followed by parallel work).
+  void warm(int us) {
+    if (workers_.empty()) return;
+    warm_until_.store(now_us() + us, std::memory_order_relaxed);
+    warm_gen_.fetch_add(1, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(m_);
+    }
+    cv_.notify_all();
+  }
   // Runs f(i) for i in [0, n); the caller participates.  Not reentrant.
   void parallel_for(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
@@ -67,6 +79,10 @@ class Pool {
   }
 
  private:
+  static int64_t now_us() {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
   static void relax() {
 #if defined(__x86_64__)
     __builtin_ia32_pause();
@@ -87,15 +103,16 @@ class Pool {
   void loop() {
     uint64_t seen = 0;
     while (true) {
-      const auto t0 = std::chrono::steady_clock::now();
+      int64_t until = now_us() + spin_us_;
       uint64_t w;
       int k = 0;
       while (((w = word_.load(std::memory_order_acquire)) >> 32) == seen && !quit_.load()) {
         relax();
-        if ((++k & 255) == 0 &&
-            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us_) {
+        if ((++k & 255) == 0 && now_us() > std::max(until, warm_until_.load(std::memory_order_relaxed))) {
           std::unique_lock<std::mutex> g(m_);
-          cv_.wait(g, [&] { return quit_.load() || (word_.load() >> 32) != seen; });
+          const uint64_t wg = warm_gen_.load();
+          cv_.wait(g, [&] { return quit_.load() || (word_.load() >> 32) != seen || warm_gen_.load() != wg; });
+          until = now_us() + spin_us_;
         }
       }
       if (quit_.load()) return;
@@ -109,6 +126,8 @@ class Pool {
   std::atomic<uint64_t> word_{0};  // (job id << 32) | next item
   std::atomic<int> done_{0};
   std::atomic<bool> quit_{false};
+  std::atomic<int64_t> warm_until_{0};
+  std::atomic<uint64_t> warm_gen_{0};
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<int> n_{0};
   uint64_t job_ = 0;

@@ -157,6 +157,11 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
 }
 
 // One thread per leaf: Vector3f accumulation in ascending input index, then / n.
+// The first CL members' indices and points are loaded before any is summed (a
+// leaf holds ~3 points: the loads of a thread overlap instead of forming a
+// dependent chain); each block's 256 centroids are staged in LDS and written as
+// coalesced 16-byte words.  The pass-through cases are flat 16-byte copies.
+constexpr int CL = 4;
 __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
                                                      B2<const VGParams*> P2, B2<const uint32_t*> vals2,
                                                      B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
@@ -175,23 +180,52 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<c
   // "Integer indices would overflow": output = *input_; presorted with every leaf
   // holding one finite point: the centroid of one point is the point (p / 1.f == p)
   if (q.overflow || (presorted && q.unsorted == 0u && n && q.nfinite == n)) {
-    for (uint32_t i = gid; i < n; i += gsz) {
-      out[3 * i] = xyz[3 * i]; out[3 * i + 1] = xyz[3 * i + 1]; out[3 * i + 2] = xyz[3 * i + 2];
-    }
+    const uint32_t nf = 3 * n;
+    const bool al = ((((uintptr_t)xyz) | ((uintptr_t)out)) & 15u) == 0;
+    const uint32_t n4 = al ? nf / 4 : 0;
+    for (uint32_t i = gid; i < n4; i += gsz) reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(xyz)[i];
+    for (uint32_t i = 4 * n4 + gid; i < nf; i += gsz) out[i] = xyz[i];
     if (gid == 0) *d_m = n;
     return;
   }
   const uint32_t ns = q.nfinite ? *d_nseg : 0u;
   if (gid == 0) *d_m = ns;
-  for (uint32_t s = gid; s < ns; s += gsz) {
-    const uint32_t b = starts[s], e = starts[s + 1];
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (uint32_t k = b; k < e; ++k) {
-      const uint32_t j = vals[k];
-      sx += xyz[3 * j]; sy += xyz[3 * j + 1]; sz += xyz[3 * j + 2];
+  __shared__ __attribute__((aligned(16))) float so[3 * 256];
+  const bool al = (((uintptr_t)out) & 15u) == 0;
+  for (uint32_t s0 = blockIdx.x * 256; s0 < ns; s0 += gsz) {
+    const uint32_t s = s0 + threadIdx.x;
+    if (s < ns) {
+      const uint32_t b = starts[s], e1 = starts[s + 1];
+      float sx = 0.f, sy = 0.f, sz = 0.f;
+      for (uint32_t k0 = b; k0 < e1; k0 += CL) {
+        uint32_t j[CL];
+        float px[CL], py[CL], pz[CL];
+#pragma unroll
+        for (int c = 0; c < CL; ++c) j[c] = vals[min(k0 + c, e1 - 1u)];
+#pragma unroll
+        for (int c = 0; c < CL; ++c) {
+          px[c] = xyz[3 * (size_t)j[c]];
+          py[c] = xyz[3 * (size_t)j[c] + 1];
+          pz[c] = xyz[3 * (size_t)j[c] + 2];
+        }
+#pragma unroll
+        for (int c = 0; c < CL; ++c)
+          if (k0 + c < e1) { sx += px[c]; sy += py[c]; sz += pz[c]; }
+      }
+      const float cnt = (float)(e1 - b);
+      so[3 * threadIdx.x] = sx / cnt;
+      so[3 * threadIdx.x + 1] = sy / cnt;
+      so[3 * threadIdx.x + 2] = sz / cnt;
     }
-    const float c = (float)(e - b);
-    out[3 * s] = sx / c; out[3 * s + 1] = sy / c; out[3 * s + 2] = sz / c;
+    __syncthreads();
+    const uint32_t m = min(256u, ns - s0);  // centroids of this block step
+    float* dst = out + 3 * (size_t)s0;
+    if (al && m == 256u) {
+      if (threadIdx.x < 192) reinterpret_cast<float4*>(dst)[threadIdx.x] = reinterpret_cast<const float4*>(so)[threadIdx.x];
+    } else {
+      for (uint32_t i = threadIdx.x; i < 3 * m; i += 256) dst[i] = so[i];
+    }
+    __syncthreads();
   }
 }
 

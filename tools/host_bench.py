@@ -20,7 +20,7 @@ os.makedirs(out, exist_ok=True)
 c = F.CONFIGS[cfg]
 src, tar, _ = F.synth_pair(c["n"], c["room"])
 r = O.Run(src, tar, c["leaf"], O.STABLE)
-for k in ("planes1", "planes2", "cand0", "cand1", "cand2"):
+for k in ("planes1", "planes2", "cand0", "cand1", "cand2", "vox1", "vox2"):
     r.get(k, np.float32).astype(np.float32).tofile(os.path.join(out, k + ".bin"))
 exe = os.path.join(ROOT, "scratch", "host_bench")
 lib = os.path.join(ROOT, "fccf-pcr_amd", "lib")
