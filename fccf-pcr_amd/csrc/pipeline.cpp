@@ -584,14 +584,17 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   struct TS { m44 T; float score, score2; };
   std::vector<TS> ctv[3];
   std::vector<int64_t> counts = {(int64_t)K, kpass, (int64_t)tot[0], (int64_t)tot[1], (int64_t)tot[2]};
+  // clustering of the three types (cheap: the neighbour sets come from the device),
+  // then every type's quick_verify + LM in ONE parallel_for (the three lists are
+  // independent), then score_range per type
+  std::vector<QT> fine[3];
+  auto tc = clk::now();
   for (int t = 0; t < 3; ++t) {
-    auto tc = clk::now();
     std::vector<QT> qv(qraw[t].size());
     for (size_t i = 0; i < qv.size(); ++i) {
       const QTd& a = qraw[t][i];
       qv[i] = {a.qw, a.qx, a.qy, a.qz, a.tx, a.ty, a.tz, 0u};
     }
-    std::vector<QT> fine;
     const uint64_t* bits = nullptr;  // the device's neighbour rows, when they fit the mailbox
     if (cbits_on && K > 0) {
       uint64_t words = 0, off = 0;
@@ -605,40 +608,50 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     const int cluster_num =
         transformation_num ? (int)(P.seclct_cluster_number * (float)qv.size() / (float)transformation_num) : 0;
     int64_t ncl = 0;
-    transform_cluster(qv, fine, cluster_num, P, &ncl, &c->pool, bits);
+    transform_cluster(qv, fine[t], cluster_num, P, &ncl, &c->pool, bits);
     counts.push_back(ncl);
-    S.fine[t] = (int64_t)fine.size();
-    S.ms[FCCF_T_CLUSTER] += ms_since(tc);
-    tc = clk::now();
+    S.fine[t] = (int64_t)fine[t].size();
+  }
+  S.ms[FCCF_T_CLUSTER] = ms_since(tc);
+  tc = clk::now();
+  std::vector<std::pair<int, int>> items;  // (type, index) of every fine candidate
+  std::vector<TS> res[3];
+  std::vector<int> npairs[3];
+  for (int t = 0; t < 3; ++t) {
+    res[t].resize(fine[t].size());
+    npairs[t].resize(fine[t].size());
+    for (size_t i = 0; i < fine[t].size(); ++i) items.push_back({t, (int)i});
+  }
+  c->pool.parallel_for((int)items.size(), [&](int k) {  // independent per candidate
+    const int t = items[k].first, i = items[k].second;
+    TS& r = res[t][i];
+    r.T = T_from_qt(fine[t][i]);
+    r.score = quick_verify(r.T, g[0].planes, g[1].planes, P, &npairs[t][i]);
+    r.score2 = 0.f;
+  });
+  for (int t = 0; t < 3; ++t) {
     std::vector<float> fdump, qdump;
-    std::vector<TS> res(fine.size());
-    std::vector<int> npairs(fine.size());
-    c->pool.parallel_for((int)fine.size(), [&](int i) {  // independent per candidate
-      res[i].T = T_from_qt(fine[i]);
-      res[i].score = quick_verify(res[i].T, g[0].planes, g[1].planes, P, &npairs[i]);
-      res[i].score2 = 0.f;
-    });
-    for (size_t i = 0; i < fine.size(); ++i) {
-      const QT& q = fine[i];
+    for (size_t i = 0; i < fine[t].size(); ++i) {
+      const QT& q = fine[t][i];
       const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
       fdump.insert(fdump.end(), a, a + 8);
-      const TS& ts = res[i];
-      if ((float)npairs[i] >= P.required_optimize_plane) ++S.lm_solves;
+      const TS& ts = res[t][i];
+      if ((float)npairs[t][i] >= P.required_optimize_plane) ++S.lm_solves;
       ctv[t].push_back(ts);
       for (int a2 = 0; a2 < 4; ++a2)
         for (int b2 = 0; b2 < 4; ++b2) qdump.push_back(ts.T.m[a2][b2]);
       qdump.push_back(ts.score);
-      qdump.push_back((float)npairs[i]);
+      qdump.push_back((float)npairs[t][i]);
     }
     // score_range (:1233-1251): exchange sort; only the first analyse_max positions matter
     auto& cv = ctv[t];
     for (size_t i = 0; i + 1 < cv.size() && (int)i < analyse_max; ++i)
       for (size_t j = i + 1; j < cv.size(); ++j)
         if (cv[i].score < cv[j].score) std::swap(cv[i], cv[j]);
-    S.ms[FCCF_T_VERIFY] += ms_since(tc);
     c->dbg_put("fine" + std::to_string(t), fdump);
     c->dbg_put("qv" + std::to_string(t), qdump);
   }
+  S.ms[FCCF_T_VERIFY] = ms_since(tc);
 
   // ---------------- device: K7 fine verify of the top analyse_max per type
   t0 = clk::now();

@@ -1,6 +1,7 @@
 // host_bench.cpp — CPU timing of libfccf's host stages (transform_cluster,
 // quick_verify + LM) on inputs dumped from the oracle (development tool; see
 // tools/host_bench.py, which writes the inputs and builds/runs this).
+#include <algorithm>
 #include <chrono>
 #include <atomic>
 #include <cstdio>
@@ -113,8 +114,11 @@ int main(int argc, char** argv) {
       if (std::getenv("HB_ITEMS") && r == reps - 1 && t == 0) {
         double sum = 0;
         for (double x : dt) sum += x;
-        std::printf("  type0 items %zu: sum of item times %.1f us, wall %.1f us\n", dt.size(), sum,
-                    std::chrono::duration<double, std::micro>(c - b).count());
+        std::vector<double> sd = dt;
+        std::sort(sd.begin(), sd.end(), std::greater<double>());
+        std::printf("  type0 items %zu: sum of item times %.1f us, wall %.1f us, slowest %.1f %.1f %.1f %.1f us\n",
+                    dt.size(), sum, std::chrono::duration<double, std::micro>(c - b).count(), sd[0], sd[1], sd[2],
+                    sd[3]);
       }
       tc += std::chrono::duration<double, std::micro>(b - a).count();
       tv += std::chrono::duration<double, std::micro>(c - b).count();

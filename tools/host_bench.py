@@ -23,7 +23,7 @@ r = O.Run(src, tar, c["leaf"], O.STABLE)
 for k in ("planes1", "planes2", "cand0", "cand1", "cand2", "vox1", "vox2"):
     r.get(k, np.float32).astype(np.float32).tofile(os.path.join(out, k + ".bin"))
 exe = os.path.join(ROOT, "scratch", "host_bench")
-lib = os.path.join(ROOT, "fccf-pcr_amd", "lib")
+lib = os.environ.get("HB_LIB", os.path.join(ROOT, "fccf-pcr_amd", "lib"))
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-o", exe,
                 os.path.join(ROOT, "tools", "host_bench.cpp"), "-L" + lib, "-lfccf", "-Wl,-rpath," + lib], check=True)
 for th in (sys.argv[3:] or ["1", "8"]):
