@@ -43,6 +43,20 @@ inline void set_avg(Group& g) {  // the recompute's averages (:580-586)
 }
 }  // namespace
 
+// compare_normal's rejection (angle_gt) for voxels j0 .. j0+7 against the group
+// normal (ax, ay, az) with double norm na: written branch-free over SoA arrays so
+// the compiler vectorises it; every lane does exactly normal_cos_pre's operations.
+static inline void angle_skip8(const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
+                               const double* __restrict__ vn, int j0, float ax,
+                               float ay, float az, double na, AngleCut cut, bool skip[8]) {
+  for (int k = 0; k < 8; ++k) {
+    const float dp = (float)dot3d((double)ax, (double)ay, (double)az, (double)nx[j0 + k], (double)ny[j0 + k],
+                                  (double)nz[j0 + k]);
+    const float c = (float)((double)dp / (na * vn[j0 + k]));
+    skip[k] = angle_gt(c, cut);
+  }
+}
+
 GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
   // compare_normal(...) == !(theta > thr) == !angle_gt(cos, cut): no acos in the O(V^2) loops
   const AngleCut cut1 = make_cut(P.normal_vector_threshold1), cut2 = make_cut(P.normal_vector_threshold2);
@@ -50,9 +64,20 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
   std::vector<Group> G;
   // stage 1 (:536-593): recompute-from-scratch == running sums in member order (App. B Q7)
   // The predicate is `same && cop` with no side effects, so `cop` is evaluated only
-  // when `same` holds; voxel normal norms are computed once.
-  std::vector<double> vn(nv);
-  for (int j = 0; j < nv; ++j) vn[j] = norm3d(vox[j].n[0], vox[j].n[1], vox[j].n[2]);
+  // when `same` holds; voxel normal norms are computed once.  The scan for a seed
+  // visits the still-unallocated voxels in index order: they are kept as a compact
+  // SoA list (padded by 8), compacted after each seed, and the angle test runs
+  // eight of them at a time; after an accept the group's averages change, so the
+  // next block starts right after it.
+  std::vector<int> ui(nv + 8, 0);
+  std::vector<float> nx(nv + 8, 0.f), ny(nv + 8, 0.f), nz(nv + 8, 0.f);
+  std::vector<double> vn(nv + 8, 1.0), vnv(nv);
+  for (int j = 0; j < nv; ++j) {
+    ui[j] = j;
+    nx[j] = vox[j].n[0]; ny[j] = vox[j].n[1]; nz[j] = vox[j].n[2];
+    vn[j] = vnv[j] = norm3d(vox[j].n[0], vox[j].n[1], vox[j].n[2]);
+  }
+  int nu = nv;  // unallocated voxels, ui[0..nu) ascending
   for (int i = 0; i < nv; ++i) {
     if (va[i]) continue;
     Group g;
@@ -61,19 +86,37 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
     add_member(g, vox[i]);
     g.fps = (float)vox[i].count;
     for (int a = 0; a < 3; ++a) { g.an[a] = vox[i].n[a]; g.ac[a] = vox[i].c[a]; }
-    g.nan_ = vn[i];
-    for (int j = 0; j < nv; ++j) {
-      if (va[j]) continue;
-      const VoxRec& v = vox[j];
-      if (angle_gt(normal_cos_pre(g.an[0], g.an[1], g.an[2], g.nan_, v.n[0], v.n[1], v.n[2], vn[j]), cut1)) continue;
-      if (compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]}, f3{v.n[0], v.n[1], v.n[2]},
-                        f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1, P.parameter_k1)) {
-        g.mem.push_back(j);
-        va[j] = 1;
-        add_member(g, v);
-        set_avg(g);
+    g.nan_ = vnv[i];
+    int p = 0;
+    while (p < nu) {
+      bool skip[8];
+      angle_skip8(nx.data(), ny.data(), nz.data(), vn.data(), p, g.an[0], g.an[1], g.an[2], g.nan_, cut1, skip);
+      const int pe = std::min(nu, p + 8);
+      int next = pe;
+      for (int q = p; q < pe; ++q) {
+        const int jj = ui[q];
+        if (va[jj] || skip[q - p]) continue;
+        const VoxRec& v = vox[jj];
+        if (compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]}, f3{v.n[0], v.n[1], v.n[2]},
+                          f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1, P.parameter_k1)) {
+          g.mem.push_back(jj);
+          va[jj] = 1;
+          add_member(g, v);
+          set_avg(g);
+          next = q + 1;
+          break;
+        }
       }
+      p = next;
     }
+    int w = 0;  // drop this seed's members from the list
+    for (int q = 0; q < nu; ++q) {
+      const int jj = ui[q];
+      if (va[jj]) continue;
+      ui[w] = jj; nx[w] = nx[q]; ny[w] = ny[q]; nz[w] = nz[q]; vn[w] = vn[q];
+      ++w;
+    }
+    nu = w;
     G.push_back(std::move(g));
   }
   // stage 2 (:595-648): seeds never mark themselves allocated (Q6)

@@ -76,6 +76,31 @@ int main(int argc, char** argv) {
     }
     std::printf("grow cloud %d: %zu voxels -> %zu groups: %.1f us\n", k, vox.size(), ng, tg / reps);
   }
+  for (int k = 1; k <= 2; ++k) {  // region growing + selection per cloud
+    auto v = rd((D + "/vox" + std::to_string(k) + ".bin").c_str());
+    std::vector<VoxRec> vox(v.size() / 8);
+    for (size_t i = 0; i < vox.size(); ++i) {
+      std::memcpy(vox[i].c, &v[8 * i], 12);
+      std::memcpy(vox[i].n, &v[8 * i + 3], 12);
+      vox[i].count = (int32_t)v[8 * i + 6];
+      vox[i].curvature = 0.f;
+    }
+    double tg = 0;
+    size_t ng = 0;
+    for (int r = 0; r < reps; ++r) {
+      auto a = clk::now();
+      GrowOut g = grow_and_select(vox.data(), (int)vox.size(), P);
+      tg += std::chrono::duration<double, std::micro>(clk::now() - a).count();
+      ng = g.groups.size();
+      if (r == 0)
+        for (const Plane& p : g.groups) {
+          uint32_t b[8];
+          std::memcpy(b, &p, 32);
+          for (uint32_t x : b) chk = chk * 1000003u + x;
+        }
+    }
+    std::printf("grow cloud %d: %zu voxels -> %zu groups: %.1f us\n", k, vox.size(), ng, tg / reps);
+  }
   double tc = 0, tv = 0;
   size_t nfine = 0, nlm = 0;
   for (int r = 0; r < reps; ++r) {
