@@ -75,11 +75,11 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   pipeline_release(c);
-  c->g_fine.reset();
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.reset();
     cs.g_cen.reset();
     cs.g_rep.reset();
+    cs.g_fine.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
   }

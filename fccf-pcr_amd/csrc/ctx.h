@@ -152,11 +152,12 @@ struct fccf_ctx {
     fccf::CachedGraph g_seg[2];      // both clouds batched: downsample, faces (pipeline.cpp)
     fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
+    fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
+                                     // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];
   hipStream_t sa[3] = {};            // cloud stage streams (shared by both sets)
   hipStream_t sb = nullptr;          // matching, fine verification, copies, stage exports
-  fccf::CachedGraph g_fine;          // fine-verify batch (K7)
   fccf::Arena arena2;  // matching (and the stage exports)
   fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;

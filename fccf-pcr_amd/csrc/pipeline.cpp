@@ -382,6 +382,23 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   HIP_CHECK(hipGetLastError());
 }
 
+// FCCF_HOST_TRACE=1 (development): host timestamps of phase B, microseconds since
+// the pair's cloud stage was enqueued, printed to stderr when the pair finishes.
+struct HostTrace {
+  bool on = std::getenv("FCCF_HOST_TRACE") != nullptr;
+  clk::time_point t0;
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    char b[64];
+    std::snprintf(b, sizeof b, " %s=%.0f", what, std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+    line += b;
+  }
+  void flush() {
+    if (on) std::fprintf(stderr, "host trace:%s\n", line.c_str());
+  }
+};
+
 // Phase B: everything after the cloud stage of the pair on CloudSet s, on c->sb.
 // after_clouds() runs as soon as the cloud stage has completed (the batch driver
 // enqueues the next pair's clouds there).
@@ -414,8 +431,12 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   }
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
   S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
+  HostTrace ht;
+  ht.t0 = ps.t_enq;
+  ht.mark("clouds");
   seg_timer_print(s);
   after_clouds();
+  ht.mark("next_enq");
   t0 = clk::now();
   S.m_tar = sc[0][3];
   S.m_src = sc[1][3];
@@ -475,6 +496,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   S.bases1 = (int64_t)base[0].size();
   S.bases2 = (int64_t)base[1].size();
   S.ms[FCCF_T_GROW] = ms_since(t0);
+  ht.mark("grow");
   if (c->debug)
     for (int k = 0; k < 2; ++k) {
       const std::string s = std::to_string(k + 1);
@@ -563,6 +585,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   S.K_pass = kpass;
   for (int t = 0; t < 3; ++t) S.cand[t] = tot[t];
   S.ms[FCCF_T_MATCH] = ms_since(t0);
+  ht.mark("match");
   if (c->debug)
     for (int t = 0; t < 3; ++t) {
       auto cv = d2h(dc[t], tot[t], st0);
@@ -613,6 +636,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     S.fine[t] = (int64_t)fine[t].size();
   }
   S.ms[FCCF_T_CLUSTER] = ms_since(tc);
+  ht.mark("cluster");
   tc = clk::now();
   std::vector<std::pair<int, int>> items;  // (type, index) of every fine candidate
   std::vector<TS> res[3];
@@ -652,6 +676,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     c->dbg_put("qv" + std::to_string(t), qdump);
   }
   S.ms[FCCF_T_VERIFY] = ms_since(tc);
+  ht.mark("verify");
 
   // ---------------- device: K7 fine verify of the top analyse_max per type
   t0 = clk::now();
@@ -709,19 +734,24 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
               P.fine_verify_voxel_size};
     // in a batch, fine verification waits for the next pair's cloud stage: chains of
     // small kernels from the two stages interleave badly, run back to back they don't
+    ht.mark("fine_setup");
     HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[5], 0));  // S1 octree bounds replayed
-    if (fine_after) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
-    c->g_fine.run(&fkey, sizeof fkey, st0, [&] {
+    if (fine_after && !std::getenv("FCCF_NO_FINE_AFTER")) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
+    ht.mark("fine_waits");
+    c->cs[s].g_fine.run(&fkey, sizeof fkey, st0, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0,
                         &fm);
     });
     HIP_CHECK(hipGetLastError());
+    ht.mark("fine_launched");
     HIP_CHECK(hipStreamSynchronize(st0));  // scores and the error word are in the mailbox
     std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
     const uint32_t ferr = fm.err;
     if (ferr) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
   }
   S.ms[FCCF_T_FINE] = ms_since(t0);
+  ht.mark("fine");
+  ht.flush();
 
   // ---------------- host: score sums (over all types) and fusion (:1539-1606)
   t0 = clk::now();
@@ -770,7 +800,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     HIP_CHECK(hipDeviceSynchronize());
     probe_collect(c->probe);
   }
-  S.graph_captures = c->g_fine.captures;
+  S.graph_captures = c->cs[s].g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
   S.graph_captures += c->cs[s].g_rep.captures;
   S.graph_captures += c->cs[s].g_cen.captures;
@@ -790,10 +820,10 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
 }
 
 void reset_capture_counts(fccf_ctx* c) {
-  c->g_fine.captures = 0;
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.captures = 0;
     cs.g_rep.captures = 0;
+    cs.g_fine.captures = 0;
     cs.g_cen.captures = 0;
   }
 }

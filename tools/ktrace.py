@@ -1,7 +1,7 @@
 """Device-side kernel timeline of registrations (development; csrc/ktrace.h).
 
 Usage (GPU box): make -C fccf-pcr_amd KTRACE=1 lib_kt/libfccf.so, then
-  FCCF_LIB=fccf-pcr_amd/lib_kt/libfccf.so python tools/ktrace.py [config] [reps]
+  FCCF_LIB=fccf-pcr_amd/lib_kt/libfccf.so python tools/ktrace.py [config] [reps] [batch]
 Prints, for the last registration, every instrumented kernel's block-(0,0) start
 time (s_memrealtime, 100 MHz) relative to the first one, the gap to the next kernel,
 and per-kernel totals of those gaps (the start-to-start cost of each kernel).
@@ -49,9 +49,13 @@ def main():
     ds, dt = ctx.upload(src), ctx.upload(tar)
     buf = ctx.upload(np.zeros((16384 * 8 // 12 + 1, 3), np.float32))
     F._lib.fccf_ktrace_arm.argtypes = [ctypes.c_void_p]
+    batch = len(sys.argv) > 3 and sys.argv[3] == "batch"
     for _ in range(reps):
         F._lib.fccf_ktrace_arm(ctypes.c_void_p(buf))
-        ctx.register_device(ds, src.shape[0], dt, tar.shape[0], cfg["leaf"])
+        if batch:  # pipelined: pair i+1's cloud stage overlaps pair i's phase B
+            ctx.register_batch([((ds, src.shape[0]), (dt, tar.shape[0]))] * 4, cfg["leaf"], on_device=True)
+        else:
+            ctx.register_device(ds, src.shape[0], dt, tar.shape[0], cfg["leaf"])
     F._lib.fccf_ktrace_arm(None)
     out = np.zeros(16384, np.uint64)
     hip.hipDeviceSynchronize()
