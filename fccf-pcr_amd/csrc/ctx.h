@@ -144,11 +144,14 @@ struct fccf_ctx {
   // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
   // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
   // Two sets never run their cloud stages at the same time, so they share streams:
-  // sa[0] the batched cloud stage, sa[2] the centroid sums, and sb for everything
-  // else (sa[1] is spare) -- within the four hardware queues a process gets.
+  // sa[0] the batched cloud stage, sa[2] the centroid sums, sa[1] fine
+  // verification, and sb for matching and everything else -- within the four
+  // hardware queues a process gets.
   struct CloudSet {
     fccf::Arena arena;
-    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [4] clouds done, [5] S1 replay done
+    fccf::Arena arena3;              // fine verification scratch of the pair on this set
+    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
+                                     // [4] clouds done, [5] S1 replay done
     fccf::CachedGraph g_seg[2];      // both clouds batched: downsample, faces (pipeline.cpp)
     fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
@@ -156,10 +159,9 @@ struct fccf_ctx {
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[2];
-  hipStream_t sa[3] = {};            // cloud stage streams (shared by both sets)
-  hipStream_t sb = nullptr;          // matching, fine verification, copies, stage exports
+  hipStream_t sa[3] = {};            // cloud stage streams (sa[1]: fine verification)
+  hipStream_t sb = nullptr;          // matching, copies, stage exports
   fccf::Arena arena2;  // matching (and the stage exports)
-  fccf::Arena arena3;  // fine verify
   fccf::PinnedBuf pinned;
   fccf::MailBuf mail;  // pipeline.cpp host_mail()
   fccf::Pool pool;

@@ -43,7 +43,7 @@ struct FineMail {
 struct HostMail {
   CloudMail clouds[2];
   MatchMail match;
-  FineMail fine;
+  FineMail fine[2];  // per cloud set: a pair's fine verification overlaps the next pair's phase B
 };
 
 }  // namespace fccf

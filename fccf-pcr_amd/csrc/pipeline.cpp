@@ -294,8 +294,42 @@ void seg_timer_print(int s) {
                v[1] * 1e3, v[2] * 1e3, v[3] * 1e3, v[4] * 1e3);
 }
 
+struct TS { m44 T; float score, score2; };  // a verified candidate: T, quick score, fine score
+
+// FCCF_HOST_TRACE=1 (development): host timestamps of phase B, microseconds since
+// the pair's cloud stage was enqueued, printed to stderr when the pair finishes.
+struct HostTrace {
+  bool on = std::getenv("FCCF_HOST_TRACE") != nullptr;
+  clk::time_point t0;
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    char b[64];
+    std::snprintf(b, sizeof b, " %s=%.0f", what, std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+    line += b;
+  }
+  void flush() {
+    if (on) std::fprintf(stderr, "host trace:%s\n", line.c_str());
+    line.clear();
+  }
+};
+
+// What the second half of phase B (fine scores -> fusion) takes over from the
+// first half (growing ... fine-verify launch) of the same pair.
+struct PhaseB {
+  fccf_stats S;
+  std::vector<TS> ctv[3];
+  std::vector<int64_t> counts;
+  int E = 0, analyse_max = 0;
+  float* T_out = nullptr;
+  fccf_stats* stats = nullptr;
+  clk::time_point t_all, t_fine;
+  HostTrace ht;
+};
+
 // State of the registration whose clouds occupy CloudSet s.
 struct PipeSet {
+  PhaseB pb;
   CloudWS w[2];
   int64_t nin[2] = {0, 0};
   uint32_t cap[2] = {1, 1};
@@ -326,6 +360,9 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   const uint32_t capmax = (uint32_t)std::max<int64_t>(std::max(ps.nin[0], ps.nin[1]), 1);
   ps.cap[0] = ps.cap[1] = capmax;
   hipStream_t st0 = c->sa[0], ss = c->sa[2];
+  // the previous pair on this set may still be in fine verification, which reads
+  // this workspace (residual clouds, S1 octree state): the stage waits for it
+  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[3], 0));
   cs.arena.ensure(2 * cloud_bytes(capmax, true) + exact_sum_bytes(6, capmax) + (1 << 20));
   cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
@@ -382,29 +419,15 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   HIP_CHECK(hipGetLastError());
 }
 
-// FCCF_HOST_TRACE=1 (development): host timestamps of phase B, microseconds since
-// the pair's cloud stage was enqueued, printed to stderr when the pair finishes.
-struct HostTrace {
-  bool on = std::getenv("FCCF_HOST_TRACE") != nullptr;
-  clk::time_point t0;
-  std::string line;
-  void mark(const char* what) {
-    if (!on) return;
-    char b[64];
-    std::snprintf(b, sizeof b, " %s=%.0f", what, std::chrono::duration<double, std::micro>(clk::now() - t0).count());
-    line += b;
-  }
-  void flush() {
-    if (on) std::fprintf(stderr, "host trace:%s\n", line.c_str());
-  }
-};
-
-// Phase B: everything after the cloud stage of the pair on CloudSet s, on c->sb.
-// after_clouds() runs as soon as the cloud stage has completed (the batch driver
-// enqueues the next pair's clouds there).
+// Phase B1: everything after the cloud stage of the pair on CloudSet s up to the
+// launch of its fine verification (matching on c->sb, fine verification on
+// c->sa[1]); phase_b2 collects the fine scores and fuses.  after_clouds() runs as
+// soon as the cloud stage has completed (the batch driver enqueues the next pair's
+// clouds there).  Between b1 and b2 of a pair the batch driver runs b1 of the next
+// pair, so fine verification overlaps the next pair's host stages.
 template <class AfterClouds>
-void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_stats* stats,
-                     AfterClouds&& after_clouds, hipEvent_t fine_after = nullptr) {
+void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_stats* stats,
+              AfterClouds&& after_clouds) {
   fccf_stats S;
   std::memset(&S, 0, sizeof S);
   PipeSet& ps = pset(c, s);
@@ -604,7 +627,6 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   // ---------------- host: clustering, quick_verify (LM), score ranking
   const int transformation_num = (int)(tot[0] + tot[1] + tot[2]);
   const int analyse_max = (int)P.fine_verify_number;
-  struct TS { m44 T; float score, score2; };
   std::vector<TS> ctv[3];
   std::vector<int64_t> counts = {(int64_t)K, kpass, (int64_t)tot[0], (int64_t)tot[1], (int64_t)tot[2]};
   // clustering of the three types (cheap: the neighbour sets come from the device),
@@ -679,18 +701,17 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   ht.mark("verify");
 
   // ---------------- device: K7 fine verify of the top analyse_max per type
-  t0 = clk::now();
+  // (launched here on c->sa[1]; phase_b2 waits for it and fuses)
+  PhaseB& pb = ps.pb;
+  pb.t_fine = clk::now();
   std::vector<m44> evals;
-  std::vector<std::pair<int, int>> who;
   for (int t = 0; t < 3; ++t)
-    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
-      evals.push_back(ctv[t][i].T);
-      who.push_back({t, i});
-    }
+    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) evals.push_back(ctv[t][i].T);
   const int E = (int)evals.size();
   if (E > MAX_EVAL) throw Error(FCCF_E_INTERNAL, "too many fine-verify evaluations");
-  std::vector<float> scores(E, 0.f);
   if (E > 0) {
+    hipStream_t sf = c->sa[1];
+    fccf::Arena& a3 = c->cs[s].arena3;
     const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
     const size_t nk = (size_t)E * (n1 + n2);
     const size_t af2 = aggr_floats(n2);
@@ -698,31 +719,31 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
                         (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
                         sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256 +
                         exact_sum_bytes(E, n1 + n2) + 256;
-    c->arena3.ensure(need);
-    c->arena3.reset();
+    a3.ensure(need);
+    a3.reset();
     FineBufs fb;
-    fb.s2t = c->arena3.take_n<float>(3 * (size_t)E * n2);
-    fb.aggr2 = c->arena3.take_n<float>((size_t)E * af2);
-    fb.state = c->arena3.take_n<OctState>(E + 1);
-    fb.k0 = c->arena3.take_n<uint64_t>(nk);
-    fb.k1 = c->arena3.take_n<uint64_t>(nk);
-    fb.v0 = c->arena3.take_n<uint32_t>(nk);
-    fb.v1 = c->arena3.take_n<uint32_t>(nk);
-    fb.starts = c->arena3.take_n<uint32_t>(nk + 1);
-    fb.term = c->arena3.take_n<float>(nk + 1);
-    fb.range = c->arena3.take_n<uint32_t>(2 * MAX_EVAL);
-    fb.nseg_e = c->arena3.take_n<uint32_t>(2 * MAX_EVAL);
-    fb.similar = c->arena3.take_n<float>(MAX_EVAL);
-    fb.all = c->arena3.take_n<float>(MAX_EVAL);
-    fb.scal = c->arena3.take_n<uint32_t>(16);
-    fb.scores = c->arena3.take_n<float>(E);
-    fb.T = c->arena3.take_n<m44>(E);
-    fb.ss = sort_scratch_carve(c->arena3.take(sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1))),
+    fb.s2t = a3.take_n<float>(3 * (size_t)E * n2);
+    fb.aggr2 = a3.take_n<float>((size_t)E * af2);
+    fb.state = a3.take_n<OctState>(E + 1);
+    fb.k0 = a3.take_n<uint64_t>(nk);
+    fb.k1 = a3.take_n<uint64_t>(nk);
+    fb.v0 = a3.take_n<uint32_t>(nk);
+    fb.v1 = a3.take_n<uint32_t>(nk);
+    fb.starts = a3.take_n<uint32_t>(nk + 1);
+    fb.term = a3.take_n<float>(nk + 1);
+    fb.range = a3.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.nseg_e = a3.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.similar = a3.take_n<float>(MAX_EVAL);
+    fb.all = a3.take_n<float>(MAX_EVAL);
+    fb.scal = a3.take_n<uint32_t>(16);
+    fb.scores = a3.take_n<float>(E);
+    fb.T = a3.take_n<m44>(E);
+    fb.ss = sort_scratch_carve(a3.take(sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1))),
                                (uint32_t)std::max<size_t>(nk, 1));
-    fb.xs = exact_sum_carve(c->arena3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
-    FineMail& fm = host_mail(c)->fine;
+    fb.xs = exact_sum_carve(a3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
+    FineMail& fm = host_mail(c)->fine[s];
     std::memcpy(fm.T, evals.data(), sizeof(m44) * E);  // pinned staging: async H2D
-    HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, st0));
+    HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, sf));
     struct {
       const void* base;
       size_t acap;
@@ -730,31 +751,51 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
       uint32_t n1, n2;
       int32_t E;
       float res;
-    } fkey = {c->arena3.base, c->arena3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E,
-              P.fine_verify_voxel_size};
-    // in a batch, fine verification waits for the next pair's cloud stage: chains of
-    // small kernels from the two stages interleave badly, run back to back they don't
+    } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size};
     ht.mark("fine_setup");
-    HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[5], 0));  // S1 octree bounds replayed
-    if (fine_after && !std::getenv("FCCF_NO_FINE_AFTER")) HIP_CHECK(hipStreamWaitEvent(st0, fine_after, 0));
-    ht.mark("fine_waits");
-    c->cs[s].g_fine.run(&fkey, sizeof fkey, st0, [&] {
-      fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, st0,
+    HIP_CHECK(hipStreamWaitEvent(sf, c->cs[s].ev[5], 0));  // S1 octree bounds replayed (after the clouds)
+    c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
+      fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm);
     });
     HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));  // fine verification of this set's pair done
     ht.mark("fine_launched");
-    HIP_CHECK(hipStreamSynchronize(st0));  // scores and the error word are in the mailbox
-    std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
-    const uint32_t ferr = fm.err;
-    if (ferr) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
   }
-  S.ms[FCCF_T_FINE] = ms_since(t0);
-  ht.mark("fine");
-  ht.flush();
+  pb.S = S;
+  for (int t = 0; t < 3; ++t) pb.ctv[t] = std::move(ctv[t]);
+  pb.counts = std::move(counts);
+  pb.E = E;
+  pb.analyse_max = analyse_max;
+  pb.T_out = T_out;
+  pb.stats = stats;
+  pb.t_all = t_all;
+  pb.ht = ht;
+}
+
+// Phase B2: the fine scores of the pair on CloudSet s (launched by phase_b1), the
+// score sums over all types and fusion (:1539-1606).
+void phase_b2(fccf_ctx* c, int s) {
+  PipeSet& ps = pset(c, s);
+  PhaseB& pb = ps.pb;
+  fccf_stats& S = pb.S;
+  auto& ctv = pb.ctv;
+  auto& counts = pb.counts;
+  const int E = pb.E, analyse_max = pb.analyse_max;
+  float* T_out = pb.T_out;
+  std::vector<float> scores(E, 0.f);
+  if (E > 0) {
+    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));  // scores and the error word are in the mailbox
+    const FineMail& fm = host_mail(c)->fine[s];
+    std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
+    if (fm.err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
+  }
+  S.ms[FCCF_T_FINE] = ms_since(pb.t_fine);
+  pb.ht.mark("fine");
+  pb.ht.flush();
 
   // ---------------- host: score sums (over all types) and fusion (:1539-1606)
-  t0 = clk::now();
+  auto t0 = clk::now();
   float score1_sum = 0.f, score2_sum = 0.f;
   {
     int e = 0;
@@ -778,8 +819,8 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     float bs = 0.f;
     m44 bt = eye44();
     for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
-      const float s = ctv[t][i].score / score1_sum + ctv[t][i].score2 / score2_sum;
-      if (s > bs) { bs = s; bt = ctv[t][i].T; }
+      const float sc = ctv[t][i].score / score1_sum + ctv[t][i].score2 / score2_sum;
+      if (sc > bs) { bs = sc; bt = ctv[t][i].T; }
     }
     if (best_best < bs) best_best = bs;
     tmp.push_back({qt_from_T(bt), bs});
@@ -795,7 +836,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) T_out[4 * i + j] = T.m[i][j];
   S.ms[FCCF_T_FUSE] = ms_since(t0);
-  S.ms_total = ms_since(t_all);
+  S.ms_total = ms_since(pb.t_all);
   if (c->probe.on()) {
     HIP_CHECK(hipDeviceSynchronize());
     probe_collect(c->probe);
@@ -816,7 +857,7 @@ void register_finish(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], 
     c->dbg_put("T", T_out, 16);
     c->dbg_put("counts", counts);
   }
-  if (stats) *stats = S;
+  if (pb.stats) *pb.stats = S;
 }
 
 void reset_capture_counts(fccf_ctx* c) {
@@ -850,7 +891,8 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
   clouds_enqueue(c, 0, src, n_src, tar, n_tar, on_device, leaf, P);
-  register_finish(c, 0, P, T_out, stats, [] {});
+  phase_b1(c, 0, P, T_out, stats, [] {});
+  phase_b2(c, 0);
 }
 
 void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src, const float* const* tar,
@@ -860,16 +902,17 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
   clouds_enqueue(c, 0, src[0], n_src[0], tar[0], n_tar[0], on_device, leaf, P);
+  // pair i: B1 (its clouds done -> enqueue pair i+1's clouds -> host stages ->
+  // launch fine verification), then B2 of pair i-1, whose fine verification ran
+  // on the GPU during pair i's host stages
   for (int i = 0; i < n; ++i) {
     const int s = i & 1;
-    register_finish(
-        c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr,
-        [&] {  // the next pair's cloud stage overlaps this pair's host stages
-          if (i + 1 < n)
-            clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
-        },
-        i + 1 < n ? c->cs[s ^ 1].ev[4] : nullptr);
+    phase_b1(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
+      if (i + 1 < n) clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+    });
+    if (i > 0) phase_b2(c, s ^ 1);
   }
+  phase_b2(c, (n - 1) & 1);
 }
 
 }  // namespace fccf
