@@ -20,6 +20,7 @@ struct VGParams {
   uint32_t nbits;     // radix bits (0 when overflow / empty, or when the keys are already sorted)
   uint32_t unsorted;  // presorted check: some key is not strictly above its predecessor
   uint32_t chk_done;  // presorted check: blocks finished
+  uint32_t nonfinite; // some output point is not finite (set by k_vg_centroid when it writes a copy)
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
@@ -40,8 +41,12 @@ struct VGBufs {
 // kernel then skips the radix passes when the keys are already strictly increasing
 // (every leaf holds one point), which leaves the result unchanged.
 // nbatch = 2 runs both clouds (argument pairs, blockIdx.y = cloud) in the same launches.
+// out_copy (optional): every output point is also written there, and
+// VGParams::nonfinite is set when one is not finite (the driver's remove-NaN after
+// the first pass, FCCF.cpp:1374-1375, is then an identity unless that flag is set).
 void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted = false, int nbatch = 1);
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted = false, int nbatch = 1,
+                B2<float*> out_copy = B2<float*>(nullptr));
 
 // ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
 struct VoxRec {  // one occupied octree leaf, Morton order

@@ -37,29 +37,48 @@ using clk = std::chrono::steady_clock;
 double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); }
 
 // ------------------------------------------------------------ remove-NaN (:1374-1375)
-__global__ void k_finite_flags(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<uint32_t*> f2) {
+// The first VoxelGrid pass writes its output twice (ds1 for the record, ds1f for the
+// second pass) and flags a non-finite output point.  Centroids of finite points are
+// finite unless a leaf sum overflows, and the pass-through output (int32 index
+// overflow) holds the input as is, so the flag is almost never set: then ds1f is
+// already the NaN-free cloud and only its count is written.  Otherwise this single
+// workgroup compacts ds1 into ds1f in order, 1024 points per step (slow, rare).
+__global__ void __launch_bounds__(1024) k_finite_fix(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
+                                                     B2<const VGParams*> P2, B2<float*> out2, B2<uint32_t*> d_m2) {
   KT();
   const int e = blockIdx.y;
-  const float* __restrict__ xyz = xyz2[e];
-  uint32_t* __restrict__ f = f2[e];
   const uint32_t n = *d_n2[e];
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    f[i] = finite3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]) ? 1u : 0u;
-}
-__global__ void k_finite_scatter(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<const uint32_t*> f2,
-                                 B2<const uint32_t*> off2, B2<float*> out2) {
-  KT();
-  const int e = blockIdx.y;
+  if (!P2[e]->nonfinite) {
+    if (threadIdx.x == 0) *d_m2[e] = n;
+    return;
+  }
   const float* __restrict__ xyz = xyz2[e];
-  const uint32_t* __restrict__ f = f2[e];
-  const uint32_t* __restrict__ off = off2[e];
   float* __restrict__ out = out2[e];
-  const uint32_t n = *d_n2[e];
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    if (f[i]) {
-      const uint32_t o = off[i];
-      out[3 * o] = xyz[3 * i]; out[3 * o + 1] = xyz[3 * i + 1]; out[3 * o + 2] = xyz[3 * i + 2];
+  __shared__ uint32_t wsum[16];
+  uint32_t base = 0;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
+    const uint32_t i = c0 + threadIdx.x;
+    float x = 0.f, y = 0.f, z = 0.f;
+    bool keep = false;
+    if (i < n) {
+      x = xyz[3 * i]; y = xyz[3 * i + 1]; z = xyz[3 * i + 2];
+      keep = finite3(x, y, z);
     }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = base, tot = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+      before += k < w ? wsum[k] : 0u;
+      tot += wsum[k];
+    }
+    const uint32_t pos = before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (keep) { out[3 * pos] = x; out[3 * pos + 1] = y; out[3 * pos + 2] = z; }
+    base += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *d_m2[e] = base;
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -129,7 +148,6 @@ struct CloudWS {
   float* in_copy = nullptr;
   uint32_t* sc = nullptr;  // [0] n_in, [1] m1, [2] m1 finite, [3] m2
   float *ds1 = nullptr, *ds1f = nullptr, *ds2 = nullptr;
-  uint32_t *fflag = nullptr, *foff = nullptr;
   VGBufs vg;
   FaceBufs fb;
   VoxRec* planar = nullptr;
@@ -142,7 +160,7 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   const size_t N = cap;
   size_t b = 0;
   b += host_input ? 12 * N : 0;                               // input copy
-  b += 12 * N * 3 + 8 * N + 64;                                // ds1, ds1f, ds2, flags, offsets
+  b += 12 * N * 3 + 64;                                        // ds1, ds1f, ds2
   b += voxel_grid_bytes(cap);                                  // K1
   b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
   b += 4 * aggr_floats(cap) + 256;                             // aggregates, state, centroid
@@ -161,8 +179,6 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.ds1 = a.take_n<float>(3 * (size_t)cap);
   w.ds1f = a.take_n<float>(3 * (size_t)cap);
   w.ds2 = a.take_n<float>(3 * (size_t)cap);
-  w.fflag = a.take_n<uint32_t>(cap);
-  w.foff = a.take_n<uint32_t>(cap);
   w.vg = voxel_grid_carve(a, cap);
   FaceBufs& f = w.fb;
   f.c0 = a.take_n<uint64_t>(cap);
@@ -208,15 +224,11 @@ void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
   const B2<VGBufs> vg(w[0].vg, w[1].vg);
   const B2<float*> ds1 = both<float*>(w, [](const CloudWS& c) { return c.ds1; });
   const B2<float*> ds1f = both<float*>(w, [](const CloudWS& c) { return c.ds1f; });
-  const B2<uint32_t*> fflag = both<uint32_t*>(w, [](const CloudWS& c) { return c.fflag; });
   voxel_grid(both<const float*>(w, [](const CloudWS& c) { return c.in; }), sc(0), cap, leaf, ds1, sc(1), vg, st,
-             false, 2);  // main :1668-1678
-  k_finite_flags<<<dim3(grid_for(cap), 2), 256, 0, st>>>(B2<const float*>(ds1), sc(1), fflag);  // driver :1374-1375
-  exclusive_scan_u32(B2<const uint32_t*>(fflag), both<uint32_t*>(w, [](const CloudWS& c) { return c.foff; }), sc(1),
-                     cap, sc(2), B2<SortScratch>(w[0].vg.ss, w[1].vg.ss), st, 2);
-  k_finite_scatter<<<dim3(grid_for(cap), 2), 256, 0, st>>>(
-      B2<const float*>(ds1), sc(1), B2<const uint32_t*>(fflag),
-      both<const uint32_t*>(w, [](const CloudWS& c) { return (const uint32_t*)c.foff; }), ds1f);
+             false, 2, ds1f);  // main :1668-1678, output also into ds1f
+  k_finite_fix<<<dim3(1, 2), 1024, 0, st>>>(B2<const float*>(ds1), sc(1),
+                                            B2<const VGParams*>(w[0].vg.params, w[1].vg.params), ds1f,
+                                            sc(2));  // driver :1374-1375
   voxel_grid(B2<const float*>(ds1f), sc(2), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds2; }), sc(3),
              vg, st, true, 2);  // driver :1377-1387
 }

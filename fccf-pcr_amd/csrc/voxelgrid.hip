@@ -93,6 +93,7 @@ __global__ void __launch_bounds__(64) k_vg_params(B2<const float*> part2, int np
   for (int a = 0; a < 3; ++a) q.min_b[a] = q.div_b[a] = 0;
   q.unsorted = 0;
   q.chk_done = 0;
+  q.nonfinite = 0;
   if (cnt > 0) {
     const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
     const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
@@ -163,12 +164,15 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
 // coalesced 16-byte words.  The pass-through cases are flat 16-byte copies.
 constexpr int CL = 4;
 __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
-                                                     B2<const VGParams*> P2, B2<const uint32_t*> vals2,
+                                                     B2<VGParams*> P2, B2<const uint32_t*> vals2,
                                                      B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
-                                                     B2<float*> out2, B2<uint32_t*> d_m2, int presorted) {
+                                                     B2<float*> out2, B2<uint32_t*> d_m2, int presorted,
+                                                     B2<float*> copy2) {
   KT();
   const int e = blockIdx.y;
   const VGParams q = *P2[e];
+  float* __restrict__ cpy = copy2[e];
+  bool bad = false;  // a non-finite output value (only tracked with a copy)
   const float* __restrict__ xyz = xyz2[e];
   const uint32_t* __restrict__ vals = vals2[e];
   const uint32_t* __restrict__ starts = starts2[e];
@@ -183,9 +187,23 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<c
     const uint32_t nf = 3 * n;
     const bool al = ((((uintptr_t)xyz) | ((uintptr_t)out)) & 15u) == 0;
     const uint32_t n4 = al ? nf / 4 : 0;
-    for (uint32_t i = gid; i < n4; i += gsz) reinterpret_cast<float4*>(out)[i] = reinterpret_cast<const float4*>(xyz)[i];
-    for (uint32_t i = 4 * n4 + gid; i < nf; i += gsz) out[i] = xyz[i];
+    for (uint32_t i = gid; i < n4; i += gsz) {
+      const float4 v = reinterpret_cast<const float4*>(xyz)[i];
+      reinterpret_cast<float4*>(out)[i] = v;
+      if (cpy) {
+        reinterpret_cast<float4*>(cpy)[i] = v;
+        bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+      }
+    }
+    for (uint32_t i = 4 * n4 + gid; i < nf; i += gsz) {
+      out[i] = xyz[i];
+      if (cpy) {
+        cpy[i] = xyz[i];
+        bad |= !isfinite(xyz[i]);
+      }
+    }
     if (gid == 0) *d_m = n;
+    if (cpy && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&P2[e]->nonfinite, 1u);
     return;
   }
   const uint32_t ns = q.nfinite ? *d_nseg : 0u;
@@ -216,17 +234,27 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<c
       so[3 * threadIdx.x] = sx / cnt;
       so[3 * threadIdx.x + 1] = sy / cnt;
       so[3 * threadIdx.x + 2] = sz / cnt;
+      bad |= !finite3(so[3 * threadIdx.x], so[3 * threadIdx.x + 1], so[3 * threadIdx.x + 2]);
     }
     __syncthreads();
     const uint32_t m = min(256u, ns - s0);  // centroids of this block step
     float* dst = out + 3 * (size_t)s0;
+    float* dcp = cpy ? cpy + 3 * (size_t)s0 : nullptr;
     if (al && m == 256u) {
-      if (threadIdx.x < 192) reinterpret_cast<float4*>(dst)[threadIdx.x] = reinterpret_cast<const float4*>(so)[threadIdx.x];
+      if (threadIdx.x < 192) {
+        const float4 v = reinterpret_cast<const float4*>(so)[threadIdx.x];
+        reinterpret_cast<float4*>(dst)[threadIdx.x] = v;
+        if (dcp) reinterpret_cast<float4*>(dcp)[threadIdx.x] = v;
+      }
     } else {
-      for (uint32_t i = threadIdx.x; i < 3 * m; i += 256) dst[i] = so[i];
+      for (uint32_t i = threadIdx.x; i < 3 * m; i += 256) {
+        dst[i] = so[i];
+        if (dcp) dcp[i] = so[i];
+      }
     }
     __syncthreads();
   }
+  if (cpy && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(&P2[e]->nonfinite, 1u);
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -237,7 +265,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 }  // namespace
 
 void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch) {
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch, B2<float*> out_copy) {
   auto F = [&](auto get) { return B2<decltype(get(b[0]))>(get(b[0]), get(b[1])); };
   const B2<VGParams*> P = F([](const VGBufs& v) { return v.params; });
   const B2<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
@@ -262,7 +290,7 @@ void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, flo
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch, unsorted);
   }
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, xyz, d_n, B2<const VGParams*>(P), B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0);
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, xyz, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0, out_copy);
 }
 
 }  // namespace fccf

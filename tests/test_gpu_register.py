@@ -184,3 +184,20 @@ def test_host_radius_search_path_matches(ctx, oracle, fccf, monkeypatch):
     T1, _ = ctx.register(src, tar, 0.1)
     compare_all(ctx, run)
     np.testing.assert_array_equal(T0.view(np.uint32), T1.view(np.uint32))
+
+
+def test_nonfinite_points_through_overflow_passthrough(ctx, oracle, fccf):
+    """A far outlier makes the first VoxelGrid pass overflow its int32 leaf index,
+    so PCL passes the cloud through unfiltered, NaN points included; the driver's
+    removeNaNFromPointCloud (FCCF.cpp:1374-1375) then has real work (the rare path
+    of k_finite_fix).  Bitwise parity with the oracle at every stage."""
+    src, tar, _ = fccf.synth_pair(60_000)
+    src = src.copy()
+    src[::997] = np.nan
+    src[5::1009, 2] = np.inf
+    far = np.array([[2500.0, -2500.0, 2500.0]], np.float32)
+    src2 = np.concatenate([src, far])
+    run = oracle.Run(src2, tar, 0.1, oracle.STABLE)
+    T, _ = ctx.register(src2, tar, 0.1)
+    compare_all(ctx, run)
+    np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
