@@ -106,15 +106,18 @@ class _SelftestCtx:
         return np.eye(4, dtype=np.float32), self._St()
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py), else None."""
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of the
+    same workload (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py from
+    rocprofv3 --pmc passes over this bench command), else None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
+            continue
+        if d.get("config", "c3") != config:
             continue
         if kernel in d.get("kernels", {}):
             return d["kernels"][kernel]["hbm_bytes_per_launch"]
@@ -219,7 +222,7 @@ def main():
             avg_s = pms * 1e-3 / pn
             achieved = (pb / pn) / avg_s / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe), "kernel": probe,
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe, args.config), "kernel": probe,
                         "avg_launch_us": avg_s * 1e6, "algorithmic_bytes_per_launch": pb / pn,
                         "launches_per_step": pn / args.steps}
     elapsed = allmax(dist, elapsed)
