@@ -175,9 +175,27 @@ __global__ void __launch_bounds__(256) k_oct_codes(B2<const float*> xyz2, B2<con
   const float* __restrict__ xyz = xyz2[e];
   uint64_t* __restrict__ codes = codes2[e];
   uint32_t* __restrict__ d_nbits = d_nbits2[e];
-  const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
   if (gid == 0) *d_nbits = S.defined ? 3u * S.depth + 1u : 1u;
-  for (uint32_t i = gid; i < n; i += gridDim.x * 256) {
+  // four points per thread: three 16-byte loads, two 16-byte stores (aligned arena
+  // buffers; a misaligned base takes the one-point loop for everything)
+  const bool al = ((((uintptr_t)xyz) | ((uintptr_t)codes)) & 15u) == 0;
+  const uint32_t nq = al ? n / 4 : 0;
+  for (uint32_t q = gid; q < nq; q += gsz) {
+    const float4* v = reinterpret_cast<const float4*>(xyz) + 3 * (size_t)q;
+    const float4 a = v[0], b = v[1], c = v[2];
+    const float p[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    uint64_t k[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = p[3 * j], y = p[3 * j + 1], z = p[3 * j + 2];
+      k[j] = finite3(x, y, z) ? oct_code(S, res, x, y, z) : ~(uint64_t)0;
+    }
+    ulonglong2* o = reinterpret_cast<ulonglong2*>(codes + 4 * (size_t)q);
+    o[0] = make_ulonglong2(k[0], k[1]);
+    o[1] = make_ulonglong2(k[2], k[3]);
+  }
+  for (uint32_t i = 4 * nq + gid; i < n; i += gsz) {
     const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
     codes[i] = finite3(x, y, z) ? oct_code(S, res, x, y, z) : ~(uint64_t)0;
   }

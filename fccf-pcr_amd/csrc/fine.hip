@@ -17,28 +17,27 @@
 namespace fccf {
 namespace {
 
+// Block (0, e) also starts evaluation e's octree from the bounds after S1 (the fused
+// cloud is S1 ++ T_e S2), and block (0, 0) writes the scalars.
 __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ s2, uint32_t n2,
-                                                      const m44* __restrict__ T, float* __restrict__ s2t) {
+                                                      const m44* __restrict__ T, float* __restrict__ s2t,
+                                                      const OctState* __restrict__ s1_state, OctState* __restrict__ st,
+                                                      uint32_t* __restrict__ scal, uint32_t n1) {
   KT();
   const int e = blockIdx.y;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[e] = *s1_state;
+    if (e == 0) {
+      scal[4] = n1;
+      scal[5] = n2;
+      scal[7] = 0u;
+    }
+  }
   const m44 M = T[e];
   float* o = s2t + (size_t)e * 3 * n2;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += gridDim.x * 256) {
     const f3 p = tf_se3(M, s2[3 * i], s2[3 * i + 1], s2[3 * i + 2]);
     o[3 * i] = p.x; o[3 * i + 1] = p.y; o[3 * i + 2] = p.z;
-  }
-}
-
-// every evaluation's octree starts from the bounds after S1 (the fused cloud is S1 ++ T_e S2)
-__global__ void k_fv_init(const OctState* __restrict__ s1_state, OctState* st, int E, uint32_t* scal, uint32_t n1,
-                          uint32_t n2) {
-  KT();
-  const int e = threadIdx.x;
-  if (e < E) st[e] = *s1_state;
-  if (e == 0) {
-    scal[4] = n1;
-    scal[5] = n2;
-    scal[7] = 0u;
   }
 }
 
@@ -163,8 +162,8 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
                        double res, FineBufs b, hipStream_t st, FineMail* mail) {
   if (E <= 0) return;
   const size_t astride = aggr_floats(n2);
-  k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t);
-  k_fv_init<<<1, 64, 0, st>>>(s1_state, b.state, E, b.scal, n1, n2);
+  k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
+                                                                  n1);
   // scal[5] holds n2 for the device-count interfaces
   uint32_t* d_n2 = b.scal + 5;
   SeqStrides sd;  // evaluation e: its own transformed S2 copy, aggregates and state; shared count

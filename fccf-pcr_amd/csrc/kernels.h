@@ -24,6 +24,7 @@ struct VGParams {
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
+constexpr int VG_KEY_BLOCKS = 512;
 
 struct VGBufs {
   uint32_t *k0, *v0, *k1, *v1;  // cap each

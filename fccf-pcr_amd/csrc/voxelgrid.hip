@@ -27,10 +27,18 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Per-block partial bbox of finite points: part[b] = {min xyz, max xyz, count(bits), 0}.
-__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<float*> part2) {
+// Block 0 also clears the pass's flags (keys' order check, the centroid kernel's
+// non-finite flag) before any later kernel of the pass can set them.
+__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<float*> part2,
+                                                 B2<VGParams*> P2) {
   KT();
   __shared__ float sh[4][7];
   const int e = blockIdx.y;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    P2[e]->unsorted = 0;
+    P2[e]->chk_done = 0;
+    P2[e]->nonfinite = 0;
+  }
   const float* __restrict__ xyz = xyz2[e];
   const uint32_t n = *d_n2[e];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -68,53 +76,89 @@ __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const
   }
 }
 
-__global__ void __launch_bounds__(64) k_vg_params(B2<const float*> part2, int nparts, float leaf, B2<VGParams*> P2) {
-  KT();
-  const float* __restrict__ part = part2[blockIdx.y];
-  VGParams* __restrict__ P = P2[blockIdx.y];
+// The pass's VoxelGrid parameters from the nparts bbox partials: leaf size, bounds,
+// int32 overflow guard, index multipliers, radix width.  Every thread of the block
+// calls it and gets the result (256 threads; min/max/count reductions are exact in
+// any order, so every block computes the same bits).
+__device__ VGParams vg_params_block(const float* __restrict__ part, int nparts, float leaf) {
+  __shared__ float sh[4][7];
+  __shared__ VGParams sq;
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t cnt = 0;
-  for (int b = threadIdx.x; b < nparts; b += 64) {
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) {
     const float* p = part + 8 * b;
     for (int a = 0; a < 3; ++a) { mn[a] = fminf(mn[a], p[a]); mx[a] = fmaxf(mx[a], p[3 + a]); }
     cnt += __float_as_uint(p[6]);
   }
   for (int a = 0; a < 3; ++a) { mn[a] = wave_min(mn[a]); mx[a] = wave_max(mx[a]); }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-  if (threadIdx.x != 0) return;
-  VGParams q;
-  const float inv = 1.0f / leaf;
-  q.inv = inv;
-  q.nfinite = cnt;
-  for (int a = 0; a < 3; ++a) { q.mn[a] = mn[a]; q.mx[a] = mx[a]; }
-  q.overflow = 0;
-  q.nbits = 0;
-  q.mul1 = q.mul2 = 0;
-  for (int a = 0; a < 3; ++a) q.min_b[a] = q.div_b[a] = 0;
-  q.unsorted = 0;
-  q.chk_done = 0;
-  q.nonfinite = 0;
-  if (cnt > 0) {
-    const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-    const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-    const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-    if (dx * dy * dz > (int64_t)2147483647) {
-      q.overflow = 1;
-    } else {
-      for (int a = 0; a < 3; ++a) {
-        q.min_b[a] = (int32_t)floorf(mn[a] * inv);
-        const int32_t max_b = (int32_t)floorf(mx[a] * inv);
-        q.div_b[a] = max_b - q.min_b[a] + 1;
-      }
-      q.mul1 = q.div_b[0];
-      q.mul2 = (int64_t)q.div_b[0] * q.div_b[1];
-      const uint64_t total = (uint64_t)q.div_b[0] * (uint64_t)q.div_b[1] * (uint64_t)q.div_b[2];
-      uint32_t nb = 1;
-      while (nb < 32 && (1ull << nb) <= total) ++nb;  // 2^nbits > total: the invalid key sorts last
-      q.nbits = nb;
-    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    for (int a = 0; a < 3; ++a) { sh[w][a] = mn[a]; sh[w][3 + a] = mx[a]; }
+    sh[w][6] = __uint_as_float(cnt);
   }
-  *P = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt = 0;
+    for (int a = 0; a < 3; ++a) { mn[a] = INFINITY; mx[a] = -INFINITY; }
+    for (int ww = 0; ww < (int)(blockDim.x >> 6); ++ww) {
+      for (int a = 0; a < 3; ++a) { mn[a] = fminf(mn[a], sh[ww][a]); mx[a] = fmaxf(mx[a], sh[ww][3 + a]); }
+      cnt += __float_as_uint(sh[ww][6]);
+    }
+    VGParams q;
+    const float inv = 1.0f / leaf;
+    q.inv = inv;
+    q.nfinite = cnt;
+    for (int a = 0; a < 3; ++a) { q.mn[a] = mn[a]; q.mx[a] = mx[a]; }
+    q.overflow = 0;
+    q.nbits = 0;
+    q.mul1 = q.mul2 = 0;
+    for (int a = 0; a < 3; ++a) q.min_b[a] = q.div_b[a] = 0;
+    q.unsorted = 0;
+    q.chk_done = 0;
+    q.nonfinite = 0;
+    if (cnt > 0) {
+      const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+      const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+      const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+      if (dx * dy * dz > (int64_t)2147483647) {
+        q.overflow = 1;
+      } else {
+        for (int a = 0; a < 3; ++a) {
+          q.min_b[a] = (int32_t)floorf(mn[a] * inv);
+          const int32_t max_b = (int32_t)floorf(mx[a] * inv);
+          q.div_b[a] = max_b - q.min_b[a] + 1;
+        }
+        q.mul1 = q.div_b[0];
+        q.mul2 = (int64_t)q.div_b[0] * q.div_b[1];
+        const uint64_t total = (uint64_t)q.div_b[0] * (uint64_t)q.div_b[1] * (uint64_t)q.div_b[2];
+        uint32_t nb = 1;
+        while (nb < 32 && (1ull << nb) <= total) ++nb;  // 2^nbits > total: the invalid key sorts last
+        q.nbits = nb;
+      }
+    }
+    sq = q;
+  }
+  __syncthreads();
+  return sq;
+}
+
+// Block (0, e) publishes the parameters for the later kernels of the pass; the
+// flags (unsorted, chk_done, nonfinite) were cleared by k_vg_bbox and are only
+// ever set with atomics, so they are not part of that write.
+__device__ void vg_params_publish(VGParams* P, const VGParams& q) {
+  for (int a = 0; a < 3; ++a) {
+    P->mn[a] = q.mn[a];
+    P->mx[a] = q.mx[a];
+    P->min_b[a] = q.min_b[a];
+    P->div_b[a] = q.div_b[a];
+  }
+  P->inv = q.inv;
+  P->nfinite = q.nfinite;
+  P->mul1 = q.mul1;
+  P->mul2 = q.mul2;
+  P->overflow = q.overflow;
+  P->nbits = q.nbits;
 }
 
 __device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, float z) {
@@ -130,11 +174,13 @@ __device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, 
 // otherwise every leaf holds exactly one point and the pass is the identity (the
 // sort tail, segmentation and centroid kernels take their shortcut).
 __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<VGParams*> P2,
-                                                 B2<uint32_t*> keys2, B2<uint32_t*> vals2, int presorted) {
+                                                 B2<uint32_t*> keys2, B2<uint32_t*> vals2, int presorted,
+                                                 B2<const float*> part2, int nparts, float leaf) {
   KT();
   const int e = blockIdx.y;
   VGParams* P = P2[e];
-  const VGParams q = *P;
+  const VGParams q = vg_params_block(part2[e], nparts, leaf);  // every block, from the bbox partials
+  if (blockIdx.x == 0 && threadIdx.x == 0) vg_params_publish(P, q);
   const uint32_t n = *d_n2[e];
   if (q.overflow) return;
   if (q.nfinite == 0) {
@@ -274,13 +320,14 @@ void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, flo
   const B2<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
   const B2<const uint32_t*> nbits(&b[0].params->nbits, &b[1].params->nbits);
   const dim3 g(grid_for(cap), nbatch);
-  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(xyz, d_n, F([](const VGBufs& v) { return v.part; }));
-  k_vg_params<<<dim3(1, nbatch), 64, 0, st>>>(F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS,
-                                               leaf, P);
+  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(xyz, d_n, F([](const VGBufs& v) { return v.part; }), P);
   const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts
   const uint32_t* m2 = nbatch > 1 ? d_m[1] : nullptr;
   const B2<const uint32_t*> unsorted(&b[0].params->unsorted, &b[1].params->unsorted);
-  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, g, 256, 0, st, xyz, d_n, P, k0, v0, presorted ? 1 : 0);
+  // the keys kernel also derives the parameters (k_vg_params folded in): each of its
+  // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
+  const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
+  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, xyz, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
   if (!presorted) {
     radix_sort_u32(k0, v0, k1, v1, d_n, cap, nbits, 32, true, ss, st, nbatch);
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
