@@ -285,6 +285,8 @@ __global__ void __launch_bounds__(256) k_gather(B2<const float*> xyz2, B2<const 
   }
 }
 
+constexpr uint32_t VFIT_BLOCKS = 512;  // 2048 waves per cloud; leaves are a few thousand at most
+
 // One wave per leaf (Morton order).  Lane k < 9 owns accumulator k of
 // computeMeanAndCovarianceMatrix (:495): [xx, xy, xz, yy, yz, zz, x, y, z], each a
 // sequential float sum over the leaf's points in index order.  Points are staged in
@@ -293,7 +295,8 @@ __global__ void __launch_bounds__(256) k_gather(B2<const float*> xyz2, B2<const 
 // sequential x/y/z sum divided by n, i.e. accumulators 6..8 / n bit-for-bit.
 __global__ void __launch_bounds__(256) k_voxel_fit(B2<FaceBufs> fb, float vpt, float cthr) {
   KT();
-  __shared__ __attribute__((aligned(16))) float pts[4][64 * 4];
+  constexpr uint32_t VB = 256;  // points per LDS burst of a wave (four per lane)
+  __shared__ __attribute__((aligned(16))) float pts[4][VB * 4];
   const FaceBufs& B = fb.v[blockIdx.y];
   const float* __restrict__ sp = B.sp;
   const uint32_t* __restrict__ starts = B.starts;
@@ -312,24 +315,52 @@ __global__ void __launch_bounds__(256) k_voxel_fit(B2<FaceBufs> fb, float vpt, f
     float acc = 0.f;
     const bool fit = (float)cnt > vpt;
     if (fit) {
-      for (uint32_t base = 0; base < cnt; base += 64) {
-        const uint32_t k = base + lane;
-        if (k < cnt) {
-          const float* q = sp + 3 * (size_t)(b + k);
-          *(float4*)(P + 4 * lane) = make_float4(q[0], q[1], q[2], 1.0f);
+      // The leaf streams through LDS in bursts of VB points; the next burst's four
+      // points per lane are loaded into registers while this one is summed, so the
+      // global-load latency (~1.5 us) hides behind a burst's ~VB dependent adds.
+      float nx[4], ny[4], nz[4];
+      auto load_burst = [&](uint32_t base) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t k = base + u * 64 + lane;
+          if (k < cnt) {
+            const float* q = sp + 3 * (size_t)(b + k);
+            nx[u] = q[0]; ny[u] = q[1]; nz[u] = q[2];
+          }
         }
+      };
+      load_burst(0);
+      for (uint32_t base = 0; base < cnt; base += VB) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (base + u * 64 + lane < cnt) *(float4*)(P + 4 * (u * 64 + lane)) = make_float4(nx[u], ny[u], nz[u], 1.0f);
+        if (base + VB < cnt) load_burst(base + VB);
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint32_t m = min(64u, cnt - base);
-        uint32_t j = 0;
-        for (; j + 8 <= m; j += 8) {
-          float a[8], c[8];
+        // sequential per accumulator (the reference's summation order); the LDS reads
+        // of the next eight points are issued before this eight's adds
+        const uint32_t m = __builtin_amdgcn_readfirstlane(min(VB, cnt - base));
+        const uint32_t m8 = m & ~7u;
+        float a[8], c[8];
+        if (m8) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) { a[q] = P[4 * (j + q) + i1]; c[q] = P[4 * (j + q) + i2]; }
+          for (int q = 0; q < 8; ++q) { a[q] = P[4 * q + i1]; c[q] = P[4 * q + i2]; }
+        }
+        for (uint32_t j = 0; j < m8; j += 8) {
+          float an[8], cn[8];
+          const bool more = j + 8 < m8;
+          if (more) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { an[q] = P[4 * (j + 8 + q) + i1]; cn[q] = P[4 * (j + 8 + q) + i2]; }
+          }
 #pragma unroll
           for (int q = 0; q < 8; ++q) acc += a[q] * c[q];
+          if (more) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { a[q] = an[q]; c[q] = cn[q]; }
+          }
         }
-        for (; j < m; ++j) acc += P[4 * j + i1] * P[4 * j + i2];
+        for (uint32_t j = m8; j < m; ++j) acc += P[4 * j + i1] * P[4 * j + i2];
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
@@ -484,7 +515,7 @@ void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float vpt, float cth
                      B2<FaceBufs> b, hipStream_t st, int nbatch) {
   const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
   const uint32_t* l2 = nbatch > 1 ? b[1].nleaf : nullptr;
-  FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, 4096), nbatch), 256, 0, st, b, vpt, cthr);
+  FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st, b, vpt, cthr);
   const B2<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
   const B2<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
   exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
