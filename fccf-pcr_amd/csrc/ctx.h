@@ -165,6 +165,7 @@ struct fccf_ctx {
   fccf::PinnedBuf pinned;
   fccf::MailBuf mail;  // pipeline.cpp host_mail()
   fccf::Pool pool;
+  fccf::AsyncTask enq;  // pipelined batch: enqueues the next pair's cloud stage
   fccf::Probe probe;
   bool debug = false;
   std::map<std::string, std::vector<uint8_t>> dbg;

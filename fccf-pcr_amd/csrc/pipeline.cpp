@@ -919,11 +919,22 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   // on the GPU during pair i's host stages
   for (int i = 0; i < n; ++i) {
     const int s = i & 1;
+    c->enq.wait();  // this pair's cloud stage is fully enqueued (its events recorded)
     phase_b1(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
-      if (i + 1 < n) clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+      if (i + 1 >= n) return;
+      // the next pair's cloud stage is enqueued from a helper thread while this
+      // thread runs the host stages (launches are ~60 us of host time); probed
+      // runs stay on this thread (the probe's launch records are not shared)
+      auto enq = [c, s, i, src, n_src, tar, n_tar, on_device, leaf, &P] {
+        HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
+        clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+      };
+      if (c->probe.on()) enq();
+      else c->enq.submit(enq);
     });
     if (i > 0) phase_b2(c, s ^ 1);
   }
+  c->enq.wait();
   phase_b2(c, (n - 1) & 1);
 }
 

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -132,6 +133,67 @@ class Pool {
   std::atomic<int> n_{0};
   uint64_t job_ = 0;
   int spin_us_ = 500;
+};
+
+// One background thread running one task at a time (the batch driver enqueues the
+// next pair's cloud stage there while the caller runs this pair's host stages).
+// wait() joins the current task and rethrows its exception, if any.
+class AsyncTask {
+ public:
+  AsyncTask() : th_([this] { loop(); }) {}
+  ~AsyncTask() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void submit(std::function<void()> f) {
+    wait();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      task_ = std::move(f);
+      busy_ = true;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [this] { return !busy_; });
+    if (err_) {
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    while (true) {
+      cv_.wait(g, [this] { return quit_ || busy_; });
+      if (quit_) return;
+      std::function<void()> f = std::move(task_);
+      g.unlock();
+      std::exception_ptr e;
+      try {
+        f();
+      } catch (...) {
+        e = std::current_exception();
+      }
+      g.lock();
+      err_ = e;
+      busy_ = false;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void()> task_;
+  std::exception_ptr err_;
+  bool busy_ = false, quit_ = false;
+  std::thread th_;
 };
 
 }  // namespace fccf
