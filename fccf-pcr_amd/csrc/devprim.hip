@@ -39,6 +39,44 @@ __device__ __forceinline__ uint32_t block_scan_256(uint32_t v, uint32_t* sh, uin
 
 __device__ __forceinline__ uint32_t passes_of(uint32_t nbits) { return (nbits + 7u) / 8u; }
 
+// Digit plan of the device-wide passes for an nbits-wide key: up to 27 bits, the
+// fewest passes of <= 9-bit digits (19..27 bits: three passes instead of four 8-bit
+// ones), wider keys 8-bit digits (the fast launches then cover 32 bits and the
+// single-workgroup tail the rest).  Every kernel of a sort derives the same plan
+// from the device-side nbits.
+constexpr int RS_MAXD = 512;  // buckets of the widest digit
+struct RsPlan {
+  uint32_t passes, width;
+};
+__device__ __forceinline__ RsPlan rs_plan(uint32_t nbits) {
+  if (nbits == 0) return {0u, 8u};
+  const uint32_t p = nbits <= 27u ? (nbits + 8u) / 9u : (nbits + 7u) / 8u;
+  return {p, (nbits + p - 1u) / p};
+}
+
+// Exclusive scan of v over the first 512 threads of an ST-thread block (threads
+// >= 512 pass 0 and get garbage); sh needs SW u32.  Every thread must call it.
+__device__ __forceinline__ uint32_t scan_512_of(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if (threadIdx.x >= 512) v = 0;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63 && wave < 8) sh[wave] = x;
+  __syncthreads();
+  uint32_t wp = 0, tot = 0;
+  for (uint32_t w = 0; w < 8; ++w) {
+    wp += w < wave ? sh[w] : 0u;
+    tot += sh[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
 // Radix-sort tiles: 4096 keys per block of ST = 1024 threads (16 waves x 4 chunks of
 // 64 keys).  A fat block keeps the per-tile ranking short (each wave ranks 256
 // keys) while the tile count, and with it the digit x tile histogram, stays small.
@@ -68,15 +106,17 @@ __device__ __forceinline__ uint32_t scan_256_of(uint32_t v, uint32_t* sh, uint32
 
 template <class K>
 __global__ void __launch_bounds__(ST) k_rs_hist(B2<const K*> keys2, B2<const uint32_t*> d_n2,
-                                                B2<const uint32_t*> d_nbits2, int shift, B2<SortScratch> ss,
+                                                B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
                                                 uint32_t nblocks) {
   KT();
   const int e = blockIdx.y;
   const K* __restrict__ keys = keys2[e];
   uint32_t* __restrict__ hist = ss[e].hist;
-  if ((uint32_t)shift >= *d_nbits2[e]) return;
-  __shared__ uint32_t cnt[256];
-  if (threadIdx.x < 256) cnt[threadIdx.x] = 0;
+  const RsPlan pl = rs_plan(*d_nbits2[e]);
+  if ((uint32_t)pass >= pl.passes) return;
+  const uint32_t shift = (uint32_t)pass * pl.width, W = pl.width, nd = 1u << W, mask = nd - 1u;
+  __shared__ uint32_t cnt[RS_MAXD];
+  if (threadIdx.x < RS_MAXD) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = *d_n2[e];
   const uint32_t base = blockIdx.x * SORT_TILE;
@@ -91,10 +131,9 @@ __global__ void __launch_bounds__(ST) k_rs_hist(B2<const K*> keys2, B2<const uin
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
     const bool ok = base + c * ST + threadIdx.x < end;
-    const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
+    const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
     uint64_t m = __ballot(ok);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (uint32_t b = 0; b < W; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       m &= bit ? bb : ~bb;
@@ -102,17 +141,18 @@ __global__ void __launch_bounds__(ST) k_rs_hist(B2<const K*> keys2, B2<const uin
     if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
   }
   __syncthreads();
-  if (threadIdx.x < 256) hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+  if (threadIdx.x < nd) hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
 // One block per digit: exclusive scan of that digit's per-block counts in place.
 __global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t nblocks, B2<const uint32_t*> d_nbits2,
-                                                  int shift) {
+                                                  int pass) {
   KT();
   const int e = blockIdx.y;
   uint32_t* __restrict__ hist = ss[e].hist;
   uint32_t* __restrict__ tot = ss[e].tot;
-  if ((uint32_t)shift >= *d_nbits2[e]) return;
+  const RsPlan pl = rs_plan(*d_nbits2[e]);
+  if ((uint32_t)pass >= pl.passes || blockIdx.x >= (1u << pl.width)) return;
   __shared__ uint32_t sh[4];
   const uint32_t d = blockIdx.x;
   uint32_t carry = 0;
@@ -133,7 +173,7 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t n
 template <class K>
 __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const uint32_t*> vin2, B2<K*> kout2,
                                                    B2<uint32_t*> vout2, B2<const uint32_t*> d_n2,
-                                                   B2<const uint32_t*> d_nbits2, int shift, B2<SortScratch> ss,
+                                                   B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
                                                    uint32_t nblocks, int iota, uint32_t* __restrict__ active) {
   KT();
   const int e = blockIdx.y;
@@ -143,15 +183,17 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
   uint32_t* __restrict__ vout = vout2[e];
   const uint32_t* __restrict__ hist = ss[e].hist;
   const uint32_t* __restrict__ tot = ss[e].tot;
-  const bool run = (uint32_t)shift < *d_nbits2[e];
+  const RsPlan pl = rs_plan(*d_nbits2[e]);
+  const bool run = (uint32_t)pass < pl.passes;
   if (active && e == 0 && blockIdx.x == 0 && threadIdx.x == 0)  // probe: any problem of the batch active
-    *active = (run || (gridDim.y > 1 && (uint32_t)shift < *d_nbits2[1])) ? 1u : 0u;
+    *active = (run || (gridDim.y > 1 && (uint32_t)pass < rs_plan(*d_nbits2[1]).passes)) ? 1u : 0u;
   const uint32_t n = *d_n2[e];
   const uint32_t tile0 = blockIdx.x * SORT_TILE;
   if (!run || tile0 >= n) return;  // grids are sized for the capacity; tiles past n are empty
-  __shared__ uint32_t gofs[256];     // global slot of the tile's first key of each digit
-  __shared__ uint32_t tex[256];      // exclusive digit offsets inside the tile
-  __shared__ uint32_t wcnt[SW][256];
+  const uint32_t shift = (uint32_t)pass * pl.width, W = pl.width, nd = 1u << W, mask = nd - 1u;
+  __shared__ uint32_t gofs[RS_MAXD];     // global slot of the tile's first key of each digit
+  __shared__ uint32_t tex[RS_MAXD];      // exclusive digit offsets inside the tile
+  __shared__ uint16_t wcnt[SW][RS_MAXD]; // per-wave digit counts, then per-wave offsets (<= 4096)
   __shared__ uint32_t sh[SW];
   __shared__ K sk[SORT_TILE];
   __shared__ uint32_t sv[SORT_TILE];
@@ -168,22 +210,21 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
   }
   {
     uint32_t t;
-    const uint32_t g = tid < 256 ? tot[tid] : 0u;
-    const uint32_t h = tid < 256 ? hist[tid * nblocks + blockIdx.x] : 0u;
-    const uint32_t ex = scan_256_of(g, sh, &t);
-    if (tid < 256) gofs[tid] = ex + h;
+    const uint32_t g = tid < nd ? tot[tid] : 0u;
+    const uint32_t h = tid < nd ? hist[tid * nblocks + blockIdx.x] : 0u;
+    const uint32_t ex = scan_512_of(g, sh, &t);
+    if (tid < nd) gofs[tid] = ex + h;
   }
-  for (uint32_t j = tid; j < SW * 256; j += ST) (&wcnt[0][0])[j] = 0;
+  for (uint32_t j = tid; j < SW * RS_MAXD; j += ST) (&wcnt[0][0])[j] = 0;
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t i = base + c * 64 + lane;
     const bool ok = i < n;
-    const uint32_t d = (uint32_t)(kk[c] >> shift) & 255u;
-    dg[c] = ok ? d : 256u;
+    const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
+    dg[c] = ok ? d : RS_MAXD;
     uint64_t m = __ballot(ok);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (uint32_t b = 0; b < W; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bb = __ballot(bit);
       m &= bit ? bb : ~bb;
@@ -191,26 +232,26 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
     const uint32_t r = mbcnt(m);
     const uint32_t pre = ok ? wcnt[wave][d] : 0u;
     rk[c] = pre + r;
-    if (ok && r == 0) wcnt[wave][d] = pre + (uint32_t)__popcll(m);
+    if (ok && r == 0) wcnt[wave][d] = (uint16_t)(pre + (uint32_t)__popcll(m));
   }
   __syncthreads();
   {  // per-wave offsets within a digit, tile digit totals, their exclusive scan
     uint32_t acc = 0;
-    if (tid < 256)
+    if (tid < nd)
       for (int w = 0; w < SW; ++w) {
         const uint32_t t = wcnt[w][tid];
-        wcnt[w][tid] = acc;
+        wcnt[w][tid] = (uint16_t)acc;
         acc += t;
       }
     uint32_t t;
-    const uint32_t ex = scan_256_of(acc, sh, &t);
-    if (tid < 256) tex[tid] = ex;
+    const uint32_t ex = scan_512_of(acc, sh, &t);
+    if (tid < nd) tex[tid] = ex;
   }
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {
     const uint32_t d = dg[c];
-    if (d > 255u) continue;
+    if (d >= (uint32_t)RS_MAXD) continue;
     const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
     sk[lp] = kk[c];
     sv[lp] = vv[c];
@@ -219,7 +260,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
   const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
   for (uint32_t j = tid; j < m; j += ST) {
     const K k = sk[j];
-    const uint32_t d = (uint32_t)(k >> shift) & 255u;
+    const uint32_t d = (uint32_t)(k >> shift) & mask;
     const uint32_t pos = gofs[d] + (j - tex[d]);
     kout[pos] = k;
     vout[pos] = sv[j];
@@ -357,7 +398,7 @@ __global__ void k_rs_copyback(B2<const K*> k12, B2<const uint32_t*> v12, B2<K*> 
                               B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2, int max_passes) {
   KT();
   const int e = blockIdx.y;
-  const uint32_t p = min(passes_of(*d_nbits2[e]), (uint32_t)max_passes);
+  const uint32_t p = min(rs_plan(*d_nbits2[e]).passes, (uint32_t)max_passes);
   if ((p & 1u) == 0u) return;
   const K* __restrict__ k1 = k12[e];
   const uint32_t* __restrict__ v1 = v12[e];
@@ -380,12 +421,11 @@ void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<con
   const int fast_passes = fast_bits / 8;
   B2<K*> kb[2] = {k0, k1};
   B2<uint32_t*> vb[2] = {v0, v1};
-  for (int p = 0; p < fast_passes; ++p) {
-    const int shift = 8 * p;
+  for (int p = 0; p < fast_passes; ++p) {  // pass p: digit p of the device-side plan (rs_plan)
     const int src = p & 1, dst = src ^ 1;
-    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(kb[src], d_n, d_nbits, shift, s, nb);
-    k_rs_rowscan<<<dim3(256, nbatch), T, 0, st>>>(s, nb, d_nbits, shift);
-    FCCF_LAUNCH("k_rs_scatter", (d_n[0], 2.0 * (sizeof(K) + 4), nbatch > 1 ? d_n[1] : nullptr, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, shift, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
+    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(kb[src], d_n, d_nbits, p, s, nb);
+    k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
+    FCCF_LAUNCH("k_rs_scatter", (d_n[0], 2.0 * (sizeof(K) + 4), nbatch > 1 ? d_n[1] : nullptr, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
   }
   if (fast_passes) {
     const uint32_t g = min(nb * 8u, 2048u);
@@ -556,7 +596,7 @@ __global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<ui
 
 size_t sort_scratch_bytes(uint32_t cap) {
   const size_t nb = rs_blocks(cap) + 1;
-  return sizeof(uint32_t) * (256 * nb + 256 + nb + 1) + 256;
+  return sizeof(uint32_t) * (256 * nb + RS_MAXD + nb + 1) + 256;
 }
 
 SortScratch sort_scratch_carve(void* base, uint32_t cap) {
@@ -564,8 +604,8 @@ SortScratch sort_scratch_carve(void* base, uint32_t cap) {
   uint32_t* p = (uint32_t*)base;
   SortScratch s;
   s.hist = p;
-  s.tot = p + 256 * nb;
-  s.blk = s.tot + 256;
+  s.tot = p + 256 * nb;  // 256 * (rs_blocks + 1) >= RS_MAXD * sort_blocks
+  s.blk = s.tot + RS_MAXD;
   return s;
 }
 
