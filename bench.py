@@ -105,6 +105,9 @@ class _SelftestCtx:
         time.sleep(0.002)
         return np.eye(4, dtype=np.float32), self._St()
 
+    def register(self, src, tar, leaf):
+        return self.register_device(0, 0, 0, 0, leaf)
+
 
 def pmc_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary of the
@@ -212,6 +215,15 @@ def main():
         per.append(time.perf_counter() - a)
     if not args.selftest:
         assert np.array_equal(T1.view(np.uint32), np.asarray(T).view(np.uint32)), "pipelined result differs"
+    # PCIe-inclusive latency: the same registration from host arrays (fccf_register);
+    # informational, never `value`
+    per_host = []
+    for _ in range(min(args.steps, 5)):
+        a = time.perf_counter()
+        T2, _ = ctx.register(src, tar, leaf)
+        per_host.append(time.perf_counter() - a)
+    if not args.selftest:
+        assert np.array_equal(T2.view(np.uint32), np.asarray(T).view(np.uint32)), "host-input result differs"
     roofline = None
     if probe:
         # Probe window right after the timed region, same inputs: every launch of
@@ -252,6 +264,7 @@ def main():
                        "parallelism": f"replicas x{ws}",
                        "pipelined": pipelined},
             "e2e_ms_median": statistics.median(per) * 1e3,  # one registration alone (latency)
+            "e2e_host_input_ms_median": statistics.median(per_host) * 1e3,  # incl. H2D of both clouds
             "K_per_registration": int(st.K),
             "K_pass": int(st.K_pass),
             "graph_captures_last_step": int(st.graph_captures),
