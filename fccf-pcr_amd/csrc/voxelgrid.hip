@@ -43,13 +43,23 @@ __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const
   const uint32_t n = *d_n2[e];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t cnt = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    if (!finite3(x, y, z)) continue;
+  auto add = [&](float x, float y, float z) {
+    if (!finite3(x, y, z)) return;
     mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
     mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
     ++cnt;
+  };
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
+  const uint32_t nq = (((uintptr_t)xyz) & 15u) == 0 ? n / 4 : 0;  // four points per thread, 16-byte loads
+  for (uint32_t qd = gid; qd < nq; qd += gsz) {
+    const float4* v = reinterpret_cast<const float4*>(xyz) + 3 * (size_t)qd;
+    const float4 a = v[0], b = v[1], c = v[2];
+    add(a.x, a.y, a.z);
+    add(a.w, b.x, b.y);
+    add(b.z, b.w, c.x);
+    add(c.y, c.z, c.w);
   }
+  for (uint32_t i = 4 * nq + gid; i < n; i += gsz) add(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
   for (int a = 0; a < 3; ++a) {
     mn[a] = wave_min(mn[a]);
     mx[a] = wave_max(mx[a]);
@@ -191,7 +201,29 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
   uint32_t* __restrict__ keys = keys2[e];
   uint32_t* __restrict__ vals = vals2[e];
   bool bad = false;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
+  // four points per thread: three 16-byte loads, one 16-byte store of keys (and of
+  // vals); the order check reads the next quad's first point
+  const bool al = ((((uintptr_t)xyz) | ((uintptr_t)keys) | ((uintptr_t)vals)) & 15u) == 0;
+  const uint32_t nq = al ? n / 4 : 0;
+  for (uint32_t qd = gid; qd < nq; qd += gsz) {
+    const float4* v = reinterpret_cast<const float4*>(xyz) + 3 * (size_t)qd;
+    const float4 a = v[0], b = v[1], c = v[2];
+    const uint32_t i0 = 4 * qd;
+    uint4 k;
+    k.x = vg_key(q, a.x, a.y, a.z);
+    k.y = vg_key(q, a.w, b.x, b.y);
+    k.z = vg_key(q, b.z, b.w, c.x);
+    k.w = vg_key(q, c.y, c.z, c.w);
+    reinterpret_cast<uint4*>(keys)[qd] = k;
+    if (presorted) {
+      reinterpret_cast<uint4*>(vals)[qd] = make_uint4(i0, i0 + 1, i0 + 2, i0 + 3);
+      bad |= k.x == 0xFFFFFFFFu || k.y == 0xFFFFFFFFu || k.z == 0xFFFFFFFFu || k.w == 0xFFFFFFFFu;
+      bad |= !(k.x < k.y) || !(k.y < k.z) || !(k.z < k.w);
+      if (i0 + 4 < n && !(k.w < vg_key(q, xyz[3 * i0 + 12], xyz[3 * i0 + 13], xyz[3 * i0 + 14]))) bad = true;
+    }
+  }
+  for (uint32_t i = 4 * nq + gid; i < n; i += gsz) {
     const uint32_t key = vg_key(q, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
     keys[i] = key;
     if (presorted) {
