@@ -4,9 +4,12 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "ctx.h"
+#include "host_stages.h"
 #include "kernels.h"
+#include "match.h"
 #include "pipeline.h"
 
 using namespace fccf;
@@ -212,6 +215,149 @@ extern "C" int fccf_stage_centroid(fccf_ctx* c, const float* xyz, int64_t n, flo
 
 extern "C" int fccf_stage_seqsum(fccf_ctx* c, const float* x, int64_t n, float* out) {
   return stage_sum(c, x, n, 1, false, out);
+}
+
+static_assert(sizeof(fccf_plane) == sizeof(MPlane) && sizeof(fccf_base) == sizeof(MBase), "table layouts");
+
+// K5 alone (match.hip) over the b1 range; the same kernels registration runs, without
+// the pinned mailbox (K_pass is counted from the per-test candidate counts here).
+extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
+                                const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2, int b1_lo, int b1_hi,
+                                const fccf_params* params, float* const cand[3], const int64_t cap[3],
+                                int64_t n_cand[3], int64_t* k_pass) {
+  if (!c || !n_cand || nF1 < 0 || nF2 < 0 || nB1 < 0 || nB2 < 0 || nF1 > MAX_PLANES || nF2 > MAX_PLANES ||
+      nB1 > MAX_BASES || nB2 > MAX_BASES || (nF1 && !F1) || (nF2 && !F2) || (nB1 && !B1) || (nB2 && !B2))
+    return FCCF_E_ARG;
+  if (b1_hi < 0) b1_hi = nB1;
+  if (b1_lo < 0 || b1_lo > b1_hi || b1_hi > nB1) return FCCF_E_ARG;
+  // every pair must name planes of its own table: the kernels index F by i1, i2
+  for (int i = 0; i < nB1; ++i)
+    if (B1[i].i1 < 0 || B1[i].i1 >= nF1 || B1[i].i2 < 0 || B1[i].i2 >= nF1) return FCCF_E_ARG;
+  for (int i = 0; i < nB2; ++i)
+    if (B2[i].i1 < 0 || B2[i].i1 >= nF2 || B2[i].i2 < 0 || B2[i].i2 >= nF2) return FCCF_E_ARG;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded(c, [&] {
+    hipStream_t st = c->sb;
+    MatchIn M;
+    std::memset(&M, 0, sizeof M);
+    if (nF1) std::memcpy(M.F1, F1, sizeof(MPlane) * nF1);
+    if (nF2) std::memcpy(M.F2, F2, sizeof(MPlane) * nF2);
+    const int nb = b1_hi - b1_lo;  // the shard: b1-major order keeps each shard's lists contiguous
+    if (nb) std::memcpy(M.B1, B1 + b1_lo, sizeof(MBase) * nb);
+    if (nB2) std::memcpy(M.B2, B2, sizeof(MBase) * nB2);
+    M.nF1 = nF1;
+    M.nF2 = nF2;
+    M.nB1 = nb;
+    M.nB2 = nB2;
+    M.ang_same = P.included_angle_same_threshold;
+    M.third_thr = P.third_plane_threshold;
+    M.third_cut = make_cut(P.third_plane_normal_threshold);
+    const int K = nb * nB2;
+    const size_t per = (size_t)std::max(1, std::max(0, nF1 - 2) * std::max(0, nF2 - 2));
+    const size_t ccap = std::max<size_t>(1, (size_t)K * per);
+    c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + 3 * ccap * (sizeof(MCand) + sizeof(QTd)) +
+                     (1 << 16));
+    c->arena2.reset();
+    MatchIn* dM = c->arena2.take_n<MatchIn>(1);
+    uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
+    int32_t* dtype = c->arena2.take_n<int32_t>(std::max(K, 1));
+    uint32_t* doff = c->arena2.take_n<uint32_t>(std::max(K, 1));
+    uint32_t* dtot = c->arena2.take_n<uint32_t>(4);
+    MCand* dc[3];
+    QTd* dq[3];
+    for (int t = 0; t < 3; ++t) {
+      dc[t] = c->arena2.take_n<MCand>(ccap);
+      dq[t] = c->arena2.take_n<QTd>(ccap);
+    }
+    HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st));
+    match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st, nullptr);
+    HIP_CHECK(hipGetLastError());
+    uint32_t tot[4] = {0, 0, 0, 0};
+    std::vector<uint32_t> cnt((size_t)std::max(K, 1));
+    HIP_CHECK(hipMemcpyAsync(tot, dtot, 16, hipMemcpyDeviceToHost, st));
+    if (K) HIP_CHECK(hipMemcpyAsync(cnt.data(), dcnt, 4 * (size_t)K, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t kp = 0;
+    for (int k = 0; k < K; ++k) kp += cnt[k] > 0;
+    if (k_pass) *k_pass = kp;
+    for (int t = 0; t < 3; ++t) {
+      n_cand[t] = K ? tot[t] : 0;
+      const int64_t nc = std::min<int64_t>(n_cand[t], cand && cap && cand[t] ? cap[t] : 0);
+      if (nc <= 0) continue;
+      std::vector<MCand> v((size_t)nc);
+      HIP_CHECK(hipMemcpyAsync(v.data(), dc[t], sizeof(MCand) * nc, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+      for (int64_t i = 0; i < nc; ++i) {  // [R | t; 0 0 0 1], row-major
+        float* o = cand[t] + 16 * i;
+        for (int r = 0; r < 3; ++r) {
+          std::memcpy(o + 4 * r, v[i].R + 3 * r, 12);
+          o[4 * r + 3] = v[i].t[r];
+        }
+        o[12] = o[13] = o[14] = 0.f;
+        o[15] = 1.f;
+      }
+    }
+  });
+}
+
+// K7 alone (fine.hip): S1's octree bounds replayed, then the batched evaluation.
+extern "C" int fccf_stage_fine_verify(fccf_ctx* c, const float* s1, int64_t n1, const float* s2, int64_t n2,
+                                      const float* T, int E, float voxel, float* scores) {
+  if (!c || !s1 || !s2 || !T || !scores || n1 < 1 || n2 < 1 || E < 1 || E > MAX_EVAL || !(voxel > 0.f) ||
+      (int64_t)E * (n1 + n2) >= ((int64_t)1 << 31))
+    return FCCF_E_ARG;
+  return guarded(c, [&] {
+    hipStream_t st = c->sb;
+    const uint32_t u1 = (uint32_t)n1, u2 = (uint32_t)n2;
+    const size_t nk = (size_t)E * (u1 + u2);
+    const size_t af1 = aggr_floats(u1), af2 = aggr_floats(u2);
+    const size_t need = 12 * ((size_t)u1 + u2) + 4 * af1 + 12 * (size_t)E * u2 + 4 * E * af2 +
+                        sizeof(OctState) * (E + 2) + (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 +
+                        sizeof(m44) * E + 64 + sort_scratch_bytes((uint32_t)nk) + 40 * 256 +
+                        exact_sum_bytes(E, u1 + u2) + 256;
+    c->arena2.ensure(need);
+    c->arena2.reset();
+    Arena& a = c->arena2;
+    float* d1 = a.take_n<float>(3 * (size_t)u1);
+    float* d2 = a.take_n<float>(3 * (size_t)u2);
+    uint32_t* dn1 = a.take_n<uint32_t>(16);
+    float* aggr1 = a.take_n<float>(af1);
+    OctState* st1 = a.take_n<OctState>(1);
+    FineBufs fb;
+    fb.s2t = a.take_n<float>(3 * (size_t)E * u2);
+    fb.aggr2 = a.take_n<float>((size_t)E * af2);
+    fb.state = a.take_n<OctState>(E + 1);
+    fb.k0 = a.take_n<uint64_t>(nk);
+    fb.k1 = a.take_n<uint64_t>(nk);
+    fb.v0 = a.take_n<uint32_t>(nk);
+    fb.v1 = a.take_n<uint32_t>(nk);
+    fb.starts = a.take_n<uint32_t>(nk + 1);
+    fb.term = a.take_n<float>(nk + 1);
+    fb.range = a.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.nseg_e = a.take_n<uint32_t>(2 * MAX_EVAL);
+    fb.similar = a.take_n<float>(MAX_EVAL);
+    fb.all = a.take_n<float>(MAX_EVAL);
+    fb.scal = a.take_n<uint32_t>(16);
+    fb.scores = a.take_n<float>(E);
+    fb.T = a.take_n<m44>(E);
+    fb.ss = sort_scratch_carve(a.take(sort_scratch_bytes((uint32_t)nk)), (uint32_t)nk);
+    fb.xs = exact_sum_carve(a.take(exact_sum_bytes(E, u1 + u2)), E, u1 + u2);
+    HIP_CHECK(hipMemcpyAsync(d1, s1, 12 * (size_t)u1, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d2, s2, 12 * (size_t)u2, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(dn1, &u1, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(fb.T, T, sizeof(m44) * E, hipMemcpyHostToDevice, st));
+    octree_replay(d1, dn1, u1, (double)voxel, aggr1, st1, st);
+    fine_verify_batch(d1, u1, st1, d2, u2, E, (double)voxel, fb, st, nullptr);
+    HIP_CHECK(hipGetLastError());
+    uint32_t err = 0;
+    HIP_CHECK(hipMemcpyAsync(scores, fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&err, fb.scal + 7, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
+  });
 }
 
 extern "C" int fccf_device_upload(fccf_ctx* c, const float* xyz, int64_t n, float** d) {

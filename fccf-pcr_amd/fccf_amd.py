@@ -81,6 +81,10 @@ _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ct
 _sig("fccf_stage_downsample_presorted", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
 _sig("fccf_stage_centroid", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_stage_seqsum", ctypes.c_int, _P, _P, _I64, _P)
+_sig("fccf_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
+     ctypes.c_int, ctypes.c_int, ctypes.POINTER(Params), ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+     ctypes.POINTER(_I64))
+_sig("fccf_stage_fine_verify", ctypes.c_int, _P, _P, _I64, _P, _I64, _P, ctypes.c_int, ctypes.c_float, _P)
 _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
 _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
      ctypes.POINTER(ctypes.c_double))
@@ -92,6 +96,25 @@ _sig("fccf_free", None, _P)
 _sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
      ctypes.c_double, _P)
 _sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P, _P, _P)
+
+
+# fccf_plane {float c[3], n[3], fps; int32 nvox} and fccf_base {int32 i1, i2; float angle; int32 type}
+PLANE_DTYPE = np.dtype([("c", "<f4", 3), ("n", "<f4", 3), ("fps", "<f4"), ("nvox", "<i4")])
+BASE_DTYPE = np.dtype([("i1", "<i4"), ("i2", "<i4"), ("angle", "<f4"), ("type", "<i4")])
+
+
+def planes_from_dump(a) -> np.ndarray:
+    """fccf_plane records from a "planesN" dump (8 floats per plane, nvox as float)."""
+    a = np.asarray(a, np.float32).reshape(-1, 8)
+    out = np.zeros(a.shape[0], PLANE_DTYPE)
+    out["c"], out["n"], out["fps"], out["nvox"] = a[:, 0:3], a[:, 3:6], a[:, 6], a[:, 7].astype(np.int32)
+    return out
+
+
+def bases_from_dump(a) -> np.ndarray:
+    """fccf_base records from a "basesN" dump (i1, i2, angle bits, type as int32)."""
+    a = np.ascontiguousarray(np.asarray(a, np.int32).reshape(-1, 4))
+    return a.view(BASE_DTYPE).reshape(-1).copy()
 
 
 class FCCFError(RuntimeError):
@@ -206,6 +229,32 @@ class Ctx:
         _check(f(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data, ctypes.byref(m)),
                "fccf_stage_downsample", self._h)
         return out[: m.value].copy()
+
+    def match(self, F1, B1, F2, B2, b1_lo: int = 0, b1_hi: int = -1, params: Params | None = None):
+        """Coplane-pair correspondence search + computer_transform (FCCF.cpp:1410-1428,
+        :841-1018) on the GPU for source pairs [b1_lo, b1_hi).  F*: PLANE_DTYPE arrays,
+        B*: BASE_DTYPE arrays.  Returns ([cand_t float32[n_t, 4, 4] for t in 0..2], k_pass)."""
+        F1, F2 = np.ascontiguousarray(F1, PLANE_DTYPE), np.ascontiguousarray(F2, PLANE_DTYPE)
+        B1, B2 = np.ascontiguousarray(B1, BASE_DTYPE), np.ascontiguousarray(B2, BASE_DTYPE)
+        p = params if params is not None else default_params()
+        ncand, kp = (_I64 * 3)(), _I64()
+        args = [self._h, F1.ctypes.data, len(F1), B1.ctypes.data, len(B1), F2.ctypes.data, len(F2),
+                B2.ctypes.data, len(B2), int(b1_lo), int(b1_hi), ctypes.byref(p)]
+        _check(_lib.fccf_stage_match(*args, None, None, ncand, ctypes.byref(kp)), "fccf_stage_match", self._h)
+        out = [np.zeros((max(int(n), 1), 4, 4), np.float32) for n in ncand]
+        ptrs = (_P * 3)(*[o.ctypes.data for o in out])
+        caps = (_I64 * 3)(*[int(n) for n in ncand])
+        _check(_lib.fccf_stage_match(*args, ptrs, caps, ncand, ctypes.byref(kp)), "fccf_stage_match", self._h)
+        return [o[: int(n)] for o, n in zip(out, ncand)], kp.value
+
+    def fine_verify(self, s1, s2, T, voxel: float = 0.5):
+        """fine_verify (FCCF.cpp:785-839) of E <= 16 transforms T[E, 4, 4]: float32[E] scores."""
+        a, b = _f32(s1), _f32(s2)
+        T = np.ascontiguousarray(np.asarray(T, np.float32).reshape(-1, 16))
+        sc = np.zeros(max(T.shape[0], 1), np.float32)
+        _check(_lib.fccf_stage_fine_verify(self._h, a.ctypes.data, a.shape[0], b.ctypes.data, b.shape[0], T.ctypes.data,
+                                           T.shape[0], float(voxel), sc.ctypes.data), "fccf_stage_fine_verify", self._h)
+        return sc[: T.shape[0]]
 
     def set_probe(self, kernel):
         """Time every launch of `kernel` with HIP events (None = off); resets totals."""

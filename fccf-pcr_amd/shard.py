@@ -1,0 +1,90 @@
+"""Sharded coplane-pair correspondence search (SURVEY.md §8(e), row "K5").
+
+The reference runs the search as one loop nest, source pairs outer, target pairs
+inner (FCCF.cpp:1410-1428), and appends every candidate transform to T_vec[type] in
+that order.  Here the source pairs B1 are split into contiguous blocks, one per rank
+(`shard_range`).  Every rank runs the GPU search (`Ctx.match`, i.e. fccf_stage_match)
+for its block against all target pairs.  The per-type candidate lists are then
+all-gathered and concatenated in rank order.  Because the loop order is b1-major, the
+result equals the unsharded list bit for bit.
+
+Plane extraction, growth and selection stay replicated on every rank (they are
+sequential and tiny), so F1, B1, F2 and B2 are already identical everywhere. The
+only exchange is the candidate gather: a variable-length all-gather of <= a few MB.
+It runs on the process group's CPU backend (gloo): libfccf owns the GPU through the
+system HIP runtime, and torch's own ROCm runtime cannot share the device in the same
+process.
+
+`gather` is injectable so the exchange logic can be tested without a GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block [lo, hi) of n items for `rank`: sizes differ by at most one,
+    lower ranks take the larger blocks, ranks past n get empty blocks."""
+    if world < 1 or not 0 <= rank < world or n < 0:
+        raise ValueError(f"bad shard: n={n} rank={rank} world={world}")
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def torch_gather(group=None):
+    """All-gather of one float32 array of any length per rank over torch.distributed
+    (CPU tensors: gloo).  Returns the arrays in rank order."""
+    import torch
+    import torch.distributed as dist
+
+    def gather(a: np.ndarray) -> list[np.ndarray]:
+        world = dist.get_world_size(group)
+        n = torch.tensor([a.size], dtype=torch.int64)
+        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(ns, n, group=group)
+        sizes = [int(x.item()) for x in ns]
+        cap = max(max(sizes), 1)
+        buf = torch.zeros(cap, dtype=torch.float32)
+        buf[: a.size] = torch.from_numpy(np.ascontiguousarray(a, np.float32).reshape(-1))
+        outs = [torch.zeros(cap, dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(outs, buf, group=group)
+        return [o[:s].numpy().copy() for o, s in zip(outs, sizes)]
+
+    return gather
+
+
+def pack(cands: list[np.ndarray], k_pass: int) -> np.ndarray:
+    """One float32 message per rank: [n0, n1, n2, k_pass] as exact integer floats
+    (all < 2^24), then the three candidate lists (16 floats per candidate)."""
+    head = np.array([len(c) for c in cands] + [k_pass], np.float64)
+    if head.max(initial=0) >= 2 ** 24:
+        raise ValueError("candidate count past the exact float32 range")
+    return np.concatenate([head.astype(np.float32)] + [np.asarray(c, np.float32).reshape(-1) for c in cands])
+
+
+def unpack(msg: np.ndarray) -> tuple[list[np.ndarray], int]:
+    n = [int(x) for x in msg[:3]]
+    k_pass = int(msg[3])
+    out, o = [], 4
+    for t in range(3):
+        out.append(msg[o: o + 16 * n[t]].reshape(n[t], 4, 4))
+        o += 16 * n[t]
+    if o != msg.size:
+        raise ValueError("malformed candidate message")
+    return out, k_pass
+
+
+def combine(msgs: list[np.ndarray]) -> tuple[list[np.ndarray], int]:
+    """Rank-ordered concatenation of every rank's lists = the reference loop order."""
+    parts = [unpack(m) for m in msgs]
+    cands = [np.concatenate([p[0][t] for p in parts]).reshape(-1, 4, 4) for t in range(3)]
+    return cands, sum(p[1] for p in parts)
+
+
+def match_sharded(ctx, F1, B1, F2, B2, rank: int, world: int, gather, params=None):
+    """This rank's block of the search on its GPU, then the ordered gather.
+    Every rank returns the full ([cand_t], k_pass), identical to ctx.match(F1, B1, F2, B2)."""
+    lo, hi = shard_range(len(B1), rank, world)
+    cands, k_pass = ctx.match(F1, B1, F2, B2, lo, hi, params)
+    return combine(gather(pack(cands, k_pass)))

@@ -142,6 +142,36 @@ int fccf_stage_centroid(fccf_ctx* ctx, const float* xyz, int64_t n, float out[4]
  * order of fine_verify's similar_num (FCCF.cpp:830-835); bit-exact. */
 int fccf_stage_seqsum(fccf_ctx* ctx, const float* x, int64_t n, float* out);
 
+/* A selected plane (facenode summary, FCCF.cpp:47-58) and a coplane pair
+ * (face_base + its roughness type, FCCF.cpp:60-65, :454-461), as the matching stage
+ * reads them.  type: 0 smooth/smooth, 1 rough/rough, 2 mixed, negative = untyped
+ * (NaN roughness: never matches). */
+typedef struct fccf_plane { float c[3], n[3]; float fps; int32_t nvox; } fccf_plane;
+typedef struct fccf_base { int32_t i1, i2; float angle; int32_t type; } fccf_base;
+
+/* Stage export: the coplane-pair correspondence search (FCCF.cpp:1410-1428) and
+ * computer_transform (:841-1018) on the GPU, for source pairs b1 in [b1_lo, b1_hi)
+ * against all nB2 target pairs (b1_hi < 0 means nB1).  F1/B1 are the driver
+ * source's planes and pairs, F2/B2 the target's (<= 17 planes, <= 136 pairs each).
+ * Candidates go to cand[t] (type t = 0..2) as row-major 4x4 matrices, 16 floats each,
+ * in the reference's (b1, b2, third plane) loop order; at most cap[t] are copied and
+ * n_cand[t] receives the full count.  *k_pass = tests with >= 1 candidate.
+ * Sharding: splitting [0, nB1) into contiguous ranges and
+ * concatenating each type's lists in range order gives the unsharded lists exactly.
+ * Uses included_angle_same_threshold, third_plane_threshold and
+ * third_plane_normal_threshold of params (NULL: defaults). */
+int fccf_stage_match(fccf_ctx* ctx, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
+                     const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2, int b1_lo, int b1_hi,
+                     const fccf_params* params, float* const cand[3], const int64_t cap[3],
+                     int64_t n_cand[3], int64_t* k_pass);
+
+/* Stage export: fine_verify (FCCF.cpp:785-839) of E <= 16 transforms on the GPU:
+ * scores[e] = score of S2 transformed by T_e against S1 over the fine_verify_voxel
+ * octree (the voxel argument).  s1/s2: residual clouds (xyz float32, n1, n2 >= 1);
+ * T_rowmajor: 16*E floats.  Bit-identical to the sequential reference arithmetic. */
+int fccf_stage_fine_verify(fccf_ctx* ctx, const float* s1_xyz, int64_t n1, const float* s2_xyz, int64_t n2,
+                           const float* T_rowmajor, int E, float voxel, float* scores);
+
 /* Roofline probe (bench.py): time every launch of one kernel (by name, e.g.
  * "k_vg_centroid") with HIP events on its own stream, also inside the captured
  * graphs, and accumulate its algorithmic bytes ("Measurement").
