@@ -217,6 +217,90 @@ extern "C" int fccf_stage_seqsum(fccf_ctx* c, const float* x, int64_t n, float* 
   return stage_sum(c, x, n, 1, false, out);
 }
 
+static_assert(sizeof(fccf_voxel) == sizeof(VoxRec) && sizeof(fccf_plane) == sizeof(Plane) &&
+                  sizeof(fccf_base) == sizeof(Base), "record layouts");
+
+// K2/K3 of one cloud (facefit.hip), as the pipeline runs them for each cloud of a pair.
+extern "C" int fccf_stage_voxel_planes(fccf_ctx* c, const float* xyz, int64_t n, const fccf_params* params,
+                                       fccf_voxel* planar, int64_t cap_planar, int64_t* n_planar, float* resid,
+                                       int64_t cap_resid, int64_t* n_resid, float centroid[4]) {
+  if (!c || (!xyz && n) || n < 0 || n > (int64_t)0x7FFFFFFF || !n_planar || !n_resid || cap_planar < 0 ||
+      cap_resid < 0 || (cap_planar && !planar) || (cap_resid && !resid))
+    return FCCF_E_ARG;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  if (n == 0) {  // no leaves: nothing to launch (compute3DCentroid of an empty cloud: zeros)
+    *n_planar = *n_resid = 0;
+    if (centroid) centroid[0] = centroid[1] = centroid[2] = 0.f, centroid[3] = 1.f;
+    return FCCF_OK;
+  }
+  return guarded(c, [&] {
+    hipStream_t st = c->sb;
+    const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
+    c->arena2.ensure(12 * (size_t)cap * 2 + sizeof(VoxRec) * (size_t)cap + face_bufs_bytes(cap) +
+                     exact_sum_bytes(3, cap) + (1 << 16));
+    c->arena2.reset();
+    float* d_in = c->arena2.take_n<float>(3 * (size_t)cap);
+    float* d_res = c->arena2.take_n<float>(3 * (size_t)cap);
+    VoxRec* d_pl = c->arena2.take_n<VoxRec>(cap);
+    uint32_t* d_n = c->arena2.take_n<uint32_t>(16);
+    float* d_cen = c->arena2.take_n<float>(4);
+    XsBufs xs = exact_sum_carve(c->arena2.take(exact_sum_bytes(3, cap)), 3, cap);
+    FaceBufs fb = face_bufs_carve(c->arena2, cap);
+    fb.centroid = d_cen;
+    const uint32_t hn = (uint32_t)n;
+    if (n) HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(d_n, &hn, 4, hipMemcpyHostToDevice, st));
+    exact_sum(d_in, 3, 3, nullptr, d_n, 1, d_cen, true, xs, st);  // compute3DCentroid (:473)
+    face_voxels_prepare(B2<const float*>(d_in), B2<const uint32_t*>(d_n), cap, (double)P.face_voxel_size,
+                        B2<FaceBufs>(fb), st, 1);
+    face_voxels_fit(B2<const uint32_t*>(d_n), cap, P.voxel_point_threshold, P.curvature_threshold, B2<float*>(d_res),
+                    B2<FaceBufs>(fb), st, 1);
+    face_voxels_orient(cap, B2<VoxRec*>(d_pl), B2<FaceBufs>(fb), st, 1);
+    HIP_CHECK(hipGetLastError());
+    uint32_t sc[4] = {0, 0, 0, 0};
+    float cen[3] = {0.f, 0.f, 0.f};
+    HIP_CHECK(hipMemcpyAsync(sc, fb.nleaf, 16, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(cen, d_cen, 12, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    *n_planar = n ? sc[2] : 0;
+    *n_resid = n ? sc[3] : 0;
+    const int64_t np = std::min(*n_planar, cap_planar), nr = std::min(*n_resid, cap_resid);
+    if (np > 0) HIP_CHECK(hipMemcpyAsync(planar, d_pl, sizeof(VoxRec) * np, hipMemcpyDeviceToHost, st));
+    if (nr > 0) HIP_CHECK(hipMemcpyAsync(resid, d_res, 12 * nr, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (centroid) {
+      std::memcpy(centroid, cen, 12);
+      centroid[3] = 1.f;
+    }
+  });
+}
+
+// Host stages (host_stages.cpp), exactly as the pipeline runs them per cloud.
+extern "C" int fccf_stage_grow(fccf_ctx* c, const fccf_voxel* vox, int64_t nv, int side, const fccf_params* params,
+                               fccf_plane* planes, int cap_planes, int* n_planes, double* theta, fccf_base* bases,
+                               int cap_bases, int* n_bases) {
+  if (!c || (!vox && nv) || nv < 0 || nv > (int64_t)0x7FFFFFFF || (side != 1 && side != 2) || !n_planes ||
+      !n_bases || cap_planes < 0 || cap_bases < 0 || (cap_planes && !planes) || (cap_bases && !bases))
+    return FCCF_E_ARG;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded(c, [&] {
+    std::vector<VoxRec> v((size_t)nv);
+    if (nv) std::memcpy(v.data(), vox, sizeof(VoxRec) * (size_t)nv);
+    const GrowOut g = grow_and_select(v.data(), (int)nv, P);
+    const std::vector<Base> b = select_base(g.planes, g.theta, P, side);
+    *n_planes = (int)g.planes.size();
+    *n_bases = (int)b.size();
+    const int np = std::min(*n_planes, cap_planes), nb = std::min(*n_bases, cap_bases);
+    if (np > 0) std::memcpy(planes, g.planes.data(), sizeof(Plane) * np);
+    if (np > 0 && theta) std::memcpy(theta, g.theta.data(), sizeof(double) * np);
+    if (nb > 0) std::memcpy(bases, b.data(), sizeof(Base) * nb);
+  });
+}
+
 static_assert(sizeof(fccf_plane) == sizeof(MPlane) && sizeof(fccf_base) == sizeof(MBase), "table layouts");
 
 // K5 alone (match.hip) over the b1 range; the same kernels registration runs, without

@@ -180,28 +180,7 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
   w.ds1f = a.take_n<float>(3 * (size_t)cap);
   w.ds2 = a.take_n<float>(3 * (size_t)cap);
   w.vg = voxel_grid_carve(a, cap);
-  FaceBufs& f = w.fb;
-  f.c0 = a.take_n<uint64_t>(cap);
-  f.c1 = a.take_n<uint64_t>(cap);
-  f.v0 = a.take_n<uint32_t>(cap);
-  f.v1 = a.take_n<uint32_t>(cap);
-  f.starts = a.take_n<uint32_t>((size_t)cap + 1);
-  f.aggr = a.take_n<float>(aggr_floats(cap));
-  f.oct = a.take_n<OctState>(1);
-  f.centroid = nullptr;  // set by clouds_enqueue: both centroids share one buffer
-  f.recs = a.take_n<VoxRec>(cap);
-  f.flag_planar = a.take_n<uint32_t>(cap);
-  f.resid_cnt = a.take_n<uint32_t>(cap);
-  f.planar_off = a.take_n<uint32_t>(cap);
-  f.resid_off = a.take_n<uint32_t>(cap);
-  f.sp = a.take_n<float>(3 * (size_t)cap);
-  f.seg_of = a.take_n<uint32_t>(cap);
-  uint32_t* s = a.take_n<uint32_t>(16);
-  f.nleaf = s;
-  f.nbits = s + 1;
-  f.nplanar = s + 2;
-  f.nresid = s + 3;
-  f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
+  w.fb = face_bufs_carve(a, cap);
   w.planar = a.take_n<VoxRec>(cap);
   w.resid = a.take_n<float>(3 * (size_t)cap);
   w.faggr = a.take_n<float>(aggr_floats(cap));

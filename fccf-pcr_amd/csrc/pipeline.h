@@ -24,6 +24,40 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
   return b;
 }
 
+// Device buffers of the 1 m face-voxel stage of one cloud (K2/K3); centroid is left
+// null for the caller to point at its compute3DCentroid output.
+inline size_t face_bufs_bytes(uint32_t cap) {
+  const size_t N = cap;
+  return 2 * 8 * N + 2 * 4 * N + 4 * (N + 1) + 4 * aggr_floats(cap) + 256 + sizeof(VoxRec) * N + 4 * 4 * N + 64 +
+         12 * N + 4 * N + sort_scratch_bytes(cap) + 24 * 256;
+}
+
+inline FaceBufs face_bufs_carve(Arena& a, uint32_t cap) {
+  FaceBufs f;
+  f.c0 = a.take_n<uint64_t>(cap);
+  f.c1 = a.take_n<uint64_t>(cap);
+  f.v0 = a.take_n<uint32_t>(cap);
+  f.v1 = a.take_n<uint32_t>(cap);
+  f.starts = a.take_n<uint32_t>((size_t)cap + 1);
+  f.aggr = a.take_n<float>(aggr_floats(cap));
+  f.oct = a.take_n<OctState>(1);
+  f.centroid = nullptr;
+  f.recs = a.take_n<VoxRec>(cap);
+  f.flag_planar = a.take_n<uint32_t>(cap);
+  f.resid_cnt = a.take_n<uint32_t>(cap);
+  f.planar_off = a.take_n<uint32_t>(cap);
+  f.resid_off = a.take_n<uint32_t>(cap);
+  f.sp = a.take_n<float>(3 * (size_t)cap);
+  f.seg_of = a.take_n<uint32_t>(cap);
+  uint32_t* s = a.take_n<uint32_t>(16);
+  f.nleaf = s;
+  f.nbits = s + 1;
+  f.nplanar = s + 2;
+  f.nresid = s + 3;
+  f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
+  return f;
+}
+
 // Releases the per-CloudSet pipeline state (fccf_ctx_destroy).
 void pipeline_release(fccf_ctx* c);
 

@@ -81,6 +81,10 @@ _sig("fccf_stage_downsample", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ct
 _sig("fccf_stage_downsample_presorted", ctypes.c_int, _P, _P, _I64, ctypes.c_float, _P, ctypes.POINTER(_I64))
 _sig("fccf_stage_centroid", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_stage_seqsum", ctypes.c_int, _P, _P, _I64, _P)
+_sig("fccf_stage_voxel_planes", ctypes.c_int, _P, _P, _I64, ctypes.POINTER(Params), _P, _I64, ctypes.POINTER(_I64), _P,
+     _I64, ctypes.POINTER(_I64), _P)
+_sig("fccf_stage_grow", ctypes.c_int, _P, _P, _I64, ctypes.c_int, ctypes.POINTER(Params), _P, ctypes.c_int,
+     ctypes.POINTER(ctypes.c_int), _P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_int))
 _sig("fccf_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
      ctypes.c_int, ctypes.c_int, ctypes.POINTER(Params), ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
      ctypes.POINTER(_I64))
@@ -98,6 +102,8 @@ _sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, c
 _sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P, _P, _P)
 
 
+# fccf_voxel {float c[3], n[3]; int32 count; float curvature}
+VOXEL_DTYPE = np.dtype([("c", "<f4", 3), ("n", "<f4", 3), ("count", "<i4"), ("curvature", "<f4")])
 # fccf_plane {float c[3], n[3], fps; int32 nvox} and fccf_base {int32 i1, i2; float angle; int32 type}
 PLANE_DTYPE = np.dtype([("c", "<f4", 3), ("n", "<f4", 3), ("fps", "<f4"), ("nvox", "<i4")])
 BASE_DTYPE = np.dtype([("i1", "<i4"), ("i2", "<i4"), ("angle", "<f4"), ("type", "<i4")])
@@ -229,6 +235,33 @@ class Ctx:
         _check(f(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data, ctypes.byref(m)),
                "fccf_stage_downsample", self._h)
         return out[: m.value].copy()
+
+    def voxel_planes(self, xyz, params: Params | None = None):
+        """face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled cloud on the GPU.
+        Returns (planar VOXEL_DTYPE[nv], residual float32[nr, 3], centroid float32[4])."""
+        a = _f32(xyz)
+        p = params if params is not None else default_params()
+        cap = max(a.shape[0], 1)
+        vox = np.zeros(cap, VOXEL_DTYPE)
+        res = np.zeros((cap, 3), np.float32)
+        cen = np.zeros(4, np.float32)
+        nv, nr = _I64(), _I64()
+        _check(_lib.fccf_stage_voxel_planes(self._h, a.ctypes.data, a.shape[0], ctypes.byref(p), vox.ctypes.data, cap,
+                                            ctypes.byref(nv), res.ctypes.data, cap, ctypes.byref(nr), cen.ctypes.data),
+               "fccf_stage_voxel_planes", self._h)
+        return vox[: nv.value].copy(), res[: nr.value].copy(), cen
+
+    def grow(self, vox, side: int, params: Params | None = None):
+        """Region growing, plane selection and select_base (FCCF.cpp:536-677, :429-468).
+        side 1 = driver source, 2 = target.  Returns (PLANE_DTYPE[F], float64 theta[F], BASE_DTYPE[B])."""
+        v = np.ascontiguousarray(vox, VOXEL_DTYPE)
+        p = params if params is not None else default_params()
+        planes, theta, bases = np.zeros(64, PLANE_DTYPE), np.zeros(64, np.float64), np.zeros(2080, BASE_DTYPE)
+        nF, nB = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.fccf_stage_grow(self._h, v.ctypes.data, len(v), int(side), ctypes.byref(p), planes.ctypes.data,
+                                    len(planes), ctypes.byref(nF), theta.ctypes.data, bases.ctypes.data, len(bases),
+                                    ctypes.byref(nB)), "fccf_stage_grow", self._h)
+        return planes[: nF.value].copy(), theta[: nF.value].copy(), bases[: nB.value].copy()
 
     def match(self, F1, B1, F2, B2, b1_lo: int = 0, b1_hi: int = -1, params: Params | None = None):
         """Coplane-pair correspondence search + computer_transform (FCCF.cpp:1410-1428,

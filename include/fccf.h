@@ -142,12 +142,37 @@ int fccf_stage_centroid(fccf_ctx* ctx, const float* xyz, int64_t n, float out[4]
  * order of fine_verify's similar_num (FCCF.cpp:830-835); bit-exact. */
 int fccf_stage_seqsum(fccf_ctx* ctx, const float* x, int64_t n, float* out);
 
+/* One planar 1 m voxel (FCCF.cpp:500-534): leaf centroid, normal oriented towards the
+ * cloud centroid, point count; curvature is the leaf's eigen33 curvature. */
+typedef struct fccf_voxel { float c[3], n[3]; int32_t count; float curvature; } fccf_voxel;
+
+/* Stage export: face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled
+ * cloud on the GPU: compute3DCentroid, the face_voxel_size octree anchored at the
+ * first point, the per-leaf plane fit and the planar / residual split.  planar
+ * receives the planar voxels in octree (Morton) order, resid_xyz the residual points
+ * (leaf order); at most cap_* entries are copied, n_* receive the full counts.
+ * centroid (may be NULL) receives (cx, cy, cz, 1).  Uses face_voxel_size,
+ * voxel_point_threshold and curvature_threshold of params (NULL: defaults). */
+int fccf_stage_voxel_planes(fccf_ctx* ctx, const float* xyz, int64_t n, const fccf_params* params,
+                            fccf_voxel* planar, int64_t cap_planar, int64_t* n_planar, float* resid_xyz,
+                            int64_t cap_resid, int64_t* n_resid, float centroid[4]);
+
 /* A selected plane (facenode summary, FCCF.cpp:47-58) and a coplane pair
  * (face_base + its roughness type, FCCF.cpp:60-65, :454-461), as the matching stage
  * reads them.  type: 0 smooth/smooth, 1 rough/rough, 2 mixed, negative = untyped
  * (NaN roughness: never matches). */
 typedef struct fccf_plane { float c[3], n[3]; float fps; int32_t nvox; } fccf_plane;
 typedef struct fccf_base { int32_t i1, i2; float angle; int32_t type; } fccf_base;
+
+/* Stage export: region growing (FCCF.cpp:536-648), range_face + plane selection
+ * (:409-427, :650-677) and select_base (:429-468) of one cloud's planar voxels
+ * (host stage; ctx supplies only the error slot).  side = 1 for the driver source,
+ * 2 for the target (the untyped sentinel differs, App. B Q5).  planes (<= 17),
+ * theta (roughness per plane, may be NULL) and bases (<= 136): at most cap_* are
+ * copied, n_* receive the full counts. */
+int fccf_stage_grow(fccf_ctx* ctx, const fccf_voxel* vox, int64_t nv, int side, const fccf_params* params,
+                    fccf_plane* planes, int cap_planes, int* n_planes, double* theta, fccf_base* bases,
+                    int cap_bases, int* n_bases);
 
 /* Stage export: the coplane-pair correspondence search (FCCF.cpp:1410-1428) and
  * computer_transform (:841-1018) on the GPU, for source pairs b1 in [b1_lo, b1_hi)

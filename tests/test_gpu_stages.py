@@ -114,3 +114,58 @@ def test_match_sharded_two_ranks_gloo(tmp_path, oracle, fccf):
     for ty in range(3):
         np.testing.assert_array_equal(bits(out[f"cand{ty}"]), bits(run.get(f"cand{ty}").reshape(-1, 4, 4)))
     assert json.loads(str(out["meta"]))["world"] == 2
+
+
+def voxels_from_dump(fccf, a):
+    a = np.asarray(a, np.float32).reshape(-1, 8)
+    v = np.zeros(len(a), fccf.VOXEL_DTYPE)
+    v["c"], v["n"], v["count"] = a[:, 0:3], a[:, 3:6], a[:, 6].astype(np.int32)
+    return v
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_voxel_planes_stage_bit_exact(ctx, case, fccf, k):
+    run, _ = case
+    vox, res, cen = ctx.voxel_planes(run.get(f"ds{k}").reshape(-1, 3))
+    ref = run.get(f"vox{k}").reshape(-1, 8)
+    assert len(vox) == len(ref) > 0
+    np.testing.assert_array_equal(bits(vox["c"]), bits(ref[:, 0:3]))
+    np.testing.assert_array_equal(bits(vox["n"]), bits(ref[:, 3:6]))
+    np.testing.assert_array_equal(vox["count"], ref[:, 6].astype(np.int32))
+    np.testing.assert_array_equal(bits(res), bits(run.get(f"res{k}").reshape(-1, 3)))
+    np.testing.assert_array_equal(bits(cen), bits(run.get(f"centroid{k}")))
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_grow_stage_bit_exact(ctx, case, fccf, k):
+    run, _ = case
+    planes, theta, bases = ctx.grow(voxels_from_dump(fccf, run.get(f"vox{k}")), k)
+    ref_p = fccf.planes_from_dump(run.get(f"planes{k}"))
+    assert len(planes) == len(ref_p) > 0
+    np.testing.assert_array_equal(planes.view(np.uint8), ref_p.view(np.uint8))
+    np.testing.assert_array_equal(theta.view(np.uint64), run.get(f"theta{k}", np.float64).view(np.uint64))
+    np.testing.assert_array_equal(bases.view(np.uint8),
+                                  fccf.bases_from_dump(run.get(f"bases{k}", np.int32)).view(np.uint8))
+
+
+def test_stage_chain_equals_registration(ctx, case, fccf):
+    """ds -> voxel_planes -> grow -> match through the stage exports alone reproduces
+    the registration's candidate lists."""
+    run, _ = case
+    tabs = []
+    for k in (1, 2):
+        vox, _, _ = ctx.voxel_planes(run.get(f"ds{k}").reshape(-1, 3))
+        planes, _, bases = ctx.grow(vox, k)
+        tabs += [planes, bases]
+    cands, _ = ctx.match(*tabs)
+    for ty in range(3):
+        np.testing.assert_array_equal(bits(cands[ty]), bits(run.get(f"cand{ty}").reshape(-1, 4, 4)))
+
+
+def test_voxel_planes_and_grow_edges(ctx, fccf):
+    vox, res, cen = ctx.voxel_planes(np.zeros((0, 3), np.float32))
+    assert len(vox) == 0 and len(res) == 0
+    planes, theta, bases = ctx.grow(vox, 1)
+    assert len(planes) == 0 and len(bases) == 0
+    with pytest.raises(fccf.FCCFError):
+        ctx.grow(vox, 3)
