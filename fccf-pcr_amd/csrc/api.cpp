@@ -387,6 +387,34 @@ extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, cons
   });
 }
 
+extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int cluster_num,
+                                  const fccf_params* params, float* fine, int64_t cap, int64_t* n_fine,
+                                  int64_t* n_clusters) {
+  if (!c || (!cand && n) || n < 0 || n > (int64_t)0x7FFFFFFF || cap < 0 || (cap && !fine) || !n_fine)
+    return FCCF_E_ARG;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded(c, [&] {
+    std::vector<QT> in((size_t)n), out;
+    for (int64_t i = 0; i < n; ++i) {
+      m44 T;
+      std::memcpy(T.m, cand + 16 * i, sizeof T.m);
+      in[i] = qt_from_T(T);
+      in[i].alloc = 0;
+    }
+    int64_t ncl = 0;
+    transform_cluster(in, out, cluster_num, P, &ncl, &c->pool, nullptr);
+    *n_fine = (int64_t)out.size();
+    if (n_clusters) *n_clusters = ncl;
+    for (int64_t i = 0; i < std::min(*n_fine, cap); ++i) {
+      const QT& q = out[i];
+      const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
+      std::memcpy(fine + 8 * i, a, sizeof a);
+    }
+  });
+}
+
 // K7 alone (fine.hip): S1's octree bounds replayed, then the batched evaluation.
 extern "C" int fccf_stage_fine_verify(fccf_ctx* c, const float* s1, int64_t n1, const float* s2, int64_t n2,
                                       const float* T, int E, float voxel, float* scores) {

@@ -88,6 +88,8 @@ _sig("fccf_stage_grow", ctypes.c_int, _P, _P, _I64, ctypes.c_int, ctypes.POINTER
 _sig("fccf_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
      ctypes.c_int, ctypes.c_int, ctypes.POINTER(Params), ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
      ctypes.POINTER(_I64))
+_sig("fccf_stage_cluster", ctypes.c_int, _P, _P, _I64, ctypes.c_int, ctypes.POINTER(Params), _P, _I64,
+     ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("fccf_stage_fine_verify", ctypes.c_int, _P, _P, _I64, _P, _I64, _P, ctypes.c_int, ctypes.c_float, _P)
 _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
 _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
@@ -279,6 +281,20 @@ class Ctx:
         caps = (_I64 * 3)(*[int(n) for n in ncand])
         _check(_lib.fccf_stage_match(*args, ptrs, caps, ncand, ctypes.byref(kp)), "fccf_stage_match", self._h)
         return [o[: int(n)] for o, n in zip(out, ncand)], kp.value
+
+    def cluster(self, cand, cluster_num: int, params: Params | None = None):
+        """transform_cluster (FCCF.cpp:1040-1231) of one type's candidates (float32[n, 4, 4]).
+        Returns (fused float32[m, 8] = qw qx qy qz tx ty tz allocated, clusters formed)."""
+        a = np.ascontiguousarray(np.asarray(cand, np.float32).reshape(-1, 16))
+        p = params if params is not None else default_params()
+        nf, ncl = _I64(), _I64()
+        _check(_lib.fccf_stage_cluster(self._h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p), None, 0,
+                                       ctypes.byref(nf), ctypes.byref(ncl)), "fccf_stage_cluster", self._h)
+        out = np.zeros((max(nf.value, 1), 8), np.float32)
+        _check(_lib.fccf_stage_cluster(self._h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p),
+                                       out.ctypes.data, nf.value, ctypes.byref(nf), ctypes.byref(ncl)),
+               "fccf_stage_cluster", self._h)
+        return out[: nf.value], ncl.value
 
     def fine_verify(self, s1, s2, T, voxel: float = 0.5):
         """fine_verify (FCCF.cpp:785-839) of E <= 16 transforms T[E, 4, 4]: float32[E] scores."""

@@ -190,6 +190,17 @@ int fccf_stage_match(fccf_ctx* ctx, const fccf_plane* F1, int nF1, const fccf_ba
                      const fccf_params* params, float* const cand[3], const int64_t cap[3],
                      int64_t n_cand[3], int64_t* k_pass);
 
+/* Stage export: the quaternion/translation records (FCCF.cpp:1437-1465) and
+ * transform_cluster (:1040-1231, with range_cluster :1020-1038 and average_normal
+ * :325-367) of one candidate type's list (host stage).  cand: n row-major 4x4
+ * matrices in list order, as fccf_stage_match returns them; cluster_num is the
+ * caller's int(seclct_cluster_number * n / total over all types) (:1458).  fine
+ * receives the fused candidates, 8 floats each (qw, qx, qy, qz, tx, ty, tz,
+ * allocated flag); at most cap are copied, *n_fine = the full count.
+ * *n_clusters (may be NULL) = clusters formed. */
+int fccf_stage_cluster(fccf_ctx* ctx, const float* cand_rowmajor, int64_t n, int cluster_num,
+                       const fccf_params* params, float* fine, int64_t cap, int64_t* n_fine, int64_t* n_clusters);
+
 /* Stage export: fine_verify (FCCF.cpp:785-839) of E <= 16 transforms on the GPU:
  * scores[e] = score of S2 transformed by T_e against S1 over the fine_verify_voxel
  * octree (the voxel argument).  s1/s2: residual clouds (xyz float32, n1, n2 >= 1);

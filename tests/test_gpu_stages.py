@@ -38,7 +38,7 @@ def test_match_stage_bit_exact(ctx, case):
         assert cands[ty].shape == ref.shape, ty
         np.testing.assert_array_equal(bits(cands[ty]), bits(ref))
     assert sum(len(c) for c in cands) > 0
-    assert 0 < k_pass <= len(t["B1"]) * len(t["B2"])
+    assert k_pass == run.get("counts", np.int64)[1] > 0
 
 
 @pytest.mark.parametrize("world", [2, 3, 8, 200])
@@ -169,3 +169,17 @@ def test_voxel_planes_and_grow_edges(ctx, fccf):
     assert len(planes) == 0 and len(bases) == 0
     with pytest.raises(fccf.FCCFError):
         ctx.grow(vox, 3)
+
+
+def test_cluster_stage_bit_exact(ctx, case, fccf):
+    run, _ = case
+    counts = run.get("counts", np.int64)  # K, K_pass, |cand t| x3, clusters t x3, ...
+    cands = [run.get(f"cand{t}").reshape(-1, 4, 4) for t in range(3)]
+    total = sum(len(c) for c in cands)
+    for t in range(3):
+        cluster_num = int(np.float32(200.0) * np.float32(len(cands[t])) / np.float32(total)) if total else 0
+        fine, ncl = ctx.cluster(cands[t], cluster_num)
+        ref = run.get(f"fine{t}").reshape(-1, 8)
+        assert fine.shape == ref.shape, t
+        np.testing.assert_array_equal(bits(fine), bits(ref))
+        assert ncl == counts[5 + t]
