@@ -152,6 +152,15 @@ def main():
     args = ap.parse_args()
 
     rank, ws, local, dist = dist_setup()
+    if ws > 1 and "FCCF_HOST_THREADS" not in os.environ:
+        # each rank's host stages get an equal share of this node's cores (<= 16 each),
+        # so N ranks' worker pools do not oversubscribe the host
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        try:
+            ncpu = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncpu = os.cpu_count() or 16
+        os.environ["FCCF_HOST_THREADS"] = str(max(2, min(16, ncpu // max(lws, 1))))
     import fccf_amd as F
     cfg = F.CONFIGS[args.config]
     if args.selftest:
@@ -262,7 +271,8 @@ def main():
                                    f"R{tuple(cfg['room'])}, voxel {leaf} m, one registration per step per GPU",
                        "n_points": cfg["n"], "leaf": leaf, "room": list(cfg["room"]),
                        "parallelism": f"replicas x{ws}",
-                       "pipelined": pipelined},
+                       "pipelined": pipelined,
+                       "host_threads_per_rank": int(os.environ.get("FCCF_HOST_THREADS", "0")) or None},
             "e2e_ms_median": statistics.median(per) * 1e3,  # one registration alone (latency)
             "e2e_host_input_ms_median": statistics.median(per_host) * 1e3,  # incl. H2D of both clouds
             "K_per_registration": int(st.K),
