@@ -295,4 +295,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        # fail fast: do not let context teardown after a device error hold the process
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(1)

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -86,6 +87,16 @@ struct MailBuf {
 // every launch argument that is not read from device memory) changes.  The
 // pipeline's sizes live in device memory, so a graph replays for any input that
 // fits the captured capacities.  FCCF_GRAPHS=0 launches eagerly instead.
+// A pipelined batch enqueues the next pair's cloud stage from a helper thread
+// while this thread waits on events of the current pair.  HIP rejects a wait on an
+// event whose recording stream is being captured at that moment, so graph captures
+// and the cross-thread event waits (pipeline.cpp) take this lock.  Captures happen
+// only when a graph's key changes, so the steady state never contends.
+inline std::mutex& capture_mutex() {
+  static std::mutex m;
+  return m;
+}
+
 struct CachedGraph {
   std::vector<uint8_t> key;
   hipGraphExec_t exec = nullptr;
@@ -108,6 +119,9 @@ struct CachedGraph {
     }
     const uint8_t* kb = (const uint8_t*)k;
     if (!exec || key.size() != kn || std::memcmp(key.data(), kb, kn) != 0) {
+      // no other thread may create a dependency on a stream while it is captured
+      // (hipErrorStreamCaptureIsolation): see capture_mutex()
+      std::lock_guard<std::mutex> lk(capture_mutex());
       reset();
       hipGraph_t g = nullptr;
       HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));

@@ -353,7 +353,10 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   hipStream_t st0 = c->sa[0], ss = c->sa[2];
   // the previous pair on this set may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for it
-  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[3], 0));
+  {
+    std::lock_guard<std::mutex> lk(capture_mutex());  // ev[3] is recorded on the fine stream (captured by phase B)
+    HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[3], 0));
+  }
   cs.arena.ensure(2 * cloud_bytes(capmax, true) + exact_sum_bytes(6, capmax) + (1 << 20));
   cs.arena.reset();
   // Inputs are staged into the workspace (H2D, or D2D for device-resident
@@ -433,7 +436,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
   c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
-  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));  // (no enqueue is in flight on the helper here)
   HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[4], 0));
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
@@ -744,7 +747,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       float res;
     } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size};
     ht.mark("fine_setup");
-    HIP_CHECK(hipStreamWaitEvent(sf, c->cs[s].ev[5], 0));  // S1 octree bounds replayed (after the clouds)
+    {
+      std::lock_guard<std::mutex> lk(capture_mutex());  // ev[5]'s stream may be capturing the next pair's clouds
+      HIP_CHECK(hipStreamWaitEvent(sf, c->cs[s].ev[5], 0));  // S1 octree bounds replayed (after the clouds)
+    }
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm);
@@ -776,6 +782,7 @@ void phase_b2(fccf_ctx* c, int s) {
   float* T_out = pb.T_out;
   std::vector<float> scores(E, 0.f);
   if (E > 0) {
+    // (ev[3]'s stream is captured only by this thread)
     HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));  // scores and the error word are in the mailbox
     const FineMail& fm = host_mail(c)->fine[s];
     std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
