@@ -33,21 +33,25 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 
 
 def torch_gather(group=None):
-    """All-gather of one float32 array of any length per rank over torch.distributed
-    (CPU tensors: gloo).  Returns the arrays in rank order."""
+    """All-gather of one float32 or float64 array of any length per rank over
+    torch.distributed (CPU tensors: gloo).  Returns the arrays in rank order."""
     import torch
     import torch.distributed as dist
 
     def gather(a: np.ndarray) -> list[np.ndarray]:
+        a = np.ascontiguousarray(a).reshape(-1)
+        if a.dtype not in (np.float32, np.float64):
+            raise TypeError(f"gather: float32/float64 only, got {a.dtype}")
+        dt = torch.float64 if a.dtype == np.float64 else torch.float32
         world = dist.get_world_size(group)
         n = torch.tensor([a.size], dtype=torch.int64)
         ns = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(ns, n, group=group)
         sizes = [int(x.item()) for x in ns]
         cap = max(max(sizes), 1)
-        buf = torch.zeros(cap, dtype=torch.float32)
-        buf[: a.size] = torch.from_numpy(np.ascontiguousarray(a, np.float32).reshape(-1))
-        outs = [torch.zeros(cap, dtype=torch.float32) for _ in range(world)]
+        buf = torch.zeros(cap, dtype=dt)
+        buf[: a.size] = torch.from_numpy(a)
+        outs = [torch.zeros(cap, dtype=dt) for _ in range(world)]
         dist.all_gather(outs, buf, group=group)
         return [o[:s].numpy().copy() for o, s in zip(outs, sizes)]
 
@@ -88,3 +92,70 @@ def match_sharded(ctx, F1, B1, F2, B2, rank: int, world: int, gather, params=Non
     lo, hi = shard_range(len(B1), rank, world)
     cands, k_pass = ctx.match(F1, B1, F2, B2, lo, hi, params)
     return combine(gather(pack(cands, k_pass)))
+
+
+# ---------------------------------------------------------------- VoxelGrid by leaf ranges
+# SURVEY.md §8(e) row D.  PCL's VoxelGrid (FCCF.cpp:1668-1678) sorts
+# points by the linear index of their leaf, i + j*div_x + k*div_x*div_y with
+# (i, j, k) = floor(p * (1/leaf)) - min_b, and averages each leaf's points in input
+# order.  That order is the lexicographic (k, j, i) order of floor(p * (1/leaf)),
+# whatever the bounding box.  So if every leaf is owned by one rank, ranks own
+# contiguous ranges of that order and each rank's points stay in input order, each
+# rank's ordinary VoxelGrid is exactly its slice of the global output.  The int32
+# overflow guard ("Integer indices would overflow": output = input) is decided on the
+# global bounding box; any subset of a passing cloud also passes.
+
+
+def leaf_coords(xyz: np.ndarray, leaf: float):
+    """floor(p * (1/leaf)) computed in float32 as PCL does (int64), and the finite mask."""
+    a = np.asarray(xyz, np.float32).reshape(-1, 3)
+    inv = np.float32(1.0) / np.float32(leaf)
+    fin = np.isfinite(a).all(axis=1)
+    with np.errstate(invalid="ignore", over="ignore"):
+        f = np.floor(a * inv)
+    return np.where(fin[:, None], f, 0).astype(np.int64), fin
+
+
+def voxel_grid_overflows(mn, mx, leaf: float) -> bool:
+    """PCL's guard, (int)((max - min) * inv) + 1 per axis in float32, on the finite bbox."""
+    inv = np.float32(1.0) / np.float32(leaf)
+    d = [int(np.float32(np.float32(mx[a]) - np.float32(mn[a])) * inv) + 1 for a in range(3)]
+    return d[0] * d[1] * d[2] > 2 ** 31 - 1
+
+
+def downsample_sharded(ctx, xyz_slice, leaf: float, rank: int, world: int, gather):
+    """Global VoxelGrid of a cloud split over ranks in input order (rank r holds the
+    r-th contiguous slice).  Every rank returns the full output, equal to
+    ctx.downsample(whole cloud)."""
+    a = np.ascontiguousarray(np.asarray(xyz_slice, np.float32).reshape(-1, 3))
+    f, fin = leaf_coords(a, leaf)
+    box = np.array([np.inf] * 3 + [-np.inf] * 3)
+    if fin.any():
+        box = np.concatenate([a[fin].min(axis=0), a[fin].max(axis=0)]).astype(np.float64)
+    bb = np.stack(gather(box))  # float32 values: exact in float64
+    mn, mx = bb[:, :3].min(axis=0), bb[:, 3:].max(axis=0)
+    if not np.isfinite(mn).all():  # no finite point on any rank
+        return np.zeros((0, 3), np.float32)
+    if voxel_grid_overflows(mn, mx, leaf):  # output = input, in input order
+        return np.concatenate([s.reshape(-1, 3) for s in gather(a.reshape(-1))])
+    inv = np.float32(1.0) / np.float32(leaf)
+    lo = np.floor(mn.astype(np.float32) * inv).astype(np.int64)
+    div = np.floor(mx.astype(np.float32) * inv).astype(np.int64) - lo + 1
+    key = np.where(fin, (f[:, 0] - lo[0]) + div[0] * ((f[:, 1] - lo[1]) + div[1] * (f[:, 2] - lo[2])), -1)
+    # splitters: quantiles of every rank's key sample, so ranks own similar counts
+    kf = np.sort(key[fin])
+    samp = kf[:: max(1, kf.size // 256)].astype(np.float64)
+    allsamp = np.sort(np.concatenate(gather(samp)))
+    cuts = [allsamp[(allsamp.size * r) // world] if allsamp.size else 0.0 for r in range(1, world)]
+    lo_cut = -np.inf if rank == 0 else cuts[rank - 1]
+    hi_cut = np.inf if rank == world - 1 else cuts[rank]
+    # exchange by owner (an all-to-all(v); gathered whole here, keys < 2^53 exact in
+    # float64): points keep input order within a source, sources arrive in rank order
+    mine = []
+    for m in gather(np.concatenate([key.astype(np.float64), a.astype(np.float64).reshape(-1)])):
+        n = m.size // 4
+        k, p = m[:n], m[n:].reshape(n, 3).astype(np.float32)
+        mine.append(p[(k >= 0) & (k >= lo_cut) & (k < hi_cut)])
+    own = np.concatenate(mine)
+    out = ctx.downsample(own, leaf) if len(own) else np.zeros((0, 3), np.float32)
+    return np.concatenate([s.reshape(-1, 3) for s in gather(np.ascontiguousarray(out, np.float32).reshape(-1))])

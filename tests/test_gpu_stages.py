@@ -183,3 +183,25 @@ def test_cluster_stage_bit_exact(ctx, case, fccf):
         assert fine.shape == ref.shape, t
         np.testing.assert_array_equal(bits(fine), bits(ref))
         assert ncl == counts[5 + t]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_downsample_sharded_by_leaf_ranges(ctx, oracle, fccf, world):
+    """§8(e) row D: the VoxelGrid split by leaf ranges over `world` ranks (one fccf_ctx
+    each, threads on one GPU), rank-ordered concatenation == the whole-cloud GPU pass
+    == the oracle, bitwise."""
+    import test_shard
+    c = fccf.CONFIGS["c2"]
+    src, _, _ = fccf.synth_pair(c["n"], c["room"])
+    src = src.copy()
+    src[[5, 777, 40_000]] = np.nan
+    whole = ctx.downsample(src, c["leaf"])
+    np.testing.assert_array_equal(bits(whole), bits(oracle.voxel_grid(src, c["leaf"])[0]))
+    ctxs = [fccf.Ctx(0) for _ in range(world)]
+    try:
+        outs = test_shard.run_sharded(src, c["leaf"], world, ctx_of=lambda r: ctxs[r])
+    finally:
+        for x in ctxs:
+            x.close()
+    for got in outs:
+        np.testing.assert_array_equal(bits(got), bits(whole))

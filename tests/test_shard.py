@@ -88,9 +88,103 @@ full, kp0 = ctx.match(None, B1, None, B2)
 assert kp == kp0, (kp, kp0)
 for a, b in zip(got, full):
     assert np.array_equal(a, b)
+xyz = test_shard.cloud(3000, 11)
+lo, hi = shard.shard_range(len(xyz), r, w)
+vctx = test_shard.StubVoxelCtx()
+got = shard.downsample_sharded(vctx, xyz[lo:hi], 0.25, r, w, shard.torch_gather())
+assert np.array_equal(got.view(np.uint32), vctx.downsample(xyz, 0.25).view(np.uint32))
 dist.barrier(); dist.destroy_process_group()
 print("ok", r)
 '''
+
+
+def cloud(n, seed, nan=True):
+    rng = np.random.default_rng(seed)
+    xyz = (rng.random((n, 3)) * np.array([6.0, 4.0, 2.0]) - 1.0).astype(np.float32)
+    if nan:
+        xyz[rng.integers(0, n, 7)] = np.nan
+        xyz[rng.integers(0, n, 3), 1] = np.inf
+    return xyz
+
+
+class StubVoxelCtx:
+    """Stand-in for the GPU VoxelGrid (tests only): a direct numpy/Python restatement of
+    PCL's semantics for small clouds — stable leaf order, sequential float32 sums."""
+
+    def downsample(self, xyz, leaf):
+        a = np.asarray(xyz, np.float32).reshape(-1, 3)
+        f, fin = shard.leaf_coords(a, leaf)
+        if not fin.any():
+            return np.zeros((0, 3), np.float32)
+        mn, mx = a[fin].min(axis=0), a[fin].max(axis=0)
+        if shard.voxel_grid_overflows(mn, mx, leaf):
+            return a.copy()
+        lo = f[fin].min(axis=0)
+        div = f[fin].max(axis=0) - lo + 1
+        key = (f[:, 0] - lo[0]) + div[0] * ((f[:, 1] - lo[1]) + div[1] * (f[:, 2] - lo[2]))
+        idx = np.flatnonzero(fin)
+        idx = idx[np.argsort(key[idx], kind="stable")]
+        out, s = [], 0
+        while s < len(idx):
+            e = s
+            acc = np.zeros(3, np.float32)
+            while e < len(idx) and key[idx[e]] == key[idx[s]]:
+                acc = (acc + a[idx[e]]).astype(np.float32)
+                e += 1
+            out.append(acc / np.float32(e - s))
+            s = e
+        return np.array(out, np.float32).reshape(-1, 3)
+
+
+def thread_gathers(world):
+    """In-process stand-in for the collective: one gather per rank thread."""
+    import threading
+    buf = [None] * world
+    bar = threading.Barrier(world)
+
+    def make(r):
+        def g(a):
+            buf[r] = np.array(a).reshape(-1)
+            bar.wait()
+            out = list(buf)
+            bar.wait()
+            return out
+        return g
+    return [make(r) for r in range(world)]
+
+
+def run_sharded(xyz, leaf, world, ctx_of=lambda r: StubVoxelCtx()):
+    import threading
+    gs, res = thread_gathers(world), [None] * world
+
+    def work(r):
+        lo, hi = shard.shard_range(len(xyz), r, world)
+        res[r] = shard.downsample_sharded(ctx_of(r), xyz[lo:hi], leaf, r, world, gs[r])
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    return res
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_downsample_sharded_equals_whole(world):
+    xyz = cloud(4000, world)
+    want = StubVoxelCtx().downsample(xyz, 0.2)
+    for got in run_sharded(xyz, 0.2, world):
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_downsample_sharded_overflow_and_empty():
+    xyz = cloud(500, 9, nan=False)
+    xyz[0] = (-3e4, -3e4, -3e4)  # (extent / leaf)^3 past int32: PCL passes the cloud through
+    xyz[1, 1] = np.nan
+    for got in run_sharded(xyz, 0.05, 3):
+        np.testing.assert_array_equal(got.view(np.uint32), xyz.view(np.uint32))
+    allnan = np.full((10, 3), np.nan, np.float32)
+    for got in run_sharded(allnan, 0.1, 2):
+        assert got.shape == (0, 3)
 
 
 def test_gloo_two_ranks(tmp_path):
