@@ -34,8 +34,29 @@ PROBE_KERNELS = ["k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter", "k_vg_
                  "k_gather", "k_voxel_fit", "k_fv_counts", "k_match_count", "k_match_emit"]
 
 
-def dist_setup():
+def spawn_ranks(n, argv):
+    """--gpus N > 1 without a launcher: start N rank processes of this script (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE set) BEFORE anything touches the GPU, wait for all
+    of them and return the worst exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def dist_setup(gpus):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; refusing to report a different n_gpus")
     if ws <= 1:
         return 0, 1, 0, None
     import torch.distributed as dist
@@ -150,8 +171,12 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="time K sequential fccf_register_device calls instead of one pipelined batch of K")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
-    rank, ws, local, dist = dist_setup()
+    rank, ws, local, dist = dist_setup(args.gpus)
     if ws > 1 and "FCCF_HOST_THREADS" not in os.environ:
         # each rank's host stages get an equal share of this node's cores (<= 16 each),
         # so N ranks' worker pools do not oversubscribe the host
@@ -297,6 +322,8 @@ def main():
 if __name__ == "__main__":
     try:
         main()
+    except SystemExit:
+        raise
     except BaseException:
         # fail fast: do not let context teardown after a device error hold the process
         import traceback

@@ -177,6 +177,47 @@ extern "C" int fccf_stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, f
   return stage_downsample(c, xyz, n, leaf, out, m, false);
 }
 
+namespace {
+__global__ void k_sortkeys_params(const uint32_t* keys, const uint32_t* d_n, VGParams* P) {
+  __shared__ uint32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  for (uint32_t i = threadIdx.x; i < *d_n; i += blockDim.x) c += keys[i] != 0xFFFFFFFFu ? 1u : 0u;
+  atomicAdd(&cnt, c);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    P->overflow = 0;
+    P->nfinite = cnt;
+    P->unsorted = 1;
+  }
+}
+}  // namespace
+
+extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm) {
+  if (!c || (!keys && n) || (!perm && n) || n < 0 || n > (int64_t)0x7FFFFFFF) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    hipStream_t st = c->sb;
+    const uint32_t cap = (uint32_t)std::max<int64_t>(n, 1);
+    c->arena2.ensure(voxel_grid_bytes(cap) + (1 << 20));
+    c->arena2.reset();
+    uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
+    VGBufs b = voxel_grid_carve(c->arena2, cap);
+    uint32_t hn = (uint32_t)n;
+    HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
+    if (n) HIP_CHECK(hipMemcpyAsync(b.k0, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+    std::vector<uint32_t> iota((size_t)n);
+    for (uint32_t i = 0; i < (uint32_t)n; ++i) iota[i] = i;
+    if (n) HIP_CHECK(hipMemcpyAsync(b.v0, iota.data(), 4 * (size_t)n, hipMemcpyHostToDevice, st));
+    k_sortkeys_params<<<1, 1024, 0, st>>>(b.k0, d_sc, b.params);
+    introsort_u32(b.k0, b.v0, b.k1, b.v1, B2<const uint32_t*>(d_sc), B2<const VGParams*>(b.params), cap, b.is, st, 1,
+                  exact_gate != 0);
+    HIP_CHECK(hipGetLastError());
+    if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
 extern "C" int fccf_stage_downsample_presorted(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out,
                                                int64_t* m) {
   return stage_downsample(c, xyz, n, leaf, out, m, true);

@@ -45,18 +45,28 @@ struct Arena {
   }
   template <class T>
   T* take_n(size_t n) { return (T*)take(sizeof(T) * (n ? n : 1)); }
-  void ensure(size_t bytes) {
-    if (bytes <= cap) return;
+  void ensure(size_t bytes);
+  ~Arena() {
+    if (base) (void)hipFree(base);
+  }
+};
+
+// Growing an arena frees and re-allocates device memory; a pipelined batch may be
+// capturing the next pair's graphs on the helper thread meanwhile, so reallocation
+// takes the capture lock too (capture_mutex below).
+inline std::mutex& capture_mutex();
+
+inline void Arena::ensure(size_t bytes) {
+  if (bytes <= cap) return;
+  std::lock_guard<std::mutex> lk(capture_mutex());
+  {
     if (base) (void)hipFree(base);
     base = nullptr;
     cap = 0;
     if (hipMalloc((void**)&base, bytes) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc arena");
     cap = bytes;
   }
-  ~Arena() {
-    if (base) (void)hipFree(base);
-  }
-};
+}
 
 struct PinnedBuf {
   void* p = nullptr;

@@ -1,0 +1,1034 @@
+// introsort.hip — K1's sort in the reference's order: libstdc++ std::sort
+// (introsort) of PCL VoxelGrid's (idx, cloud_point_index) pairs, compared by idx
+// only.  Reference: FCCF.cpp:1668-1678 (main) and :1377-1387 (driver), both through
+// pcl::VoxelGrid<PointXYZ>::applyFilter, whose std::sort leaves the points of one
+// leaf in introsort's (unstable) order; the centroid sums them in that order
+// (SURVEY.md App. A2 steps 6-7).  The result equals std::sort bit for bit
+// (tests/test_gpu_introsort.py, tools/introsort_model.cpp).
+//
+// libstdc++ std::sort = __introsort_loop(depth 2*lg(n)) + a final insertion sort:
+//  * a segment of more than 16 elements is partitioned after
+//    __move_median_to_first(first, first+1, mid, last-1); at depth 0 it is heap sorted;
+//  * __unguarded_partition(first+1, last, pivot=*first) swaps the k-th element >= P
+//    from the left (L[k]) with the k-th element <= P from the right (R[k]) for
+//    k = 1..K, the prefix where L[k] < R[k], and returns cut = min(L[K+1], R[K]).
+//    So an element >= P with ge-rank k is swapped iff (#<=P after it) >= k, an
+//    element <= P with right-rank k iff (#>=P before it) >= k: prefix counts decide
+//    every move, no sequential scan is needed;
+//  * the final insertion sort is stable and every leaf segment is bounded by its
+//    neighbours, so the output is each leaf segment stably sorted in place.
+//
+// GPU structure (per cloud; both clouds of a registration in the same launches):
+//  k_is_prep   stable compaction of non-finite points (PCL skips them), sort length;
+//  rounds      the first R levels over segments > IS_LCAP, many workgroups each:
+//              k_is_count (pivot, per-tile ge/le counts and tile-local position
+//              lists) and k_is_scatter (ranks from the tile prefix, every element
+//              written to its destination in the other buffer, cut by atomicMin);
+//  k_is_own    one workgroup per remaining subtree (dequeued): partitions in global
+//              memory while a segment exceeds IS_LCAP, then the whole subtree in LDS
+//              (workgroup partitions above IS_WCAP, one wave per smaller subtree),
+//              the stable leaf sort, and the write of the sorted keys/values.
+// HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); k_is_own reads and
+// writes each element once more (8 + 8 B) when its subtree fits in LDS.
+#define KT_TU 9  // ktrace.h source tag
+#include "probe.h"
+#include "kernels.h"
+
+namespace fccf {
+namespace {
+
+constexpr uint32_t IS_TILE = 4096;   // elements per round tile
+constexpr int IS_TT = 256;           // round kernels: threads per block
+constexpr int IS_TC = IS_TILE / IS_TT;  // 16 elements per thread
+constexpr uint32_t IS_LCAP = 7680;   // largest segment finished in LDS (15 per thread: 2 blocks per CU fit)
+constexpr int IS_OT = 512;           // owner: threads per block
+constexpr int IS_OW = IS_OT / 64;    // owner: waves
+constexpr int IS_OC = IS_LCAP / IS_OT;  // 15 elements per thread in a workgroup partition
+constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a workgroup partition
+constexpr uint32_t IS_WCAP = 1024;   // largest segment partitioned by one wave
+constexpr int IS_WC = IS_WCAP / 64;  // 16 elements per lane
+constexpr uint32_t IS_THRESHOLD = 16;  // libstdc++ _S_threshold
+constexpr int IS_STACK = 48;
+constexpr int IS_WLIST = 512;
+// packed u32 subtree of at most IS_WCAP elements: off (13 bits) | len (11) | depth (6)
+__device__ __forceinline__ uint32_t wpack(uint32_t off, uint32_t len, int d) { return off | (len << 13) | ((uint32_t)d << 24); }
+constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int depth0(uint32_t n) { return n ? 2 * (31 - __clz((int)n)) : 0; }  // 2*std::__lg(n)
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+// __move_median_to_first(first, first+1, mid, last-1): the position whose element
+// becomes the pivot (requires l - f > 16, so the three positions are distinct)
+template <class KP>
+__device__ __forceinline__ uint32_t median_pos(KP K, uint32_t f, uint32_t l) {
+  const uint32_t A = f + 1, B = f + (l - f) / 2, C = l - 1;
+  const uint32_t a = K[A], b = K[B], c = K[C];
+  if (a < b) {
+    if (b < c) return B;
+    if (a < c) return C;
+    return A;
+  }
+  if (a < c) return A;
+  if (b < c) return C;
+  return B;
+}
+
+// std::__adjust_heap / __make_heap / __sort_heap on (K, V) pairs by key (one thread)
+template <class KP, class VP>
+__device__ void adjust_heap(KP K, VP V, int64_t hole, int64_t len, uint32_t vk, uint32_t vv) {
+  const int64_t top = hole;
+  int64_t sc = hole;
+  while (sc < (len - 1) / 2) {
+    sc = 2 * (sc + 1);
+    if (K[sc] < K[sc - 1]) sc--;
+    K[hole] = K[sc];
+    V[hole] = V[sc];
+    hole = sc;
+  }
+  if ((len & 1) == 0 && sc == (len - 2) / 2) {
+    sc = 2 * (sc + 1);
+    K[hole] = K[sc - 1];
+    V[hole] = V[sc - 1];
+    hole = sc - 1;
+  }
+  int64_t parent = (hole - 1) / 2;
+  while (hole > top && K[parent] < vk) {
+    K[hole] = K[parent];
+    V[hole] = V[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  K[hole] = vk;
+  V[hole] = vv;
+}
+template <class KP, class VP>
+__device__ void heap_sort(KP K, VP V, int64_t len) {  // std::__partial_sort(first, last, last)
+  if (len < 2) return;
+  for (int64_t parent = (len - 2) / 2;; parent--) {
+    adjust_heap(K, V, parent, len, K[parent], V[parent]);
+    if (parent == 0) break;
+  }
+  for (int64_t last = len - 1; last > 0; --last) {
+    const uint32_t vk = K[last], vv = V[last];
+    K[last] = K[0];
+    V[last] = V[0];
+    adjust_heap(K, V, 0, last, vk, vv);
+  }
+}
+
+// Exclusive scan over the whole block (blockDim a multiple of 64, <= 1024); sh >= 16 u32.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint32_t wp = 0, tot = 0;
+  for (uint32_t w = 0; w < nw; ++w) {
+    wp += w < wave ? sh[w] : 0u;
+    tot += sh[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
+struct Child {
+  uint32_t f, l;
+  int32_t d;
+};
+// children of round r-1's partitioned segments in position order (r == 0: the root)
+__device__ __forceinline__ Child child_of(const IsBufs& W, int r, uint32_t nsort, uint32_t i) {
+  if (r == 0) return {0u, nsort, depth0(nsort)};
+  const IsSeg s = W.segs[(size_t)(r - 1) * W.segmax + i / 2];
+  // a cut lies in (f, l) by construction; clamped so that a defect cannot address
+  // outside the segment (it would show as a wrong order, never as a fault)
+  const uint32_t c = min(max(W.cuts[(size_t)(r - 1) * W.segmax + i / 2], s.f + 1), s.l - 1);
+  return (i & 1) ? Child{c, s.l, s.depth - 1} : Child{s.f, c, s.depth - 1};
+}
+__device__ __forceinline__ uint32_t nchildren(const IsBufs& W, int r) { return r == 0 ? 1u : 2u * W.rounds[r - 1].nseg; }
+__device__ __forceinline__ bool is_large(const Child& c) { return c.l - c.f > IS_LCAP && c.d > 0; }
+__device__ __forceinline__ uint32_t tiles_of(uint32_t len) { return (len - 1 + IS_TILE - 1) / IS_TILE; }
+
+// largest u < n with pre[u] <= x (pre ascending, pre[0] = 0)
+__device__ __forceinline__ uint32_t upper_index(const uint32_t* pre, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------- k_is_prep
+// PCL pushes only finite points into its index vector, in input order: compact the
+// (key, index) pairs of finite points (rare: only when some point is not finite) and
+// mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_own's dequeue head.
+// exact_gate (the driver's presorted second pass): sort only when the order check failed.
+__global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*> V2, B2<const uint32_t*> d_n2,
+                                                   B2<const VGParams*> P2, B2<IsBufs> W2, int exact_gate) {
+  KT();
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const VGParams* P = P2[e];
+  const uint32_t n = *d_n2[e];
+  uint32_t ns = (P->overflow || P->nfinite == 0) ? 0u : P->nfinite;
+  if (exact_gate && P->unsorted == 0u) ns = 0;
+  if (threadIdx.x == 0) {
+    W.ctl[0] = ns;
+    W.ctl[1] = 0;
+    W.ctl[2] = 0;
+  }
+  if (ns == 0 || ns >= n) return;
+  uint32_t* K = K2[e];
+  uint32_t* V = V2[e];
+  __shared__ uint32_t sh[16];
+  uint32_t out = 0;
+  for (uint32_t b = 0; b < n; b += 1024) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t k = i < n ? K[i] : IS_NONE, v = i < n ? V[i] : 0u;
+    const uint32_t keep = k != IS_NONE;
+    uint32_t tot;
+    const uint32_t o = block_excl_scan(keep, sh, &tot);  // its barriers order these reads before the writes
+    if (keep) {
+      K[out + o] = k;
+      V[out + o] = v;
+    }
+    out += tot;
+    __syncthreads();
+  }
+  for (uint32_t i = ns + threadIdx.x; i < n; i += 1024) K[i] = IS_NONE;
+}
+
+// ---------------------------------------------------------------- rounds
+// This round's large segments, built by every block from the previous round's
+// table and cuts (tiny); block 0 publishes them, initialises the cuts and appends the
+// finished-as-small children to the owned list.  Dynamic LDS: 4 * segmax u32.
+__device__ uint32_t build_round(const IsBufs& W, int r, uint32_t nsort, uint32_t* tf, uint32_t* tl, int32_t* td,
+                                uint32_t* t0, uint32_t* sh, uint32_t* ntiles_out) {
+  const uint32_t nch = nchildren(W, r);
+  const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
+  uint32_t nseg = 0, ntiles = 0, nown = 0;
+  for (uint32_t b = 0; b < nch; b += blockDim.x) {
+    const uint32_t i = b + threadIdx.x;
+    Child c = {0u, 0u, 0};
+    if (i < nch) c = child_of(W, r, nsort, i);
+    const bool lg = i < nch && is_large(c);
+    const bool ow = i < nch && !lg && c.l > c.f;
+    const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
+    uint32_t s_lg, s_nt, s_ow;
+    const uint32_t p_lg = block_excl_scan(lg ? 1u : 0u, sh, &s_lg);
+    const uint32_t p_nt = block_excl_scan(nt, sh, &s_nt);
+    const uint32_t p_ow = block_excl_scan(ow ? 1u : 0u, sh, &s_ow);
+    if (lg) {
+      tf[nseg + p_lg] = c.f;
+      tl[nseg + p_lg] = c.l;
+      td[nseg + p_lg] = c.d;
+      t0[nseg + p_lg] = ntiles + p_nt;
+    }
+    if (ow && blockIdx.x == 0) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
+    nseg += s_lg;
+    ntiles += s_nt;
+    nown += s_ow;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
+      W.segs[(size_t)r * W.segmax + j] = IsSeg{tf[j], tl[j], td[j], t0[j]};
+      W.cuts[(size_t)r * W.segmax + j] = tl[j];
+    }
+    if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
+  }
+  *ntiles_out = ntiles;
+  return nseg;
+}
+
+// Per-tile ge/le counts against the segment's pivot and the tile-local position
+// lists (offsets from the tile start, in position order).
+__global__ void __launch_bounds__(IS_TT) k_is_count(B2<const uint32_t*> K2, B2<IsBufs> W2, int r) {
+  KT();
+  extern __shared__ uint32_t dyn[];
+  __shared__ uint32_t sh[16];
+  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t nsort = W.ctl[0];
+  uint32_t* tf = dyn;
+  uint32_t* tl = tf + W.segmax;
+  int32_t* td = (int32_t*)(tl + W.segmax);
+  uint32_t* t0 = (uint32_t*)(td + W.segmax);
+  uint32_t ntiles;
+  const uint32_t nseg = build_round(W, r, nsort, tf, tl, td, t0, sh, &ntiles);
+  const uint32_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  const uint32_t j = upper_index(t0, nseg, t);
+  const uint32_t f = tf[j], l = tl[j], i = t - t0[j];
+  const uint32_t* __restrict__ K = K2[e];
+  const uint32_t m = median_pos(K, f, l);
+  const uint32_t P = K[m], kf = K[f];
+  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t kk[IS_TC];
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    kk[c] = p < b ? (p == m ? kf : K[p]) : 0u;
+  }
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const bool ok = a + c * IS_TT + threadIdx.x < b;
+    const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+    if (lane == 0) {
+      cg[c * 4 + w] = (uint32_t)__popcll(bg);
+      cl[c * 4 + w] = (uint32_t)__popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (w == 0) {  // 64 (chunk, wave) entries in position order: one per lane
+    uint32_t xg = cg[lane], xl = cl[lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+      if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+    }
+    pg[lane] = xg - cg[lane];
+    pl[lane] = xl - cl[lane];
+    if (lane == 63) {
+      W.cnt[2 * (size_t)t] = xg;
+      W.cnt[2 * (size_t)t + 1] = xl;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    const bool ok = p < b;
+    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    if (ge) W.gel[a + pg[c * 4 + w] + mbcnt(bg)] = (uint16_t)(p - a);
+    if (le) W.lel[a + pl[c * 4 + w] + mbcnt(bl)] = (uint16_t)(p - a);
+  }
+}
+
+// Every element of the round's large segments to its place after the partition,
+// written to the other buffer; the cut by atomicMin.  Dynamic LDS: segmax + 2 * maxtiles u32.
+__global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
+                                                      B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
+  KT();
+  extern __shared__ uint32_t dyn[];
+  __shared__ uint32_t sh[16];
+  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  __shared__ uint32_t scut;
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const IsRound rd = W.rounds[r];
+  const uint32_t t = blockIdx.x;
+  if (t >= rd.ntiles) return;
+  uint32_t* t0 = dyn;
+  uint32_t* preg = t0 + W.segmax;
+  uint32_t* prel = preg + W.maxtiles;
+  const IsSeg* segs = W.segs + (size_t)r * W.segmax;
+  for (uint32_t j = threadIdx.x; j < rd.nseg; j += blockDim.x) t0[j] = segs[j].tile0;
+  if (threadIdx.x == 0) scut = IS_NONE;
+  __syncthreads();
+  const uint32_t j = upper_index(t0, rd.nseg, t);
+  const IsSeg s = segs[j];
+  const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0;
+  // exclusive prefix of the segment's tile counts
+  uint32_t rg = 0, rl = 0;
+  for (uint32_t u0 = 0; u0 < nt; u0 += blockDim.x) {
+    const uint32_t u = u0 + threadIdx.x;
+    const uint32_t g = u < nt ? W.cnt[2 * (size_t)(s.tile0 + u)] : 0u;
+    const uint32_t q = u < nt ? W.cnt[2 * (size_t)(s.tile0 + u) + 1] : 0u;
+    uint32_t sg, sl;
+    const uint32_t xg = block_excl_scan(g, sh, &sg);
+    const uint32_t xl = block_excl_scan(q, sh, &sl);
+    if (u < nt) {
+      preg[u] = rg + xg;
+      prel[u] = rl + xl;
+    }
+    rg += sg;
+    rl += sl;
+  }
+  const uint32_t le_tot = rl;
+  __syncthreads();
+  const uint32_t* __restrict__ K = Ki2[e];
+  const uint32_t* __restrict__ V = Vi2[e];
+  uint32_t* __restrict__ Ko = Ko2[e];
+  uint32_t* __restrict__ Vo = Vo2[e];
+  const uint32_t m = median_pos(K, f, l);
+  const uint32_t P = K[m], kf = K[f], vf = V[f], vm = V[m];
+  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t kk[IS_TC], vv[IS_TC];
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    const bool ok = p < b;
+    kk[c] = ok ? (p == m ? kf : K[p]) : 0u;
+    vv[c] = ok ? (p == m ? vf : V[p]) : 0u;
+  }
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const bool ok = a + c * IS_TT + threadIdx.x < b;
+    const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+    if (lane == 0) {
+      cg[c * 4 + w] = (uint32_t)__popcll(bg);
+      cl[c * 4 + w] = (uint32_t)__popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    uint32_t xg = cg[lane], xl = cl[lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+      if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+    }
+    pg[lane] = xg - cg[lane] + preg[i];
+    pl[lane] = xl - cl[lane] + prel[i];
+  }
+  __syncthreads();
+  uint32_t cut = IS_NONE;
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    const bool ok = p < b;
+    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    if (!ok) continue;
+    const uint32_t gx = pg[c * 4 + w] + mbcnt(bg);  // # >= P before p in the segment
+    const uint32_t lx = pl[c * 4 + w] + mbcnt(bl);  // # <= P before p
+    uint32_t dst = p;
+    if (ge) {
+      const uint32_t k1 = gx + 1;
+      if (le_tot - lx - (le ? 1u : 0u) >= k1) {  // swapped with R[k1], the (le_tot-k1)-th <= P from the left
+        const uint32_t x = le_tot - k1;
+        const uint32_t u = upper_index(prel, nt, x);
+        const uint32_t au = f + 1 + u * IS_TILE;
+        dst = au + W.lel[au + (x - prel[u])];
+      } else {
+        cut = min(cut, p);  // L[K+1]
+      }
+    }
+    if (le) {
+      const uint32_t kr = le_tot - lx;  // right rank
+      if (gx >= kr) {  // swapped with L[kr], the (kr-1)-th >= P from the left
+        const uint32_t x = kr - 1;
+        const uint32_t u = upper_index(preg, nt, x);
+        const uint32_t au = f + 1 + u * IS_TILE;
+        dst = au + W.gel[au + (x - preg[u])];
+        cut = min(cut, p);  // R[K]
+      }
+    }
+    if (dst <= f || dst >= l) {  // cannot happen; never write outside the segment
+      W.ctl[2] |= 0x100u;
+      continue;
+    }
+    Ko[dst] = kk[c];
+    Vo[dst] = vv[c];
+  }
+  cut = wave_min_u32(cut);
+  if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (scut != IS_NONE) atomicMin(&W.cuts[(size_t)r * W.segmax + j], scut);
+    if (i == 0) {
+      Ko[f] = P;
+      Vo[f] = vm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_is_own
+// exchange slots: a workgroup partition swaps < IS_LCAP / 2 pairs, a wave one < IS_WCAP / 2
+constexpr uint32_t IS_XCH = IS_LCAP / 2 > IS_OW * IS_WCAP / 2 ? IS_LCAP / 2 : IS_OW * IS_WCAP / 2;
+struct OwnLds {
+  uint32_t k[IS_LCAP], v[IS_LCAP];
+  uint16_t xch[IS_XCH];             // partition exchange slots (workgroup, or one region per wave)
+  uint32_t heads[IS_LCAP / 32];     // leaf starts
+  uint32_t cg[IS_OE], cl[IS_OE], pg[IS_OE], pl[IS_OE];
+  uint2 wstk[IS_STACK];             // workgroup-phase stack {off, len | depth << 16}
+  uint32_t wlist[IS_WLIST];         // subtrees for the waves (wpack)
+  uint32_t vstk[IS_OW][IS_STACK];   // per-wave stacks (wpack)
+  uint4 gstk[IS_STACK];             // global-phase stack {f, l, depth, -}
+  uint32_t gsp;                     // its depth
+  uint32_t bc[8];                   // broadcasts
+  uint32_t sh[16];
+};
+
+// Exclusive prefix (plus carries) of the IS_OE (chunk, wave) counts in position
+// order, by wave 0 (two entries per lane).
+__device__ __forceinline__ void block_chunk_scan(OwnLds& S, uint32_t cg0, uint32_t cl0) {
+  const uint32_t lane = lane_id(), i0 = 2 * lane, i1 = 2 * lane + 1;
+  const uint32_t g0 = i0 < IS_OE ? S.cg[i0] : 0u, g1 = i1 < IS_OE ? S.cg[i1] : 0u;
+  const uint32_t l0 = i0 < IS_OE ? S.cl[i0] : 0u, l1 = i1 < IS_OE ? S.cl[i1] : 0u;
+  uint32_t xg = g0 + g1, xl = l0 + l1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+    if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+  }
+  if (i0 < IS_OE) {
+    S.pg[i0] = cg0 + xg - g0 - g1;
+    S.pl[i0] = cl0 + xl - l0 - l1;
+  }
+  if (i1 < IS_OE) {
+    S.pg[i1] = cg0 + xg - g1;
+    S.pl[i1] = cl0 + xl - l1;
+  }
+}
+
+__device__ __forceinline__ void mark_leaf(OwnLds& S, uint32_t off) { atomicOr(&S.heads[off >> 5], 1u << (off & 31)); }
+
+// One partition of [f, l) (17 <= l - f <= IS_WCAP) in LDS by one wave; returns the cut.
+__device__ uint32_t wave_partition(OwnLds& S, uint32_t f, uint32_t l, uint16_t* xch) {
+  const uint32_t lane = lane_id();
+  const uint32_t m = median_pos(S.k, f, l);
+  if (lane == 0) {
+    const uint32_t tk = S.k[f], tv = S.v[f];
+    S.k[f] = S.k[m];
+    S.v[f] = S.v[m];
+    S.k[m] = tk;
+    S.v[m] = tv;
+  }
+  wsync();
+  const uint32_t P = S.k[f];
+  const uint32_t n = l - f - 1;
+  uint32_t kk[IS_WC], vv[IS_WC];
+  uint64_t bg[IS_WC], bl[IS_WC];
+#pragma unroll
+  for (int c = 0; c < IS_WC; ++c) {
+    const uint32_t q = c * 64 + lane;
+    const bool ok = q < n;
+    kk[c] = ok ? S.k[f + 1 + q] : 0u;
+    vv[c] = ok ? S.v[f + 1 + q] : 0u;
+    bg[c] = __ballot(ok && kk[c] >= P);
+    bl[c] = __ballot(ok && kk[c] <= P);
+  }
+  uint32_t le_tot = 0;
+#pragma unroll
+  for (int c = 0; c < IS_WC; ++c) le_tot += (uint32_t)__popcll(bl[c]);
+  uint32_t cut = IS_NONE;
+  uint32_t kg[IS_WC], kl[IS_WC];  // 1-based swap ranks (0 = not swapped)
+  uint32_t gx = 0, lx = 0;        // counts before this chunk
+#pragma unroll
+  for (int c = 0; c < IS_WC; ++c) {
+    const uint32_t q = c * 64 + lane, p = f + 1 + q;
+    const bool ge = (bg[c] >> lane) & 1ull, le = (bl[c] >> lane) & 1ull;
+    const uint32_t g = gx + mbcnt(bg[c]), h = lx + mbcnt(bl[c]);
+    kg[c] = 0;
+    kl[c] = 0;
+    if (ge) {
+      if (le_tot - h - (le ? 1u : 0u) >= g + 1) kg[c] = g + 1;
+      else cut = min(cut, p);
+    }
+    if (le) {
+      const uint32_t kr = le_tot - h;
+      if (g >= kr) {
+        kl[c] = kr;
+        cut = min(cut, p);
+      }
+    }
+    if (kg[c]) xch[kg[c] - 1] = (uint16_t)p;
+    gx += (uint32_t)__popcll(bg[c]);
+    lx += (uint32_t)__popcll(bl[c]);
+  }
+  wsync();
+  uint32_t dl[IS_WC];
+#pragma unroll
+  for (int c = 0; c < IS_WC; ++c) {
+    dl[c] = 0;
+    if (kl[c]) {
+      dl[c] = xch[kl[c] - 1];  // L[kr]
+      xch[kl[c] - 1] = (uint16_t)(f + 1 + c * 64 + lane);
+    }
+  }
+  wsync();
+#pragma unroll
+  for (int c = 0; c < IS_WC; ++c) {
+    if (kg[c]) {
+      const uint32_t d = xch[kg[c] - 1];  // R[k]
+      S.k[d] = kk[c];
+      S.v[d] = vv[c];
+    }
+    if (kl[c]) {
+      S.k[dl[c]] = kk[c];
+      S.v[dl[c]] = vv[c];
+    }
+  }
+  wsync();
+  return min(max(wave_min_u32(cut), f + 1), l - 1);
+}
+
+// The introsort subtree of [off, off+len) (len <= IS_WCAP) by one wave, in LDS.
+__device__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* stk, uint16_t* xch) {
+  const uint32_t lane = lane_id();
+  int sp = 0;
+  stk[sp++] = packed;
+  while (sp > 0) {
+    const uint32_t it = stk[--sp];
+    const uint32_t f = it & 0x1FFFu, n = (it >> 13) & 0x7FFu;
+    const int dd = (int)(it >> 24);
+    if (n <= IS_THRESHOLD) {
+      if (lane == 0 && n) mark_leaf(S, f);
+      continue;
+    }
+    if (dd == 0) {
+      if (lane == 0) {
+        heap_sort(S.k + f, S.v + f, (int64_t)n);
+        for (uint32_t q = 0; q < n; ++q) mark_leaf(S, f + q);
+      }
+      wsync();
+      continue;
+    }
+    const uint32_t c = wave_partition(S, f, f + n, xch);
+    stk[sp++] = wpack(c, f + n - c, dd - 1);
+    stk[sp++] = wpack(f, c - f, dd - 1);
+  }
+}
+
+// One partition of [f, l) (IS_WCAP < l - f <= IS_LCAP) in LDS by the whole block.
+__device__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    const uint32_t m = median_pos(S.k, f, l);
+    const uint32_t tk = S.k[f], tv = S.v[f];
+    S.k[f] = S.k[m];
+    S.v[f] = S.v[m];
+    S.k[m] = tk;
+    S.v[m] = tv;
+    S.bc[4] = IS_NONE;
+  }
+  __syncthreads();
+  const uint32_t P = S.k[f];
+  const uint32_t n = l - f - 1;
+  uint32_t kk[IS_OC], vv[IS_OC];
+#pragma unroll
+  for (int c = 0; c < IS_OC; ++c) {
+    const uint32_t q = c * IS_OT + threadIdx.x;
+    const bool ok = q < n;
+    kk[c] = ok ? S.k[f + 1 + q] : 0u;
+    vv[c] = ok ? S.v[f + 1 + q] : 0u;
+    const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+    if (lane == 0) {
+      S.cg[c * IS_OW + w] = (uint32_t)__popcll(bg);
+      S.cl[c * IS_OW + w] = (uint32_t)__popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (w == 0) block_chunk_scan(S, 0u, 0u);
+  __syncthreads();
+  if (threadIdx.x == 0) S.bc[5] = S.pl[IS_OE - 1] + S.cl[IS_OE - 1];
+  __syncthreads();
+  const uint32_t le_tot = S.bc[5];
+  uint32_t cut = IS_NONE;
+  uint32_t kg[IS_OC], kl[IS_OC];
+#pragma unroll
+  for (int c = 0; c < IS_OC; ++c) {
+    const uint32_t q = c * IS_OT + threadIdx.x, p = f + 1 + q;
+    const bool ok = q < n;
+    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    const uint32_t g = S.pg[c * IS_OW + w] + mbcnt(bg), h = S.pl[c * IS_OW + w] + mbcnt(bl);
+    kg[c] = 0;
+    kl[c] = 0;
+    if (ge) {
+      if (le_tot - h - (le ? 1u : 0u) >= g + 1) kg[c] = g + 1;
+      else cut = min(cut, p);
+    }
+    if (le) {
+      const uint32_t kr = le_tot - h;
+      if (g >= kr) {
+        kl[c] = kr;
+        cut = min(cut, p);
+      }
+    }
+    if (kg[c]) S.xch[kg[c] - 1] = (uint16_t)p;
+  }
+  cut = wave_min_u32(cut);
+  if (lane == 0 && cut != IS_NONE) atomicMin(&S.bc[4], cut);
+  __syncthreads();
+  uint32_t dl[IS_OC];
+#pragma unroll
+  for (int c = 0; c < IS_OC; ++c) {
+    dl[c] = 0;
+    if (kl[c]) {
+      dl[c] = S.xch[kl[c] - 1];
+      S.xch[kl[c] - 1] = (uint16_t)(f + 1 + c * IS_OT + threadIdx.x);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < IS_OC; ++c) {
+    if (kg[c]) {
+      const uint32_t d = S.xch[kg[c] - 1];
+      S.k[d] = kk[c];
+      S.v[d] = vv[c];
+    }
+    if (kl[c]) {
+      S.k[dl[c]] = kk[c];
+      S.v[dl[c]] = vv[c];
+    }
+  }
+  __syncthreads();
+  const uint32_t r = min(max(S.bc[4], f + 1), l - 1);
+  __syncthreads();
+  return r;
+}
+
+// The subtree of [f, f+len) (len <= IS_LCAP, depth d) from (Ki, Vi), finished in LDS;
+// the sorted run is written to (Ko, Vo) at the same positions.
+__device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, uint32_t* Ko, uint32_t* Vo, uint32_t f,
+                           uint32_t len, int d) {
+  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
+    S.k[q] = Ki[f + q];
+    S.v[q] = Vi[f + q];
+  }
+  for (uint32_t q = threadIdx.x; q < (len + 31) / 32; q += IS_OT) S.heads[q] = 0;
+  if (threadIdx.x == 0) {
+    S.bc[0] = 0;  // stack depth
+    S.bc[1] = 0;  // wave-list count
+    S.bc[2] = 0;  // wave-list head
+    if (len <= IS_THRESHOLD) {
+      S.heads[0] = 1u;
+    } else {
+      S.wstk[0] = make_uint2(0u, len | ((uint32_t)d << 16));
+      S.bc[0] = 1;
+    }
+  }
+  __syncthreads();
+  // workgroup phase: thread 0 walks the stack; entries above IS_WCAP are partitioned
+  // by the whole block, the others go to the leaves / heap sort / the wave list
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t go = 0;
+      while (S.bc[0] > 0 && !go) {
+        const uint2 it = S.wstk[--S.bc[0]];
+        const uint32_t off = it.x, n = it.y & 0xFFFFu;
+        const int dd = (int)(it.y >> 16);
+        if (n <= IS_THRESHOLD) {
+          if (n) mark_leaf(S, off);
+        } else if (dd == 0) {
+          heap_sort(S.k + off, S.v + off, (int64_t)n);
+          for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
+        } else if (n <= IS_WCAP) {
+          S.wlist[S.bc[1]++] = wpack(off, n, dd);
+        } else {
+          S.bc[6] = off;
+          S.bc[7] = it.y;
+          go = 1;
+        }
+      }
+      S.bc[3] = go;
+    }
+    __syncthreads();
+    if (!S.bc[3]) break;
+    const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
+    const int dd = (int)(S.bc[7] >> 16);
+    const uint32_t c = block_partition(S, off, off + n);
+    if (threadIdx.x == 0) {
+      const uint32_t nd = (uint32_t)(dd - 1) << 16;
+      S.wstk[S.bc[0]++] = make_uint2(c, (off + n - c) | nd);
+      S.wstk[S.bc[0]++] = make_uint2(off, (c - off) | nd);
+    }
+    __syncthreads();
+  }
+  // wave phase: each wave takes subtrees from the list
+  {
+    uint16_t* xch = S.xch + w * (IS_WCAP / 2);
+    for (;;) {
+      uint32_t idx = 0;
+      if (lane == 0) idx = atomicAdd(&S.bc[2], 1u);
+      idx = __shfl(idx, 0, 64);
+      if (idx >= S.bc[1]) break;
+      wave_sort(S, S.wlist[idx], S.vstk[w], xch);
+    }
+  }
+  __syncthreads();
+  // the final insertion sort: each leaf segment stably sorted in place
+  for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
+    uint32_t a = p;
+    while (a > 0 && !((S.heads[a >> 5] >> (a & 31)) & 1u)) --a;
+    uint32_t b = p + 1;
+    while (b < len && !((S.heads[b >> 5] >> (b & 31)) & 1u)) ++b;
+    const uint32_t key = S.k[p];
+    uint32_t rank = 0;
+    for (uint32_t q = a; q < b; ++q) {
+      const uint32_t kq = S.k[q];
+      rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
+    }
+    Ko[f + a + rank] = key;
+    Vo[f + a + rank] = S.v[p];
+  }
+  __syncthreads();
+}
+
+// One partition of [f, l) (l - f > IS_LCAP) in global memory by the whole block,
+// in place in (K, V); (SK, SV) at the same positions is scratch.  Returns the cut.
+__device__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
+                                     uint32_t l) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    const uint32_t m = median_pos(K, f, l);
+    const uint32_t tk = K[f], tv = V[f];
+    K[f] = K[m];
+    V[f] = V[m];
+    K[m] = tk;
+    V[m] = tv;
+    S.bc[4] = IS_NONE;
+    S.bc[0] = 0;  // running >= count
+    S.bc[1] = 0;  // running <= count
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint32_t P = K[f];
+  const uint32_t n = l - f - 1, H = (l - f) / 2;
+  // totals of <= P
+  uint32_t lc = 0;
+  for (uint32_t q = threadIdx.x; q < n; q += IS_OT) lc += K[f + 1 + q] <= P ? 1u : 0u;
+  uint32_t le_tot;
+  (void)block_excl_scan(lc, S.sh, &le_tot);
+  uint32_t cut = IS_NONE;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (threadIdx.x == 0) {
+      S.bc[0] = 0;
+      S.bc[1] = 0;
+    }
+    __syncthreads();
+    for (uint32_t s0 = 0; s0 < n; s0 += IS_LCAP) {
+      uint32_t kk[IS_OC], vv[IS_OC];
+#pragma unroll
+      for (int c = 0; c < IS_OC; ++c) {
+        const uint32_t q = s0 + c * IS_OT + threadIdx.x;
+        const bool ok = q < n;
+        kk[c] = ok ? K[f + 1 + q] : 0u;
+        vv[c] = ok ? V[f + 1 + q] : 0u;
+        const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+        if (lane == 0) {
+          S.cg[c * IS_OW + w] = (uint32_t)__popcll(bg);
+          S.cl[c * IS_OW + w] = (uint32_t)__popcll(bl);
+        }
+      }
+      __syncthreads();
+      if (w == 0) block_chunk_scan(S, S.bc[0], S.bc[1]);
+      __syncthreads();
+      if (threadIdx.x == 0) {  // running counts for the next superchunk
+        S.bc[0] = S.pg[IS_OE - 1] + S.cg[IS_OE - 1];
+        S.bc[1] = S.pl[IS_OE - 1] + S.cl[IS_OE - 1];
+      }
+#pragma unroll
+      for (int c = 0; c < IS_OC; ++c) {
+        const uint32_t q = s0 + c * IS_OT + threadIdx.x, p = f + 1 + q;
+        const bool ok = q < n;
+        const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+        const uint64_t bg = __ballot(ge), bl = __ballot(le);
+        const uint32_t g = S.pg[c * IS_OW + w] + mbcnt(bg), h = S.pl[c * IS_OW + w] + mbcnt(bl);
+        if (ge) {
+          const uint32_t k1 = g + 1;
+          if (le_tot - h - (le ? 1u : 0u) >= k1) {
+            if (pass == 0) {  // publish: the value R[k1] receives
+              SK[f + k1 - 1] = kk[c];
+              SV[f + k1 - 1] = vv[c];
+            } else {  // take L[k1]'s partner's value
+              K[p] = SK[f + H + k1 - 1];
+              V[p] = SV[f + H + k1 - 1];
+            }
+          } else {
+            cut = min(cut, p);
+          }
+        }
+        if (le) {
+          const uint32_t kr = le_tot - h;
+          if (g >= kr) {
+            if (pass == 0) {
+              SK[f + H + kr - 1] = kk[c];
+              SV[f + H + kr - 1] = vv[c];
+            } else {
+              K[p] = SK[f + kr - 1];
+              V[p] = SV[f + kr - 1];
+            }
+            cut = min(cut, p);
+          }
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  cut = wave_min_u32(cut);
+  if (lane == 0 && cut != IS_NONE) atomicMin(&S.bc[4], cut);
+  __syncthreads();
+  const uint32_t r = min(max(S.bc[4], f + 1), l - 1);
+  __syncthreads();
+  return r;
+}
+
+// One workgroup per remaining subtree: the final children of the last round first
+// (they may exceed IS_LCAP), then the owned list, dequeued from ctl[1].
+__global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<uint32_t*> K12,
+                                                  B2<uint32_t*> V12, B2<IsBufs> W2, int R) {
+  KT();
+  __shared__ OwnLds S;
+  __shared__ uint32_t s_idx;
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t nsort = W.ctl[0];
+  if (nsort == 0) return;
+  const uint32_t nfin = nchildren(W, R);
+  const uint32_t nown = R ? W.rounds[R - 1].nown : 0u;
+  uint32_t* Kb[2] = {K02[e], K12[e]};
+  uint32_t* Vb[2] = {V02[e], V12[e]};
+  for (;;) {
+    if (threadIdx.x == 0) s_idx = atomicAdd(&W.ctl[1], 1u);
+    __syncthreads();
+    const uint32_t idx = s_idx;
+    __syncthreads();
+    if (idx >= nfin + nown) break;
+    uint32_t f, l, buf;
+    int d;
+    if (idx < nfin) {
+      const Child c = child_of(W, R, nsort, idx);
+      f = c.f;
+      l = c.l;
+      d = c.d;
+      buf = (uint32_t)(R & 1);
+    } else {
+      const IsOwn o = W.own[idx - nfin];
+      f = o.f;
+      l = o.l;
+      d = o.depth;
+      buf = o.buf;
+    }
+    if (l <= f) continue;
+    uint32_t* K = Kb[buf];
+    uint32_t* V = Vb[buf];
+    if (threadIdx.x == 0) {
+      S.gstk[0] = make_uint4(f, l, (uint32_t)d, 0u);
+      S.gsp = 1;
+    }
+    __syncthreads();
+    for (;;) {
+      const uint32_t sp = S.gsp;
+      __syncthreads();
+      if (sp == 0) break;
+      const uint4 it = S.gstk[sp - 1];
+      const uint32_t gf = it.x, gl = it.y, len = gl - gf;
+      const int gd = (int)it.z;
+      __syncthreads();
+      if (threadIdx.x == 0) S.gsp = sp - 1;
+      __syncthreads();
+      if (len <= IS_LCAP) {
+        lds_finish(S, K, V, Kb[0], Vb[0], gf, len, gd);
+      } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
+        if (threadIdx.x == 0) {
+          heap_sort(K + gf, V + gf, (int64_t)len);
+          W.ctl[2] |= 2u;
+        }
+        __threadfence_block();
+        __syncthreads();
+        if (buf != 0)
+          for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
+            Kb[0][gf + q] = K[gf + q];
+            Vb[0][gf + q] = V[gf + q];
+          }
+        __syncthreads();
+      } else {
+        const uint32_t c = global_partition(S, K, V, Kb[buf ^ 1u], Vb[buf ^ 1u], gf, gl);
+        if (threadIdx.x == 0) {
+          W.ctl[2] |= 1u;
+          uint32_t s = S.gsp;
+          S.gstk[s++] = make_uint4(c, gl, (uint32_t)(gd - 1), 0u);
+          S.gstk[s++] = make_uint4(gf, c, (uint32_t)(gd - 1), 0u);
+          S.gsp = s;
+        }
+        __threadfence_block();
+        __syncthreads();
+      }
+    }
+  }
+}
+
+}  // namespace
+
+uint32_t introsort_segmax(uint32_t cap) { return cap / IS_LCAP + 2; }
+uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
+
+int introsort_rounds(uint32_t cap) {
+  static const int env = [] {
+    const char* s = std::getenv("FCCF_IS_ROUNDS");
+    return s ? std::atoi(s) : -1;
+  }();
+  int r = 0;
+  if (cap > IS_LCAP) {
+    while ((uint64_t)IS_LCAP << r < cap) ++r;  // ceil(log2(cap / IS_LCAP))
+    r += 2;
+  }
+  if (env >= 0) r = env;
+  return r > IS_RMAX ? IS_RMAX : r;
+}
+
+size_t introsort_bytes(uint32_t cap) {
+  const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
+  const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
+  return 256 + 64 + 8 * mt + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
+         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 8 * 256;
+}
+
+IsBufs introsort_carve(void* base, uint32_t cap) {
+  char* p = (char*)base;
+  auto take = [&](size_t b) {
+    char* r = p;
+    p += (b + 255) & ~size_t(255);
+    return (void*)r;
+  };
+  IsBufs b;
+  b.segmax = introsort_segmax(cap);
+  b.maxtiles = introsort_maxtiles(cap);
+  b.ownmax = 2 * b.segmax * (IS_RMAX + 1) + 4;
+  b.ctl = (uint32_t*)take(64);
+  b.cnt = (uint32_t*)take(8 * (size_t)b.maxtiles);
+  b.gel = (uint16_t*)take(2 * ((size_t)cap + 64));
+  b.lel = (uint16_t*)take(2 * ((size_t)cap + 64));
+  b.rounds = (IsRound*)take(sizeof(IsRound) * IS_RMAX);
+  b.segs = (IsSeg*)take(sizeof(IsSeg) * (size_t)b.segmax * IS_RMAX);
+  b.cuts = (uint32_t*)take(4 * (size_t)b.segmax * IS_RMAX);
+  b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
+  return b;
+}
+
+void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                   B2<const VGParams*> P, uint32_t cap, B2<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate) {
+  const int R = exact_gate ? 0 : introsort_rounds(cap);
+  k_is_prep<<<dim3(1, nbatch), 1024, 0, st>>>(k0, v0, d_n, P, b, exact_gate ? 1 : 0);
+  const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap);
+  const size_t lds_count = 16 * (size_t)segmax, lds_scatter = 4 * ((size_t)segmax + 2 * (size_t)maxtiles);
+  for (int r = 0; r < R; ++r) {
+    const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
+    const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
+    k_is_count<<<dim3(maxtiles, nbatch), IS_TT, lds_count, st>>>(B2<const uint32_t*>(ki), b, r);
+    k_is_scatter<<<dim3(maxtiles, nbatch), IS_TT, lds_scatter, st>>>(B2<const uint32_t*>(ki),
+                                                                      B2<const uint32_t*>(vi), ko, vo, b, r);
+  }
+  k_is_own<<<dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st>>>(k0, v0, k1, v1, b, R);
+}
+
+}  // namespace fccf

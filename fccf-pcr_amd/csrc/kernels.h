@@ -26,6 +26,42 @@ struct VGParams {
 constexpr int VG_BBOX_BLOCKS = 512;
 constexpr int VG_KEY_BLOCKS = 512;
 
+// K1's sort in libstdc++ std::sort order (introsort.hip): workspace of one cloud.
+constexpr int IS_RMAX = 24;          // most partition rounds before the owner kernel
+constexpr int IS_OWN_BLOCKS = 256;   // owner workgroups per cloud (two per CU fit)
+struct IsRound {
+  uint32_t nseg, ntiles, nown, pad;  // large segments, their tiles, owned entries so far
+};
+struct IsSeg {
+  uint32_t f, l;
+  int32_t depth;
+  uint32_t tile0;
+};
+struct IsOwn {
+  uint32_t f, l;
+  int32_t depth;
+  uint32_t buf;  // which of the two key/value buffers holds the segment
+};
+struct IsBufs {
+  uint32_t* ctl;        // [0] sort length, [1] owner dequeue head, [2] slow paths taken (1 global partition, 2 heap)
+  uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
+  uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
+  IsRound* rounds;      // IS_RMAX
+  IsSeg* segs;          // IS_RMAX x segmax
+  uint32_t* cuts;       // IS_RMAX x segmax
+  IsOwn* own;           // ownmax
+  uint32_t segmax, maxtiles, ownmax;
+};
+size_t introsort_bytes(uint32_t cap);
+IsBufs introsort_carve(void* base, uint32_t cap);
+int introsort_rounds(uint32_t cap);
+// Sort (k0, v0)[0..n) -- keys with 0xFFFFFFFF for non-finite points, values the input
+// positions -- exactly as std::sort orders PCL's index vector of the finite points;
+// the result is left in (k0, v0) with the invalid keys after it.  (k1, v1) are the
+// other buffer.  exact_gate: sort only if P->unsorted (the presorted second pass).
+void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
+                   B2<const VGParams*> P, uint32_t cap, B2<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate);
+
 struct VGBufs {
   uint32_t *k0, *v0, *k1, *v1;  // cap each
   uint32_t* starts;             // cap + 1
@@ -33,14 +69,16 @@ struct VGBufs {
   VGParams* params;
   uint32_t* nseg;
   SortScratch ss;
+  IsBufs is;
 };
 
-// xyz[0..*d_n) -> out[0..*d_m), PCL VoxelGrid<PointXYZ> semantics with stable
-// (ascending input index) accumulation inside a leaf.
+// xyz[0..*d_n) -> out[0..*d_m), PCL VoxelGrid<PointXYZ> semantics: the points of a
+// leaf are accumulated in the order libstdc++ std::sort leaves them (introsort.hip).
 // presorted: the input is expected to be in (nearly) ascending leaf order -- the
 // driver's second pass over main's output (:1377-1387 after :1668-1678).  A check
-// kernel then skips the radix passes when the keys are already strictly increasing
-// (every leaf holds one point), which leaves the result unchanged.
+// kernel then skips the sort when the keys are already strictly increasing (every
+// leaf holds one point, so the order cannot matter); otherwise one workgroup per
+// cloud runs the whole std::sort.
 // nbatch = 2 runs both clouds (argument pairs, blockIdx.y = cloud) in the same launches.
 // out_copy (optional): every output point is also written there, and
 // VGParams::nonfinite is set when one is not finite (the driver's remove-NaN after

@@ -7,7 +7,7 @@ namespace fccf {
 
 inline size_t voxel_grid_bytes(uint32_t cap) {
   return 4 * sizeof(uint32_t) * (size_t)cap + sizeof(uint32_t) * ((size_t)cap + 1) + sizeof(float) * VG_BBOX_BLOCKS * 8 +
-         sizeof(VGParams) + 64 + sort_scratch_bytes(cap) + 7 * 256;
+         sizeof(VGParams) + 64 + sort_scratch_bytes(cap) + introsort_bytes(cap) + 8 * 256;
 }
 
 inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
@@ -21,6 +21,7 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
   b.params = a.take_n<VGParams>(1);
   b.nseg = a.take_n<uint32_t>(16);
   b.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
+  b.is = introsort_carve(a.take(introsort_bytes(cap)), cap);
   return b;
 }
 

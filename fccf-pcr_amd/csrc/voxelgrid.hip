@@ -5,11 +5,11 @@
 //   bbox over finite points -> int32 overflow guard (output = input) ->
 //   idx = ijk0 + ijk1*div0 + ijk2*div0*div1 with ijk = int(floor(p*inv) - float(min_b))
 //   -> sort (idx, index) -> one centroid per run, Vector3f sum / n, ascending idx.
-// PCL sorts with unstable std::sort; this kernel sums each leaf in ascending input
-// index order (a conforming std::sort outcome), exactly as the oracle's stable mode.
+// PCL sorts with libstdc++ std::sort (introsort, unstable); introsort.hip reproduces
+// its order, so each leaf is summed in exactly the reference's order.
 //
-// HBM traffic per pass (algorithmic): read 12 B/pt, write 12 B/leaf; the radix sort
-// adds 2 x (4+4) B/pt per 8-bit digit pass.
+// HBM traffic per pass (algorithmic): read 12 B/pt, write 12 B/leaf; the sort adds
+// its rounds and the owner pass (introsort.hip).
 #define KT_TU 2  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
@@ -179,7 +179,7 @@ __device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, 
   return (uint32_t)((int64_t)i0 + (int64_t)i1 * q.mul1 + (int64_t)i2 * q.mul2);
 }
 
-// Leaf keys.  presorted (the driver's second pass): vals = identity, and a key not
+// Leaf keys and vals = identity.  presorted (the driver's second pass): a key not
 // strictly above its predecessor -- or any non-finite point -- sets P->unsorted;
 // otherwise every leaf holds exactly one point and the pass is the identity (the
 // sort tail, segmentation and centroid kernels take their shortcut).
@@ -216,8 +216,8 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
     k.z = vg_key(q, b.z, b.w, c.x);
     k.w = vg_key(q, c.y, c.z, c.w);
     reinterpret_cast<uint4*>(keys)[qd] = k;
+    reinterpret_cast<uint4*>(vals)[qd] = make_uint4(i0, i0 + 1, i0 + 2, i0 + 3);
     if (presorted) {
-      reinterpret_cast<uint4*>(vals)[qd] = make_uint4(i0, i0 + 1, i0 + 2, i0 + 3);
       bad |= k.x == 0xFFFFFFFFu || k.y == 0xFFFFFFFFu || k.z == 0xFFFFFFFFu || k.w == 0xFFFFFFFFu;
       bad |= !(k.x < k.y) || !(k.y < k.z) || !(k.z < k.w);
       if (i0 + 4 < n && !(k.w < vg_key(q, xyz[3 * i0 + 12], xyz[3 * i0 + 13], xyz[3 * i0 + 14]))) bad = true;
@@ -226,8 +226,8 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
   for (uint32_t i = 4 * nq + gid; i < n; i += gsz) {
     const uint32_t key = vg_key(q, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
     keys[i] = key;
+    vals[i] = i;
     if (presorted) {
-      vals[i] = i;
       if (key == 0xFFFFFFFFu) bad = true;
       if (i + 1 < n && !(key < vg_key(q, xyz[3 * i + 3], xyz[3 * i + 4], xyz[3 * i + 5]))) bad = true;
     }
@@ -360,12 +360,14 @@ void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, flo
   // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
   const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
   FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, xyz, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
+  const B2<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
+  const B2<const VGParams*> Pc(P[0], P[1]);
   if (!presorted) {
-    radix_sort_u32(k0, v0, k1, v1, d_n, cap, nbits, 32, true, ss, st, nbatch);
+    introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, false);
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch);
-  } else {  // usually already in leaf order: a tail-only sort and segmentation that run only if not
-    radix_sort_u32(k0, v0, k1, v1, d_n, cap, nbits, 0, false, ss, st, nbatch, unsorted);
+  } else {  // usually already in leaf order: a sort and segmentation that run only if not
+    introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, true);
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch, unsorted);
   }

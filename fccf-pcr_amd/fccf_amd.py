@@ -95,6 +95,7 @@ _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
 _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
      ctypes.POINTER(ctypes.c_double))
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
+_sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
 _sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
@@ -237,6 +238,15 @@ class Ctx:
         _check(f(self._h, a.ctypes.data, a.shape[0], float(leaf), out.ctypes.data, ctypes.byref(m)),
                "fccf_stage_downsample", self._h)
         return out[: m.value].copy()
+
+    def sort_keys(self, keys, exact_gate: bool = False) -> np.ndarray:
+        """K1's sort (std::sort order) of u32 leaf keys on the GPU; returns the input
+        positions of the keys != 0xFFFFFFFF in sorted order (test hook)."""
+        k = np.ascontiguousarray(keys, np.uint32)
+        perm = np.zeros(max(k.size, 1), np.uint32)
+        _check(_lib.fccf_debug_sort_keys(self._h, k.ctypes.data, k.size, int(exact_gate), perm.ctypes.data),
+               "fccf_debug_sort_keys", self._h)
+        return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
 
     def voxel_planes(self, xyz, params: Params | None = None):
         """face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled cloud on the GPU.

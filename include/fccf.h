@@ -220,6 +220,13 @@ int fccf_probe_read(fccf_ctx* ctx, double* total_ms, int64_t* launches, double* 
 int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes,
                    int64_t* n_bytes);
 
+/* Test hook of K1's sort (the std::sort of pcl::VoxelGrid's index vector,
+ * FCCF.cpp:1668-1678): keys[0..n) (0xFFFFFFFF = a non-finite point, skipped as PCL
+ * skips it) with values = input positions, sorted on the GPU in libstdc++ std::sort
+ * order; perm_out[0..n) receives the values in sorted order (the finite ones first).
+ * exact_gate != 0 runs the presorted second pass's single-workgroup form. */
+int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm_out);
+
 /* PLY I/O (the reference's pcl::io::loadPLYFile<PointXYZ> surface, FCCF.cpp:1655-1665):
  * ascii / binary_little_endian / binary_big_endian, float x,y,z (double converted).
  * *xyz is malloc'd by the library; release with fccf_free. */

@@ -1574,6 +1574,33 @@ extern "C" int64_t orc_voxel_grid(const float* xyz, int64_t n, float leaf, int o
   return (int64_t)npts(o);
 }
 
+extern "C" int64_t orc_sort_pairs(const uint32_t* keys, int64_t n, uint32_t* perm) {
+  std::vector<IdxPair> iv;  // pcl::VoxelGrid::applyFilter's index_vector (App. A2 steps 5-6)
+  for (int64_t i = 0; i < n; ++i)
+    if (keys[i] != 0xFFFFFFFFu) iv.push_back({keys[i], (unsigned int)i});
+  std::sort(iv.begin(), iv.end(), std::less<IdxPair>());
+  for (size_t i = 0; i < iv.size(); ++i) perm[i] = iv[i].cloud_point_index;
+  return (int64_t)iv.size();
+}
+
+extern "C" void orc_sort_adversary(int64_t n, uint32_t* keys) {
+  // M. D. McIlroy, "A killer adversary for quicksort" (1999): values are frozen lazily
+  // so that every partition is as unbalanced as the comparisons allow
+  std::vector<int64_t> val((size_t)n, -1);
+  std::vector<uint32_t> idx((size_t)n);
+  for (int64_t i = 0; i < n; ++i) idx[(size_t)i] = (uint32_t)i;
+  int64_t nsolid = 0, candidate = 0;
+  const int64_t gas = n;
+  std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+    if (val[x] < 0 && val[y] < 0) val[(int64_t)x == candidate ? x : y] = nsolid++;
+    if (val[x] < 0) candidate = x;
+    else if (val[y] < 0) candidate = y;
+    const int64_t vx = val[x] < 0 ? gas : val[x], vy = val[y] < 0 ? gas : val[y];
+    return vx < vy;
+  });
+  for (int64_t i = 0; i < n; ++i) keys[i] = (uint32_t)(val[(size_t)i] < 0 ? gas : val[(size_t)i]);
+}
+
 extern "C" void orc_eigen33(const float cov[9], float* ev, float vec[3]) {
   float m[3][3];
   for (int i = 0; i < 3; ++i)

@@ -39,6 +39,13 @@ void orc_times(orc_ctx* c, double out_ms[9]);
 /* Single stages (known-answer tests). */
 int64_t orc_voxel_grid(const float* xyz, int64_t n, float leaf, int order, float* out_xyz,
                        int* overflow);
+/* std::sort of PCL VoxelGrid's (idx, cloud_point_index) pairs (compared by idx only)
+ * over the keys != 0xFFFFFFFF in input order; perm_out receives cloud_point_index in
+ * sorted order.  Returns the number of sorted pairs. */
+int64_t orc_sort_pairs(const uint32_t* keys, int64_t n, uint32_t* perm_out);
+/* Keys that drive libstdc++ std::sort to its depth limit (McIlroy's adversary run
+ * against this std::sort), for the heap-sort fallback tests. */
+void orc_sort_adversary(int64_t n, uint32_t* keys_out);
 /* pcl::eigen33 + curvature on a symmetric 3x3 (row-major) covariance. */
 void orc_eigen33(const float cov[9], float* eigenvalue, float vec[3]);
 /* compute_normal_angel (FCCF.cpp:369-377). */

@@ -27,6 +27,9 @@ def _load():
     lib.orc_times.argtypes = [P, P]
     lib.orc_voxel_grid.restype = I64
     lib.orc_voxel_grid.argtypes = [P, I64, ctypes.c_float, ctypes.c_int, P, ctypes.POINTER(ctypes.c_int)]
+    lib.orc_sort_adversary.argtypes = [I64, P]
+    lib.orc_sort_pairs.restype = I64
+    lib.orc_sort_pairs.argtypes = [P, I64, P]
     lib.orc_eigen33.argtypes = [P, P, P]
     lib.orc_normal_angle.restype = ctypes.c_float
     lib.orc_normal_angle.argtypes = [ctypes.c_float] * 6
@@ -79,6 +82,20 @@ def voxel_grid(xyz, leaf, order=STABLE):
     ovf = ctypes.c_int(0)
     m = lib.orc_voxel_grid(a.ctypes.data, a.shape[0], float(leaf), int(order), out.ctypes.data, ctypes.byref(ovf))
     return out[:m].copy(), bool(ovf.value)
+
+
+def sort_pairs(keys):
+    """std::sort order of PCL's (idx, index) pairs for the keys != 0xFFFFFFFF."""
+    k = np.ascontiguousarray(keys, np.uint32)
+    perm = np.zeros(max(k.size, 1), np.uint32)
+    m = lib.orc_sort_pairs(k.ctypes.data, k.size, perm.ctypes.data)
+    return perm[:m].copy()
+
+
+def sort_adversary(n):
+    k = np.zeros(max(n, 1), np.uint32)
+    lib.orc_sort_adversary(n, k.ctypes.data)
+    return k[:n].copy()
 
 
 def eigen33(cov):

@@ -22,3 +22,27 @@ def test_bench_two_ranks_gloo(tmp_path):
     # value = K summed over both ranks / the slowest rank's wall time
     assert abs(d["value"] - 2 * 5 * 100 / (d["ms_per_step"] * 5 / 1e3)) / d["value"] < 1e-6
     assert d["data"] == "selftest-stub" and "cpu_baseline" not in d
+
+
+def test_bench_gpus2_self_launch(tmp_path):
+    """--gpus 2 with no external launcher: bench.py starts its own two rank processes
+    and reports n_gpus 2 (never silently one GPU)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--config", "c2", "--selftest"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "replicas x2"
+    assert abs(d["value"] - 2 * 4 * 100 / (d["ms_per_step"] * 4 / 1e3)) / d["value"] < 1e-6
+
+
+def test_bench_world_size_mismatch_fails(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--config", "c2", "--selftest"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=str(tmp_path))
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -1,0 +1,104 @@
+"""K1's sort in the reference's order: the GPU reproduction of libstdc++ std::sort
+(introsort) over PCL VoxelGrid's (idx, cloud_point_index) pairs (FCCF.cpp:1668-1678,
+:1377-1387), compared with the oracle's std::sort, and the
+VoxelGrid passes built on it compared with the oracle's INTROSORT mode.
+
+Integer permutation work: the bar is bit-exact equality.  The CPU tests pin the
+oracle side (std::sort is a valid sort, the adversary reaches the heap-sort depth).
+"""
+import numpy as np
+import pytest
+
+INVALID = np.uint32(0xFFFFFFFF)
+
+
+def _keys_cases(fccf, oracle):
+    rng = np.random.default_rng(7)
+    cases = {}
+    for n in (0, 1, 2, 3, 16, 17, 18, 33, 64, 65, 100, 1000, 1023, 1024, 1025, 4096, 7680, 7681, 7700, 15000, 40000):
+        cases[f"rand8_{n}"] = rng.integers(0, 8, n).astype(np.uint32)
+        cases[f"randbig_{n}"] = rng.integers(0, 1 << 30, n).astype(np.uint32)
+    cases["sorted_50k"] = np.arange(50_000, dtype=np.uint32) // 3
+    cases["reversed_50k"] = (np.arange(50_000, dtype=np.uint32) // 3)[::-1].copy()
+    cases["const_30k"] = np.full(30_000, 5, np.uint32)
+    cases["dups_300k"] = rng.integers(0, 60_000, 300_000).astype(np.uint32)
+    # spatially ordered leaf keys of a synthetic room (the VoxelGrid workload's structure)
+    pts = fccf.synth_scene(200_000, seed=3)
+    inv = np.float32(1.0) / np.float32(0.05)
+    mn = pts.min(0)
+    minb = np.floor(mn * inv).astype(np.int64)
+    div = np.floor(pts.max(0) * inv).astype(np.int64) - minb + 1
+    ijk = (np.floor(pts * inv) - minb.astype(np.float32)).astype(np.int64)
+    cases["room_200k"] = (ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]).astype(np.uint32)
+    k = cases["room_200k"].copy()
+    k[rng.integers(0, k.size, 500)] = INVALID  # non-finite points: PCL skips them
+    cases["room_200k_nan"] = k
+    cases["all_invalid_100"] = np.full(100, INVALID, np.uint32)
+    # depth-limit (heap sort) paths: McIlroy adversaries against this std::sort
+    for n in (200, 5000, 20_000):
+        cases[f"adversary_{n}"] = oracle.sort_adversary(n)
+    return cases
+
+
+def test_oracle_sort_pairs_is_a_sort(oracle):
+    rng = np.random.default_rng(1)
+    k = rng.integers(0, 50, 10_000).astype(np.uint32)
+    k[::97] = INVALID
+    p = oracle.sort_pairs(k)
+    assert p.size == np.count_nonzero(k != INVALID)
+    assert np.all(np.diff(k[p].astype(np.int64)) >= 0)
+    assert np.array_equal(np.sort(p), np.flatnonzero(k != INVALID))
+    # unstable: equal keys are not all in input order (otherwise the order would not matter)
+    assert not np.array_equal(p, np.flatnonzero(k != INVALID)[np.argsort(k[k != INVALID], kind="stable")])
+
+
+def test_oracle_adversary_is_deep(oracle):
+    k = oracle.sort_adversary(4096)
+    assert k.size == 4096 and np.all(np.diff(k[oracle.sort_pairs(k)].astype(np.int64)) >= 0)
+
+
+@pytest.mark.gpu
+def test_sort_keys_equals_std_sort(ctx, fccf, oracle):
+    bad = []
+    for name, k in _keys_cases(fccf, oracle).items():
+        got = ctx.sort_keys(k)
+        ref = oracle.sort_pairs(k)
+        if not np.array_equal(got, ref):
+            bad.append((name, k.size, int(np.count_nonzero(got[:ref.size] != ref)) if got.size == ref.size else -1))
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_sort_keys_exact_gate_equals_std_sort(ctx, fccf, oracle):
+    """The presorted pass's single-workgroup form (no rounds) on the same cases."""
+    bad = []
+    for name, k in _keys_cases(fccf, oracle).items():
+        if k.size > 60_000:
+            continue
+        if not np.array_equal(ctx.sort_keys(k, exact_gate=True), oracle.sort_pairs(k)):
+            bad.append(name)
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_sort_keys_c3_leaf_keys(ctx, fccf, oracle):
+    """The headline workload's first-pass keys (1M points, 0.05 m): deep, unbalanced tree."""
+    c = fccf.CONFIGS["c3"]
+    src, tar, _ = fccf.synth_pair(c["n"], c["room"])
+    for pts in (src, tar):
+        inv = np.float32(1.0) / np.float32(c["leaf"])
+        minb = np.floor(pts.min(0) * inv).astype(np.int64)
+        div = np.floor(pts.max(0) * inv).astype(np.int64) - minb + 1
+        ijk = (np.floor(pts * inv) - minb.astype(np.float32)).astype(np.int64)
+        k = (ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]).astype(np.uint32)
+        assert np.array_equal(ctx.sort_keys(k), oracle.sort_pairs(k))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,leaf,seed", [(20_000, 0.1, 1), (150_000, 0.05, 2), (1_000_000, 0.05, 5)])
+def test_downsample_equals_reference_order(ctx, fccf, oracle, n, leaf, seed):
+    pts = fccf.synth_scene(n, seed=seed)
+    out = ctx.downsample(pts, leaf)
+    ref, _ = oracle.voxel_grid(pts, leaf, oracle.INTROSORT)
+    assert out.shape == ref.shape
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
