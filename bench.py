@@ -314,6 +314,10 @@ def main():
                                    for k, v in table.items()}
         if ws == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(src, tar, leaf, args.cpu_budget)
+            # the CPU and GPU runs must do the same work (same plane pairs, same K)
+            if out["cpu_baseline"]["K"] != out["K_per_registration"]:
+                raise SystemExit(f"bench.py: cpu_baseline K {out['cpu_baseline']['K']} != GPU K "
+                                 f"{out['K_per_registration']}")
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

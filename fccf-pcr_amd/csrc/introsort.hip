@@ -31,6 +31,9 @@
 // HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); k_is_own reads and
 // writes each element once more (8 + 8 B) when its subtree fits in LDS.
 #define KT_TU 9  // ktrace.h source tag
+#include <cstdio>
+#include <cstdlib>
+
 #include "probe.h"
 #include "kernels.h"
 
@@ -40,19 +43,22 @@ namespace {
 constexpr uint32_t IS_TILE = 4096;   // elements per round tile
 constexpr int IS_TT = 256;           // round kernels: threads per block
 constexpr int IS_TC = IS_TILE / IS_TT;  // 16 elements per thread
-constexpr uint32_t IS_LCAP = 7680;   // largest segment finished in LDS (15 per thread: 2 blocks per CU fit)
-constexpr int IS_OT = 512;           // owner: threads per block
+constexpr uint32_t IS_LCAP = 8192;   // largest segment finished in LDS
+constexpr int IS_OT = 1024;          // owner: threads per block (16 waves, one block per CU)
 constexpr int IS_OW = IS_OT / 64;    // owner: waves
-constexpr int IS_OC = IS_LCAP / IS_OT;  // 15 elements per thread in a workgroup partition
+constexpr int IS_OC = IS_LCAP / IS_OT;  // 8 elements per thread in a workgroup partition
 constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a workgroup partition
-constexpr uint32_t IS_WCAP = 1024;   // largest segment partitioned by one wave
-constexpr int IS_WC = IS_WCAP / 64;  // 16 elements per lane
+constexpr uint32_t IS_WCAP = 512;    // largest segment partitioned by one wave
+constexpr int IS_WC = IS_WCAP / 64;  // 8 elements per lane
 constexpr uint32_t IS_THRESHOLD = 16;  // libstdc++ _S_threshold
-constexpr int IS_STACK = 48;
+constexpr int IS_STACK = 96;  // a wave's stack also holds its register-mode subtree (depth <= 48 each)
 constexpr int IS_WLIST = 512;
 // packed u32 subtree of at most IS_WCAP elements: off (13 bits) | len (11) | depth (6)
 __device__ __forceinline__ uint32_t wpack(uint32_t off, uint32_t len, int d) { return off | (len << 13) | ((uint32_t)d << 24); }
 constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
+#ifndef IS_STATS
+#define IS_STATS 1  // path counters in IsBufs::ctl[3..] (tests/tools read them)
+#endif
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
@@ -87,7 +93,7 @@ __device__ __forceinline__ uint32_t median_pos(KP K, uint32_t f, uint32_t l) {
 
 // std::__adjust_heap / __make_heap / __sort_heap on (K, V) pairs by key (one thread)
 template <class KP, class VP>
-__device__ void adjust_heap(KP K, VP V, int64_t hole, int64_t len, uint32_t vk, uint32_t vv) {
+__device__ __forceinline__ void adjust_heap(KP K, VP V, int64_t hole, int64_t len, uint32_t vk, uint32_t vv) {
   const int64_t top = hole;
   int64_t sc = hole;
   while (sc < (len - 1) / 2) {
@@ -114,7 +120,7 @@ __device__ void adjust_heap(KP K, VP V, int64_t hole, int64_t len, uint32_t vk, 
   V[hole] = vv;
 }
 template <class KP, class VP>
-__device__ void heap_sort(KP K, VP V, int64_t len) {  // std::__partial_sort(first, last, last)
+__device__ __forceinline__ void heap_sort(KP K, VP V, int64_t len) {  // std::__partial_sort(first, last, last)
   if (len < 2) return;
   for (int64_t parent = (len - 2) / 2;; parent--) {
     adjust_heap(K, V, parent, len, K[parent], V[parent]);
@@ -193,8 +199,7 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
   if (exact_gate && P->unsorted == 0u) ns = 0;
   if (threadIdx.x == 0) {
     W.ctl[0] = ns;
-    W.ctl[1] = 0;
-    W.ctl[2] = 0;
+    for (int i = 1; i < 16; ++i) W.ctl[i] = 0;
   }
   if (ns == 0 || ns >= n) return;
   uint32_t* K = K2[e];
@@ -221,7 +226,7 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
 // This round's large segments, built by every block from the previous round's
 // table and cuts (tiny); block 0 publishes them, initialises the cuts and appends the
 // finished-as-small children to the owned list.  Dynamic LDS: 4 * segmax u32.
-__device__ uint32_t build_round(const IsBufs& W, int r, uint32_t nsort, uint32_t* tf, uint32_t* tl, int32_t* td,
+__device__ __forceinline__ uint32_t build_round(const IsBufs& W, int r, uint32_t nsort, uint32_t* tf, uint32_t* tl, int32_t* td,
                                 uint32_t* t0, uint32_t* sh, uint32_t* ntiles_out) {
   const uint32_t nch = nchildren(W, r);
   const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
@@ -470,6 +475,9 @@ struct OwnLds {
   uint32_t vstk[IS_OW][IS_STACK];   // per-wave stacks (wpack)
   uint4 gstk[IS_STACK];             // global-phase stack {f, l, depth, -}
   uint32_t gsp;                     // its depth
+  uint32_t* stat;                   // IsBufs::ctl (path counters)
+  uint32_t lstat[4];                // this subtree's counters (flushed to stat once per subtree)
+  uint32_t* prg;                    // dev progress record (null = off)
   uint32_t bc[8];                   // broadcasts
   uint32_t sh[16];
 };
@@ -498,93 +506,230 @@ __device__ __forceinline__ void block_chunk_scan(OwnLds& S, uint32_t cg0, uint32
 
 __device__ __forceinline__ void mark_leaf(OwnLds& S, uint32_t off) { atomicOr(&S.heads[off >> 5], 1u << (off & 31)); }
 
-// One partition of [f, l) (17 <= l - f <= IS_WCAP) in LDS by one wave; returns the cut.
-__device__ uint32_t wave_partition(OwnLds& S, uint32_t f, uint32_t l, uint16_t* xch) {
+// Position of the r-th (0-based) set bit of m (r < popcount(m)).
+__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t r) {
+  uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)m);
+  if (r >= c) {
+    r -= c;
+    m >>= 32;
+    pos = 32;
+  }
+  uint32_t x = (uint32_t)m;
+#pragma unroll
+  for (int wdt = 16; wdt >= 2; wdt >>= 1) {
+    c = (uint32_t)__popc(x & ((1u << wdt) - 1u));
+    if (r >= c) {
+      r -= c;
+      x >>= wdt;
+      pos += (uint32_t)wdt;
+    }
+  }
+  return pos + (r >= (x & 1u) ? 1u : 0u);
+}
+
+// One partition of [f, l) (17 <= l - f <= 64 * C) in LDS by one wave; returns the cut.
+// C (chunks of 64 per lane) is chosen per segment: a wave executes every unrolled
+// chunk at full cost whatever its exec mask, and most partitions are small.  The
+// median-to-first swap is applied in registers (position m holds the old first
+// element, position f receives the pivot).  C == 1: swap partners are selected
+// straight from the ballot masks; larger C exchange positions through LDS slots.
+// The cut is the first position that is a non-swapped >= element or a swapped <=
+// element (min(L[K+1], R[K])), found from ballots.
+template <int C>
+__device__ __forceinline__ uint32_t wave_partition(OwnLds& S, uint32_t f, uint32_t l, uint16_t* xch) {
   const uint32_t lane = lane_id();
   const uint32_t m = median_pos(S.k, f, l);
-  if (lane == 0) {
-    const uint32_t tk = S.k[f], tv = S.v[f];
-    S.k[f] = S.k[m];
-    S.v[f] = S.v[m];
-    S.k[m] = tk;
-    S.v[m] = tv;
-  }
-  wsync();
-  const uint32_t P = S.k[f];
+  const uint32_t kf = S.k[f], vf = S.v[f], P = S.k[m], vm = S.v[m];
   const uint32_t n = l - f - 1;
-  uint32_t kk[IS_WC], vv[IS_WC];
-  uint64_t bg[IS_WC], bl[IS_WC];
-#pragma unroll
-  for (int c = 0; c < IS_WC; ++c) {
-    const uint32_t q = c * 64 + lane;
-    const bool ok = q < n;
-    kk[c] = ok ? S.k[f + 1 + q] : 0u;
-    vv[c] = ok ? S.v[f + 1 + q] : 0u;
-    bg[c] = __ballot(ok && kk[c] >= P);
-    bl[c] = __ballot(ok && kk[c] <= P);
-  }
+  uint32_t kk[C], vv[C];
   uint32_t le_tot = 0;
 #pragma unroll
-  for (int c = 0; c < IS_WC; ++c) le_tot += (uint32_t)__popcll(bl[c]);
-  uint32_t cut = IS_NONE;
-  uint32_t kg[IS_WC], kl[IS_WC];  // 1-based swap ranks (0 = not swapped)
-  uint32_t gx = 0, lx = 0;        // counts before this chunk
-#pragma unroll
-  for (int c = 0; c < IS_WC; ++c) {
+  for (int c = 0; c < C; ++c) {
     const uint32_t q = c * 64 + lane, p = f + 1 + q;
-    const bool ge = (bg[c] >> lane) & 1ull, le = (bl[c] >> lane) & 1ull;
-    const uint32_t g = gx + mbcnt(bg[c]), h = lx + mbcnt(bl[c]);
-    kg[c] = 0;
-    kl[c] = 0;
-    if (ge) {
-      if (le_tot - h - (le ? 1u : 0u) >= g + 1) kg[c] = g + 1;
-      else cut = min(cut, p);
+    const bool ok = q < n;
+    kk[c] = ok ? S.k[p] : 0u;
+    vv[c] = ok ? S.v[p] : 0u;
+    if (p == m) {
+      kk[c] = kf;
+      vv[c] = vf;
     }
-    if (le) {
-      const uint32_t kr = le_tot - h;
-      if (g >= kr) {
-        kl[c] = kr;
-        cut = min(cut, p);
+    le_tot += (uint32_t)__popcll(__ballot(ok && kk[c] <= P));
+  }
+  uint32_t cut = IS_NONE;
+  // sw[c]: 1-based swap rank as a >= element (low 16 bits) / as a <= element (high 16)
+  uint32_t sw[C];
+  uint32_t gx = 0, lx = 0;  // counts before this chunk
+  uint64_t bg0 = 0, bl0 = 0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const bool ok = c * 64 + lane < n;
+    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    if (c == 0) {
+      bg0 = bg;
+      bl0 = bl;
+    }
+    const uint32_t g = gx + mbcnt(bg), h = lx + mbcnt(bl);
+    const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
+    const bool sl = le && g >= le_tot - h;
+    sw[c] = (sg ? g + 1 : 0u) | ((sl ? le_tot - h : 0u) << 16);
+    const uint64_t cand = __ballot((ge && !sg) || sl);
+    if (cut == IS_NONE && cand) cut = f + 1 + (uint32_t)(c * 64) + (uint32_t)(__ffsll((unsigned long long)cand) - 1);
+    if (C > 1 && sg) xch[g] = (uint16_t)(f + 1 + c * 64 + lane);
+    gx += (uint32_t)__popcll(bg);
+    lx += (uint32_t)__popcll(bl);
+  }
+  if (C == 1) {
+    const uint32_t kg = sw[0] & 0xFFFFu, kl = sw[0] >> 16;
+    uint32_t d = f + 1 + lane;  // own position: only m must be rewritten when not swapped
+    if (kg) d = f + 1 + select64(bl0, le_tot - kg);
+    else if (kl) d = f + 1 + select64(bg0, kl - 1);
+    if (kg || kl || d == m) {
+      S.k[d] = kk[0];
+      S.v[d] = vv[0];
+    }
+  } else {
+    wsync();
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const uint32_t kl = sw[c] >> 16;
+      if (kl) {  // take L[kr], leave R[kr] (this position) for its partner
+        const uint32_t d = xch[kl - 1];
+        xch[kl - 1] = (uint16_t)(f + 1 + c * 64 + lane);
+        sw[c] = (sw[c] & 0xFFFFu) | (d << 16);
       }
     }
-    if (kg[c]) xch[kg[c] - 1] = (uint16_t)p;
-    gx += (uint32_t)__popcll(bg[c]);
-    lx += (uint32_t)__popcll(bl[c]);
-  }
-  wsync();
-  uint32_t dl[IS_WC];
+    wsync();
 #pragma unroll
-  for (int c = 0; c < IS_WC; ++c) {
-    dl[c] = 0;
-    if (kl[c]) {
-      dl[c] = xch[kl[c] - 1];  // L[kr]
-      xch[kl[c] - 1] = (uint16_t)(f + 1 + c * 64 + lane);
+    for (int c = 0; c < C; ++c) {
+      const uint32_t p = f + 1 + c * 64 + lane, kg = sw[c] & 0xFFFFu, dl = sw[c] >> 16;
+      uint32_t d = p;
+      if (kg) d = xch[kg - 1];  // R[k]
+      if (dl) d = dl;
+      if (kg || dl || p == m) {
+        S.k[d] = kk[c];
+        S.v[d] = vv[c];
+      }
     }
   }
+  if (lane == 0) {
+    S.k[f] = P;
+    S.v[f] = vm;
+  }
   wsync();
+  return min(max(cut, f + 1), l - 1);
+}
+
+// The whole introsort subtree of [f, f+n) (n <= 64) in registers: lane i holds
+// position f + i; each partition is ballots, partner selection from the masks and one
+// ds_bpermute per word; the leaves are then stably sorted by shuffles and the run is
+// written back in final order (every position marked as its own leaf).  stk: free
+// stack slots of the calling wave (packed a | b << 8 | depth << 16, lane indices).
+__device__ __forceinline__ void wave_sort_regs(OwnLds& S, uint32_t f, uint32_t n, int d, uint32_t* stk) {
+  const uint32_t lane = lane_id();
+  const bool live = lane < n;
+  uint32_t k = live ? S.k[f + lane] : 0xFFFFFFFFu, v = live ? S.v[f + lane] : 0u;
+  uint64_t hd = 1ull;  // leaf starts (lane indices)
+  int sp = 0;
+  stk[sp++] = n << 8 | ((uint32_t)d << 16);
+  for (uint32_t guard = 0; sp > 0; ++guard) {
+    if (guard > 256 || sp >= IS_STACK / 2) {  // cannot happen
+      if (lane == 0) S.stat[2] |= 0x800u;
+      break;
+    }
+    // stack words are wave-uniform: readfirstlane keeps every index below scalar (a
+    // divergent lane index would turn each readlane into a waterfall loop)
+    const uint32_t it = __builtin_amdgcn_readfirstlane(stk[--sp]);
+    const uint32_t a = it & 0xFFu, b = (it >> 8) & 0xFFu, m = b - a;
+    const int dd = (int)(it >> 16);
+    if (m <= IS_THRESHOLD) {
+      hd |= 1ull << a;
+      continue;
+    }
+    if (dd == 0) {  // depth limit: heap sort this range in LDS (rare)
+      if (live) {
+        S.k[f + lane] = k;
+        S.v[f + lane] = v;
+      }
+      wsync();
+      if (lane == 0) heap_sort(S.k + f + a, S.v + f + a, (int64_t)m);
+      wsync();
+      if (live) {
+        k = S.k[f + lane];
+        v = S.v[f + lane];
+      }
+      hd |= (m == 64 ? ~0ull : ((1ull << m) - 1ull)) << a;  // each element its own leaf
+      continue;
+    }
+    // __move_median_to_first(a, a+1, mid, b-1), applied in registers
+    const uint32_t A = a + 1, B = a + m / 2, C = b - 1;
+    const uint32_t ka = __builtin_amdgcn_readlane(k, A), kb = __builtin_amdgcn_readlane(k, B),
+                   kc = __builtin_amdgcn_readlane(k, C);
+    uint32_t mm;
+    if (ka < kb) mm = kb < kc ? B : (ka < kc ? C : A);
+    else mm = ka < kc ? A : (kb < kc ? C : B);
+    const uint32_t P = __builtin_amdgcn_readlane(k, mm), vm = __builtin_amdgcn_readlane(v, mm);
+    const uint32_t kf = __builtin_amdgcn_readlane(k, a), vf = __builtin_amdgcn_readlane(v, a);
+    if (lane == a) {
+      k = P;
+      v = vm;
+    } else if (lane == mm) {
+      k = kf;
+      v = vf;
+    }
+    const bool in = lane > a && lane < b;
+    const uint64_t bg = __ballot(in && k >= P), bl = __ballot(in && k <= P);
+    const uint32_t le_tot = (uint32_t)__popcll(bl);
+    const bool ge = (bg >> lane) & 1ull, le = (bl >> lane) & 1ull;
+    const uint32_t g = mbcnt(bg), h = mbcnt(bl);
+    const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
+    const bool sl = le && g >= le_tot - h;
+    uint32_t src = lane;  // the lane whose element lands here (swaps are symmetric)
+    if (sg) src = select64(bl, le_tot - (g + 1));
+    else if (sl) src = select64(bg, le_tot - h - 1);
+    const uint64_t cand = __ballot((ge && !sg) || sl);
+    k = (uint32_t)__shfl((int)k, (int)src, 64);
+    v = (uint32_t)__shfl((int)v, (int)src, 64);
+    const uint32_t cut = cand ? (uint32_t)(__ffsll((unsigned long long)cand) - 1) : A;
+    stk[sp++] = cut | (b << 8) | ((uint32_t)(dd - 1) << 16);
+    stk[sp++] = a | (cut << 8) | ((uint32_t)(dd - 1) << 16);
+  }
+  // stable sort of each leaf (<= 16 lanes): rank by key, ties by lane
+  const uint32_t ls = 63u - (uint32_t)__clzll((long long)(hd & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+  const uint64_t above = lane == 63 ? 0ull : (hd & ~((2ull << lane) - 1ull));
+  const uint32_t le_ = above ? min(n, (uint32_t)(__ffsll((unsigned long long)above) - 1)) : n;
+  uint32_t rank = 0;
 #pragma unroll
-  for (int c = 0; c < IS_WC; ++c) {
-    if (kg[c]) {
-      const uint32_t d = xch[kg[c] - 1];  // R[k]
-      S.k[d] = kk[c];
-      S.v[d] = vv[c];
-    }
-    if (kl[c]) {
-      S.k[dl[c]] = kk[c];
-      S.v[dl[c]] = vv[c];
+  for (int j = 0; j < (int)IS_THRESHOLD; ++j) {
+    const uint32_t q = min(ls + (uint32_t)j, 63u);
+    const uint32_t kq = (uint32_t)__shfl((int)k, (int)q, 64);
+    if (ls + (uint32_t)j < le_ && (kq < k || (kq == k && ls + (uint32_t)j < lane))) ++rank;
+  }
+  wsync();
+  if (live) {
+    S.k[f + ls + rank] = k;
+    S.v[f + ls + rank] = v;
+  }
+  if (lane == 0) {  // every position of the run is final: one leaf each
+    for (uint32_t q = 0; q < n; q += 32 - ((f + q) & 31)) {
+      const uint32_t bit = (f + q) & 31, cnt = min(32u - bit, n - q);
+      atomicOr(&S.heads[(f + q) >> 5], (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bit);
     }
   }
   wsync();
-  return min(max(wave_min_u32(cut), f + 1), l - 1);
 }
 
 // The introsort subtree of [off, off+len) (len <= IS_WCAP) by one wave, in LDS.
-__device__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* stk, uint16_t* xch) {
+__device__ __forceinline__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* stk, uint16_t* xch) {
   const uint32_t lane = lane_id();
   int sp = 0;
   stk[sp++] = packed;
-  while (sp > 0) {
-    const uint32_t it = stk[--sp];
+  for (uint32_t guard = 0; sp > 0; ++guard) {
+    if (guard > 4 * IS_WCAP || sp >= IS_STACK / 2) {  // cannot happen
+      if (lane == 0) S.stat[2] |= 0x400u;
+      break;
+    }
+    const uint32_t it = __builtin_amdgcn_readfirstlane(stk[--sp]);
     const uint32_t f = it & 0x1FFFu, n = (it >> 13) & 0x7FFu;
     const int dd = (int)(it >> 24);
     if (n <= IS_THRESHOLD) {
@@ -599,14 +744,24 @@ __device__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* stk, uint16_t* x
       wsync();
       continue;
     }
-    const uint32_t c = wave_partition(S, f, f + n, xch);
+    if (n <= 64) {  // the rest of this subtree in registers
+      if (IS_STATS && lane == 0) atomicAdd(&S.lstat[0], 1u);
+      wave_sort_regs(S, f, n, dd, stk + sp);
+      continue;
+    }
+    if (IS_STATS && lane == 0) atomicAdd(&S.lstat[2], 1u);
+    uint32_t c;
+    if (n <= 128) c = wave_partition<2>(S, f, f + n, xch);
+    else if (n <= 256) c = wave_partition<4>(S, f, f + n, xch);
+    else c = wave_partition<IS_WC>(S, f, f + n, xch);
     stk[sp++] = wpack(c, f + n - c, dd - 1);
     stk[sp++] = wpack(f, c - f, dd - 1);
   }
 }
 
-// One partition of [f, l) (IS_WCAP < l - f <= IS_LCAP) in LDS by the whole block.
-__device__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
+// One partition of [f, l) (IS_WCAP < l - f <= IS_OT * C) in LDS by the whole block.
+template <int C>
+__device__ __forceinline__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     const uint32_t m = median_pos(S.k, f, l);
@@ -617,12 +772,16 @@ __device__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
     S.v[m] = tv;
     S.bc[4] = IS_NONE;
   }
+  for (uint32_t i = C * IS_OW + threadIdx.x; i < IS_OE; i += IS_OT) {  // unused (chunk, wave) entries
+    S.cg[i] = 0;
+    S.cl[i] = 0;
+  }
   __syncthreads();
   const uint32_t P = S.k[f];
   const uint32_t n = l - f - 1;
-  uint32_t kk[IS_OC], vv[IS_OC];
+  uint32_t kk[C], vv[C];
 #pragma unroll
-  for (int c = 0; c < IS_OC; ++c) {
+  for (int c = 0; c < C; ++c) {
     const uint32_t q = c * IS_OT + threadIdx.x;
     const bool ok = q < n;
     kk[c] = ok ? S.k[f + 1 + q] : 0u;
@@ -640,52 +799,40 @@ __device__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
   __syncthreads();
   const uint32_t le_tot = S.bc[5];
   uint32_t cut = IS_NONE;
-  uint32_t kg[IS_OC], kl[IS_OC];
+  uint32_t sw[C];  // swap rank as >= (low 16 bits) / as <= (high 16), later the <= destination
 #pragma unroll
-  for (int c = 0; c < IS_OC; ++c) {
+  for (int c = 0; c < C; ++c) {
     const uint32_t q = c * IS_OT + threadIdx.x, p = f + 1 + q;
     const bool ok = q < n;
     const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
     const uint64_t bg = __ballot(ge), bl = __ballot(le);
     const uint32_t g = S.pg[c * IS_OW + w] + mbcnt(bg), h = S.pl[c * IS_OW + w] + mbcnt(bl);
-    kg[c] = 0;
-    kl[c] = 0;
-    if (ge) {
-      if (le_tot - h - (le ? 1u : 0u) >= g + 1) kg[c] = g + 1;
-      else cut = min(cut, p);
-    }
-    if (le) {
-      const uint32_t kr = le_tot - h;
-      if (g >= kr) {
-        kl[c] = kr;
-        cut = min(cut, p);
-      }
-    }
-    if (kg[c]) S.xch[kg[c] - 1] = (uint16_t)p;
+    const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
+    const bool sl = le && g >= le_tot - h;
+    sw[c] = (sg ? g + 1 : 0u) | ((sl ? le_tot - h : 0u) << 16);
+    const uint64_t cand = __ballot((ge && !sg) || sl);
+    if (cut == IS_NONE && cand) cut = p - lane + (uint32_t)(__ffsll((unsigned long long)cand) - 1);
+    if (sg) S.xch[g] = (uint16_t)p;
   }
-  cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&S.bc[4], cut);
   __syncthreads();
-  uint32_t dl[IS_OC];
 #pragma unroll
-  for (int c = 0; c < IS_OC; ++c) {
-    dl[c] = 0;
-    if (kl[c]) {
-      dl[c] = S.xch[kl[c] - 1];
-      S.xch[kl[c] - 1] = (uint16_t)(f + 1 + c * IS_OT + threadIdx.x);
+  for (int c = 0; c < C; ++c) {
+    const uint32_t kl = sw[c] >> 16;
+    if (kl) {
+      const uint32_t d = S.xch[kl - 1];
+      S.xch[kl - 1] = (uint16_t)(f + 1 + c * IS_OT + threadIdx.x);
+      sw[c] = (sw[c] & 0xFFFFu) | (d << 16);
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < IS_OC; ++c) {
-    if (kg[c]) {
-      const uint32_t d = S.xch[kg[c] - 1];
+  for (int c = 0; c < C; ++c) {
+    const uint32_t kg = sw[c] & 0xFFFFu, dl = sw[c] >> 16;
+    if (kg || dl) {
+      const uint32_t d = kg ? (uint32_t)S.xch[kg - 1] : dl;
       S.k[d] = kk[c];
       S.v[d] = vv[c];
-    }
-    if (kl[c]) {
-      S.k[dl[c]] = kk[c];
-      S.v[dl[c]] = vv[c];
     }
   }
   __syncthreads();
@@ -696,15 +843,17 @@ __device__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
 
 // The subtree of [f, f+len) (len <= IS_LCAP, depth d) from (Ki, Vi), finished in LDS;
 // the sorted run is written to (Ko, Vo) at the same positions.
-__device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, uint32_t* Ko, uint32_t* Vo, uint32_t f,
+__device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, uint32_t* Ko, uint32_t* Vo, uint32_t f,
                            uint32_t len, int d) {
   const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+  const uint64_t t0 = IS_STATS ? wall_clock64() : 0;
   for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
     S.k[q] = Ki[f + q];
     S.v[q] = Vi[f + q];
   }
   for (uint32_t q = threadIdx.x; q < (len + 31) / 32; q += IS_OT) S.heads[q] = 0;
   if (threadIdx.x == 0) {
+    for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
     S.bc[0] = 0;  // stack depth
     S.bc[1] = 0;  // wave-list count
     S.bc[2] = 0;  // wave-list head
@@ -721,6 +870,10 @@ __device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, ui
   for (;;) {
     if (threadIdx.x == 0) {
       uint32_t go = 0;
+      if (S.bc[0] >= IS_STACK - 2) {  // cannot happen
+        S.stat[2] |= 0x1000u;
+        S.bc[0] = 0;
+      }
       while (S.bc[0] > 0 && !go) {
         const uint2 it = S.wstk[--S.bc[0]];
         const uint32_t off = it.x, n = it.y & 0xFFFFu;
@@ -729,6 +882,7 @@ __device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, ui
           if (n) mark_leaf(S, off);
         } else if (dd == 0) {
           heap_sort(S.k + off, S.v + off, (int64_t)n);
+          if (IS_STATS) atomicAdd(&S.stat[7], 1u);
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
         } else if (n <= IS_WCAP) {
           S.wlist[S.bc[1]++] = wpack(off, n, dd);
@@ -741,10 +895,20 @@ __device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, ui
       S.bc[3] = go;
     }
     __syncthreads();
+    if (S.prg && threadIdx.x == 0) {
+      S.prg[24] += 1;
+      S.prg[25] = S.bc[7] & 0xFFFFu;
+      S.prg[6] = 10;
+      __threadfence_system();
+    }
     if (!S.bc[3]) break;
     const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
     const int dd = (int)(S.bc[7] >> 16);
-    const uint32_t c = block_partition(S, off, off + n);
+    if (IS_STATS && threadIdx.x == 0) atomicAdd(&S.lstat[1], 1u);
+    uint32_t c;
+    if (n <= 2 * IS_OT) c = block_partition<2>(S, off, off + n);
+    else if (n <= 4 * IS_OT) c = block_partition<4>(S, off, off + n);
+    else c = block_partition<IS_OC>(S, off, off + n);
     if (threadIdx.x == 0) {
       const uint32_t nd = (uint32_t)(dd - 1) << 16;
       S.wstk[S.bc[0]++] = make_uint2(c, (off + n - c) | nd);
@@ -752,24 +916,45 @@ __device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, ui
     }
     __syncthreads();
   }
+  const uint64_t t1 = IS_STATS ? wall_clock64() : 0;
   // wave phase: each wave takes subtrees from the list
   {
     uint16_t* xch = S.xch + w * (IS_WCAP / 2);
     for (;;) {
       uint32_t idx = 0;
       if (lane == 0) idx = atomicAdd(&S.bc[2], 1u);
-      idx = __shfl(idx, 0, 64);
+      idx = __builtin_amdgcn_readfirstlane(idx);
+      if (S.prg && lane == 0) {
+        S.prg[8 + w] = idx | (S.bc[1] << 16);
+        S.prg[6] = 11;
+        __threadfence_system();
+      }
       if (idx >= S.bc[1]) break;
-      wave_sort(S, S.wlist[idx], S.vstk[w], xch);
+      wave_sort(S, __builtin_amdgcn_readfirstlane(S.wlist[idx]), S.vstk[w], xch);
     }
   }
   __syncthreads();
+  if (S.prg && threadIdx.x == 0) {
+    S.prg[6] = 12;
+    __threadfence_system();
+  }
+  const uint64_t t2 = IS_STATS ? wall_clock64() : 0;
   // the final insertion sort: each leaf segment stably sorted in place
   for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
-    uint32_t a = p;
-    while (a > 0 && !((S.heads[a >> 5] >> (a & 31)) & 1u)) --a;
-    uint32_t b = p + 1;
-    while (b < len && !((S.heads[b >> 5] >> (b & 31)) & 1u)) ++b;
+    // leaf [a, b) around p: the nearest head at or below p and above p (leaves hold
+    // at most 16 elements, so each search spans at most two head words)
+    uint32_t a = 0, b = len;
+    {
+      uint32_t wi = p >> 5, m = S.heads[wi] & (0xFFFFFFFFu >> (31 - (p & 31)));
+      while (!m && wi > 0) m = S.heads[--wi];
+      if (m) a = (wi << 5) + 31 - __clz((int)m);
+      uint32_t wj = (p + 1) >> 5, nw = (len + 31) >> 5;
+      uint32_t q = (p + 1) & 31;
+      uint32_t mm = wj < nw ? (S.heads[wj] & (0xFFFFFFFFu << q)) : 0u;
+      if (q == 0 && wj < nw) mm = S.heads[wj];
+      while (!mm && ++wj < nw) mm = S.heads[wj];
+      if (mm) b = min(len, (wj << 5) + (uint32_t)__ffs((int)mm) - 1);
+    }
     const uint32_t key = S.k[p];
     uint32_t rank = 0;
     for (uint32_t q = a; q < b; ++q) {
@@ -780,11 +965,22 @@ __device__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, ui
     Vo[f + a + rank] = S.v[p];
   }
   __syncthreads();
+  if (IS_STATS && threadIdx.x == 0) {  // wall_clock64 ticks (100 MHz) per phase, summed over subtrees
+    const uint64_t t3 = wall_clock64();
+    atomicAdd(&S.stat[9], (uint32_t)(t1 - t0));
+    atomicAdd(&S.stat[10], (uint32_t)(t2 - t1));
+    atomicAdd(&S.stat[11], (uint32_t)(t3 - t2));
+    atomicAdd(&S.stat[5], S.lstat[1]);
+    atomicAdd(&S.stat[12], S.lstat[0]);
+    atomicMax(&S.stat[13], (uint32_t)(t3 - t0));
+    atomicAdd(&S.stat[6], S.lstat[2]);
+    atomicAdd(&S.stat[7], S.lstat[3]);
+  }
 }
 
 // One partition of [f, l) (l - f > IS_LCAP) in global memory by the whole block,
 // in place in (K, V); (SK, SV) at the same positions is scratch.  Returns the cut.
-__device__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
+__device__ __forceinline__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
                                      uint32_t l) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
@@ -798,7 +994,7 @@ __device__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32
     S.bc[0] = 0;  // running >= count
     S.bc[1] = 0;  // running <= count
   }
-  __threadfence_block();
+  __threadfence();
   __syncthreads();
   const uint32_t P = K[f];
   const uint32_t n = l - f - 1, H = (l - f) / 2;
@@ -870,7 +1066,7 @@ __device__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32
           }
         }
       }
-      __threadfence_block();
+      __threadfence();
       __syncthreads();
     }
   }
@@ -895,6 +1091,17 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
   if (nsort == 0) return;
   const uint32_t nfin = nchildren(W, R);
   const uint32_t nown = R ? W.rounds[R - 1].nown : 0u;
+  if (threadIdx.x == 0) S.stat = W.ctl;
+  uint32_t* const prg = W.prog ? W.prog + 32 * (blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
+  if (threadIdx.x == 0) S.prg = prg;
+  auto mark = [&](uint32_t code, uint32_t x) {
+    if (prg && threadIdx.x == 0) {
+      prg[6] = code;
+      prg[7] = x;
+      __threadfence_system();
+    }
+  };
+  mark(1, 0);
   uint32_t* Kb[2] = {K02[e], K12[e]};
   uint32_t* Vb[2] = {V02[e], V12[e]};
   for (;;) {
@@ -902,6 +1109,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
     __syncthreads();
     const uint32_t idx = s_idx;
     __syncthreads();
+    mark(2, idx);
     if (idx >= nfin + nown) break;
     uint32_t f, l, buf;
     int d;
@@ -921,29 +1129,49 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
     if (l <= f) continue;
     uint32_t* K = Kb[buf];
     uint32_t* V = Vb[buf];
+    const uint64_t te0 = IS_STATS ? wall_clock64() : 0;
     if (threadIdx.x == 0) {
       S.gstk[0] = make_uint4(f, l, (uint32_t)d, 0u);
       S.gsp = 1;
     }
     __syncthreads();
-    for (;;) {
+    for (uint32_t guard = 0;; ++guard) {
       const uint32_t sp = S.gsp;
       __syncthreads();
+      if (W.prog && threadIdx.x == 0) {
+        uint32_t* pr = W.prog + 32 * (blockIdx.y * gridDim.x + blockIdx.x);
+        pr[0] = idx;
+        pr[1] = sp;
+        pr[2] = sp ? S.gstk[sp - 1].x : 0u;
+        pr[3] = sp ? S.gstk[sp - 1].y : 0u;
+        pr[4] = sp ? S.gstk[sp - 1].z : 0u;
+        pr[5] = guard;
+        __threadfence_system();
+      }
       if (sp == 0) break;
+      if (guard > 4 * l || sp >= IS_STACK - 2) {  // cannot happen: every step shrinks a segment
+        if (threadIdx.x == 0) W.ctl[2] |= 0x200u;
+        break;
+      }
       const uint4 it = S.gstk[sp - 1];
       const uint32_t gf = it.x, gl = it.y, len = gl - gf;
       const int gd = (int)it.z;
       __syncthreads();
       if (threadIdx.x == 0) S.gsp = sp - 1;
       __syncthreads();
+      mark(4 + (len <= IS_LCAP ? 0u : 1u), gf);
       if (len <= IS_LCAP) {
+        if (IS_STATS && threadIdx.x == 0) {
+          atomicAdd(&W.ctl[4], 1u);
+          atomicAdd(&W.ctl[8], len);
+        }
         lds_finish(S, K, V, Kb[0], Vb[0], gf, len, gd);
       } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
         if (threadIdx.x == 0) {
           heap_sort(K + gf, V + gf, (int64_t)len);
           W.ctl[2] |= 2u;
         }
-        __threadfence_block();
+        __threadfence();
         __syncthreads();
         if (buf != 0)
           for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
@@ -952,6 +1180,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
           }
         __syncthreads();
       } else {
+        if (IS_STATS && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
         const uint32_t c = global_partition(S, K, V, Kb[buf ^ 1u], Vb[buf ^ 1u], gf, gl);
         if (threadIdx.x == 0) {
           W.ctl[2] |= 1u;
@@ -960,11 +1189,17 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
           S.gstk[s++] = make_uint4(gf, c, (uint32_t)(gd - 1), 0u);
           S.gsp = s;
         }
-        __threadfence_block();
+        __threadfence();
         __syncthreads();
       }
     }
+    if (IS_STATS && threadIdx.x == 0) {
+      atomicMax(&W.ctl[14], (uint32_t)(wall_clock64() - te0));  // slowest entry (ticks)
+      atomicAdd(&W.ctl[15], (uint32_t)(wall_clock64() - te0));  // all entries
+    }
+    mark(3, idx);
   }
+  mark(9, 0);
 }
 
 }  // namespace
@@ -1012,23 +1247,34 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.segs = (IsSeg*)take(sizeof(IsSeg) * (size_t)b.segmax * IS_RMAX);
   b.cuts = (uint32_t*)take(4 * (size_t)b.segmax * IS_RMAX);
   b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
+  b.prog = nullptr;
   return b;
 }
 
 void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                    B2<const VGParams*> P, uint32_t cap, B2<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate) {
   const int R = exact_gate ? 0 : introsort_rounds(cap);
+  static const bool trace = std::getenv("FCCF_IS_TRACE") != nullptr;  // dev: sync + log after each launch
+  auto step = [&](const char* what, int r) {
+    if (!trace) return;
+    const hipError_t e = hipStreamSynchronize(st);
+    std::fprintf(stderr, "introsort %s r=%d: %s\n", what, r, hipGetErrorString(e));
+  };
   k_is_prep<<<dim3(1, nbatch), 1024, 0, st>>>(k0, v0, d_n, P, b, exact_gate ? 1 : 0);
+  step("prep", 0);
   const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap);
   const size_t lds_count = 16 * (size_t)segmax, lds_scatter = 4 * ((size_t)segmax + 2 * (size_t)maxtiles);
   for (int r = 0; r < R; ++r) {
     const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
     k_is_count<<<dim3(maxtiles, nbatch), IS_TT, lds_count, st>>>(B2<const uint32_t*>(ki), b, r);
+    step("count", r);
     k_is_scatter<<<dim3(maxtiles, nbatch), IS_TT, lds_scatter, st>>>(B2<const uint32_t*>(ki),
                                                                       B2<const uint32_t*>(vi), ko, vo, b, r);
+    step("scatter", r);
   }
   k_is_own<<<dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st>>>(k0, v0, k1, v1, b, R);
+  step("own", R);
 }
 
 }  // namespace fccf

@@ -50,6 +50,7 @@ struct IsBufs {
   IsSeg* segs;          // IS_RMAX x segmax
   uint32_t* cuts;       // IS_RMAX x segmax
   IsOwn* own;           // ownmax
+  uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   uint32_t segmax, maxtiles, ownmax;
 };
 size_t introsort_bytes(uint32_t cap);

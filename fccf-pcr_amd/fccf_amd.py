@@ -96,6 +96,7 @@ _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctype
      ctypes.POINTER(ctypes.c_double))
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
+_sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
 _sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
@@ -247,6 +248,14 @@ class Ctx:
         _check(_lib.fccf_debug_sort_keys(self._h, k.ctypes.data, k.size, int(exact_gate), perm.ctypes.data),
                "fccf_debug_sort_keys", self._h)
         return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
+
+    def sort_stats(self) -> dict:
+        a = np.zeros(16, np.uint32)
+        _check(_lib.fccf_debug_sort_stats(self._h, a.ctypes.data), "fccf_debug_sort_stats", self._h)
+        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_subtrees=int(a[4]),
+                    block_parts=int(a[5]), wave_parts=int(a[6]), us_wave_busy_or_heaps=int(a[7]) / 100, lds_elems=int(a[8]),
+                    reg_subtrees=int(a[12]), us_block_phase=int(a[9]) / 100, us_wave_phase=int(a[10]) / 100, us_final=int(a[11]) / 100,
+                    us_max_subtree=int(a[13]) / 100, us_max_entry=int(a[14]) / 100, us_all_entries=int(a[15]) / 100)
 
     def voxel_planes(self, xyz, params: Params | None = None):
         """face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled cloud on the GPU.

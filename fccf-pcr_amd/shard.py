@@ -94,16 +94,10 @@ def match_sharded(ctx, F1, B1, F2, B2, rank: int, world: int, gather, params=Non
     return combine(gather(pack(cands, k_pass)))
 
 
-# ---------------------------------------------------------------- VoxelGrid by leaf ranges
-# SURVEY.md §8(e) row D.  PCL's VoxelGrid (FCCF.cpp:1668-1678) sorts
-# points by the linear index of their leaf, i + j*div_x + k*div_x*div_y with
-# (i, j, k) = floor(p * (1/leaf)) - min_b, and averages each leaf's points in input
-# order.  That order is the lexicographic (k, j, i) order of floor(p * (1/leaf)),
-# whatever the bounding box.  So if every leaf is owned by one rank, ranks own
-# contiguous ranges of that order and each rank's points stay in input order, each
-# rank's ordinary VoxelGrid is exactly its slice of the global output.  The int32
-# overflow guard ("Integer indices would overflow": output = input) is decided on the
-# global bounding box; any subset of a passing cloud also passes.
+# ---------------------------------------------------------------- VoxelGrid (row D)
+# SURVEY.md §8(e) row D.  Helpers shared with the tests' CPU stand-in: PCL's leaf
+# coordinates floor(p * (1/leaf)) in float32 and its int32 overflow guard
+# ("Integer indices would overflow": output = input) on the finite bounding box.
 
 
 def leaf_coords(xyz: np.ndarray, leaf: float):
@@ -126,36 +120,15 @@ def voxel_grid_overflows(mn, mx, leaf: float) -> bool:
 def downsample_sharded(ctx, xyz_slice, leaf: float, rank: int, world: int, gather):
     """Global VoxelGrid of a cloud split over ranks in input order (rank r holds the
     r-th contiguous slice).  Every rank returns the full output, equal to
-    ctx.downsample(whole cloud)."""
-    a = np.ascontiguousarray(np.asarray(xyz_slice, np.float32).reshape(-1, 3))
-    f, fin = leaf_coords(a, leaf)
-    box = np.array([np.inf] * 3 + [-np.inf] * 3)
-    if fin.any():
-        box = np.concatenate([a[fin].min(axis=0), a[fin].max(axis=0)]).astype(np.float64)
-    bb = np.stack(gather(box))  # float32 values: exact in float64
-    mn, mx = bb[:, :3].min(axis=0), bb[:, 3:].max(axis=0)
-    if not np.isfinite(mn).all():  # no finite point on any rank
+    ctx.downsample(whole cloud).
+
+    PCL orders the points of a leaf by one std::sort over the cloud's whole index
+    vector (FCCF.cpp:1668-1678); that introsort's partition tree spans every leaf, so
+    no split by leaf ranges reproduces the within-leaf summation order.  The pass is
+    therefore replicated: the slices are gathered in rank order (= input order) and
+    each rank runs the whole-cloud pass (one ~0.1 ms GPU pass at c3)."""
+    a = np.ascontiguousarray(np.asarray(xyz_slice, np.float32).reshape(-1))
+    whole = np.concatenate([np.asarray(s, np.float32).reshape(-1) for s in gather(a)]).reshape(-1, 3)
+    if whole.shape[0] == 0:
         return np.zeros((0, 3), np.float32)
-    if voxel_grid_overflows(mn, mx, leaf):  # output = input, in input order
-        return np.concatenate([s.reshape(-1, 3) for s in gather(a.reshape(-1))])
-    inv = np.float32(1.0) / np.float32(leaf)
-    lo = np.floor(mn.astype(np.float32) * inv).astype(np.int64)
-    div = np.floor(mx.astype(np.float32) * inv).astype(np.int64) - lo + 1
-    key = np.where(fin, (f[:, 0] - lo[0]) + div[0] * ((f[:, 1] - lo[1]) + div[1] * (f[:, 2] - lo[2])), -1)
-    # splitters: quantiles of every rank's key sample, so ranks own similar counts
-    kf = np.sort(key[fin])
-    samp = kf[:: max(1, kf.size // 256)].astype(np.float64)
-    allsamp = np.sort(np.concatenate(gather(samp)))
-    cuts = [allsamp[(allsamp.size * r) // world] if allsamp.size else 0.0 for r in range(1, world)]
-    lo_cut = -np.inf if rank == 0 else cuts[rank - 1]
-    hi_cut = np.inf if rank == world - 1 else cuts[rank]
-    # exchange by owner (an all-to-all(v); gathered whole here, keys < 2^53 exact in
-    # float64): points keep input order within a source, sources arrive in rank order
-    mine = []
-    for m in gather(np.concatenate([key.astype(np.float64), a.astype(np.float64).reshape(-1)])):
-        n = m.size // 4
-        k, p = m[:n], m[n:].reshape(n, 3).astype(np.float32)
-        mine.append(p[(k >= 0) & (k >= lo_cut) & (k < hi_cut)])
-    own = np.concatenate(mine)
-    out = ctx.downsample(own, leaf) if len(own) else np.zeros((0, 3), np.float32)
-    return np.concatenate([s.reshape(-1, 3) for s in gather(np.ascontiguousarray(out, np.float32).reshape(-1))])
+    return ctx.downsample(whole, leaf)

@@ -11,7 +11,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
-STABLE, INTROSORT = 0, 1
+STABLE, INTROSORT = 0, 1  # within-leaf VoxelGrid order: INTROSORT is the reference's (std::sort)
 
 
 def _load():
@@ -46,7 +46,7 @@ lib = _load()
 class Run:
     """One oracle registration (FCCF.cpp main + computer_transform_guess)."""
 
-    def __init__(self, src, tar, leaf, order=STABLE):
+    def __init__(self, src, tar, leaf, order=INTROSORT):
         s = np.ascontiguousarray(src, np.float32)
         t = np.ascontiguousarray(tar, np.float32)
         self.h = lib.orc_register(s.ctypes.data, s.shape[0], t.ctypes.data, t.shape[0], float(leaf), int(order))
@@ -76,7 +76,7 @@ class Run:
             self.h = None
 
 
-def voxel_grid(xyz, leaf, order=STABLE):
+def voxel_grid(xyz, leaf, order=INTROSORT):
     a = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
     out = np.zeros((max(a.shape[0], 1), 3), np.float32)
     ovf = ctypes.c_int(0)

@@ -60,7 +60,7 @@ def test_fixtures_present():
 def test_oracle_reproduces_golden(oracle, fccf, path):
     g = load(path)
     src, tar = inputs(fccf, g)
-    run = oracle.Run(src, tar, float(g["leaf"]), oracle.STABLE)
+    run = oracle.Run(src, tar, float(g["leaf"]), oracle.INTROSORT)
     check(run.get, g, False)
 
 

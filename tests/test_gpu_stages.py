@@ -24,7 +24,7 @@ def bits(a):
 def case(request, oracle, fccf):
     c = fccf.CONFIGS[request.param]
     src, tar, _ = fccf.synth_pair(c["n"], c["room"])
-    run = oracle.Run(src, tar, c["leaf"], oracle.STABLE)
+    run = oracle.Run(src, tar, c["leaf"], oracle.INTROSORT)
     tabs = dict(F1=fccf.planes_from_dump(run.get("planes1")), B1=fccf.bases_from_dump(run.get("bases1", np.int32)),
                 F2=fccf.planes_from_dump(run.get("planes2")), B2=fccf.bases_from_dump(run.get("bases2", np.int32)))
     return run, tabs
@@ -101,7 +101,7 @@ def test_match_sharded_two_ranks_gloo(tmp_path, oracle, fccf):
     all-gathered over gloo; rank 0's combined lists equal the oracle's."""
     c = fccf.CONFIGS["c2"]
     src, tar, _ = fccf.synth_pair(c["n"], c["room"])
-    run = oracle.Run(src, tar, c["leaf"], oracle.STABLE)
+    run = oracle.Run(src, tar, c["leaf"], oracle.INTROSORT)
     np.savez(tmp_path / "in.npz", planes1=run.get("planes1"), bases1=run.get("bases1", np.int32),
              planes2=run.get("planes2"), bases2=run.get("bases2", np.int32))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
@@ -187,16 +187,16 @@ def test_cluster_stage_bit_exact(ctx, case, fccf):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_downsample_sharded_by_leaf_ranges(ctx, oracle, fccf, world):
-    """§8(e) row D: the VoxelGrid split by leaf ranges over `world` ranks (one fccf_ctx
-    each, threads on one GPU), rank-ordered concatenation == the whole-cloud GPU pass
-    == the oracle, bitwise."""
+    """§8(e) row D: a cloud held as `world` input-order slices (one fccf_ctx per rank,
+    threads on one GPU): every rank's output == the whole-cloud GPU pass == the
+    oracle (reference std::sort order), bitwise."""
     import test_shard
     c = fccf.CONFIGS["c2"]
     src, _, _ = fccf.synth_pair(c["n"], c["room"])
     src = src.copy()
     src[[5, 777, 40_000]] = np.nan
     whole = ctx.downsample(src, c["leaf"])
-    np.testing.assert_array_equal(bits(whole), bits(oracle.voxel_grid(src, c["leaf"])[0]))
+    np.testing.assert_array_equal(bits(whole), bits(oracle.voxel_grid(src, c["leaf"], oracle.INTROSORT)[0]))
     ctxs = [fccf.Ctx(0) for _ in range(world)]
     try:
         outs = test_shard.run_sharded(src, c["leaf"], world, ctx_of=lambda r: ctxs[r])

@@ -13,7 +13,7 @@ def bits(a):
 
 
 def check(ctx, oracle, xyz, leaf, presorted=False):
-    ref, ovf = oracle.voxel_grid(xyz, leaf)
+    ref, ovf = oracle.voxel_grid(xyz, leaf, oracle.INTROSORT)
     got = ctx.downsample(xyz, leaf, presorted)
     assert got.shape == ref.shape, (got.shape, ref.shape, ovf)
     np.testing.assert_array_equal(bits(got), bits(ref))

@@ -108,8 +108,9 @@ def cloud(n, seed, nan=True):
 
 
 class StubVoxelCtx:
-    """Stand-in for the GPU VoxelGrid (tests only): a direct numpy/Python restatement of
-    PCL's semantics for small clouds — stable leaf order, sequential float32 sums."""
+    """Stand-in for the GPU VoxelGrid (tests only) with PCL's leaf keys, overflow guard
+    and sequential float32 sums; the within-leaf order here is the input order (the
+    exchange logic under test does not depend on it)."""
 
     def downsample(self, xyz, leaf):
         a = np.asarray(xyz, np.float32).reshape(-1, 3)
