@@ -250,7 +250,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
   });
 }
 
-extern "C" int fccf_debug_sort_stats(fccf_ctx* c, uint32_t out[16]) {
+extern "C" int fccf_debug_sort_stats(fccf_ctx* c, uint32_t out[32]) {
   if (!c || !out) return FCCF_E_ARG;
   std::memcpy(out, c->sort_stats, sizeof c->sort_stats);
   return FCCF_OK;

@@ -192,7 +192,7 @@ struct fccf_ctx {
   fccf::AsyncTask enq;  // pipelined batch: enqueues the next pair's cloud stage
   fccf::Probe probe;
   bool debug = false;
-  uint32_t sort_stats[16] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
+  uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;
 

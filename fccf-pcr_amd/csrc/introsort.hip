@@ -24,12 +24,13 @@
 //              k_is_count (pivot, per-tile ge/le counts and tile-local position
 //              lists) and k_is_scatter (ranks from the tile prefix, every element
 //              written to its destination in the other buffer, cut by atomicMin);
-//  k_is_own    one workgroup per remaining subtree (dequeued): partitions in global
-//              memory while a segment exceeds IS_LCAP, then the whole subtree in LDS
-//              (workgroup partitions above IS_WCAP, one wave per smaller subtree),
-//              the stable leaf sort, and the write of the sorted keys/values.
-// HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); k_is_own reads and
-// writes each element once more (8 + 8 B) when its subtree fits in LDS.
+//  k_is_block  one workgroup per remaining segment (dequeued): partitions in global
+//              memory while a segment exceeds IS_LCAP, then in LDS down to subtrees
+//              of <= IS_WCAP, which become wave tasks; leaves are finished here;
+//  k_is_wave   every wave of the GPU finishes tasks in its own LDS slice (wave
+//              partitions, register-resident subtrees of <= 64, stable leaf sort).
+// HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); the block and wave
+// kernels read and write each element once more each (8 + 8 B).
 #define KT_TU 9  // ktrace.h source tag
 #include <cstdio>
 #include <cstdlib>
@@ -40,19 +41,19 @@
 namespace fccf {
 namespace {
 
-constexpr uint32_t IS_TILE = 4096;   // elements per round tile
+constexpr uint32_t IS_TILE = 2048;   // elements per round tile
 constexpr int IS_TT = 256;           // round kernels: threads per block
-constexpr int IS_TC = IS_TILE / IS_TT;  // 16 elements per thread
-constexpr uint32_t IS_LCAP = 8192;   // largest segment finished in LDS
-constexpr int IS_OT = 1024;          // owner: threads per block (16 waves, one block per CU)
-constexpr int IS_OW = IS_OT / 64;    // owner: waves
+constexpr int IS_TC = IS_TILE / IS_TT;  // 8 elements per thread
+constexpr uint32_t IS_LCAP = 8192;   // largest segment a block kernel workgroup holds in LDS
+constexpr int IS_OT = 1024;          // block kernel: threads per block (16 waves, one block per CU)
+constexpr int IS_OW = IS_OT / 64;    // block kernel: waves
 constexpr int IS_OC = IS_LCAP / IS_OT;  // 8 elements per thread in a workgroup partition
 constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a workgroup partition
-constexpr uint32_t IS_WCAP = 512;    // largest segment partitioned by one wave
+constexpr uint32_t IS_WCAP = 512;    // largest subtree finished by one wave (wave kernel)
 constexpr int IS_WC = IS_WCAP / 64;  // 8 elements per lane
+constexpr int IS_WT = 256;           // wave kernel: threads per block
 constexpr uint32_t IS_THRESHOLD = 16;  // libstdc++ _S_threshold
 constexpr int IS_STACK = 96;  // a wave's stack also holds its register-mode subtree (depth <= 48 each)
-constexpr int IS_WLIST = 512;
 // packed u32 subtree of at most IS_WCAP elements: off (13 bits) | len (11) | depth (6)
 __device__ __forceinline__ uint32_t wpack(uint32_t off, uint32_t len, int d) { return off | (len << 13) | ((uint32_t)d << 24); }
 constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
@@ -169,7 +170,7 @@ __device__ __forceinline__ Child child_of(const IsBufs& W, int r, uint32_t nsort
   return (i & 1) ? Child{c, s.l, s.depth - 1} : Child{s.f, c, s.depth - 1};
 }
 __device__ __forceinline__ uint32_t nchildren(const IsBufs& W, int r) { return r == 0 ? 1u : 2u * W.rounds[r - 1].nseg; }
-__device__ __forceinline__ bool is_large(const Child& c) { return c.l - c.f > IS_LCAP && c.d > 0; }
+__device__ __forceinline__ bool is_large(const Child& c, uint32_t tier) { return c.l - c.f > tier && c.d > 0; }
 __device__ __forceinline__ uint32_t tiles_of(uint32_t len) { return (len - 1 + IS_TILE - 1) / IS_TILE; }
 
 // largest u < n with pre[u] <= x (pre ascending, pre[0] = 0)
@@ -186,7 +187,7 @@ __device__ __forceinline__ uint32_t upper_index(const uint32_t* pre, uint32_t n,
 // ---------------------------------------------------------------- k_is_prep
 // PCL pushes only finite points into its index vector, in input order: compact the
 // (key, index) pairs of finite points (rare: only when some point is not finite) and
-// mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_own's dequeue head.
+// mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_block's dequeue head.
 // exact_gate (the driver's presorted second pass): sort only when the order check failed.
 __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*> V2, B2<const uint32_t*> d_n2,
                                                    B2<const VGParams*> P2, B2<IsBufs> W2, int exact_gate) {
@@ -199,7 +200,7 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
   if (exact_gate && P->unsorted == 0u) ns = 0;
   if (threadIdx.x == 0) {
     W.ctl[0] = ns;
-    for (int i = 1; i < 16; ++i) W.ctl[i] = 0;
+    for (int i = 1; i < 32; ++i) W.ctl[i] = 0;
   }
   if (ns == 0 || ns >= n) return;
   uint32_t* K = K2[e];
@@ -223,11 +224,23 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
 }
 
 // ---------------------------------------------------------------- rounds
-// This round's large segments, built by every block from the previous round's
-// table and cuts (tiny); block 0 publishes them, initialises the cuts and appends the
-// finished-as-small children to the owned list.  Dynamic LDS: 4 * segmax u32.
-__device__ __forceinline__ uint32_t build_round(const IsBufs& W, int r, uint32_t nsort, uint32_t* tf, uint32_t* tl, int32_t* td,
-                                uint32_t* t0, uint32_t* sh, uint32_t* ntiles_out) {
+// k_is_plan (one block per cloud): this round's large segments -- the children of the
+// previous round's, or the root -- with their pivots (__move_median_to_first applied
+// to the round's input), tile ranges and the tile -> segment map; small children go
+// to the owned list.  The tile kernels then read one descriptor each instead of
+// rebuilding the table (their dependent-load chains set the round's latency).
+// Dynamic LDS: 4 * segmax u32.
+__global__ void __launch_bounds__(1024) k_is_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2, B2<IsBufs> W2, int r) {
+  KT();
+  extern __shared__ uint32_t dyn[];
+  __shared__ uint32_t sh[16];
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t nsort = W.ctl[0];
+  uint32_t* tf = dyn;
+  uint32_t* tl = tf + W.segmax;
+  int32_t* td = (int32_t*)(tl + W.segmax);
+  uint32_t* t0 = (uint32_t*)(td + W.segmax);
   const uint32_t nch = nchildren(W, r);
   const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
   uint32_t nseg = 0, ntiles = 0, nown = 0;
@@ -235,7 +248,7 @@ __device__ __forceinline__ uint32_t build_round(const IsBufs& W, int r, uint32_t
     const uint32_t i = b + threadIdx.x;
     Child c = {0u, 0u, 0};
     if (i < nch) c = child_of(W, r, nsort, i);
-    const bool lg = i < nch && is_large(c);
+    const bool lg = i < nch && is_large(c, W.tier);
     const bool ow = i < nch && !lg && c.l > c.f;
     const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
     uint32_t s_lg, s_nt, s_ow;
@@ -248,53 +261,46 @@ __device__ __forceinline__ uint32_t build_round(const IsBufs& W, int r, uint32_t
       td[nseg + p_lg] = c.d;
       t0[nseg + p_lg] = ntiles + p_nt;
     }
-    if (ow && blockIdx.x == 0) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
+    if (ow) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
     nseg += s_lg;
     ntiles += s_nt;
     nown += s_ow;
   }
   __syncthreads();
-  if (blockIdx.x == 0) {
-    for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
-      W.segs[(size_t)r * W.segmax + j] = IsSeg{tf[j], tl[j], td[j], t0[j]};
-      W.cuts[(size_t)r * W.segmax + j] = tl[j];
-    }
-    if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
+  const uint32_t* __restrict__ K = K2[e];
+  const uint32_t* __restrict__ V = V2[e];
+  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
+    const uint32_t f = tf[j], l = tl[j];
+    const uint32_t m = median_pos(K, f, l);
+    W.segs[(size_t)r * W.segmax + j] = IsSeg{f, l, td[j], t0[j], m, K[m], K[f], V[f], V[m]};
+    W.cuts[(size_t)r * W.segmax + j] = l;
   }
-  *ntiles_out = ntiles;
-  return nseg;
+  for (uint32_t t = threadIdx.x; t < W.maxtiles; t += blockDim.x)
+    W.tseg[t] = t < ntiles ? upper_index(t0, nseg, t) : IS_NONE;
+  if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
 }
 
 // Per-tile ge/le counts against the segment's pivot and the tile-local position
 // lists (offsets from the tile start, in position order).
 __global__ void __launch_bounds__(IS_TT) k_is_count(B2<const uint32_t*> K2, B2<IsBufs> W2, int r) {
   KT();
-  extern __shared__ uint32_t dyn[];
-  __shared__ uint32_t sh[16];
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
-  const uint32_t nsort = W.ctl[0];
-  uint32_t* tf = dyn;
-  uint32_t* tl = tf + W.segmax;
-  int32_t* td = (int32_t*)(tl + W.segmax);
-  uint32_t* t0 = (uint32_t*)(td + W.segmax);
-  uint32_t ntiles;
-  const uint32_t nseg = build_round(W, r, nsort, tf, tl, td, t0, sh, &ntiles);
   const uint32_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  const uint32_t j = upper_index(t0, nseg, t);
-  const uint32_t f = tf[j], l = tl[j], i = t - t0[j];
+  const uint32_t j = W.tseg[t];
+  if (j == IS_NONE) return;
+  const IsSeg s = W.segs[(size_t)r * W.segmax + j];
+  const uint32_t f = s.f, l = s.l, i = t - s.tile0, m = s.m, P = s.P, kf = s.kf;
   const uint32_t* __restrict__ K = K2[e];
-  const uint32_t m = median_pos(K, f, l);
-  const uint32_t P = K[m], kf = K[f];
   const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   uint32_t kk[IS_TC];
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const uint32_t p = a + c * IS_TT + threadIdx.x;
-    kk[c] = p < b ? (p == m ? kf : K[p]) : 0u;
+    kk[c] = p < b ? K[p] : 0u;
+    if (p == m) kk[c] = kf;
   }
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
@@ -306,16 +312,19 @@ __global__ void __launch_bounds__(IS_TT) k_is_count(B2<const uint32_t*> K2, B2<I
     }
   }
   __syncthreads();
-  if (w == 0) {  // 64 (chunk, wave) entries in position order: one per lane
-    uint32_t xg = cg[lane], xl = cl[lane];
+  if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
+    const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+    uint32_t xg = xg0, xl = xl0;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
       if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
     }
-    pg[lane] = xg - cg[lane];
-    pl[lane] = xl - cl[lane];
-    if (lane == 63) {
+    if (lane < IS_TC * 4) {
+      pg[lane] = xg - xg0;
+      pl[lane] = xl - xl0;
+    }
+    if (lane == IS_TC * 4 - 1) {
       W.cnt[2 * (size_t)t] = xg;
       W.cnt[2 * (size_t)t + 1] = xl;
     }
@@ -333,7 +342,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_count(B2<const uint32_t*> K2, B2<I
 }
 
 // Every element of the round's large segments to its place after the partition,
-// written to the other buffer; the cut by atomicMin.  Dynamic LDS: segmax + 2 * maxtiles u32.
+// written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
 __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
                                                       B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
   KT();
@@ -343,19 +352,33 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
   __shared__ uint32_t scut;
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
-  const IsRound rd = W.rounds[r];
   const uint32_t t = blockIdx.x;
-  if (t >= rd.ntiles) return;
-  uint32_t* t0 = dyn;
-  uint32_t* preg = t0 + W.segmax;
+  const uint32_t j = W.tseg[t];
+  if (j == IS_NONE) return;
+  const IsSeg s = W.segs[(size_t)r * W.segmax + j];
+  const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0, m = s.m, P = s.P;
+  uint32_t* preg = dyn;
   uint32_t* prel = preg + W.maxtiles;
-  const IsSeg* segs = W.segs + (size_t)r * W.segmax;
-  for (uint32_t j = threadIdx.x; j < rd.nseg; j += blockDim.x) t0[j] = segs[j].tile0;
+  const uint32_t* __restrict__ K = Ki2[e];
+  const uint32_t* __restrict__ V = Vi2[e];
+  uint32_t* __restrict__ Ko = Ko2[e];
+  uint32_t* __restrict__ Vo = Vo2[e];
+  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  // the tile's elements are loaded first: their latency overlaps the prefix below
+  uint32_t kk[IS_TC], vv[IS_TC];
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    const bool ok = p < b;
+    kk[c] = ok ? K[p] : 0u;
+    vv[c] = ok ? V[p] : 0u;
+    if (p == m) {
+      kk[c] = s.kf;
+      vv[c] = s.vf;
+    }
+  }
   if (threadIdx.x == 0) scut = IS_NONE;
-  __syncthreads();
-  const uint32_t j = upper_index(t0, rd.nseg, t);
-  const IsSeg s = segs[j];
-  const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0;
   // exclusive prefix of the segment's tile counts
   uint32_t rg = 0, rl = 0;
   for (uint32_t u0 = 0; u0 < nt; u0 += blockDim.x) {
@@ -373,23 +396,6 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     rl += sl;
   }
   const uint32_t le_tot = rl;
-  __syncthreads();
-  const uint32_t* __restrict__ K = Ki2[e];
-  const uint32_t* __restrict__ V = Vi2[e];
-  uint32_t* __restrict__ Ko = Ko2[e];
-  uint32_t* __restrict__ Vo = Vo2[e];
-  const uint32_t m = median_pos(K, f, l);
-  const uint32_t P = K[m], kf = K[f], vf = V[f], vm = V[m];
-  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-  uint32_t kk[IS_TC], vv[IS_TC];
-#pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
-    const uint32_t p = a + c * IS_TT + threadIdx.x;
-    const bool ok = p < b;
-    kk[c] = ok ? (p == m ? kf : K[p]) : 0u;
-    vv[c] = ok ? (p == m ? vf : V[p]) : 0u;
-  }
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const bool ok = a + c * IS_TT + threadIdx.x < b;
@@ -401,54 +407,57 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
   }
   __syncthreads();
   if (w == 0) {
-    uint32_t xg = cg[lane], xl = cl[lane];
+    const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+    uint32_t xg = xg0, xl = xl0;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
       if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
     }
-    pg[lane] = xg - cg[lane] + preg[i];
-    pl[lane] = xl - cl[lane] + prel[i];
+    if (lane < IS_TC * 4) {
+      pg[lane] = xg - xg0 + preg[i];
+      pl[lane] = xl - xl0 + prel[i];
+    }
   }
   __syncthreads();
+  // destinations: the swapped elements' partner positions come from the lists (all
+  // list loads issued before any store)
   uint32_t cut = IS_NONE;
+  uint32_t dst[IS_TC];
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const uint32_t p = a + c * IS_TT + threadIdx.x;
     const bool ok = p < b;
     const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
     const uint64_t bg = __ballot(ge), bl = __ballot(le);
-    if (!ok) continue;
     const uint32_t gx = pg[c * 4 + w] + mbcnt(bg);  // # >= P before p in the segment
     const uint32_t lx = pl[c * 4 + w] + mbcnt(bl);  // # <= P before p
-    uint32_t dst = p;
-    if (ge) {
-      const uint32_t k1 = gx + 1;
-      if (le_tot - lx - (le ? 1u : 0u) >= k1) {  // swapped with R[k1], the (le_tot-k1)-th <= P from the left
-        const uint32_t x = le_tot - k1;
-        const uint32_t u = upper_index(prel, nt, x);
-        const uint32_t au = f + 1 + u * IS_TILE;
-        dst = au + W.lel[au + (x - prel[u])];
-      } else {
-        cut = min(cut, p);  // L[K+1]
-      }
+    const bool sg = ge && le_tot - lx - (le ? 1u : 0u) >= gx + 1;
+    const bool sl = le && gx >= le_tot - lx;
+    if ((ge && !sg) || sl) cut = min(cut, p);  // L[K+1] / R[K]
+    dst[c] = ok ? p : IS_NONE;
+    if (sg) {  // R[gx+1]: the (le_tot-gx-1)-th <= P from the left
+      const uint32_t x = le_tot - gx - 1;
+      const uint32_t u = upper_index(prel, nt, x);
+      const uint32_t au = f + 1 + u * IS_TILE;
+      dst[c] = au + W.lel[au + (x - prel[u])];
+    } else if (sl) {  // L[kr]: the (kr-1)-th >= P from the left
+      const uint32_t x = le_tot - lx - 1;
+      const uint32_t u = upper_index(preg, nt, x);
+      const uint32_t au = f + 1 + u * IS_TILE;
+      dst[c] = au + W.gel[au + (x - preg[u])];
     }
-    if (le) {
-      const uint32_t kr = le_tot - lx;  // right rank
-      if (gx >= kr) {  // swapped with L[kr], the (kr-1)-th >= P from the left
-        const uint32_t x = kr - 1;
-        const uint32_t u = upper_index(preg, nt, x);
-        const uint32_t au = f + 1 + u * IS_TILE;
-        dst = au + W.gel[au + (x - preg[u])];
-        cut = min(cut, p);  // R[K]
-      }
-    }
-    if (dst <= f || dst >= l) {  // cannot happen; never write outside the segment
+  }
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t d = dst[c];
+    if (d == IS_NONE) continue;
+    if (d <= f || d >= l) {  // cannot happen; never write outside the segment
       W.ctl[2] |= 0x100u;
       continue;
     }
-    Ko[dst] = kk[c];
-    Vo[dst] = vv[c];
+    Ko[d] = kk[c];
+    Vo[d] = vv[c];
   }
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
@@ -457,54 +466,77 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     if (scut != IS_NONE) atomicMin(&W.cuts[(size_t)r * W.segmax + j], scut);
     if (i == 0) {
       Ko[f] = P;
-      Vo[f] = vm;
+      Vo[f] = s.vm;
     }
   }
 }
 
-// ---------------------------------------------------------------- k_is_own
-// exchange slots: a workgroup partition swaps < IS_LCAP / 2 pairs, a wave one < IS_WCAP / 2
-constexpr uint32_t IS_XCH = IS_LCAP / 2 > IS_OW * IS_WCAP / 2 ? IS_LCAP / 2 : IS_OW * IS_WCAP / 2;
-struct OwnLds {
+// ---------------------------------------------------------------- finish: block + wave kernels
+// After the rounds every segment is at most IS_LCAP long (leftovers beyond it are
+// split by one workgroup in global memory first).  k_is_block: one 1024-thread
+// workgroup per segment (dequeued), the segment in LDS, workgroup partitions while a
+// subtree exceeds IS_WCAP; leaves (<= 16) and heap-sorted ranges are finished there,
+// subtrees of <= IS_WCAP become tasks.  k_is_wave: every wave of the GPU takes tasks
+// (dequeued), finishes each in its own LDS slice (wave partitions, register-resident
+// subtrees of <= 64) and writes it.  Tasks keep the waves of the whole chip busy
+// instead of the 16 waves of one workgroup.
+
+// exchange slots of a workgroup partition: it swaps < IS_LCAP / 2 pairs
+struct BlockLds {
   uint32_t k[IS_LCAP], v[IS_LCAP];
-  uint16_t xch[IS_XCH];             // partition exchange slots (workgroup, or one region per wave)
+  uint16_t xch[IS_LCAP / 2];
   uint32_t heads[IS_LCAP / 32];     // leaf starts
+  uint32_t intask[IS_LCAP / 32];    // positions handed to the wave kernel
   uint32_t cg[IS_OE], cl[IS_OE], pg[IS_OE], pl[IS_OE];
-  uint2 wstk[IS_STACK];             // workgroup-phase stack {off, len | depth << 16}
-  uint32_t wlist[IS_WLIST];         // subtrees for the waves (wpack)
-  uint32_t vstk[IS_OW][IS_STACK];   // per-wave stacks (wpack)
-  uint4 gstk[IS_STACK];             // global-phase stack {f, l, depth, -}
-  uint32_t gsp;                     // its depth
-  uint32_t* stat;                   // IsBufs::ctl (path counters)
-  uint32_t lstat[4];                // this subtree's counters (flushed to stat once per subtree)
-  uint32_t* prg;                    // dev progress record (null = off)
+  uint2 wstk[IS_STACK / 2];         // workgroup-phase stack {off, len | depth << 16}
+  uint4 gstk[IS_STACK / 2];         // global-phase stack {f, l, depth, -}
+  uint32_t gsp;
   uint32_t bc[8];                   // broadcasts
   uint32_t sh[16];
+  uint32_t* stat;                   // IsBufs::ctl
 };
 
+// One wave's slice of the wave kernel
+struct WaveLds {
+  uint32_t k[IS_WCAP], v[IS_WCAP];
+  uint16_t xch[IS_WCAP / 2];
+  uint32_t heads[IS_WCAP / 32];
+  uint32_t stk[IS_STACK];
+  uint32_t lstat[4];
+  uint32_t* stat;
+};
+
+template <class SL>
+__device__ __forceinline__ void mark_leaf(SL& S, uint32_t off) { atomicOr(&S.heads[off >> 5], 1u << (off & 31)); }
+
 // Exclusive prefix (plus carries) of the IS_OE (chunk, wave) counts in position
-// order, by wave 0 (two entries per lane).
-__device__ __forceinline__ void block_chunk_scan(OwnLds& S, uint32_t cg0, uint32_t cl0) {
-  const uint32_t lane = lane_id(), i0 = 2 * lane, i1 = 2 * lane + 1;
-  const uint32_t g0 = i0 < IS_OE ? S.cg[i0] : 0u, g1 = i1 < IS_OE ? S.cg[i1] : 0u;
-  const uint32_t l0 = i0 < IS_OE ? S.cl[i0] : 0u, l1 = i1 < IS_OE ? S.cl[i1] : 0u;
-  uint32_t xg = g0 + g1, xl = l0 + l1;
+// order, by wave 0 (IS_OE / 64 consecutive entries per lane).
+__device__ __forceinline__ void block_chunk_scan(BlockLds& S, uint32_t cg0, uint32_t cl0) {
+  constexpr uint32_t PER = (IS_OE + 63) / 64;
+  const uint32_t lane = lane_id(), i0 = PER * lane;
+  uint32_t sg = 0, sl = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q)
+    if (i0 + q < IS_OE) {
+      sg += S.cg[i0 + q];
+      sl += S.cl[i0 + q];
+    }
+  uint32_t xg = sg, xl = sl;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
     if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
   }
-  if (i0 < IS_OE) {
-    S.pg[i0] = cg0 + xg - g0 - g1;
-    S.pl[i0] = cl0 + xl - l0 - l1;
-  }
-  if (i1 < IS_OE) {
-    S.pg[i1] = cg0 + xg - g1;
-    S.pl[i1] = cl0 + xl - l1;
-  }
+  uint32_t rg = cg0 + xg - sg, rl = cl0 + xl - sl;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q)
+    if (i0 + q < IS_OE) {
+      S.pg[i0 + q] = rg;
+      S.pl[i0 + q] = rl;
+      rg += S.cg[i0 + q];
+      rl += S.cl[i0 + q];
+    }
 }
-
-__device__ __forceinline__ void mark_leaf(OwnLds& S, uint32_t off) { atomicOr(&S.heads[off >> 5], 1u << (off & 31)); }
 
 // Position of the r-th (0-based) set bit of m (r < popcount(m)).
 __device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t r) {
@@ -535,8 +567,8 @@ __device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t r) {
 // straight from the ballot masks; larger C exchange positions through LDS slots.
 // The cut is the first position that is a non-swapped >= element or a swapped <=
 // element (min(L[K+1], R[K])), found from ballots.
-template <int C>
-__device__ __forceinline__ uint32_t wave_partition(OwnLds& S, uint32_t f, uint32_t l, uint16_t* xch) {
+template <int C, class SL>
+__device__ __forceinline__ uint32_t wave_partition(SL& S, uint32_t f, uint32_t l, uint16_t* xch) {
   const uint32_t lane = lane_id();
   const uint32_t m = median_pos(S.k, f, l);
   const uint32_t kf = S.k[f], vf = S.v[f], P = S.k[m], vm = S.v[m];
@@ -625,7 +657,8 @@ __device__ __forceinline__ uint32_t wave_partition(OwnLds& S, uint32_t f, uint32
 // ds_bpermute per word; the leaves are then stably sorted by shuffles and the run is
 // written back in final order (every position marked as its own leaf).  stk: free
 // stack slots of the calling wave (packed a | b << 8 | depth << 16, lane indices).
-__device__ __forceinline__ void wave_sort_regs(OwnLds& S, uint32_t f, uint32_t n, int d, uint32_t* stk) {
+template <class SL>
+__device__ __forceinline__ void wave_sort_regs(SL& S, uint32_t f, uint32_t n, int d, uint32_t* stk) {
   const uint32_t lane = lane_id();
   const bool live = lane < n;
   uint32_t k = live ? S.k[f + lane] : 0xFFFFFFFFu, v = live ? S.v[f + lane] : 0u;
@@ -720,7 +753,8 @@ __device__ __forceinline__ void wave_sort_regs(OwnLds& S, uint32_t f, uint32_t n
 }
 
 // The introsort subtree of [off, off+len) (len <= IS_WCAP) by one wave, in LDS.
-__device__ __forceinline__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* stk, uint16_t* xch) {
+template <class SL>
+__device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk, uint16_t* xch) {
   const uint32_t lane = lane_id();
   int sp = 0;
   stk[sp++] = packed;
@@ -751,9 +785,9 @@ __device__ __forceinline__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* 
     }
     if (IS_STATS && lane == 0) atomicAdd(&S.lstat[2], 1u);
     uint32_t c;
-    if (n <= 128) c = wave_partition<2>(S, f, f + n, xch);
-    else if (n <= 256) c = wave_partition<4>(S, f, f + n, xch);
-    else c = wave_partition<IS_WC>(S, f, f + n, xch);
+    if (n <= 128) c = wave_partition<2, SL>(S, f, f + n, xch);
+    else if (n <= 256) c = wave_partition<4, SL>(S, f, f + n, xch);
+    else c = wave_partition<IS_WC, SL>(S, f, f + n, xch);
     stk[sp++] = wpack(c, f + n - c, dd - 1);
     stk[sp++] = wpack(f, c - f, dd - 1);
   }
@@ -761,7 +795,7 @@ __device__ __forceinline__ void wave_sort(OwnLds& S, uint32_t packed, uint32_t* 
 
 // One partition of [f, l) (IS_WCAP < l - f <= IS_OT * C) in LDS by the whole block.
 template <int C>
-__device__ __forceinline__ uint32_t block_partition(OwnLds& S, uint32_t f, uint32_t l) {
+__device__ __forceinline__ uint32_t block_partition(BlockLds& S, uint32_t f, uint32_t l) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     const uint32_t m = median_pos(S.k, f, l);
@@ -841,22 +875,22 @@ __device__ __forceinline__ uint32_t block_partition(OwnLds& S, uint32_t f, uint3
   return r;
 }
 
-// The subtree of [f, f+len) (len <= IS_LCAP, depth d) from (Ki, Vi), finished in LDS;
-// the sorted run is written to (Ko, Vo) at the same positions.
-__device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const uint32_t* Vi, uint32_t* Ko, uint32_t* Vo, uint32_t f,
-                           uint32_t len, int d) {
-  const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t t0 = IS_STATS ? wall_clock64() : 0;
+// The segment [f, f+len) (len <= IS_LCAP, depth d) from (Ki, Vi): workgroup
+// partitions in LDS down to subtrees of <= IS_WCAP, which become wave tasks; the
+// leaves and heap-sorted ranges are stably sorted here.  The whole run is written
+// to (Ko, Vo) (task ranges in their current order, for the wave kernel).
+__device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const uint32_t* Ki, const uint32_t* Vi,
+                                          uint32_t* Ko, uint32_t* Vo, uint32_t f, uint32_t len, int d) {
   for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
     S.k[q] = Ki[f + q];
     S.v[q] = Vi[f + q];
   }
-  for (uint32_t q = threadIdx.x; q < (len + 31) / 32; q += IS_OT) S.heads[q] = 0;
+  for (uint32_t q = threadIdx.x; q < (len + 31) / 32; q += IS_OT) {
+    S.heads[q] = 0;
+    S.intask[q] = 0;
+  }
   if (threadIdx.x == 0) {
-    for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
     S.bc[0] = 0;  // stack depth
-    S.bc[1] = 0;  // wave-list count
-    S.bc[2] = 0;  // wave-list head
     if (len <= IS_THRESHOLD) {
       S.heads[0] = 1u;
     } else {
@@ -865,15 +899,9 @@ __device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const 
     }
   }
   __syncthreads();
-  // workgroup phase: thread 0 walks the stack; entries above IS_WCAP are partitioned
-  // by the whole block, the others go to the leaves / heap sort / the wave list
   for (;;) {
     if (threadIdx.x == 0) {
       uint32_t go = 0;
-      if (S.bc[0] >= IS_STACK - 2) {  // cannot happen
-        S.stat[2] |= 0x1000u;
-        S.bc[0] = 0;
-      }
       while (S.bc[0] > 0 && !go) {
         const uint2 it = S.wstk[--S.bc[0]];
         const uint32_t off = it.x, n = it.y & 0xFFFFu;
@@ -884,30 +912,34 @@ __device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const 
           heap_sort(S.k + off, S.v + off, (int64_t)n);
           if (IS_STATS) atomicAdd(&S.stat[7], 1u);
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
-        } else if (n <= IS_WCAP) {
-          S.wlist[S.bc[1]++] = wpack(off, n, dd);
+        } else if (n <= IS_WCAP) {  // a wave task
+          const uint32_t ti = atomicAdd(&W.ctl[16], 1u);
+          W.tasks[ti] = make_uint4(f + off, n, (uint32_t)dd, 0u);
+          for (uint32_t q = off; q < off + n; q += 32 - (q & 31)) {
+            const uint32_t bit = q & 31, cnt = min(32u - bit, off + n - q);
+            atomicOr(&S.intask[q >> 5], (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bit);
+          }
         } else {
           S.bc[6] = off;
           S.bc[7] = it.y;
           go = 1;
         }
       }
+      if (S.bc[0] >= IS_STACK / 2 - 2) {  // cannot happen
+        S.stat[2] |= 0x1000u;
+        S.bc[0] = 0;
+      }
       S.bc[3] = go;
     }
     __syncthreads();
-    if (S.prg && threadIdx.x == 0) {
-      S.prg[24] += 1;
-      S.prg[25] = S.bc[7] & 0xFFFFu;
-      S.prg[6] = 10;
-      __threadfence_system();
-    }
     if (!S.bc[3]) break;
     const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
     const int dd = (int)(S.bc[7] >> 16);
-    if (IS_STATS && threadIdx.x == 0) atomicAdd(&S.lstat[1], 1u);
+    if (IS_STATS && threadIdx.x == 0) atomicAdd(&S.stat[5], 1u);
     uint32_t c;
     if (n <= 2 * IS_OT) c = block_partition<2>(S, off, off + n);
     else if (n <= 4 * IS_OT) c = block_partition<4>(S, off, off + n);
+    else if (n <= 8 * IS_OT) c = block_partition<8>(S, off, off + n);
     else c = block_partition<IS_OC>(S, off, off + n);
     if (threadIdx.x == 0) {
       const uint32_t nd = (uint32_t)(dd - 1) << 16;
@@ -916,46 +948,32 @@ __device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const 
     }
     __syncthreads();
   }
-  const uint64_t t1 = IS_STATS ? wall_clock64() : 0;
-  // wave phase: each wave takes subtrees from the list
-  {
-    uint16_t* xch = S.xch + w * (IS_WCAP / 2);
-    for (;;) {
-      uint32_t idx = 0;
-      if (lane == 0) idx = atomicAdd(&S.bc[2], 1u);
-      idx = __builtin_amdgcn_readfirstlane(idx);
-      if (S.prg && lane == 0) {
-        S.prg[8 + w] = idx | (S.bc[1] << 16);
-        S.prg[6] = 11;
-        __threadfence_system();
-      }
-      if (idx >= S.bc[1]) break;
-      wave_sort(S, __builtin_amdgcn_readfirstlane(S.wlist[idx]), S.vstk[w], xch);
-    }
-  }
-  __syncthreads();
-  if (S.prg && threadIdx.x == 0) {
-    S.prg[6] = 12;
-    __threadfence_system();
-  }
-  const uint64_t t2 = IS_STATS ? wall_clock64() : 0;
-  // the final insertion sort: each leaf segment stably sorted in place
+  // leaves: stable sort in place (the final insertion sort); task ranges as they are
   for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
-    // leaf [a, b) around p: the nearest head at or below p and above p (leaves hold
-    // at most 16 elements, so each search spans at most two head words)
+    const uint32_t key = S.k[p];
+    if ((S.intask[p >> 5] >> (p & 31)) & 1u) {
+      Ko[f + p] = key;
+      Vo[f + p] = S.v[p];
+      continue;
+    }
     uint32_t a = 0, b = len;
     {
       uint32_t wi = p >> 5, m = S.heads[wi] & (0xFFFFFFFFu >> (31 - (p & 31)));
       while (!m && wi > 0) m = S.heads[--wi];
       if (m) a = (wi << 5) + 31 - __clz((int)m);
       uint32_t wj = (p + 1) >> 5, nw = (len + 31) >> 5;
-      uint32_t q = (p + 1) & 31;
+      const uint32_t q = (p + 1) & 31;
       uint32_t mm = wj < nw ? (S.heads[wj] & (0xFFFFFFFFu << q)) : 0u;
-      if (q == 0 && wj < nw) mm = S.heads[wj];
       while (!mm && ++wj < nw) mm = S.heads[wj];
       if (mm) b = min(len, (wj << 5) + (uint32_t)__ffs((int)mm) - 1);
+      // a leaf never reaches into a task range: tasks start at a head-less position
+      // bounded by the next head or task start, so clip at the first task position
+      for (uint32_t x = p + 1; x < b; ++x)
+        if ((S.intask[x >> 5] >> (x & 31)) & 1u) {
+          b = x;
+          break;
+        }
     }
-    const uint32_t key = S.k[p];
     uint32_t rank = 0;
     for (uint32_t q = a; q < b; ++q) {
       const uint32_t kq = S.k[q];
@@ -965,22 +983,11 @@ __device__ __forceinline__ void lds_finish(OwnLds& S, const uint32_t* Ki, const 
     Vo[f + a + rank] = S.v[p];
   }
   __syncthreads();
-  if (IS_STATS && threadIdx.x == 0) {  // wall_clock64 ticks (100 MHz) per phase, summed over subtrees
-    const uint64_t t3 = wall_clock64();
-    atomicAdd(&S.stat[9], (uint32_t)(t1 - t0));
-    atomicAdd(&S.stat[10], (uint32_t)(t2 - t1));
-    atomicAdd(&S.stat[11], (uint32_t)(t3 - t2));
-    atomicAdd(&S.stat[5], S.lstat[1]);
-    atomicAdd(&S.stat[12], S.lstat[0]);
-    atomicMax(&S.stat[13], (uint32_t)(t3 - t0));
-    atomicAdd(&S.stat[6], S.lstat[2]);
-    atomicAdd(&S.stat[7], S.lstat[3]);
-  }
 }
 
 // One partition of [f, l) (l - f > IS_LCAP) in global memory by the whole block,
 // in place in (K, V); (SK, SV) at the same positions is scratch.  Returns the cut.
-__device__ __forceinline__ uint32_t global_partition(OwnLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
+__device__ __forceinline__ uint32_t global_partition(BlockLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
                                      uint32_t l) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
@@ -1066,9 +1073,10 @@ __device__ __forceinline__ uint32_t global_partition(OwnLds& S, uint32_t* K, uin
           }
         }
       }
-      __threadfence();
-      __syncthreads();
+      __syncthreads();  // superchunks are independent within a pass
     }
+    __threadfence();  // pass 0's scratch (or pass 1's in-place writes) visible to every wave
+    __syncthreads();
   }
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&S.bc[4], cut);
@@ -1078,30 +1086,20 @@ __device__ __forceinline__ uint32_t global_partition(OwnLds& S, uint32_t* K, uin
   return r;
 }
 
-// One workgroup per remaining subtree: the final children of the last round first
+// One workgroup per remaining segment: the final children of the last round first
 // (they may exceed IS_LCAP), then the owned list, dequeued from ctl[1].
-__global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<uint32_t*> K12,
-                                                  B2<uint32_t*> V12, B2<IsBufs> W2, int R) {
+__global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<uint32_t*> K12,
+                                                    B2<uint32_t*> V12, B2<IsBufs> W2, int R) {
   KT();
-  __shared__ OwnLds S;
+  __shared__ BlockLds S;
   __shared__ uint32_t s_idx;
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
   const uint32_t nsort = W.ctl[0];
   if (nsort == 0) return;
+  if (threadIdx.x == 0) S.stat = W.ctl;
   const uint32_t nfin = nchildren(W, R);
   const uint32_t nown = R ? W.rounds[R - 1].nown : 0u;
-  if (threadIdx.x == 0) S.stat = W.ctl;
-  uint32_t* const prg = W.prog ? W.prog + 32 * (blockIdx.y * gridDim.x + blockIdx.x) : nullptr;
-  if (threadIdx.x == 0) S.prg = prg;
-  auto mark = [&](uint32_t code, uint32_t x) {
-    if (prg && threadIdx.x == 0) {
-      prg[6] = code;
-      prg[7] = x;
-      __threadfence_system();
-    }
-  };
-  mark(1, 0);
   uint32_t* Kb[2] = {K02[e], K12[e]};
   uint32_t* Vb[2] = {V02[e], V12[e]};
   for (;;) {
@@ -1109,7 +1107,6 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
     __syncthreads();
     const uint32_t idx = s_idx;
     __syncthreads();
-    mark(2, idx);
     if (idx >= nfin + nown) break;
     uint32_t f, l, buf;
     int d;
@@ -1129,7 +1126,6 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
     if (l <= f) continue;
     uint32_t* K = Kb[buf];
     uint32_t* V = Vb[buf];
-    const uint64_t te0 = IS_STATS ? wall_clock64() : 0;
     if (threadIdx.x == 0) {
       S.gstk[0] = make_uint4(f, l, (uint32_t)d, 0u);
       S.gsp = 1;
@@ -1138,18 +1134,8 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
     for (uint32_t guard = 0;; ++guard) {
       const uint32_t sp = S.gsp;
       __syncthreads();
-      if (W.prog && threadIdx.x == 0) {
-        uint32_t* pr = W.prog + 32 * (blockIdx.y * gridDim.x + blockIdx.x);
-        pr[0] = idx;
-        pr[1] = sp;
-        pr[2] = sp ? S.gstk[sp - 1].x : 0u;
-        pr[3] = sp ? S.gstk[sp - 1].y : 0u;
-        pr[4] = sp ? S.gstk[sp - 1].z : 0u;
-        pr[5] = guard;
-        __threadfence_system();
-      }
       if (sp == 0) break;
-      if (guard > 4 * l || sp >= IS_STACK - 2) {  // cannot happen: every step shrinks a segment
+      if (guard > 4 * (l - f) || sp >= IS_STACK / 2 - 2) {  // cannot happen: every step shrinks a segment
         if (threadIdx.x == 0) W.ctl[2] |= 0x200u;
         break;
       }
@@ -1159,13 +1145,9 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
       __syncthreads();
       if (threadIdx.x == 0) S.gsp = sp - 1;
       __syncthreads();
-      mark(4 + (len <= IS_LCAP ? 0u : 1u), gf);
       if (len <= IS_LCAP) {
-        if (IS_STATS && threadIdx.x == 0) {
-          atomicAdd(&W.ctl[4], 1u);
-          atomicAdd(&W.ctl[8], len);
-        }
-        lds_finish(S, K, V, Kb[0], Vb[0], gf, len, gd);
+        if (IS_STATS && threadIdx.x == 0) atomicAdd(&W.ctl[4], 1u);
+        lds_block(S, W, K, V, Kb[0], Vb[0], gf, len, gd);
       } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
         if (threadIdx.x == 0) {
           heap_sort(K + gf, V + gf, (int64_t)len);
@@ -1193,18 +1175,89 @@ __global__ void __launch_bounds__(IS_OT) k_is_own(B2<uint32_t*> K02, B2<uint32_t
         __syncthreads();
       }
     }
-    if (IS_STATS && threadIdx.x == 0) {
-      atomicMax(&W.ctl[14], (uint32_t)(wall_clock64() - te0));  // slowest entry (ticks)
-      atomicAdd(&W.ctl[15], (uint32_t)(wall_clock64() - te0));  // all entries
-    }
-    mark(3, idx);
   }
-  mark(9, 0);
+}
+
+// Every wave takes wave tasks (dequeued from ctl[17]): the subtree in its LDS slice,
+// finished and stably leaf-sorted, written back in place in buffer 0.
+__global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<IsBufs> W2) {
+  KT();
+  __shared__ WaveLds WL[IS_WT / 64];
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  WaveLds& S = WL[w];
+  if (lane == 0) {
+    S.stat = W.ctl;
+    for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
+  }
+  wsync();
+  const uint32_t ntasks = W.ctl[16];
+  uint32_t* __restrict__ K = K02[e];
+  uint32_t* __restrict__ V = V02[e];
+  for (;;) {
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(&W.ctl[17], 1u);
+    idx = __builtin_amdgcn_readfirstlane(idx);
+    if (idx >= ntasks) break;
+    const uint4 tk = W.tasks[idx];
+    const uint32_t f = __builtin_amdgcn_readfirstlane(tk.x), n = __builtin_amdgcn_readfirstlane(tk.y);
+    const int d = (int)__builtin_amdgcn_readfirstlane(tk.z);
+#pragma unroll
+    for (int c = 0; c < IS_WC; ++c) {
+      const uint32_t q = c * 64 + lane;
+      if (q < n) {
+        S.k[q] = K[f + q];
+        S.v[q] = V[f + q];
+      }
+    }
+    if (lane < IS_WCAP / 32) S.heads[lane] = 0;
+    wsync();
+    wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
+    wsync();
+#pragma unroll
+    for (int c = 0; c < IS_WC; ++c) {
+      const uint32_t p = c * 64 + lane;
+      if (p >= n) continue;
+      uint32_t a = 0, b = n;
+      {
+        uint32_t wi = p >> 5, m = S.heads[wi] & (0xFFFFFFFFu >> (31 - (p & 31)));
+        while (!m && wi > 0) m = S.heads[--wi];
+        if (m) a = (wi << 5) + 31 - __clz((int)m);
+        uint32_t wj = (p + 1) >> 5;
+        const uint32_t nw = (n + 31) >> 5, q = (p + 1) & 31;
+        uint32_t mm = wj < nw ? (S.heads[wj] & (0xFFFFFFFFu << q)) : 0u;
+        while (!mm && ++wj < nw) mm = S.heads[wj];
+        if (mm) b = min(n, (wj << 5) + (uint32_t)__ffs((int)mm) - 1);
+      }
+      const uint32_t key = S.k[p];
+      uint32_t rank = 0;
+      for (uint32_t q = a; q < b; ++q) {
+        const uint32_t kq = S.k[q];
+        rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
+      }
+      K[f + a + rank] = key;
+      V[f + a + rank] = S.v[p];
+    }
+    wsync();
+  }
+  if (IS_STATS && lane == 0) {
+    atomicAdd(&W.ctl[6], S.lstat[2]);
+    atomicAdd(&W.ctl[12], S.lstat[0]);
+  }
 }
 
 }  // namespace
 
-uint32_t introsort_segmax(uint32_t cap) { return cap / IS_LCAP + 2; }
+uint32_t introsort_tier() {
+  static const uint32_t t = [] {
+    const char* s = std::getenv("FCCF_IS_TIER");  // dev: round threshold (default 4096)
+    const uint32_t v = s ? (uint32_t)std::atoi(s) : 4096u;
+    return v < 64u ? 64u : (v > IS_LCAP ? IS_LCAP : v);
+  }();
+  return t;
+}
+uint32_t introsort_segmax(uint32_t cap) { return cap / introsort_tier() + 2; }
 uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
 
 int introsort_rounds(uint32_t cap) {
@@ -1213,9 +1266,12 @@ int introsort_rounds(uint32_t cap) {
     return s ? std::atoi(s) : -1;
   }();
   int r = 0;
-  if (cap > IS_LCAP) {
-    while ((uint64_t)IS_LCAP << r < cap) ++r;  // ceil(log2(cap / IS_LCAP))
-    r += 2;
+  const uint32_t tier = introsort_tier();
+  if (cap > tier) {
+    // ceil(log2(cap / tier)) balanced levels, plus the deeper tail of unbalanced
+    // splits (structured clouds: ~15 rounds at 1M points before all segments are <= 4096)
+    while ((uint64_t)tier << r < cap) ++r;
+    r += 7;
   }
   if (env >= 0) r = env;
   return r > IS_RMAX ? IS_RMAX : r;
@@ -1224,7 +1280,7 @@ int introsort_rounds(uint32_t cap) {
 size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
-  return 256 + 64 + 8 * mt + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
+  return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
          (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 8 * 256;
 }
 
@@ -1239,15 +1295,18 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.segmax = introsort_segmax(cap);
   b.maxtiles = introsort_maxtiles(cap);
   b.ownmax = 2 * b.segmax * (IS_RMAX + 1) + 4;
-  b.ctl = (uint32_t*)take(64);
+  b.ctl = (uint32_t*)take(256);
   b.cnt = (uint32_t*)take(8 * (size_t)b.maxtiles);
+  b.tseg = (uint32_t*)take(4 * (size_t)b.maxtiles);
   b.gel = (uint16_t*)take(2 * ((size_t)cap + 64));
   b.lel = (uint16_t*)take(2 * ((size_t)cap + 64));
   b.rounds = (IsRound*)take(sizeof(IsRound) * IS_RMAX);
   b.segs = (IsSeg*)take(sizeof(IsSeg) * (size_t)b.segmax * IS_RMAX);
   b.cuts = (uint32_t*)take(4 * (size_t)b.segmax * IS_RMAX);
   b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
+  b.tasks = (uint4*)take(sizeof(uint4) * ((size_t)cap / 16 + 64));
   b.prog = nullptr;
+  b.tier = introsort_tier();
   return b;
 }
 
@@ -1263,18 +1322,22 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   k_is_prep<<<dim3(1, nbatch), 1024, 0, st>>>(k0, v0, d_n, P, b, exact_gate ? 1 : 0);
   step("prep", 0);
   const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap);
-  const size_t lds_count = 16 * (size_t)segmax, lds_scatter = 4 * ((size_t)segmax + 2 * (size_t)maxtiles);
+  const size_t lds_plan = 16 * (size_t)segmax, lds_scatter = 8 * (size_t)maxtiles;
   for (int r = 0; r < R; ++r) {
     const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
-    k_is_count<<<dim3(maxtiles, nbatch), IS_TT, lds_count, st>>>(B2<const uint32_t*>(ki), b, r);
+    k_is_plan<<<dim3(1, nbatch), 1024, lds_plan, st>>>(B2<const uint32_t*>(ki), B2<const uint32_t*>(vi), b, r);
+    step("plan", r);
+    k_is_count<<<dim3(maxtiles, nbatch), IS_TT, 0, st>>>(B2<const uint32_t*>(ki), b, r);
     step("count", r);
     k_is_scatter<<<dim3(maxtiles, nbatch), IS_TT, lds_scatter, st>>>(B2<const uint32_t*>(ki),
                                                                       B2<const uint32_t*>(vi), ko, vo, b, r);
     step("scatter", r);
   }
-  k_is_own<<<dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st>>>(k0, v0, k1, v1, b, R);
-  step("own", R);
+  k_is_block<<<dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st>>>(k0, v0, k1, v1, b, R);
+  step("block", R);
+  k_is_wave<<<dim3(IS_WAVE_BLOCKS, nbatch), IS_WT, 0, st>>>(k0, v0, b);
+  step("wave", R);
 }
 
 }  // namespace fccf

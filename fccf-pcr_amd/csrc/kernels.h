@@ -28,7 +28,8 @@ constexpr int VG_KEY_BLOCKS = 512;
 
 // K1's sort in libstdc++ std::sort order (introsort.hip): workspace of one cloud.
 constexpr int IS_RMAX = 24;          // most partition rounds before the owner kernel
-constexpr int IS_OWN_BLOCKS = 256;   // owner workgroups per cloud (two per CU fit)
+constexpr int IS_OWN_BLOCKS = 256;   // block-kernel workgroups per cloud (one per CU)
+constexpr int IS_WAVE_BLOCKS = 512;  // wave-kernel workgroups per cloud (4 waves each)
 struct IsRound {
   uint32_t nseg, ntiles, nown, pad;  // large segments, their tiles, owned entries so far
 };
@@ -36,6 +37,7 @@ struct IsSeg {
   uint32_t f, l;
   int32_t depth;
   uint32_t tile0;
+  uint32_t m, P, kf, vf, vm;  // median position, pivot key, the first element, the median's value
 };
 struct IsOwn {
   uint32_t f, l;
@@ -43,15 +45,19 @@ struct IsOwn {
   uint32_t buf;  // which of the two key/value buffers holds the segment
 };
 struct IsBufs {
-  uint32_t* ctl;        // [0] sort length, [1] owner dequeue head, [2] slow paths taken (1 global partition, 2 heap)
+  uint32_t* ctl;        // [0] sort length, [1] block dequeue head, [2] slow paths taken (1 global partition,
+                        // 2 heap), [3..15] counters, [16] wave tasks, [17] wave dequeue head
   uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
+  uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles)
   uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
   IsRound* rounds;      // IS_RMAX
   IsSeg* segs;          // IS_RMAX x segmax
   uint32_t* cuts;       // IS_RMAX x segmax
   IsOwn* own;           // ownmax
+  uint4* tasks;         // wave tasks {f, n, depth, -} (count in ctl[16])
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   uint32_t segmax, maxtiles, ownmax;
+  uint32_t tier;        // rounds split segments longer than this (<= the owner's LDS capacity)
 };
 size_t introsort_bytes(uint32_t cap);
 IsBufs introsort_carve(void* base, uint32_t cap);

@@ -250,12 +250,11 @@ class Ctx:
         return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
 
     def sort_stats(self) -> dict:
-        a = np.zeros(16, np.uint32)
+        a = np.zeros(32, np.uint32)
         _check(_lib.fccf_debug_sort_stats(self._h, a.ctypes.data), "fccf_debug_sort_stats", self._h)
-        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_subtrees=int(a[4]),
-                    block_parts=int(a[5]), wave_parts=int(a[6]), us_wave_busy_or_heaps=int(a[7]) / 100, lds_elems=int(a[8]),
-                    reg_subtrees=int(a[12]), us_block_phase=int(a[9]) / 100, us_wave_phase=int(a[10]) / 100, us_final=int(a[11]) / 100,
-                    us_max_subtree=int(a[13]) / 100, us_max_entry=int(a[14]) / 100, us_all_entries=int(a[15]) / 100)
+        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_segments=int(a[4]),
+                    block_parts=int(a[5]), wave_parts=int(a[6]), heaps=int(a[7]), reg_subtrees=int(a[12]),
+                    wave_tasks=int(a[16]))
 
     def voxel_planes(self, xyz, params: Params | None = None):
         """face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled cloud on the GPU.

@@ -227,9 +227,9 @@ int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes
  * exact_gate != 0 runs the presorted second pass's single-workgroup form. */
 int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm_out);
 /* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags,
- * [3] global partitions, [4] LDS subtrees, [5] workgroup partitions, [6] wave
- * partitions, [7] heap sorts, [8] elements finished in LDS. */
-int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[16]);
+ * [3] global partitions, [4] LDS segments, [5] workgroup partitions, [6] wave
+ * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks. */
+int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
 
 /* PLY I/O (the reference's pcl::io::loadPLYFile<PointXYZ> surface, FCCF.cpp:1655-1665):
  * ascii / binary_little_endian / binary_big_endian, float x,y,z (double converted).
