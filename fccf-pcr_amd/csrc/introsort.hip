@@ -52,6 +52,7 @@ constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a w
 constexpr uint32_t IS_WCAP = 512;    // largest subtree finished by one wave (wave kernel)
 constexpr int IS_WC = IS_WCAP / 64;  // 8 elements per lane
 constexpr int IS_WT = 256;           // wave kernel: threads per block
+constexpr uint32_t IS_TASK_BIG = 128;  // wave tasks above this are dequeued first
 constexpr uint32_t IS_THRESHOLD = 16;  // libstdc++ _S_threshold
 constexpr int IS_STACK = 96;  // a wave's stack also holds its register-mode subtree (depth <= 48 each)
 // packed u32 subtree of at most IS_WCAP elements: off (13 bits) | len (11) | depth (6)
@@ -652,84 +653,92 @@ __device__ __forceinline__ uint32_t wave_partition(SL& S, uint32_t f, uint32_t l
   return min(max(cut, f + 1), l - 1);
 }
 
-// The whole introsort subtree of [f, f+n) (n <= 64) in registers: lane i holds
-// position f + i; each partition is ballots, partner selection from the masks and one
-// ds_bpermute per word; the leaves are then stably sorted by shuffles and the run is
-// written back in final order (every position marked as its own leaf).  stk: free
-// stack slots of the calling wave (packed a | b << 8 | depth << 16, lane indices).
+// The whole introsort subtree of [f, f+n) (n <= 64) in registers, level by level:
+// lane i holds position f + i, the segments of a level are bit runs of the head mask
+// H (all segments of one level share the depth), and every segment of the level is
+// partitioned in the same pass -- per-lane pivots by shuffles, ranks and partners
+// from the ballot masks restricted to the lane's segment, one shuffle per word for
+// the swaps.  Leaves are then stably sorted by shuffles and written back in final
+// order (every position marked as its own leaf).
 template <class SL>
-__device__ __forceinline__ void wave_sort_regs(SL& S, uint32_t f, uint32_t n, int d, uint32_t* stk) {
+__device__ __forceinline__ void wave_sort_regs(SL& S, uint32_t f, uint32_t n, int d, uint32_t* /*stk*/) {
   const uint32_t lane = lane_id();
   const bool live = lane < n;
   uint32_t k = live ? S.k[f + lane] : 0xFFFFFFFFu, v = live ? S.v[f + lane] : 0u;
-  uint64_t hd = 1ull;  // leaf starts (lane indices)
-  int sp = 0;
-  stk[sp++] = n << 8 | ((uint32_t)d << 16);
-  for (uint32_t guard = 0; sp > 0; ++guard) {
-    if (guard > 256 || sp >= IS_STACK / 2) {  // cannot happen
-      if (lane == 0) S.stat[2] |= 0x800u;
-      break;
-    }
-    // stack words are wave-uniform: readfirstlane keeps every index below scalar (a
-    // divergent lane index would turn each readlane into a waterfall loop)
-    const uint32_t it = __builtin_amdgcn_readfirstlane(stk[--sp]);
-    const uint32_t a = it & 0xFFu, b = (it >> 8) & 0xFFu, m = b - a;
-    const int dd = (int)(it >> 16);
-    if (m <= IS_THRESHOLD) {
-      hd |= 1ull << a;
-      continue;
-    }
-    if (dd == 0) {  // depth limit: heap sort this range in LDS (rare)
+  const uint64_t below = (1ull << lane) - 1ull;             // lanes < lane
+  const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;  // lanes <= lane
+  uint64_t H = 1ull;                                         // segment starts
+  uint64_t single = 0ull;                                    // heap-sorted positions (own leaves)
+  for (int dd = d, guard = 0; guard < 64; --dd, ++guard) {
+    // the lane's segment [a, b)
+    const uint32_t a = 63u - (uint32_t)__clzll((long long)(H & upto));
+    const uint64_t hi = H & ~upto;
+    const uint32_t b = hi ? min(n, (uint32_t)(__ffsll((unsigned long long)hi) - 1)) : n;
+    const uint32_t len = live ? b - a : 0u;
+    const bool act = len > IS_THRESHOLD && !((single >> lane) & 1ull);
+    if (!__ballot(act)) break;
+    if (dd == 0) {  // depth limit: heap sort every remaining segment in LDS (rare)
       if (live) {
         S.k[f + lane] = k;
         S.v[f + lane] = v;
       }
       wsync();
-      if (lane == 0) heap_sort(S.k + f + a, S.v + f + a, (int64_t)m);
+      const uint64_t starts = __ballot(act && lane == a);
+      if (lane == 0)
+        for (uint64_t m = starts; m; m &= m - 1) {
+          const uint32_t sa = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          const uint64_t h2 = H & ~((2ull << sa) - 1ull);
+          const uint32_t sb = h2 ? min(n, (uint32_t)(__ffsll((unsigned long long)h2) - 1)) : n;
+          heap_sort(S.k + f + sa, S.v + f + sa, (int64_t)(sb - sa));
+        }
       wsync();
       if (live) {
         k = S.k[f + lane];
         v = S.v[f + lane];
       }
-      hd |= (m == 64 ? ~0ull : ((1ull << m) - 1ull)) << a;  // each element its own leaf
-      continue;
+      single |= __ballot(act);
+      break;
     }
-    // __move_median_to_first(a, a+1, mid, b-1), applied in registers
-    const uint32_t A = a + 1, B = a + m / 2, C = b - 1;
-    const uint32_t ka = __builtin_amdgcn_readlane(k, A), kb = __builtin_amdgcn_readlane(k, B),
-                   kc = __builtin_amdgcn_readlane(k, C);
+    // __move_median_to_first(a, a+1, mid, b-1) of the lane's segment
+    const uint32_t A = a + 1, B = a + (b - a) / 2, C = b - 1;
+    const uint32_t ka = (uint32_t)__shfl((int)k, (int)min(A, 63u), 64), kb = (uint32_t)__shfl((int)k, (int)min(B, 63u), 64),
+                   kc = (uint32_t)__shfl((int)k, (int)min(C, 63u), 64);
     uint32_t mm;
     if (ka < kb) mm = kb < kc ? B : (ka < kc ? C : A);
     else mm = ka < kc ? A : (kb < kc ? C : B);
-    const uint32_t P = __builtin_amdgcn_readlane(k, mm), vm = __builtin_amdgcn_readlane(v, mm);
-    const uint32_t kf = __builtin_amdgcn_readlane(k, a), vf = __builtin_amdgcn_readlane(v, a);
-    if (lane == a) {
-      k = P;
-      v = vm;
-    } else if (lane == mm) {
-      k = kf;
-      v = vf;
+    mm = min(mm, 63u);
+    const uint32_t P = (uint32_t)__shfl((int)k, (int)mm, 64), vm = (uint32_t)__shfl((int)v, (int)mm, 64);
+    const uint32_t kf = (uint32_t)__shfl((int)k, (int)a, 64), vf = (uint32_t)__shfl((int)v, (int)a, 64);
+    if (act) {
+      if (lane == a) {
+        k = P;
+        v = vm;
+      } else if (lane == mm) {
+        k = kf;
+        v = vf;
+      }
     }
-    const bool in = lane > a && lane < b;
-    const uint64_t bg = __ballot(in && k >= P), bl = __ballot(in && k <= P);
+    const bool in = act && lane > a;
+    const uint64_t seg = (b >= 64 ? ~0ull : ((1ull << b) - 1ull)) & ~((2ull << a) - 1ull);  // (a, b)
+    const uint64_t bg = __ballot(in && k >= P) & seg, bl = __ballot(in && k <= P) & seg;
     const uint32_t le_tot = (uint32_t)__popcll(bl);
     const bool ge = (bg >> lane) & 1ull, le = (bl >> lane) & 1ull;
-    const uint32_t g = mbcnt(bg), h = mbcnt(bl);
+    const uint32_t g = (uint32_t)__popcll(bg & below), h = (uint32_t)__popcll(bl & below);
     const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
     const bool sl = le && g >= le_tot - h;
     uint32_t src = lane;  // the lane whose element lands here (swaps are symmetric)
     if (sg) src = select64(bl, le_tot - (g + 1));
     else if (sl) src = select64(bg, le_tot - h - 1);
-    const uint64_t cand = __ballot((ge && !sg) || sl);
+    const uint64_t cand = __ballot((ge && !sg) || sl) & seg;
+    const uint32_t cut = cand ? (uint32_t)(__ffsll((unsigned long long)cand) - 1) : A;
     k = (uint32_t)__shfl((int)k, (int)src, 64);
     v = (uint32_t)__shfl((int)v, (int)src, 64);
-    const uint32_t cut = cand ? (uint32_t)(__ffsll((unsigned long long)cand) - 1) : A;
-    stk[sp++] = cut | (b << 8) | ((uint32_t)(dd - 1) << 16);
-    stk[sp++] = a | (cut << 8) | ((uint32_t)(dd - 1) << 16);
+    H |= __ballot(act && lane == cut);
   }
-  // stable sort of each leaf (<= 16 lanes): rank by key, ties by lane
-  const uint32_t ls = 63u - (uint32_t)__clzll((long long)(hd & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
-  const uint64_t above = lane == 63 ? 0ull : (hd & ~((2ull << lane) - 1ull));
+  // stable sort of each leaf (<= 16 lanes; heap-sorted positions are their own leaves)
+  const uint64_t HL = H | single | (single << 1);
+  const uint32_t ls = 63u - (uint32_t)__clzll((long long)(HL & upto));
+  const uint64_t above = HL & ~upto;
   const uint32_t le_ = above ? min(n, (uint32_t)(__ffsll((unsigned long long)above) - 1)) : n;
   uint32_t rank = 0;
 #pragma unroll
@@ -912,9 +921,9 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
           heap_sort(S.k + off, S.v + off, (int64_t)n);
           if (IS_STATS) atomicAdd(&S.stat[7], 1u);
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
-        } else if (n <= IS_WCAP) {  // a wave task
-          const uint32_t ti = atomicAdd(&W.ctl[16], 1u);
-          W.tasks[ti] = make_uint4(f + off, n, (uint32_t)dd, 0u);
+        } else if (n <= IS_WCAP) {  // a wave task: large ones from the front, small from the back
+          if (n > IS_TASK_BIG) W.tasks[atomicAdd(&W.ctl[16], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
+          else W.tasks[W.taskmax - 1u - atomicAdd(&W.ctl[18], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
           for (uint32_t q = off; q < off + n; q += 32 - (q & 31)) {
             const uint32_t bit = q & 31, cnt = min(32u - bit, off + n - q);
             atomicOr(&S.intask[q >> 5], (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bit);
@@ -1192,7 +1201,8 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
     for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
   }
   wsync();
-  const uint32_t ntasks = W.ctl[16];
+  // large tasks first (longest-processing-time order keeps the tail short)
+  const uint32_t nbig = W.ctl[16], ntasks = nbig + W.ctl[18];
   uint32_t* __restrict__ K = K02[e];
   uint32_t* __restrict__ V = V02[e];
   for (;;) {
@@ -1200,7 +1210,7 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
     if (lane == 0) idx = atomicAdd(&W.ctl[17], 1u);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= ntasks) break;
-    const uint4 tk = W.tasks[idx];
+    const uint4 tk = W.tasks[idx < nbig ? idx : W.taskmax - 1u - (idx - nbig)];
     const uint32_t f = __builtin_amdgcn_readfirstlane(tk.x), n = __builtin_amdgcn_readfirstlane(tk.y);
     const int d = (int)__builtin_amdgcn_readfirstlane(tk.z);
 #pragma unroll
@@ -1304,7 +1314,8 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.segs = (IsSeg*)take(sizeof(IsSeg) * (size_t)b.segmax * IS_RMAX);
   b.cuts = (uint32_t*)take(4 * (size_t)b.segmax * IS_RMAX);
   b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
-  b.tasks = (uint4*)take(sizeof(uint4) * ((size_t)cap / 16 + 64));
+  b.taskmax = cap / 16 + 64;
+  b.tasks = (uint4*)take(sizeof(uint4) * (size_t)b.taskmax);
   b.prog = nullptr;
   b.tier = introsort_tier();
   return b;

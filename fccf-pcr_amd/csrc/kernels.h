@@ -46,7 +46,8 @@ struct IsOwn {
 };
 struct IsBufs {
   uint32_t* ctl;        // [0] sort length, [1] block dequeue head, [2] slow paths taken (1 global partition,
-                        // 2 heap), [3..15] counters, [16] wave tasks, [17] wave dequeue head
+                        // 2 heap), [3..15] counters, [16] large wave tasks, [17] wave dequeue head,
+                        // [18] small wave tasks (stored from the end)
   uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
   uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles)
   uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
@@ -56,7 +57,7 @@ struct IsBufs {
   IsOwn* own;           // ownmax
   uint4* tasks;         // wave tasks {f, n, depth, -} (count in ctl[16])
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
-  uint32_t segmax, maxtiles, ownmax;
+  uint32_t segmax, maxtiles, ownmax, taskmax;
   uint32_t tier;        // rounds split segments longer than this (<= the owner's LDS capacity)
 };
 size_t introsort_bytes(uint32_t cap);
