@@ -30,8 +30,45 @@ METRIC = "coplane-pair correspondences/sec + end-to-end registration ms, 1M-pt p
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM"); every kernel here is HBM/latency bound
 # Kernels with a probe site (fccf-pcr_amd/csrc, FCCF_PROBED) and their algorithmic bytes per launch
 # ("Measurement").  The roofline reports the one with the most GPU time per step.
-PROBE_KERNELS = ["k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter", "k_vg_keys", "k_vg_centroid",
-                 "k_gather", "k_voxel_fit", "k_fv_counts", "k_match_count", "k_match_emit"]
+PROBE_KERNELS = ["k_is_wave", "k_is_scatter", "k_is_block", "k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter",
+                 "k_vg_keys", "k_vg_centroid", "k_gather", "k_voxel_fit", "k_fv_counts", "k_match_count",
+                 "k_match_emit"]
+
+
+def stage_roofline(st):
+    """algorithmic bytes of the N-proportional stages over their
+    device spans (HIP events between the cloud-stage graphs, fccf_stats.dev_ms), per
+    stage and aggregated.  Per cloud c: D = 12 N_c + 12 M1_c + 12 M1_c + 12 M_c (both
+    VoxelGrid passes), P = 12 M_c + 32 V_c (1 m voxel fit, V = occupied leaves),
+    F = 12 (S1 + S2) per fine_verify evaluation."""
+    N = (st.n_src, st.n_tar)
+    M1 = (st.m1_src, st.m1_tar)
+    M = (st.m_src, st.m_tar)
+    V = (st.leaves1, st.leaves2)
+    bytes_ = {"D": sum(12 * N[c] + 24 * M1[c] + 12 * M[c] for c in range(2)),
+              "P": sum(12 * M[c] + 32 * V[c] for c in range(2)),
+              "F": 12 * (st.res1 + st.res2) * st.fine_evals}
+    ms = {"D": st.dev_ms[0] + st.dev_ms[1], "P": st.dev_ms[2], "F": st.dev_ms[3]}
+    out = {}
+    for k in ("D", "P", "F"):
+        gbs = bytes_[k] / (ms[k] * 1e-3) / 1e9 if ms[k] > 0 else None
+        out[k] = {"bytes": int(bytes_[k]), "ms": round(ms[k], 4), "achieved_GBps": gbs,
+                  "frac": gbs / HBM_PEAK_GBS if gbs else None}
+    tb, tm = sum(bytes_.values()), sum(ms.values())
+    agg = tb / (tm * 1e-3) / 1e9 if tm > 0 else None
+    out["aggregate"] = {"bytes": int(tb), "ms": round(tm, 4), "achieved_GBps": agg,
+                        "frac": agg / HBM_PEAK_GBS if agg else None}
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def spawn_ranks(n, argv):
@@ -89,21 +126,39 @@ def allsum(dist, v):
 
 def cpu_baseline(src, tar, leaf, budget_s):
     """The oracle (single-threaded C++ restatement of FCCF.cpp, introsort mode =
-    the reference's std::sort) on the same workload, repeated within a time budget."""
+    the reference's std::sort) on the same workload, repeated within a time budget,
+    pinned to one host core (taskset-style pinning, CPU model recorded)."""
     import oracle_py
-    times, K = [], None
-    t_end = time.time() + budget_s
-    while not times or (time.time() < t_end and len(times) < 20):
-        t0 = time.perf_counter()
-        run = oracle_py.Run(src, tar, leaf, oracle_py.INTROSORT)
-        times.append(time.perf_counter() - t0)
-        K = int(run.get("counts", np.int64)[0])
-        del run
+    times, K, stages, ref_win = [], None, None, []
+    try:
+        prev = os.sched_getaffinity(0)
+        core = min(prev)
+        os.sched_setaffinity(0, {core})
+    except (AttributeError, OSError):
+        prev, core = None, None
+    try:
+        t_end = time.time() + budget_s
+        while not times or (time.time() < t_end and len(times) < 20):
+            t0 = time.perf_counter()
+            run = oracle_py.Run(src, tar, leaf, oracle_py.INTROSORT)
+            times.append(time.perf_counter() - t0)
+            K = int(run.get("counts", np.int64)[0])
+            stages = run.times()
+            ref_win.append(times[-1] * 1e3 - float(run.get("main_vg_ms", np.float64)[0]))
+            del run
+    finally:
+        if prev is not None:
+            os.sched_setaffinity(0, prev)
     med = statistics.median(times)
+    names = ["downsample", "voxelfit", "grow_select", "match", "cluster", "verify", "fine", "fuse", "total"]
     return {"value": K / med, "unit": "correspondences/s", "cores": 1, "kind": "port",
-            "ms_per_registration": med * 1e3, "K": K,
+            "ms_per_registration": med * 1e3, "K": K, "pinned_cpu": core, "cpu_model": cpu_model(),
+            "host_nproc": os.cpu_count(),
+            "stage_ms_last": {n: round(float(v), 3) for n, v in zip(names, stages)} if stages is not None else None,
+            # the reference's own timer window (FCCF.cpp:1681-1685) excludes main's VoxelGrid
+            "ref_window_ms_median": statistics.median(ref_win),
             "sample": f"{len(times)} full registrations of the same c3 pair (median), oracle/ C++ restatement, "
-                      f"introsort summation order, 1 thread"}
+                      f"introsort summation order, 1 thread pinned to CPU {core}"}
 
 
 class _SelftestCtx:
@@ -242,11 +297,16 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier(dist)
     # latency: single registrations, one at a time (untimed for `value`)
-    per = []
+    per, ref_win, stage_rl = [], [], None
     for _ in range(min(args.steps, 10)):
         a = time.perf_counter()
-        T1, st = reg()
+        T1, st1 = reg()
         per.append(time.perf_counter() - a)
+        if not args.selftest:
+            # the reference's timer window (FCCF.cpp:1681-1685) excludes main's VoxelGrid
+            # pass: the registration minus that pass's device span
+            ref_win.append(per[-1] * 1e3 - st1.dev_ms[0])
+            stage_rl = stage_roofline(st1)
     if not args.selftest:
         assert np.array_equal(T1.view(np.uint32), np.asarray(T).view(np.uint32)), "pipelined result differs"
     # PCIe-inclusive latency: the same registration from host arrays (fccf_register);
@@ -300,6 +360,8 @@ def main():
                        "host_threads_per_rank": int(os.environ.get("FCCF_HOST_THREADS", "0")) or None},
             "e2e_ms_median": statistics.median(per) * 1e3,  # one registration alone (latency)
             "e2e_host_input_ms_median": statistics.median(per_host) * 1e3,  # incl. H2D of both clouds
+            "ref_window_ms_median": statistics.median(ref_win) if ref_win else None,
+            "device_ms": {k: round(v, 4) for k, v in st1.as_dict()["dev_ms"].items()} if not args.selftest else None,
             "K_per_registration": int(st.K),
             "K_pass": int(st.K_pass),
             "graph_captures_last_step": int(st.graph_captures),
@@ -309,6 +371,7 @@ def main():
             "trans_err_m_vs_gt": float(np.linalg.norm(T[:3, 3] - T_gt[:3, 3])),
         }
         if roofline is not None:
+            roofline["stage"] = stage_rl
             out["roofline"] = roofline
             out["kernel_table"] = {k: {a: (round(b, 4) if isinstance(b, float) else b) for a, b in v.items()}
                                    for k, v in table.items()}

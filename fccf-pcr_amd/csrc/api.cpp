@@ -64,8 +64,10 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   bool ok = true;
   for (auto& s : c->sa) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
   ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
-  for (auto& cs : c->cs)
+  for (auto& cs : c->cs) {
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    for (auto& e : cs.tev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  }
   if (!ok) {
     fccf_ctx_destroy(c);
     return FCCF_E_HIP;
@@ -85,6 +87,8 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
     cs.g_rep.reset();
     cs.g_fine.reset();
     for (auto& e : cs.ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : cs.tev)
       if (e) (void)hipEventDestroy(e);
   }
   for (auto& s : c->sa)

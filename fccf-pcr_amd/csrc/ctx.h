@@ -176,7 +176,9 @@ struct fccf_ctx {
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
     hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
                                      // [4] clouds done, [5] S1 replay done
-    fccf::CachedGraph g_seg[2];      // both clouds batched: downsample, faces (pipeline.cpp)
+    hipEvent_t tev[6] = {};          // timing: cloud start, pass 1 done, pass 2 done, faces done,
+                                     // fine start, fine done (fccf_stats::dev_ms)
+    fccf::CachedGraph g_seg[3];      // both clouds batched: main's VoxelGrid, faces, the driver's pass
     fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per

@@ -4,6 +4,7 @@
 #include "host_stages.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -145,6 +146,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
     }
   }
   // range_face (:409-427): exchange sort on voxel counts, emulated on indices
+  const auto t_sel = std::chrono::steady_clock::now();  // range_face + selection from here
   std::vector<int> ord(G.size());
   for (size_t i = 0; i < G.size(); ++i) ord[i] = (int)i;
   for (size_t i = 0; i + 1 < ord.size(); ++i)
@@ -177,6 +179,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
     }
     if ((float)cur > P.select_plane_number) break;
   }
+  out.ms_select = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sel).count();
   return out;
 }
 

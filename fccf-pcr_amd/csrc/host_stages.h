@@ -32,6 +32,7 @@ struct GrowOut {
   std::vector<double> theta;     // roughness per selected plane
   std::vector<Plane> groups;     // all groups after stage 2 + range_face (debug)
   std::vector<int32_t> galloc;   // their is_allocate flags
+  double ms_select = 0.0;        // host time of range_face + selection
 };
 
 // face_extrate region growing (:536-648), range_face (:409-427), selection (:650-677).

@@ -278,7 +278,11 @@ __global__ void __launch_bounds__(1024) k_is_plan(B2<const uint32_t*> K2, B2<con
   }
   for (uint32_t t = threadIdx.x; t < W.maxtiles; t += blockDim.x)
     W.tseg[t] = t < ntiles ? upper_index(t0, nseg, t) : IS_NONE;
-  if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
+  uint32_t ne = 0;  // elements partitioned this round (the scatter probe's unit count)
+  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) ne += tl[j] - tf[j];
+  uint32_t ne_tot;
+  (void)block_excl_scan(ne, sh, &ne_tot);
+  if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, ne_tot};
 }
 
 // Per-tile ge/le counts against the segment's pivot and the tile-local position
@@ -922,6 +926,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
           if (IS_STATS) atomicAdd(&S.stat[7], 1u);
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
         } else if (n <= IS_WCAP) {  // a wave task: large ones from the front, small from the back
+          atomicAdd(&W.ctl[19], n);  // the wave probe's unit count
           if (n > IS_TASK_BIG) W.tasks[atomicAdd(&W.ctl[16], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
           else W.tasks[W.taskmax - 1u - atomicAdd(&W.ctl[18], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
           for (uint32_t q = off; q < off + n; q += 32 - (q & 31)) {
@@ -1155,7 +1160,10 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       if (threadIdx.x == 0) S.gsp = sp - 1;
       __syncthreads();
       if (len <= IS_LCAP) {
-        if (IS_STATS && threadIdx.x == 0) atomicAdd(&W.ctl[4], 1u);
+        if (threadIdx.x == 0) {
+          atomicAdd(&W.ctl[4], 1u);
+          atomicAdd(&W.ctl[20], len);  // the block probe's unit count
+        }
         lds_block(S, W, K, V, Kb[0], Vb[0], gf, len, gd);
       } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
         if (threadIdx.x == 0) {
@@ -1341,13 +1349,19 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
     step("plan", r);
     k_is_count<<<dim3(maxtiles, nbatch), IS_TT, 0, st>>>(B2<const uint32_t*>(ki), b, r);
     step("count", r);
-    k_is_scatter<<<dim3(maxtiles, nbatch), IS_TT, lds_scatter, st>>>(B2<const uint32_t*>(ki),
-                                                                      B2<const uint32_t*>(vi), ko, vo, b, r);
+    // algorithmic bytes: key + value read and written, plus a 2-byte list entry
+    FCCF_LAUNCH("k_is_scatter",
+                (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
+                k_is_scatter, dim3(maxtiles, nbatch), IS_TT, lds_scatter, st, B2<const uint32_t*>(ki),
+                B2<const uint32_t*>(vi), ko, vo, b, r);
     step("scatter", r);
   }
-  k_is_block<<<dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st>>>(k0, v0, k1, v1, b, R);
+  // algorithmic bytes: each element's key and value read once and written once
+  FCCF_LAUNCH("k_is_block", (b[0].ctl + 20, 16.0, nbatch > 1 ? b[1].ctl + 20 : nullptr, 16.0, 0.0), k_is_block,
+              dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
-  k_is_wave<<<dim3(IS_WAVE_BLOCKS, nbatch), IS_WT, 0, st>>>(k0, v0, b);
+  FCCF_LAUNCH("k_is_wave", (b[0].ctl + 19, 16.0, nbatch > 1 ? b[1].ctl + 19 : nullptr, 16.0, 0.0), k_is_wave,
+              dim3(IS_WAVE_BLOCKS, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
 }
 

@@ -197,14 +197,22 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
 template <class T, class F>
 B2<T> both(const CloudWS* w, F get) { return B2<T>(get(w[0]), get(w[1])); }
 
+// main's VoxelGrid pass (:1668-1678), its output also into ds1f
+void seg_pass1(CloudWS* w, float leaf, hipStream_t st) {
+  const uint32_t cap = w[0].cap;
+  auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
+  const B2<VGBufs> vg(w[0].vg, w[1].vg);
+  voxel_grid(both<const float*>(w, [](const CloudWS& c) { return c.in; }), sc(0), cap, leaf,
+             both<float*>(w, [](const CloudWS& c) { return c.ds1; }), sc(1), vg, st, false, 2,
+             both<float*>(w, [](const CloudWS& c) { return c.ds1f; }));
+}
+// the driver's remove-NaN and second VoxelGrid pass (:1374-1387)
 void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
   const uint32_t cap = w[0].cap;
   auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
   const B2<VGBufs> vg(w[0].vg, w[1].vg);
   const B2<float*> ds1 = both<float*>(w, [](const CloudWS& c) { return c.ds1; });
   const B2<float*> ds1f = both<float*>(w, [](const CloudWS& c) { return c.ds1f; });
-  voxel_grid(both<const float*>(w, [](const CloudWS& c) { return c.in; }), sc(0), cap, leaf, ds1, sc(1), vg, st,
-             false, 2, ds1f);  // main :1668-1678, output also into ds1f
   k_finite_fix<<<dim3(1, 2), 1024, 0, st>>>(B2<const float*>(ds1), sc(1),
                                             B2<const VGParams*>(w[0].vg.params, w[1].vg.params), ds1f,
                                             sc(2));  // driver :1374-1375
@@ -391,7 +399,11 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     if (seg_timing) HIP_CHECK(hipEventRecord(tm.ev[i], q));
   };
   mark(0, st0);
-  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_downsample(w, leaf, st0); });
+  HIP_CHECK(hipEventRecord(cs.tev[0], st0));
+  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_pass1(w, leaf, st0); });
+  HIP_CHECK(hipEventRecord(cs.tev[1], st0));
+  cs.g_seg[2].run(&key, sizeof key, st0, [&] { seg_downsample(w, leaf, st0); });
+  HIP_CHECK(hipEventRecord(cs.tev[2], st0));
   mark(1, st0);
   HIP_CHECK(hipEventRecord(cs.ev[0], st0));
   HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[0], 0));
@@ -407,6 +419,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
                      &host_mail(c)->clouds[s], B2<const uint32_t*>(w[0].sc, w[1].sc));
   mark(4, st0);
   tm.armed = seg_timing;
+  HIP_CHECK(hipEventRecord(cs.tev[3], st0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
   cs.g_rep.run(&key, sizeof key, st0, [&] { seg_s1_replay(w, P, st0); });
   HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
@@ -447,7 +460,17 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     else vox[k] = d2h(w[k].planar, fsc[k][2], st0);  // past the mailbox: copy from HBM
   }
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
-  S.ms[FCCF_T_DOWNSAMPLE] = ms_since(t0);  // downsample + voxel fit (one device span)
+  {  // device spans of the cloud stage (its events have completed with ev[4])
+    float d[3] = {};
+    for (int i = 0; i < 3; ++i) HIP_CHECK(hipEventElapsedTime(&d[i], c->cs[s].tev[i], c->cs[s].tev[i + 1]));
+    for (int i = 0; i < 3; ++i) S.dev_ms[i] = d[i];
+    S.ms[FCCF_T_DOWNSAMPLE] = d[0] + d[1];
+    S.ms[FCCF_T_VOXELFIT] = d[2];
+  }
+  S.m1_tar = sc[0][1];
+  S.m1_src = sc[1][1];
+  S.leaves1 = fsc[0][0];
+  S.leaves2 = fsc[1][0];
   HostTrace ht;
   ht.t0 = ps.t_enq;
   ht.mark("clouds");
@@ -502,9 +525,12 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // ---------------- host: growing + selection + select_base
   GrowOut g[2];
   std::vector<Base> base[2];
+  double sel_ms[2] = {0.0, 0.0};
   c->pool.parallel_for(2, [&](int k) {  // the two clouds are independent
     g[k] = grow_and_select(vox[k].data(), (int)vox[k].size(), P);
+    const auto tb = clk::now();
     base[k] = select_base(g[k].planes, g[k].theta, P, k + 1);
+    sel_ms[k] = g[k].ms_select + ms_since(tb);
   });
   S.groups1 = (int64_t)g[0].groups.size();
   S.groups2 = (int64_t)g[1].groups.size();
@@ -512,7 +538,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   S.planes2 = (int64_t)g[1].planes.size();
   S.bases1 = (int64_t)base[0].size();
   S.bases2 = (int64_t)base[1].size();
-  S.ms[FCCF_T_GROW] = ms_since(t0);
+  S.ms[FCCF_T_SELECT] = std::max(sel_ms[0], sel_ms[1]);  // range_face + selection + select_base
+  S.ms[FCCF_T_GROW] = ms_since(t0) - S.ms[FCCF_T_SELECT];
   ht.mark("grow");
   if (c->debug)
     for (int k = 0; k < 2; ++k) {
@@ -751,11 +778,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       std::lock_guard<std::mutex> lk(capture_mutex());  // ev[5]'s stream may be capturing the next pair's clouds
       HIP_CHECK(hipStreamWaitEvent(sf, c->cs[s].ev[5], 0));  // S1 octree bounds replayed (after the clouds)
     }
+    HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm);
     });
     HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
     HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));  // fine verification of this set's pair done
     ht.mark("fine_launched");
   }
@@ -787,7 +816,11 @@ void phase_b2(fccf_ctx* c, int s) {
     const FineMail& fm = host_mail(c)->fine[s];
     std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
     if (fm.err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
+    float d = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
+    S.dev_ms[3] = d;
   }
+  S.fine_evals = E;
   S.ms[FCCF_T_FINE] = ms_since(pb.t_fine);
   pb.ht.mark("fine");
   pb.ht.flush();

@@ -46,10 +46,13 @@ class Stats(ctypes.Structure):
         "planes1", "planes2", "bases1", "bases2", "K", "K_pass")] + [
         ("cand", ctypes.c_int64 * 3), ("fine", ctypes.c_int64 * 3), ("lm_solves", ctypes.c_int64),
         ("overflow_passthrough", ctypes.c_int32), ("graph_captures", ctypes.c_int32),
-        ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double)]
+        ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double),
+        ("m1_src", ctypes.c_int64), ("m1_tar", ctypes.c_int64), ("leaves1", ctypes.c_int64), ("leaves2", ctypes.c_int64),
+        ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4)]
 
     def as_dict(self):
-        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms")}
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "dev_ms")}
+        d["dev_ms"] = dict(zip(("vg_main", "vg_driver", "faces", "fine"), list(self.dev_ms)))
         d["cand"] = list(self.cand)
         d["fine"] = list(self.fine)
         d["ms"] = dict(zip(T_NAMES, list(self.ms)))

@@ -79,8 +79,15 @@ typedef struct fccf_stats {
   int64_t lm_solves;             /* quick_verify refinements run                  */
   int32_t overflow_passthrough;  /* VoxelGrid int32 guard tripped (any pass)      */
   int32_t graph_captures;        /* device-stage graphs (re)captured by this call */
-  double ms[FCCF_T_COUNT];       /* stage wall times                              */
+  double ms[FCCF_T_COUNT];       /* stage times: DOWNSAMPLE and VOXELFIT are device
+                                    spans (HIP events), the others host wall times  */
   double ms_total;               /* host arrays (or resident device arrays) -> T  */
+  /* appended in round 2 (SURVEY.md §8(d) stage roofline inputs) */
+  int64_t m1_src, m1_tar;        /* after main's VoxelGrid pass (FCCF.cpp:1668-1678) */
+  int64_t leaves1, leaves2;      /* occupied 1 m octree leaves (driver source / target) */
+  int64_t fine_evals;            /* fine_verify evaluations E                      */
+  double dev_ms[4];              /* device spans: main's VoxelGrid pass, the driver's
+                                    remove-NaN + second pass, face voxels, fine verify */
 } fccf_stats;
 
 typedef struct fccf_ctx fccf_ctx;

@@ -1535,7 +1535,9 @@ extern "C" orc_ctx* orc_register(const float* src_xyz, int64_t n_src, const floa
   int ovf = 0;
   Cloud cs = voxel_grid(src, leaf, order, &ovf);  // main :1668-1672
   Cloud ct = voxel_grid(tar, leaf, order, &ovf);  // main :1674-1678
-  cx->ms[0] += ms_since(t0);
+  const double main_vg_ms = ms_since(t0);
+  cx->ms[0] += main_vg_ms;
+  cx->st.put1("main_vg_ms", main_vg_ms);  // outside the reference's timer window (:1681-1685)
   cx->st.put("ds_src", cs);
   cx->st.put("ds_tar", ct);
   M4f best = identity4();
