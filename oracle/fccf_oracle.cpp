@@ -128,16 +128,63 @@ static inline float cos_f(float x) { return (float)std::cos((double)x); }
 static inline float sin_f(float x) { return (float)std::sin((double)x); }
 
 // ------------------------------------------------------ predicates (:369-407)
-static float compute_normal_angel(float x1, float y1, float z1, float x2, float y2, float z2) {
+// The acos convention of FCCF.cpp:374 `float theta=acos(cos_theta)*180/M_PI;`
+// (cos_theta is float, no `using namespace std` in FCCF.cpp).  Which overload
+// the unqualified call binds to depends on whether some PCL/VTK/FLANN header
+// brought libstdc++'s <math.h> wrapper (`using std::acos;`) into the global
+// namespace, and acosf's last bit on the glibc the reference was built with.
+// The three candidates are switchable (orc_set_acos_mode) so that a test can
+// count the threshold decisions that would flip between them:
+//   ACOS_CR_FLOAT   float overload, correctly rounded acosf (the default and
+//                   the convention the HIP product's cosine cut points follow)
+//   ACOS_LIBM_FLOAT float overload, this host's glibc acosf
+//   ACOS_DOUBLE     C's double acos: the whole expression in double, then float
+enum { ACOS_CR_FLOAT = 0, ACOS_LIBM_FLOAT = 1, ACOS_DOUBLE = 2, ACOS_MODES = 3 };
+static int g_acos_mode = ACOS_CR_FLOAT;
+static float theta_of_cos(float cos_theta, int mode) {
+  switch (mode) {
+    case ACOS_LIBM_FLOAT: return (float)((double)(::acosf(cos_theta) * 180.0f) / M_PI);
+    case ACOS_DOUBLE: return (float)(std::acos((double)cos_theta) * 180.0 / M_PI);
+    default: return (float)((double)(acos_f(cos_theta) * 180.0f) / M_PI);
+  }
+}
+static float normal_cos(float x1, float y1, float z1, float x2, float y2, float z2) {
   const double n1[3] = {x1, y1, z1}, n2[3] = {x2, y2, z2};
   float n1n3 = (float)dotd(n1, n2);
-  float cos_theta = (float)((double)n1n3 / (normd(n1) * normd(n2)));
-  float theta = (float)((double)(acos_f(cos_theta) * 180.0f) / M_PI);
-  return theta;
+  return (float)((double)n1n3 / (normd(n1) * normd(n2)));
 }
-static bool compare_normal(float x1, float y1, float z1, float x2, float y2, float z2, float thr) {
-  float theta = compute_normal_angel(x1, y1, z1, x2, y2, z2);
-  return !(theta > thr);
+static float compute_normal_angel(float x1, float y1, float z1, float x2, float y2, float z2) {
+  return theta_of_cos(normal_cos(x1, y1, z1, x2, y2, z2), g_acos_mode);
+}
+
+// Decision audit: every thresholded use of the angle (sites below) evaluates
+// its predicate under all three conventions; `flips` counts the evaluations
+// where the conventions disagree, `differ` those where the angles' bits do.
+enum { SITE_GROW = 0, SITE_MERGE, SITE_ROUGH, SITE_BASE, SITE_THIRD, SITE_CLUSTER, SITE_VERIFY, SITE_PAIR, SITE_N, SITE_ANGLE_ONLY = SITE_N };
+struct AcosAudit { uint64_t evals[SITE_N + 1], differ[SITE_N + 1], flips[SITE_N + 1]; };
+static AcosAudit g_audit;
+// Records one evaluation of a decision whose inputs under the three conventions
+// are v[] (angles or quantities derived from them) and whose outcomes are d[].
+template <class T>
+static void audit_site(int site, const T v[ACOS_MODES], const bool d[ACOS_MODES]) {
+  g_audit.evals[site]++;
+  if (std::memcmp(&v[0], &v[1], sizeof(T)) || std::memcmp(&v[0], &v[2], sizeof(T))) g_audit.differ[site]++;
+  if (d[0] != d[1] || d[0] != d[2]) g_audit.flips[site]++;
+}
+template <class Pred>
+static bool angle_decide(int site, float x1, float y1, float z1, float x2, float y2, float z2, Pred pred,
+                         float* theta_out = nullptr, float* all_out = nullptr) {
+  const float c = normal_cos(x1, y1, z1, x2, y2, z2);
+  float th[ACOS_MODES];
+  bool d[ACOS_MODES];
+  for (int m = 0; m < ACOS_MODES; ++m) { th[m] = theta_of_cos(c, m); d[m] = pred(th[m]); }
+  audit_site(site, th, d);
+  if (theta_out) *theta_out = th[g_acos_mode];
+  if (all_out) std::memcpy(all_out, th, sizeof th);
+  return d[g_acos_mode];
+}
+static bool compare_normal(int site, float x1, float y1, float z1, float x2, float y2, float z2, float thr) {
+  return angle_decide(site, x1, y1, z1, x2, y2, z2, [thr](float t) { return !(t > thr); });
 }
 static bool compare_plane(float nx1, float ny1, float nz1, float cx1, float cy1, float cz1, float nx2,
                           float ny2, float nz2, float cx2, float cy2, float cz2, float l, float k) {
@@ -602,7 +649,7 @@ static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
     for (int a = 0; a < 3; ++a) { f.an[a] = vox[i].n[a]; f.ac[a] = vox[i].c[a]; }
     for (size_t j = 0; j < vox.size(); ++j) {
       if (valloc[j]) continue;
-      bool same = compare_normal(f.an[0], f.an[1], f.an[2], vox[j].n[0], vox[j].n[1], vox[j].n[2],
+      bool same = compare_normal(SITE_GROW, f.an[0], f.an[1], f.an[2], vox[j].n[0], vox[j].n[1], vox[j].n[2],
                                  P.normal_vector_threshold1);
       bool cop = compare_plane(f.an[0], f.an[1], f.an[2], f.ac[0], f.ac[1], f.ac[2], vox[j].n[0], vox[j].n[1],
                                vox[j].n[2], vox[j].c[0], vox[j].c[1], vox[j].c[2], P.parameter_l1, P.parameter_k1);
@@ -625,7 +672,8 @@ static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
         if (j == i || groth[j].alloc) continue;
         Face& a = groth[i];
         Face& b = groth[j];
-        bool same = compare_normal(a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2], P.normal_vector_threshold2);
+        bool same = compare_normal(SITE_MERGE, a.an[0], a.an[1], a.an[2], b.an[0], b.an[1], b.an[2],
+                                   P.normal_vector_threshold2);
         bool cop = compare_plane(a.an[0], a.an[1], a.an[2], a.ac[0], a.ac[1], a.ac[2], b.an[0], b.an[1], b.an[2],
                                  b.ac[0], b.ac[1], b.ac[2], P.parameter_l2, P.parameter_k2);
         if (same && cop) {
@@ -648,13 +696,24 @@ static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
     const Face& f = groth[i];
     if (!f.alloc) {
       out.planes.push_back(f);
-      double sum = 0;
+      double sum = 0, alt[ACOS_MODES] = {0, 0, 0};
       for (int m : f.members) {
-        double th = compute_normal_angel(f.an[0], f.an[1], f.an[2], vox[m].n[0], vox[m].n[1], vox[m].n[2]);
+        float thf, tha[ACOS_MODES];
+        angle_decide(SITE_ANGLE_ONLY, f.an[0], f.an[1], f.an[2], vox[m].n[0], vox[m].n[1], vox[m].n[2],
+                     [](float) { return false; }, &thf, tha);
+        double th = thf;
         sum += std::fabs(th);
+        for (int a = 0; a < ACOS_MODES; ++a) alt[a] += std::fabs((double)tha[a]);
       }
       sum /= (double)f.members.size();
       out.theta.push_back(sum);
+      // the roughness class select_base derives from it (:445-452)
+      bool rd[ACOS_MODES];
+      for (int a = 0; a < ACOS_MODES; ++a) {
+        alt[a] /= (double)f.members.size();
+        rd[a] = alt[a] <= (double)P.rough_threshold_gl;
+      }
+      audit_site(SITE_ROUGH, alt, rd);
       cur++;
     }
     if (cur > P.select_plane_number) break;
@@ -662,16 +721,18 @@ static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
 }
 
 // ------------------------------------------------------ select_base (:429-468)
-struct Base { int i1, i2; float angle; };
+struct Base { int i1, i2; float angle; float alt[3]; };
 static void select_base(const std::vector<Face>& F, const std::vector<double>& th, const Params& P,
                         std::vector<Base>& base, std::vector<int>& type) {
   const double t1 = P.rough_threshold_gl;
   for (size_t i = 0; i < F.size(); ++i)
     for (size_t j = 0; j < F.size(); ++j) {
       if (!(i < j)) continue;
-      float ang = compute_normal_angel(F[i].an[0], F[i].an[1], F[i].an[2], F[j].an[0], F[j].an[1], F[j].an[2]);
-      if (P.included_angle_min_threshold < ang && ang < P.included_angle_max_threshold) {
-        base.push_back({(int)i, (int)j, ang});
+      float ang, alt[ACOS_MODES];
+      const float lo = P.included_angle_min_threshold, hi = P.included_angle_max_threshold;
+      if (angle_decide(SITE_BASE, F[i].an[0], F[i].an[1], F[i].an[2], F[j].an[0], F[j].an[1], F[j].an[2],
+                       [lo, hi](float t) { return lo < t && t < hi; }, &ang, alt)) {
+        base.push_back({(int)i, (int)j, ang, {alt[0], alt[1], alt[2]}});
         if (th[i] <= t1 && th[j] <= t1) type.push_back(0);
         else if (th[i] > t1 && th[j] > t1) type.push_back(1);
         else if (th[i] <= t1 && th[j] > t1) type.push_back(2);
@@ -723,8 +784,10 @@ static void computer_transform(std::vector<M4f>* out, int i11, int i12, int i21,
     for (int k3 : three) {
       for (size_t q = 0; q < F2.size(); ++q) {
         if ((int)q == i21 || (int)q == i22) continue;
-        float a3 = compute_normal_angel(F1[k3].an[0], F1[k3].an[1], F1[k3].an[2], pn[q].x, pn[q].y, pn[q].z);
-        if (a3 < P.third_plane_normal_threshold && std::fabs(dotf(n2cm2, pn[q])) > P.third_plane_threshold) {
+        const float thr3 = P.third_plane_normal_threshold;
+        const bool a3ok = angle_decide(SITE_THIRD, F1[k3].an[0], F1[k3].an[1], F1[k3].an[2], pn[q].x, pn[q].y,
+                                       pn[q].z, [thr3](float t) { return t < thr3; });
+        if (a3ok && std::fabs(dotf(n2cm2, pn[q])) > P.third_plane_threshold) {
           getthree = true;
           V3f k1 = {F1[k3].an[0], F1[k3].an[1], F1[k3].an[2]};
           V3f k2 = pn[q];
@@ -860,8 +923,8 @@ static void transform_cluster(std::vector<QT>& in, std::vector<QT>& fine, int cl
       QT& o = in[e.second];
       Qf q2 = {o.qw, o.qx, o.qy, o.qz};
       V3f p2 = quat_rotate(q2, V3f{1, 0, 0});
-      float dq = compute_normal_angel(p1.x, p1.y, p1.z, p2.x, p2.y, p2.z);
-      if (dq < P.cluster_angel_threshold) {
+      const float thrc = P.cluster_angel_threshold;
+      if (angle_decide(SITE_CLUSTER, p1.x, p1.y, p1.z, p2.x, p2.y, p2.z, [thrc](float t) { return t < thrc; })) {
         o.alloc = true;
         cl.push_back(o);
       }
@@ -1198,12 +1261,14 @@ static float quick_verify(M4f& T, const std::vector<Face>& F1, const std::vector
     std::vector<int> cand;
     bool find = false;
     for (size_t j = 0; j < F2.size(); ++j) {
-      float ang = compute_normal_angel(a.an[0], a.an[1], a.an[2], n2[j].x, n2[j].y, n2[j].z);
+      const float thrv = P.quick_verify_angel_threshold;
+      const bool angok = angle_decide(SITE_VERIFY, a.an[0], a.an[1], a.an[2], n2[j].x, n2[j].y, n2[j].z,
+                                      [thrv](float t) { return t < thrv; });
       const double dn1[3] = {a.an[0], a.an[1], a.an[2]}, dn2[3] = {n2[j].x, n2[j].y, n2[j].z};
       const double dc1[3] = {a.ac[0], a.ac[1], a.ac[2]}, dc2[3] = {c2[j].x, c2[j].y, c2[j].z};
       float d1 = (float)dotd(dn1, dc1), d2 = (float)dotd(dn2, dc2);
       float dist = std::fabs(d1 - d2);
-      if (ang < P.quick_verify_angel_threshold && dist < P.quick_verify_distance_threshold) {
+      if (angok && dist < P.quick_verify_distance_threshold) {
         find = true;
         cand.push_back((int)j);
       }
@@ -1405,6 +1470,13 @@ static void computer_transform_guess(Cloud source, Cloud target, float leaf, int
       // out-of-range reads are undefined in the reference; here they never match.
       int ta = i1 < type1.size() ? type1[i1] : -1;
       int tb = i2 < type2.size() ? type2[i2] : -2;
+      float dv[ACOS_MODES];
+      bool dd[ACOS_MODES];
+      for (int a = 0; a < ACOS_MODES; ++a) {
+        dv[a] = std::fabs(b1[i1].alt[a] - b2[i2].alt[a]);
+        dd[a] = dv[a] < angth;
+      }
+      audit_site(SITE_PAIR, dv, dd);
       if (std::fabs(b1[i1].angle - b2[i2].angle) < angth && ta == tb) {
         ++kpass;
         computer_transform(tv, b1[i1].i1, b1[i1].i2, b2[i2].i1, b2[i2].i2, f1.planes, f2.planes, ta, P);
@@ -1614,6 +1686,20 @@ extern "C" void orc_eigen33(const float cov[9], float* ev, float vec[3]) {
 
 extern "C" float orc_normal_angle(float x1, float y1, float z1, float x2, float y2, float z2) {
   return compute_normal_angel(x1, y1, z1, x2, y2, z2);
+}
+extern "C" int orc_set_acos_mode(int mode) {
+  const int prev = g_acos_mode;
+  if (mode >= 0 && mode < ACOS_MODES) g_acos_mode = mode;
+  return prev;
+}
+extern "C" void orc_acos_audit(uint64_t out[3 * SITE_N], int reset) {
+  if (out)
+    for (int i = 0; i < SITE_N; ++i) {
+      out[i] = g_audit.evals[i];
+      out[SITE_N + i] = g_audit.differ[i];
+      out[2 * SITE_N + i] = g_audit.flips[i];
+    }
+  if (reset) g_audit = AcosAudit{};
 }
 
 extern "C" void orc_quat_from_rot(const float R[9], float q[4]) {

@@ -50,6 +50,15 @@ void orc_sort_adversary(int64_t n, uint32_t* keys_out);
 void orc_eigen33(const float cov[9], float* eigenvalue, float vec[3]);
 /* compute_normal_angel (FCCF.cpp:369-377). */
 float orc_normal_angle(float x1, float y1, float z1, float x2, float y2, float z2);
+/* acos convention of FCCF.cpp:374 used by every angle (0 = float overload,
+ * correctly rounded acosf — default; 1 = this host's glibc acosf; 2 = C's
+ * double acos).  Returns the previous mode; out-of-range modes are ignored. */
+int orc_set_acos_mode(int mode);
+/* Per-site decision audit since the last reset, 8 sites (grow, merge, rough,
+ * base, third, cluster, verify, pair): out[0..7] evaluations, out[8..15]
+ * decision inputs whose bits differ between the conventions, out[16..23]
+ * decisions that flip between them.  reset != 0 clears the counters after. */
+void orc_acos_audit(uint64_t out[24], int reset);
 /* Eigen::Quaternionf(Matrix3f) and toRotationMatrix (row-major). */
 void orc_quat_from_rot(const float R[9], float q_wxyz[4]);
 void orc_rot_from_quat(const float q_wxyz[4], float R[9]);

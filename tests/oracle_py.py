@@ -35,6 +35,9 @@ def _load():
     lib.orc_normal_angle.argtypes = [ctypes.c_float] * 6
     lib.orc_quat_from_rot.argtypes = [P, P]
     lib.orc_rot_from_quat.argtypes = [P, P]
+    lib.orc_set_acos_mode.restype = ctypes.c_int
+    lib.orc_set_acos_mode.argtypes = [ctypes.c_int]
+    lib.orc_acos_audit.argtypes = [P, ctypes.c_int]
     lib.orc_lm_refine.restype = ctypes.c_int
     lib.orc_lm_refine.argtypes = [P, ctypes.c_int, P, P]
     return lib
@@ -108,6 +111,24 @@ def eigen33(cov):
 
 def normal_angle(a, b):
     return lib.orc_normal_angle(*[float(x) for x in list(a) + list(b)])
+
+
+# acos conventions of FCCF.cpp:374 (see oracle/fccf_oracle.cpp theta_of_cos)
+ACOS_CR_FLOAT, ACOS_LIBM_FLOAT, ACOS_DOUBLE = 0, 1, 2
+AUDIT_SITES = ("grow", "merge", "rough", "base", "third", "cluster", "verify", "pair")
+
+
+def set_acos_mode(mode):
+    """Select the acos convention; returns the previous one."""
+    return lib.orc_set_acos_mode(int(mode))
+
+
+def acos_audit(reset=True):
+    """{site: (evaluations, angles differing in bits, decisions flipping)} since the last reset."""
+    a = np.zeros(3 * len(AUDIT_SITES), np.uint64)
+    lib.orc_acos_audit(a.ctypes.data, int(bool(reset)))
+    n = len(AUDIT_SITES)
+    return {s: (int(a[i]), int(a[n + i]), int(a[2 * n + i])) for i, s in enumerate(AUDIT_SITES)}
 
 
 def quat_from_rot(R):
