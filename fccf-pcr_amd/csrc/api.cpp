@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <cstring>
 #include <vector>
+#include <atomic>
+#include <thread>
 
 #include "ctx.h"
 #include "host_stages.h"
@@ -162,6 +164,7 @@ int stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float
     float* d_out = c->arena2.take_n<float>(3 * (size_t)cap);
     uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
     VGBufs b = voxel_grid_carve(c->arena2, cap);
+    b.is.stats = 1;  // path counters for fccf_debug_sort_stats
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
@@ -208,6 +211,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     c->arena2.reset();
     uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
     VGBufs b = voxel_grid_carve(c->arena2, cap);
+    b.is.stats = 1;  // path counters for fccf_debug_sort_stats
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
     if (n) HIP_CHECK(hipMemcpyAsync(b.k0, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
@@ -251,6 +255,75 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
+// Forces the interleaving behind the pipelined batch's capture lock (ctx.h
+// capture_mutex): this thread captures a graph on stream X and, inside the
+// capture, releases a second thread that waits on an event last recorded on X
+// (as the batch's helper thread waits on ev[3]/ev[5]); the capture then holds
+// for hold_ms.  guard = 1 waits through guarded_stream_wait (the product path),
+// guard = 0 calls hipStreamWaitEvent directly (the pre-fix code).
+// out[0] = ms the waiting thread spent in its wait call, out[1] = ms between the
+// release and the end of the capture, out[2] = the wait's FCCF error (0 = ok),
+// out[3] = 1 if the wait returned only after the capture had ended.
+extern "C" int fccf_debug_capture_race(fccf_ctx* c, int hold_ms, int guard, double out[4]) {
+  if (!c || !out || hold_ms < 0 || hold_ms > 10000) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    using clk = std::chrono::steady_clock;
+    hipStream_t X = nullptr, Y = nullptr;
+    hipEvent_t E = nullptr;
+    void* buf = nullptr;
+    HIP_CHECK(hipStreamCreateWithFlags(&X, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&Y, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&E, hipEventDisableTiming));
+    HIP_CHECK(hipMalloc(&buf, 256));
+    HIP_CHECK(hipEventRecord(E, X));
+    HIP_CHECK(hipStreamSynchronize(X));
+    std::atomic<int> released{0};
+    std::atomic<int64_t> t_released{0}, t_cap_end{0};
+    clk::time_point w0, w1;
+    int werr = 0;
+    std::thread waiter([&] {
+      while (!released.load()) std::this_thread::yield();
+      w0 = clk::now();
+      try {
+        if (guard) guarded_stream_wait(Y, E);
+        else HIP_CHECK(hipStreamWaitEvent(Y, E, 0));
+      } catch (const Error& e) {
+        werr = e.code;
+      }
+      w1 = clk::now();
+    });
+    const auto base = clk::now();
+    CachedGraph g;
+    const uint8_t key = 1;
+    try {
+      g.run(&key, 1, X, [&] {
+        HIP_CHECK(hipMemsetAsync(buf, 0, 256, X));
+        t_released = (clk::now() - base).count();
+        released = 1;
+        std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
+        HIP_CHECK(hipMemsetAsync(buf, 1, 256, X));
+        t_cap_end = (clk::now() - base).count();
+      });
+    } catch (...) {
+      released = 1;
+      waiter.join();
+      throw;
+    }
+    waiter.join();
+    HIP_CHECK(hipStreamSynchronize(X));
+    (void)hipStreamSynchronize(Y);
+    auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+    out[0] = ms(w1 - w0);
+    out[1] = ms(clk::duration(t_cap_end.load() - t_released.load()));
+    out[2] = werr;
+    out[3] = (w1 - base).count() >= t_cap_end.load() ? 1.0 : 0.0;
+    (void)hipFree(buf);
+    (void)hipEventDestroy(E);
+    (void)hipStreamDestroy(Y);
+    (void)hipStreamDestroy(X);
   });
 }
 

@@ -107,18 +107,35 @@ inline std::mutex& capture_mutex() {
   return m;
 }
 
+// A wait on an event that another thread's stream may be capturing right now.
+inline void guarded_stream_wait(hipStream_t st, hipEvent_t ev) {
+  std::lock_guard<std::mutex> lk(capture_mutex());
+  HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
+}
+
 struct CachedGraph {
   std::vector<uint8_t> key;
   hipGraphExec_t exec = nullptr;
   int captures = 0;  // since the owner last cleared it
+  // Patching: one kernel node (found by its function after the capture) whose
+  // arguments are rewritten before every replay, so the graph can read inputs that
+  // change from call to call (caller-owned clouds) without staging them.
+  hipGraph_t graph = nullptr;
+  hipGraphNode_t pnode = nullptr;
+  hipKernelNodeParams pparams{};
   void reset() {
     if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
     exec = nullptr;
+    graph = nullptr;
+    pnode = nullptr;
     key.clear();
   }
   ~CachedGraph() { reset(); }
+  // body enqueues the work; pfunc/pargs (optional): the patched kernel and its
+  // current arguments (kernelParams layout: one pointer per argument).
   template <class F>
-  void run(const void* k, size_t kn, hipStream_t st, F body) {
+  void run(const void* k, size_t kn, hipStream_t st, F body, const void* pfunc = nullptr, void** pargs = nullptr) {
     static const bool enabled = [] {
       const char* e = std::getenv("FCCF_GRAPHS");
       return !(e && e[0] == '0');
@@ -144,13 +161,20 @@ struct CachedGraph {
       }
       HIP_CHECK(hipStreamEndCapture(st, &g));
       const hipError_t e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
       if (e != hipSuccess) {
+        (void)hipGraphDestroy(g);
         exec = nullptr;
         throw Error(FCCF_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
       }
+      graph = g;
+      if (pfunc) find_node(pfunc);
       key.assign(kb, kb + kn);
       ++captures;
+    } else if (pfunc) {
+      hipKernelNodeParams np = pparams;
+      np.kernelParams = pargs;
+      np.extra = nullptr;
+      HIP_CHECK(hipGraphExecKernelNodeSetParams(exec, pnode, &np));
     }
     static const bool trace = std::getenv("FCCF_HOST_TRACE") != nullptr;
     const auto h0 = std::chrono::steady_clock::now();
@@ -158,6 +182,31 @@ struct CachedGraph {
     if (trace)
       std::fprintf(stderr, "graph launch host %.1f us\n",
                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count());
+  }
+
+ private:
+  void find_node(const void* func) {
+    size_t n = 0;
+    HIP_CHECK(hipGraphGetNodes(graph, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n) HIP_CHECK(hipGraphGetNodes(graph, nodes.data(), &n));
+    int found = 0;
+    for (hipGraphNode_t nd : nodes) {
+      hipGraphNodeType t;
+      HIP_CHECK(hipGraphNodeGetType(nd, &t));
+      if (t != hipGraphNodeTypeKernel) continue;
+      hipKernelNodeParams p{};
+      HIP_CHECK(hipGraphKernelNodeGetParams(nd, &p));
+      if (p.func != func) continue;
+      pnode = nd;
+      pparams = p;
+      ++found;
+    }
+    if (found != 1) {
+      reset();
+      throw Error(FCCF_E_HIP, "graph patch: the patched kernel must occur exactly once, found " +
+                                  std::to_string(found));
+    }
   }
 };
 

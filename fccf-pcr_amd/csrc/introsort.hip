@@ -59,7 +59,7 @@ constexpr int IS_STACK = 96;  // a wave's stack also holds its register-mode sub
 __device__ __forceinline__ uint32_t wpack(uint32_t off, uint32_t len, int d) { return off | (len << 13) | ((uint32_t)d << 24); }
 constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
 #ifndef IS_STATS
-#define IS_STATS 1  // path counters in IsBufs::ctl[3..] (tests/tools read them)
+#define IS_STATS 1  // path counters in IsBufs::ctl[3..], when IsBufs::stats (debug sorts only)
 #endif
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -499,7 +499,14 @@ struct BlockLds {
   uint32_t bc[8];                   // broadcasts
   uint32_t sh[16];
   uint32_t* stat;                   // IsBufs::ctl
+  uint32_t son;                     // path counters on (IS_STATS && IsBufs::stats)
+  // wave tasks of the current segment, packed off | n << 13 | depth << 23, handed
+  // to the global list with one atomic per class when the segment is done
+  uint32_t tb[IS_LCAP / (IS_TASK_BIG + 1) + 1];  // > IS_TASK_BIG elements
+  uint32_t ts[IS_LCAP / (IS_THRESHOLD + 1) + 1];  // the rest
+  uint32_t ntb, nts, units;
 };
+static_assert(IS_LCAP <= 8192 && IS_WCAP < 1024, "task packing: 13-bit offsets, 10-bit sizes");
 
 // One wave's slice of the wave kernel
 struct WaveLds {
@@ -509,6 +516,7 @@ struct WaveLds {
   uint32_t stk[IS_STACK];
   uint32_t lstat[4];
   uint32_t* stat;
+  uint32_t son;  // path counters on (IS_STATS && IsBufs::stats)
 };
 
 template <class SL>
@@ -792,11 +800,11 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
       continue;
     }
     if (n <= 64) {  // the rest of this subtree in registers
-      if (IS_STATS && lane == 0) atomicAdd(&S.lstat[0], 1u);
+      if (S.son && lane == 0) atomicAdd(&S.lstat[0], 1u);
       wave_sort_regs(S, f, n, dd, stk + sp);
       continue;
     }
-    if (IS_STATS && lane == 0) atomicAdd(&S.lstat[2], 1u);
+    if (S.son && lane == 0) atomicAdd(&S.lstat[2], 1u);
     uint32_t c;
     if (n <= 128) c = wave_partition<2, SL>(S, f, f + n, xch);
     else if (n <= 256) c = wave_partition<4, SL>(S, f, f + n, xch);
@@ -904,6 +912,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
   }
   if (threadIdx.x == 0) {
     S.bc[0] = 0;  // stack depth
+    S.ntb = S.nts = S.units = 0;
     if (len <= IS_THRESHOLD) {
       S.heads[0] = 1u;
     } else {
@@ -923,12 +932,13 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
           if (n) mark_leaf(S, off);
         } else if (dd == 0) {
           heap_sort(S.k + off, S.v + off, (int64_t)n);
-          if (IS_STATS) atomicAdd(&S.stat[7], 1u);
+          if (S.son) atomicAdd(&S.stat[7], 1u);
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
         } else if (n <= IS_WCAP) {  // a wave task: large ones from the front, small from the back
-          atomicAdd(&W.ctl[19], n);  // the wave probe's unit count
-          if (n > IS_TASK_BIG) W.tasks[atomicAdd(&W.ctl[16], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
-          else W.tasks[W.taskmax - 1u - atomicAdd(&W.ctl[18], 1u)] = make_uint4(f + off, n, (uint32_t)dd, 0u);
+          S.units += n;  // the wave probe's unit count
+          const uint32_t pk = off | (n << 13) | ((uint32_t)dd << 23);
+          if (n > IS_TASK_BIG) S.tb[S.ntb++] = pk;
+          else S.ts[S.nts++] = pk;
           for (uint32_t q = off; q < off + n; q += 32 - (q & 31)) {
             const uint32_t bit = q & 31, cnt = min(32u - bit, off + n - q);
             atomicOr(&S.intask[q >> 5], (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << bit);
@@ -949,7 +959,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     if (!S.bc[3]) break;
     const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
     const int dd = (int)(S.bc[7] >> 16);
-    if (IS_STATS && threadIdx.x == 0) atomicAdd(&S.stat[5], 1u);
+    if (S.son && threadIdx.x == 0) atomicAdd(&S.stat[5], 1u);
     uint32_t c;
     if (n <= 2 * IS_OT) c = block_partition<2>(S, off, off + n);
     else if (n <= 4 * IS_OT) c = block_partition<4>(S, off, off + n);
@@ -961,6 +971,20 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
       S.wstk[S.bc[0]++] = make_uint2(off, (c - off) | nd);
     }
     __syncthreads();
+  }
+  // the segment's wave tasks into the global list: one slot reservation per class
+  if (threadIdx.x == 0) {
+    S.bc[1] = S.ntb ? atomicAdd(&W.ctl[16], S.ntb) : 0u;
+    S.bc[2] = S.nts ? atomicAdd(&W.ctl[18], S.nts) : 0u;
+    if (S.units) atomicAdd(&W.ctl[19], S.units);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < S.ntb + S.nts; i += IS_OT) {
+    const bool big = i < S.ntb;
+    const uint32_t pk = big ? S.tb[i] : S.ts[i - S.ntb];
+    const uint4 t = make_uint4(f + (pk & 0x1FFFu), (pk >> 13) & 0x3FFu, pk >> 23, 0u);
+    if (big) W.tasks[S.bc[1] + i] = t;
+    else W.tasks[W.taskmax - 1u - (S.bc[2] + i - S.ntb)] = t;
   }
   // leaves: stable sort in place (the final insertion sort); task ranges as they are
   for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
@@ -1111,13 +1135,23 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
   const IsBufs W = W2[e];
   const uint32_t nsort = W.ctl[0];
   if (nsort == 0) return;
-  if (threadIdx.x == 0) S.stat = W.ctl;
+  if (threadIdx.x == 0) {
+    S.stat = W.ctl;
+    S.son = IS_STATS && W.stats;
+  }
   const uint32_t nfin = nchildren(W, R);
   const uint32_t nown = R ? W.rounds[R - 1].nown : 0u;
-  uint32_t* Kb[2] = {K02[e], K12[e]};
-  uint32_t* Vb[2] = {V02[e], V12[e]};
+  uint32_t* const K0 = K02[e];
+  uint32_t* const V0 = V02[e];
+  uint32_t* const K1 = K12[e];
+  uint32_t* const V1 = V12[e];
+  uint32_t units = 0;  // elements this workgroup sorted in LDS (the block probe's unit count)
   for (;;) {
-    if (threadIdx.x == 0) s_idx = atomicAdd(&W.ctl[1], 1u);
+    if (threadIdx.x == 0) {
+      // look before taking: once the list is drained, leave without another atomic
+      const uint32_t seen = __hip_atomic_load(&W.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_idx = seen >= nfin + nown ? seen : atomicAdd(&W.ctl[1], 1u);
+    }
     __syncthreads();
     const uint32_t idx = s_idx;
     __syncthreads();
@@ -1138,8 +1172,8 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       buf = o.buf;
     }
     if (l <= f) continue;
-    uint32_t* K = Kb[buf];
-    uint32_t* V = Vb[buf];
+    uint32_t* K = buf ? K1 : K0;  // selects: a dynamically indexed local array lives in scratch
+    uint32_t* V = buf ? V1 : V0;
     if (threadIdx.x == 0) {
       S.gstk[0] = make_uint4(f, l, (uint32_t)d, 0u);
       S.gsp = 1;
@@ -1160,11 +1194,9 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       if (threadIdx.x == 0) S.gsp = sp - 1;
       __syncthreads();
       if (len <= IS_LCAP) {
-        if (threadIdx.x == 0) {
-          atomicAdd(&W.ctl[4], 1u);
-          atomicAdd(&W.ctl[20], len);  // the block probe's unit count
-        }
-        lds_block(S, W, K, V, Kb[0], Vb[0], gf, len, gd);
+        if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[4], 1u);
+        units += len;
+        lds_block(S, W, K, V, K0, V0, gf, len, gd);
       } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
         if (threadIdx.x == 0) {
           heap_sort(K + gf, V + gf, (int64_t)len);
@@ -1174,13 +1206,13 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
         __syncthreads();
         if (buf != 0)
           for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
-            Kb[0][gf + q] = K[gf + q];
-            Vb[0][gf + q] = V[gf + q];
+            K0[gf + q] = K[gf + q];
+            V0[gf + q] = V[gf + q];
           }
         __syncthreads();
       } else {
-        if (IS_STATS && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
-        const uint32_t c = global_partition(S, K, V, Kb[buf ^ 1u], Vb[buf ^ 1u], gf, gl);
+        if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
+        const uint32_t c = global_partition(S, K, V, buf ? K0 : K1, buf ? V0 : V1, gf, gl);
         if (threadIdx.x == 0) {
           W.ctl[2] |= 1u;
           uint32_t s = S.gsp;
@@ -1193,9 +1225,10 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       }
     }
   }
+  if (threadIdx.x == 0 && units) atomicAdd(&W.ctl[20], units);
 }
 
-// Every wave takes wave tasks (dequeued from ctl[17]): the subtree in its LDS slice,
+// Every wave takes its share of the wave tasks: the subtree in its LDS slice,
 // finished and stably leaf-sorted, written back in place in buffer 0.
 __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<IsBufs> W2) {
   KT();
@@ -1206,18 +1239,19 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
   WaveLds& S = WL[w];
   if (lane == 0) {
     S.stat = W.ctl;
+    S.son = IS_STATS && W.stats;
     for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
   }
   wsync();
-  // large tasks first (longest-processing-time order keeps the tail short)
+  // Static assignment, no queue: wave g of the grid takes tasks g, g + NW, g + 2 NW ...
+  // of the list, which holds the large tasks first, so the largest ones are spread
+  // one per wave (a dynamic dequeue from one counter serialises on that counter:
+  // ~18 ns per atomic, which at thousands of tasks was the kernel's whole time).
   const uint32_t nbig = W.ctl[16], ntasks = nbig + W.ctl[18];
   uint32_t* __restrict__ K = K02[e];
   uint32_t* __restrict__ V = V02[e];
-  for (;;) {
-    uint32_t idx = 0;
-    if (lane == 0) idx = atomicAdd(&W.ctl[17], 1u);
-    idx = __builtin_amdgcn_readfirstlane(idx);
-    if (idx >= ntasks) break;
+  const uint32_t nw = gridDim.x * (IS_WT / 64);
+  for (uint32_t idx = blockIdx.x * (IS_WT / 64) + w; idx < ntasks; idx += nw) {
     const uint4 tk = W.tasks[idx < nbig ? idx : W.taskmax - 1u - (idx - nbig)];
     const uint32_t f = __builtin_amdgcn_readfirstlane(tk.x), n = __builtin_amdgcn_readfirstlane(tk.y);
     const int d = (int)__builtin_amdgcn_readfirstlane(tk.z);
@@ -1259,7 +1293,7 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
     }
     wsync();
   }
-  if (IS_STATS && lane == 0) {
+  if (S.son && lane == 0) {
     atomicAdd(&W.ctl[6], S.lstat[2]);
     atomicAdd(&W.ctl[12], S.lstat[0]);
   }
@@ -1326,6 +1360,7 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.tasks = (uint4*)take(sizeof(uint4) * (size_t)b.taskmax);
   b.prog = nullptr;
   b.tier = introsort_tier();
+  b.stats = 0;
   return b;
 }
 

@@ -21,6 +21,7 @@ struct VGParams {
   uint32_t unsorted;  // presorted check: some key is not strictly above its predecessor
   uint32_t chk_done;  // presorted check: blocks finished
   uint32_t nonfinite; // some output point is not finite (set by k_vg_centroid when it writes a copy)
+  const float* src;   // the pass's input points (set by k_vg_bbox, read by the later kernels)
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
@@ -46,8 +47,8 @@ struct IsOwn {
 };
 struct IsBufs {
   uint32_t* ctl;        // [0] sort length, [1] block dequeue head, [2] slow paths taken (1 global partition,
-                        // 2 heap), [3..15] counters, [16] large wave tasks, [17] wave dequeue head,
-                        // [18] small wave tasks (stored from the end)
+                        // 2 heap), [3..15] counters, [16] large wave tasks, [18] small wave tasks
+                        // (stored from the end), [19]/[20] wave/block probe unit counts
   uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
   uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles)
   uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
@@ -59,6 +60,7 @@ struct IsBufs {
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   uint32_t segmax, maxtiles, ownmax, taskmax;
   uint32_t tier;        // rounds split segments longer than this (<= the owner's LDS capacity)
+  uint32_t stats;       // path counters in ctl[3..15] (debug sorts; each costs a global atomic)
 };
 size_t introsort_bytes(uint32_t cap);
 IsBufs introsort_carve(void* base, uint32_t cap);
@@ -91,9 +93,30 @@ struct VGBufs {
 // out_copy (optional): every output point is also written there, and
 // VGParams::nonfinite is set when one is not finite (the driver's remove-NaN after
 // the first pass, FCCF.cpp:1374-1375, is then an identity unless that flag is set).
-void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
+// The arguments of a pass's entry kernel (k_vg_bbox), the only launch of the pass
+// that takes the input points and their count: a cached graph replays the pass for
+// other caller-owned inputs by rewriting this one node (CachedGraph::patch), so the
+// inputs are read in place, never staged.  set_n: the count is n (by value) and the
+// kernel stores it to d_n for the later kernels; otherwise it is read from d_n.
+struct VGEntry {
+  B2<const float*> xyz;
+  B2<uint32_t*> d_n;
+  B2<uint32_t> n;
+  int set_n = 0;
+  B2<float*> part;
+  B2<VGParams*> P;
+  void* args[6];
+  void bind() {
+    args[0] = &xyz; args[1] = &d_n; args[2] = &n; args[3] = &set_n; args[4] = &part; args[5] = &P;
+  }
+};
+const void* vg_entry_kernel();
+// One VoxelGrid pass per batch entry.  n_in (optional): the counts by value (see
+// VGEntry.set_n), stored to d_n; entry (optional): receives the entry kernel's arguments.
+void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
                 B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted = false, int nbatch = 1,
-                B2<float*> out_copy = B2<float*>(nullptr));
+                B2<float*> out_copy = B2<float*>(nullptr), const uint32_t* n_in = nullptr,
+                VGEntry* entry = nullptr);
 
 // ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
 struct VoxRec {  // one occupied octree leaf, Morton order

@@ -144,8 +144,7 @@ namespace {
 // ------------------------------------------------------------ per-cloud device state
 struct CloudWS {
   uint32_t cap = 0;
-  const float* in = nullptr;
-  float* in_copy = nullptr;
+  float* in_copy = nullptr;  // host inputs are copied here; device inputs are read in place
   uint32_t* sc = nullptr;  // [0] n_in, [1] m1, [2] m1 finite, [3] m2
   float *ds1 = nullptr, *ds1f = nullptr, *ds2 = nullptr;
   VGBufs vg;
@@ -197,14 +196,15 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
 template <class T, class F>
 B2<T> both(const CloudWS* w, F get) { return B2<T>(get(w[0]), get(w[1])); }
 
-// main's VoxelGrid pass (:1668-1678), its output also into ds1f
-void seg_pass1(CloudWS* w, float leaf, hipStream_t st) {
+// main's VoxelGrid pass (:1668-1678) over the inputs xin (n points each), its
+// output also into ds1f; entry receives its entry kernel's arguments (graph patch)
+void seg_pass1(CloudWS* w, const float* const xin[2], const uint32_t n[2], float leaf, hipStream_t st,
+               VGEntry* entry) {
   const uint32_t cap = w[0].cap;
   auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
   const B2<VGBufs> vg(w[0].vg, w[1].vg);
-  voxel_grid(both<const float*>(w, [](const CloudWS& c) { return c.in; }), sc(0), cap, leaf,
-             both<float*>(w, [](const CloudWS& c) { return c.ds1; }), sc(1), vg, st, false, 2,
-             both<float*>(w, [](const CloudWS& c) { return c.ds1f; }));
+  voxel_grid(B2<const float*>(xin[0], xin[1]), sc(0), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds1; }),
+             sc(1), vg, st, false, 2, both<float*>(w, [](const CloudWS& c) { return c.ds1f; }), n, entry);
 }
 // the driver's remove-NaN and second VoxelGrid pass (:1374-1387)
 void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
@@ -334,6 +334,7 @@ struct PipeSet {
   uint32_t cap[2] = {1, 1};
   float* cen = nullptr;  // both cloud centroids: cloud k at cen[3k .. 3k+2]
   XsBufs xs;             // their exact-sum scratch (6 rows)
+  VGEntry entry;         // arguments of pass 1's entry kernel, patched into g_seg[0] per call
   clk::time_point t_enq;
 };
 
@@ -361,28 +362,23 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   hipStream_t st0 = c->sa[0], ss = c->sa[2];
   // the previous pair on this set may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for it
-  {
-    std::lock_guard<std::mutex> lk(capture_mutex());  // ev[3] is recorded on the fine stream (captured by phase B)
-    HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[3], 0));
-  }
+  guarded_stream_wait(st0, cs.ev[3]);  // ev[3] is recorded on the fine stream (captured by phase B)
   cs.arena.ensure(2 * cloud_bytes(capmax, true) + exact_sum_bytes(6, capmax) + (1 << 20));
   cs.arena.reset();
-  // Inputs are staged into the workspace (H2D, or D2D for device-resident
-  // clouds) so the captured graphs never depend on caller pointers.
-  uint32_t* hn = (uint32_t*)c->pinned.get(64) + 8 * s;
+  // Host inputs are copied into the workspace; device-resident inputs are read in
+  // place: their pointers and counts are patched into pass 1's entry kernel node.
+  const float* xin[2] = {nullptr, nullptr};
+  uint32_t nv[2] = {0, 0};
   ps.cen = cs.arena.take_n<float>(8);
   ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
     carve_cloud(cs.arena, w[k], capmax, true);
     w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
-    const uint32_t n = (uint32_t)ps.nin[k];
-    if (n)
-      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)n,
-                               on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st0));
-    w[k].in = w[k].in_copy;
-    hn[k] = n;
-    HIP_CHECK(hipMemcpyAsync(w[k].sc, hn + k, 4, hipMemcpyHostToDevice, st0));
+    nv[k] = (uint32_t)ps.nin[k];
+    if (nv[k] && !on_device)
+      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)nv[k], hipMemcpyHostToDevice, st0));
+    xin[k] = on_device ? hin[k] : w[k].in_copy;
   }
   struct {
     const void* base;
@@ -400,7 +396,11 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   };
   mark(0, st0);
   HIP_CHECK(hipEventRecord(cs.tev[0], st0));
-  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_pass1(w, leaf, st0); });
+  ps.entry.xyz = B2<const float*>(xin[0], xin[1]);
+  ps.entry.n = B2<uint32_t>(nv[0], nv[1]);
+  ps.entry.bind();
+  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_pass1(w, xin, nv, leaf, st0, &ps.entry); }, vg_entry_kernel(),
+                  ps.entry.args);
   HIP_CHECK(hipEventRecord(cs.tev[1], st0));
   cs.g_seg[2].run(&key, sizeof key, st0, [&] { seg_downsample(w, leaf, st0); });
   HIP_CHECK(hipEventRecord(cs.tev[2], st0));
@@ -774,10 +774,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       float res;
     } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size};
     ht.mark("fine_setup");
-    {
-      std::lock_guard<std::mutex> lk(capture_mutex());  // ev[5]'s stream may be capturing the next pair's clouds
-      HIP_CHECK(hipStreamWaitEvent(sf, c->cs[s].ev[5], 0));  // S1 octree bounds replayed (after the clouds)
-    }
+    // S1 octree bounds replayed (after the clouds); ev[5]'s stream may be capturing the next pair's clouds
+    guarded_stream_wait(sf, c->cs[s].ev[5]);
     HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,

@@ -27,20 +27,23 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Per-block partial bbox of finite points: part[b] = {min xyz, max xyz, count(bits), 0}.
-// Block 0 also clears the pass's flags (keys' order check, the centroid kernel's
-// non-finite flag) before any later kernel of the pass can set them.
-__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<float*> part2,
-                                                 B2<VGParams*> P2) {
+// The pass's entry kernel (VGEntry): block 0 also publishes the input pointer (and,
+// with set_n, the count) and clears the pass's flags (keys' order check, the
+// centroid kernel's non-finite flag) before any later kernel of the pass runs.
+__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint32_t*> d_n2, B2<uint32_t> n2,
+                                                 int set_n, B2<float*> part2, B2<VGParams*> P2) {
   KT();
   __shared__ float sh[4][7];
   const int e = blockIdx.y;
+  const float* __restrict__ xyz = xyz2[e];
+  const uint32_t n = set_n ? n2[e] : *d_n2[e];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     P2[e]->unsorted = 0;
     P2[e]->chk_done = 0;
     P2[e]->nonfinite = 0;
+    P2[e]->src = xyz;
+    if (set_n) *d_n2[e] = n;
   }
-  const float* __restrict__ xyz = xyz2[e];
-  const uint32_t n = *d_n2[e];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   uint32_t cnt = 0;
   auto add = [&](float x, float y, float z) {
@@ -183,7 +186,7 @@ __device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, 
 // strictly above its predecessor -- or any non-finite point -- sets P->unsorted;
 // otherwise every leaf holds exactly one point and the pass is the identity (the
 // sort tail, segmentation and centroid kernels take their shortcut).
-__global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const uint32_t*> d_n2, B2<VGParams*> P2,
+__global__ void __launch_bounds__(256) k_vg_keys(B2<const uint32_t*> d_n2, B2<VGParams*> P2,
                                                  B2<uint32_t*> keys2, B2<uint32_t*> vals2, int presorted,
                                                  B2<const float*> part2, int nparts, float leaf) {
   KT();
@@ -197,7 +200,7 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
     if (presorted && n && blockIdx.x == 0 && threadIdx.x == 0) P->unsorted = 1u;
     return;
   }
-  const float* __restrict__ xyz = xyz2[e];
+  const float* __restrict__ xyz = P->src;
   uint32_t* __restrict__ keys = keys2[e];
   uint32_t* __restrict__ vals = vals2[e];
   bool bad = false;
@@ -241,8 +244,7 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const float*> xyz2, B2<const
 // dependent chain); each block's 256 centroids are staged in LDS and written as
 // coalesced 16-byte words.  The pass-through cases are flat 16-byte copies.
 constexpr int CL = 4;
-__global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
-                                                     B2<VGParams*> P2, B2<const uint32_t*> vals2,
+__global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B2<VGParams*> P2, B2<const uint32_t*> vals2,
                                                      B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
                                                      B2<float*> out2, B2<uint32_t*> d_m2, int presorted,
                                                      B2<float*> copy2) {
@@ -251,7 +253,7 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const float*> xyz2, B2<c
   const VGParams q = *P2[e];
   float* __restrict__ cpy = copy2[e];
   bool bad = false;  // a non-finite output value (only tracked with a copy)
-  const float* __restrict__ xyz = xyz2[e];
+  const float* __restrict__ xyz = q.src;
   const uint32_t* __restrict__ vals = vals2[e];
   const uint32_t* __restrict__ starts = starts2[e];
   const uint32_t* __restrict__ d_nseg = d_nseg2[e];
@@ -342,8 +344,12 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch, B2<float*> out_copy) {
+const void* vg_entry_kernel() { return (const void*)k_vg_bbox; }
+
+void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float leaf, B2<float*> out,
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch, B2<float*> out_copy,
+                const uint32_t* n_in, VGEntry* entry) {
+  const B2<const uint32_t*> d_n(d_nw[0], d_nw[1]);
   auto F = [&](auto get) { return B2<decltype(get(b[0]))>(get(b[0]), get(b[1])); };
   const B2<VGParams*> P = F([](const VGBufs& v) { return v.params; });
   const B2<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
@@ -352,14 +358,26 @@ void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, flo
   const B2<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
   const B2<const uint32_t*> nbits(&b[0].params->nbits, &b[1].params->nbits);
   const dim3 g(grid_for(cap), nbatch);
-  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(xyz, d_n, F([](const VGBufs& v) { return v.part; }), P);
+  VGEntry en;
+  en.xyz = xyz;
+  en.d_n = d_nw;
+  en.n = n_in ? B2<uint32_t>(n_in[0], nbatch > 1 ? n_in[1] : 0u) : B2<uint32_t>(0u);
+  en.set_n = n_in ? 1 : 0;
+  en.part = F([](const VGBufs& v) { return v.part; });
+  en.P = P;
+  en.bind();
+  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(en.xyz, en.d_n, en.n, en.set_n, en.part, en.P);
+  if (entry) {
+    *entry = en;
+    entry->bind();
+  }
   const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts
   const uint32_t* m2 = nbatch > 1 ? d_m[1] : nullptr;
   const B2<const uint32_t*> unsorted(&b[0].params->unsorted, &b[1].params->unsorted);
   // the keys kernel also derives the parameters (k_vg_params folded in): each of its
   // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
   const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
-  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, xyz, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
+  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
   const B2<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
   const B2<const VGParams*> Pc(P[0], P[1]);
   if (!presorted) {
@@ -371,7 +389,7 @@ void voxel_grid(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, flo
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch, unsorted);
   }
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, xyz, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0, out_copy);
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0, out_copy);
 }
 
 }  // namespace fccf

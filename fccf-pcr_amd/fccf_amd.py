@@ -100,6 +100,7 @@ _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctype
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
 _sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
+_sig("fccf_debug_capture_race", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P)
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
 _sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
@@ -258,6 +259,14 @@ class Ctx:
         return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_segments=int(a[4]),
                     block_parts=int(a[5]), wave_parts=int(a[6]), heaps=int(a[7]), reg_subtrees=int(a[12]),
                     wave_tasks=int(a[16]))
+
+    def capture_race(self, hold_ms: int = 200, guard: bool = True) -> dict:
+        """Test hook: a graph capture held for hold_ms concurrent with another thread's
+        wait on an event of the capturing stream (fccf_debug_capture_race)."""
+        a = np.zeros(4, np.float64)
+        _check(_lib.fccf_debug_capture_race(self._h, int(hold_ms), int(bool(guard)), a.ctypes.data),
+               "fccf_debug_capture_race", self._h)
+        return dict(wait_ms=float(a[0]), hold_ms=float(a[1]), wait_error=int(a[2]), after_capture=bool(a[3]))
 
     def voxel_planes(self, xyz, params: Params | None = None):
         """face_extrate's voxel pass (FCCF.cpp:473-534) of one downsampled cloud on the GPU.

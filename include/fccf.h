@@ -237,6 +237,13 @@ int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exa
  * [3] global partitions, [4] LDS segments, [5] workgroup partitions, [6] wave
  * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks. */
 int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
+/* Forces a graph capture on one stream concurrent with another thread's wait on
+ * an event last recorded on that stream (the pipelined batch's hazard, guarded by
+ * the capture lock).  guard 1 = the product's guarded wait, 0 = an unguarded
+ * hipStreamWaitEvent.  out: [0] ms in the wait call, [1] ms the capture held after
+ * releasing the waiter, [2] the wait's error code, [3] 1 if it returned after the
+ * capture ended.  Test hook. */
+int fccf_debug_capture_race(fccf_ctx* ctx, int hold_ms, int guard, double out[4]);
 
 /* PLY I/O (the reference's pcl::io::loadPLYFile<PointXYZ> surface, FCCF.cpp:1655-1665):
  * ascii / binary_little_endian / binary_big_endian, float x,y,z (double converted).

@@ -86,6 +86,37 @@ def test_register_device_resident_matches_host_path(ctx, fccf):
     np.testing.assert_array_equal(T1.view(np.uint32), T2.view(np.uint32))
 
 
+def test_device_inputs_read_in_place_across_buffers(ctx, oracle, fccf):
+    """Device-resident clouds are read in place: the cached cloud-stage graph is
+    replayed with pass 1's entry node patched to each call's pointers and counts
+    (CachedGraph patch, VGEntry).  Alternating buffers, counts that change under the
+    same capacity, and a 4-byte-misaligned input (the kernels' scalar-load path) must
+    each equal the oracle bitwise."""
+    src, tar, _ = fccf.synth_pair(60_000)
+    rng = np.random.default_rng(11)
+    src2 = (src + rng.normal(0, 0.002, src.shape)).astype(np.float32)
+    runs = [(src, tar), (src2, tar), (src, tar[:59_000]), (tar, src)]
+    pad = np.zeros(3 * (src2.shape[0] + 1), np.float32)
+    pad[1:1 + src2.size] = src2.reshape(-1)  # src2 at byte offset 4
+    bufs = {}
+    try:
+        for i, (s, t) in enumerate(runs):
+            ds, dt = ctx.upload(s), ctx.upload(t)
+            bufs[i] = (ds, dt)
+            T, _ = ctx.register_device(ds, s.shape[0], dt, t.shape[0], 0.1)
+            np.testing.assert_array_equal(T.view(np.uint32), oracle.Run(s, t, 0.1).T.view(np.uint32))
+        dp = ctx.upload(pad.reshape(-1, 3))
+        bufs["pad"] = (dp,)
+        T, _ = ctx.register_device(dp + 4, src2.shape[0], bufs[1][1], tar.shape[0], 0.1)
+        np.testing.assert_array_equal(T.view(np.uint32), oracle.Run(src2, tar, 0.1).T.view(np.uint32))
+        T, _ = ctx.register_device(bufs[0][0], src.shape[0], bufs[0][1], tar.shape[0], 0.1)  # back to the first
+        np.testing.assert_array_equal(T.view(np.uint32), oracle.Run(src, tar, 0.1).T.view(np.uint32))
+    finally:
+        for b in bufs.values():
+            for d in b:
+                ctx.free(d)
+
+
 def test_register_repeatable(ctx, fccf):
     src, tar, _ = fccf.synth_pair(50_000)
     a, _ = ctx.register(src, tar, 0.1)
