@@ -213,6 +213,44 @@ def probe_pass(ctx, reg, kernel, steps):
     return ms, n, b
 
 
+def ingest_pass(F, ctx, src, tar, leaf, T_ref, reps=3):
+    """f2, informational: the reference's PLY -> T path
+    (FCCF.cpp:1655-1685) with the clouds streamed from PLY files into HBM
+    (fccf_ply_load_device: chunked decode overlapped with the upload), and a pipelined
+    batch from host arrays (uploads on the copy stream, overlapping the previous
+    pair's compute).  Files are written to a scratch directory first (untimed)."""
+    import tempfile
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for fmt, binary in (("binary", True), ("ascii", False)):
+            ps, pt = os.path.join(td, f"s_{fmt}.ply"), os.path.join(td, f"t_{fmt}.ply")
+            F.ply_write(ps, src, binary)
+            F.ply_write(pt, tar, binary)
+            load, e2e = [], []
+            for _ in range(reps):
+                a = time.perf_counter()
+                ds, ns = ctx.ply_load(ps)
+                dt, nt = ctx.ply_load(pt)
+                b = time.perf_counter()
+                T3, _ = ctx.register_device(ds, ns, dt, nt, leaf)
+                c = time.perf_counter()
+                ctx.free(ds)
+                ctx.free(dt)
+                assert np.array_equal(T3.view(np.uint32), np.asarray(T_ref).view(np.uint32)), "PLY-path result differs"
+                load.append(b - a)
+                e2e.append(c - a)
+            nbytes = os.path.getsize(ps) + os.path.getsize(pt)
+            out[fmt] = {"file_MB": round(nbytes / 1e6, 2), "load_ms_median": statistics.median(load) * 1e3,
+                        "load_GBps": nbytes / statistics.median(load) / 1e9,
+                        "ply_to_T_ms_median": statistics.median(e2e) * 1e3}
+    k = 8
+    a = time.perf_counter()
+    Tb, _ = ctx.register_batch([(src, tar)] * k, leaf)
+    out["host_input_batch_ms_per_registration"] = (time.perf_counter() - a) / k * 1e3
+    assert np.array_equal(Tb[-1].view(np.uint32), np.asarray(T_ref).view(np.uint32)), "host batch result differs"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -318,6 +356,7 @@ def main():
         per_host.append(time.perf_counter() - a)
     if not args.selftest:
         assert np.array_equal(T2.view(np.uint32), np.asarray(T).view(np.uint32)), "host-input result differs"
+    ingest = None if args.selftest or rank != 0 else ingest_pass(F, ctx, src, tar, leaf, T)
     roofline = None
     if probe:
         # Probe window right after the timed region, same inputs: every launch of
@@ -370,6 +409,8 @@ def main():
             "rot_err_deg_vs_gt": rot_err,
             "trans_err_m_vs_gt": float(np.linalg.norm(T[:3, 3] - T_gt[:3, 3])),
         }
+        if ingest is not None:
+            out["ingest"] = ingest
         if roofline is not None:
             roofline["stage"] = stage_rl
             out["roofline"] = roofline

@@ -69,6 +69,7 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   for (auto& cs : c->cs) {
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (auto& e : cs.tev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&cs.ev_in, hipEventDisableTiming) == hipSuccess;
   }
   if (!ok) {
     fccf_ctx_destroy(c);
@@ -92,6 +93,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : cs.tev)
       if (e) (void)hipEventDestroy(e);
+    if (cs.ev_in) (void)hipEventDestroy(cs.ev_in);
   }
   for (auto& s : c->sa)
     if (s) (void)hipStreamDestroy(s);
@@ -636,6 +638,13 @@ extern "C" int fccf_device_upload(fccf_ctx* c, const float* xyz, int64_t n, floa
     if (hipMalloc((void**)&p, 12 * (size_t)std::max<int64_t>(n, 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
     if (n) HIP_CHECK(hipMemcpy(p, xyz, 12 * (size_t)n, hipMemcpyHostToDevice));
     *d = p;
+  });
+}
+
+extern "C" int fccf_device_download(fccf_ctx* c, const float* d, int64_t n, float* xyz) {
+  if (!c || (!d && n) || (!xyz && n) || n < 0) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    if (n) HIP_CHECK(hipMemcpy(xyz, d, 12 * (size_t)n, hipMemcpyDeviceToHost));
   });
 }
 

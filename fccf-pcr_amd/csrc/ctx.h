@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/fccf.h"
+#include "ingest.h"
 #include "pool.h"
 #include "probe.h"
 
@@ -223,6 +224,8 @@ struct fccf_ctx {
   struct CloudSet {
     fccf::Arena arena;
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
+    fccf::Arena inarena;             // staged host inputs of the pair on this set (copy stream)
+    hipEvent_t ev_in = nullptr;      // their copies done
     hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
                                      // [4] clouds done, [5] S1 replay done
     hipEvent_t tev[6] = {};          // timing: cloud start, pass 1 done, pass 2 done, faces done,
@@ -242,6 +245,7 @@ struct fccf_ctx {
   fccf::Pool pool;
   fccf::AsyncTask enq;  // pipelined batch: enqueues the next pair's cloud stage
   fccf::Probe probe;
+  fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)
   bool debug = false;
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   std::map<std::string, std::vector<uint8_t>> dbg;

@@ -48,27 +48,37 @@ int main(int argc, char** argv) {
     if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--stats")) stats = true;
   }
+  // The clouds are streamed from the files straight into HBM (fccf_ply_load_device:
+  // chunked decode overlapped with the upload).  The ctx is created first, silently,
+  // so the observable order stays the reference's: both loads (either failure prints
+  // "Couldn't read file" and exits 0), then "Leaf size", then the registration.
+  fccf_ctx* ctx = nullptr;
+  const int crc = fccf_ctx_create(&ctx, device);
   float *src = nullptr, *tar = nullptr;
   int64_t ns = 0, nt = 0;
-  if (fccf_ply_read(argv[1], &src, &ns) != FCCF_OK) {
-    std::cerr << "Couldn't read file \n";
-    return 0;
-  }
-  if (fccf_ply_read(argv[2], &tar, &nt) != FCCF_OK) {
-    std::cerr << "Couldn't read file \n";
-    fccf_free(src);
-    return 0;
+  const char* path[2] = {argv[1], argv[2]};
+  float** dst[2] = {&src, &tar};
+  int64_t* cnt[2] = {&ns, &nt};
+  for (int k = 0; k < 2; ++k) {
+    const int lrc = crc == FCCF_OK ? fccf_ply_load_device(ctx, path[k], dst[k], cnt[k])
+                                   : fccf_ply_read(path[k], dst[k], cnt[k]);
+    if (lrc != FCCF_OK) {
+      if (lrc != FCCF_E_IO) {
+        std::cerr << "fccf: " << fccf_strerror(lrc) << "\n";
+        return 2;
+      }
+      std::cerr << "Couldn't read file \n";
+      return 0;
+    }
   }
   std::cout << "Leaf size : " << leaf << std::endl;
-  fccf_ctx* ctx = nullptr;
-  int rc = fccf_ctx_create(&ctx, device);
-  if (rc != FCCF_OK) {
-    std::cerr << "fccf: " << fccf_strerror(rc) << "\n";
+  if (crc != FCCF_OK) {
+    std::cerr << "fccf: " << fccf_strerror(crc) << "\n";
     return 2;
   }
   float T[16];
   fccf_stats st;
-  rc = fccf_register(ctx, src, ns, tar, nt, leaf, nullptr, T, &st);
+  int rc = fccf_register_device(ctx, src, ns, tar, nt, leaf, nullptr, T, &st);
   if (rc != FCCF_OK) {
     std::cerr << "fccf: " << fccf_strerror(rc) << "\n";
     return 2;
@@ -82,8 +92,8 @@ int main(int argc, char** argv) {
                  (long long)st.planes1, (long long)st.planes2, (long long)st.K, (long long)st.K_pass,
                  (long long)st.cand[0], (long long)st.cand[1], (long long)st.cand[2], st.ms_total);
   }
+  fccf_device_free(ctx, src);
+  fccf_device_free(ctx, tar);
   fccf_ctx_destroy(ctx);
-  fccf_free(src);
-  fccf_free(tar);
   return 0;
 }

@@ -144,7 +144,6 @@ namespace {
 // ------------------------------------------------------------ per-cloud device state
 struct CloudWS {
   uint32_t cap = 0;
-  float* in_copy = nullptr;  // host inputs are copied here; device inputs are read in place
   uint32_t* sc = nullptr;  // [0] n_in, [1] m1, [2] m1 finite, [3] m2
   float *ds1 = nullptr, *ds1f = nullptr, *ds2 = nullptr;
   VGBufs vg;
@@ -155,10 +154,9 @@ struct CloudWS {
   OctState* fstate = nullptr;
 };
 
-size_t cloud_bytes(uint32_t cap, bool host_input) {
+size_t cloud_bytes(uint32_t cap, bool) {
   const size_t N = cap;
   size_t b = 0;
-  b += host_input ? 12 * N : 0;                               // input copy
   b += 12 * N * 3 + 64;                                        // ds1, ds1f, ds2
   b += voxel_grid_bytes(cap);                                  // K1
   b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
@@ -171,9 +169,8 @@ size_t cloud_bytes(uint32_t cap, bool host_input) {
   return b;
 }
 
-void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool host_input) {
+void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool) {
   w.cap = cap;
-  if (host_input) w.in_copy = a.take_n<float>(3 * (size_t)cap);
   w.sc = a.take_n<uint32_t>(16);
   w.ds1 = a.take_n<float>(3 * (size_t)cap);
   w.ds1f = a.take_n<float>(3 * (size_t)cap);
@@ -343,11 +340,35 @@ PipeSet& pset(fccf_ctx* c, int s) {
   return *(PipeSet*)c->cs[s].ws;
 }
 
-// Phase A: stage the inputs and enqueue the cloud device stage of one pair on
-// CloudSet s (returns at once).  cloud 0 = driver source = TAR file; cloud 1 =
-// driver target = SRC file (:1683).
+// Host inputs of the pair for CloudSet s: both clouds copied into the set's input
+// arena on the ctx's copy stream (ingest.h; the runtime's pageable path), after the
+// previous pair on this set has finished reading it (its first pass, before ev[0]).
+// ev_in marks the copies; clouds_enqueue makes st0 wait for it.  The pipelined batch
+// stages pair i+1 while pair i's cloud stage still runs, so the host link is busy
+// while the GPU computes instead of in front of the next cloud stage.
+struct Staged {
+  const float *src, *tar;
+};
+Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar) {
+  auto& cs = c->cs[s];
+  c->ingest.init();
+  cs.inarena.ensure(12 * (size_t)(n_src + n_tar) + 1024);  // (takes the capture lock to reallocate)
+  cs.inarena.reset();
+  float* dt = cs.inarena.take_n<float>(3 * (size_t)n_tar);
+  float* ds = cs.inarena.take_n<float>(3 * (size_t)n_src);
+  hipStream_t su = c->ingest.su;
+  guarded_stream_wait(su, cs.ev[0]);
+  if (n_tar) HIP_CHECK(hipMemcpyAsync(dt, tar, 12 * (size_t)n_tar, hipMemcpyHostToDevice, su));
+  if (n_src) HIP_CHECK(hipMemcpyAsync(ds, src, 12 * (size_t)n_src, hipMemcpyHostToDevice, su));
+  HIP_CHECK(hipEventRecord(cs.ev_in, su));
+  return {ds, dt};
+}
+
+// Phase A: enqueue the cloud device stage of one pair on CloudSet s (returns at
+// once).  src/tar are device clouds (staged ones wait for ev_in).  cloud 0 = driver
+// source = TAR file; cloud 1 = driver target = SRC file (:1683).
 void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
-                    bool on_device, float leaf, const fccf_params& P) {
+                    bool staged, float leaf, const fccf_params& P) {
   auto& cs = c->cs[s];
   PipeSet& ps = pset(c, s);
   ps.t_enq = clk::now();
@@ -363,23 +384,24 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   // the previous pair on this set may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for it
   guarded_stream_wait(st0, cs.ev[3]);  // ev[3] is recorded on the fine stream (captured by phase B)
-  cs.arena.ensure(2 * cloud_bytes(capmax, true) + exact_sum_bytes(6, capmax) + (1 << 20));
+  cs.arena.ensure(2 * cloud_bytes(capmax, false) + exact_sum_bytes(6, capmax) + (1 << 20));
   cs.arena.reset();
-  // Host inputs are copied into the workspace; device-resident inputs are read in
-  // place: their pointers and counts are patched into pass 1's entry kernel node.
+  // The inputs (caller-owned device clouds, or the staged copies of host arrays) are
+  // read in place: their pointers and counts are patched into pass 1's entry kernel
+  // node.
   const float* xin[2] = {nullptr, nullptr};
   uint32_t nv[2] = {0, 0};
   ps.cen = cs.arena.take_n<float>(8);
   ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
-    carve_cloud(cs.arena, w[k], capmax, true);
+    carve_cloud(cs.arena, w[k], capmax, false);
     w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
     nv[k] = (uint32_t)ps.nin[k];
-    if (nv[k] && !on_device)
-      HIP_CHECK(hipMemcpyAsync(w[k].in_copy, hin[k], 12 * (size_t)nv[k], hipMemcpyHostToDevice, st0));
-    xin[k] = on_device ? hin[k] : w[k].in_copy;
+    xin[k] = hin[k];
   }
+  // host inputs: staged by stage_inputs() into cs.inarena on the copy stream
+  if (staged) HIP_CHECK(hipStreamWaitEvent(st0, cs.ev_in, 0));
   struct {
     const void* base;
     size_t acap;
@@ -919,7 +941,12 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
                   float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
-  clouds_enqueue(c, 0, src, n_src, tar, n_tar, on_device, leaf, P);
+  if (!on_device) {
+    const Staged in = stage_inputs(c, 0, src, n_src, tar, n_tar);
+    src = in.src;
+    tar = in.tar;
+  }
+  clouds_enqueue(c, 0, src, n_src, tar, n_tar, !on_device, leaf, P);
   phase_b1(c, 0, P, T_out, stats, [] {});
   phase_b2(c, 0);
 }
@@ -930,24 +957,39 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   if (n <= 0) return;
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
-  clouds_enqueue(c, 0, src[0], n_src[0], tar[0], n_tar[0], on_device, leaf, P);
+  // Host inputs: pair i+1's clouds are staged on the copy stream at the start of
+  // pair i (from the helper thread: the pageable copy blocks its caller), so the host
+  // link works while pair i's cloud stage runs.
+  std::vector<Staged> in(on_device ? 0 : n);
+  auto dsrc = [&](int i) { return on_device ? src[i] : in[(size_t)i].src; };
+  auto dtar = [&](int i) { return on_device ? tar[i] : in[(size_t)i].tar; };
+  if (!on_device) in[0] = stage_inputs(c, 0, src[0], n_src[0], tar[0], n_tar[0]);
+  clouds_enqueue(c, 0, dsrc(0), n_src[0], dtar(0), n_tar[0], !on_device, leaf, P);
   // pair i: B1 (its clouds done -> enqueue pair i+1's clouds -> host stages ->
   // launch fine verification), then B2 of pair i-1, whose fine verification ran
   // on the GPU during pair i's host stages
   for (int i = 0; i < n; ++i) {
     const int s = i & 1;
     c->enq.wait();  // this pair's cloud stage is fully enqueued (its events recorded)
+    if (!on_device && i + 1 < n) {
+      auto stage = [c, s, i, src, n_src, tar, n_tar, &in] {
+        HIP_CHECK(hipSetDevice(c->device));
+        in[(size_t)i + 1] = stage_inputs(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1]);
+      };
+      if (c->probe.on()) stage();
+      else c->enq.submit(stage);
+    }
     phase_b1(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
       if (i + 1 >= n) return;
       // the next pair's cloud stage is enqueued from a helper thread while this
       // thread runs the host stages (launches are ~60 us of host time); probed
       // runs stay on this thread (the probe's launch records are not shared)
-      auto enq = [c, s, i, src, n_src, tar, n_tar, on_device, leaf, &P] {
+      auto enq = [c, s, i, n_src, n_tar, on_device, leaf, &P, dsrc, dtar] {
         HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
-        clouds_enqueue(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1], on_device, leaf, P);
+        clouds_enqueue(c, s ^ 1, dsrc(i + 1), n_src[i + 1], dtar(i + 1), n_tar[i + 1], !on_device, leaf, P);
       };
       if (c->probe.on()) enq();
-      else c->enq.submit(enq);
+      else c->enq.submit(enq);  // (after the staging task, which submit() joins first)
     });
     if (i > 0) phase_b2(c, s ^ 1);
   }

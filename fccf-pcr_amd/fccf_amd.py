@@ -105,6 +105,8 @@ _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINT
      ctypes.POINTER(_I64))
 _sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
 _sig("fccf_free", None, _P)
+_sig("fccf_ply_load_device", ctypes.c_int, _P, ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_I64))
+_sig("fccf_device_download", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
      ctypes.c_double, _P)
 _sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P, _P, _P)
@@ -230,6 +232,19 @@ class Ctx:
         d = _P()
         _check(_lib.fccf_device_upload(self._h, a.ctypes.data, a.shape[0], ctypes.byref(d)), "fccf_device_upload", self._h)
         return int(d.value or 0)
+
+    def ply_load(self, path: str):
+        """Stream a PLY file into a new HBM buffer (fccf_ply_load_device): (device ptr, n)."""
+        d, n = _P(), _I64()
+        _check(_lib.fccf_ply_load_device(self._h, path.encode(), ctypes.byref(d), ctypes.byref(n)),
+               f"fccf_ply_load_device({path})", self._h)
+        return int(d.value or 0), n.value
+
+    def download(self, dptr: int, n: int) -> np.ndarray:
+        """n xyz points of an HBM buffer of this ctx back to the host (test hook)."""
+        out = np.zeros((max(n, 1), 3), np.float32)
+        _check(_lib.fccf_device_download(self._h, _P(dptr), int(n), out.ctypes.data), "fccf_device_download", self._h)
+        return out[:n]
 
     def free(self, dptr: int):
         _check(_lib.fccf_device_free(self._h, _P(dptr)), "fccf_device_free", self._h)

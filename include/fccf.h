@@ -128,6 +128,8 @@ int fccf_register_batch(fccf_ctx* ctx, int n, const float* const* src_xyz, const
  * xyz points to a new HBM buffer on ctx's device; release with fccf_device_free. */
 int fccf_device_upload(fccf_ctx* ctx, const float* xyz, int64_t n, float** d_xyz);
 int fccf_device_free(fccf_ctx* ctx, float* d_xyz);
+/* n xyz points of a device buffer back to host memory (tests). */
+int fccf_device_download(fccf_ctx* ctx, const float* d_xyz, int64_t n, float* xyz);
 
 /* Stage export: PCL VoxelGrid<PointXYZ> (FCCF.cpp:1668-1678) on the GPU.
  * out_xyz capacity 3*n floats; *m receives the output count.  Output order is
@@ -251,6 +253,12 @@ int fccf_debug_capture_race(fccf_ctx* ctx, int hold_ms, int guard, double out[4]
 int fccf_ply_read(const char* path, float** xyz, int64_t* n);
 int fccf_ply_write(const char* path, const float* xyz, int64_t n, int binary);
 void fccf_free(void* p);
+/* Streaming PLY ingest: the vertex rows of path are decoded in
+ * chunks by the ctx's ingest threads into pinned staging slots, each chunk uploaded
+ * to a new HBM buffer on the ctx's copy stream while the next is decoded.  Same
+ * values as fccf_ply_read.  *d_xyz is released with fccf_device_free; the buffer is
+ * complete when the call returns.  FCCF_E_IO for a file loadPLYFile would reject. */
+int fccf_ply_load_device(fccf_ctx* ctx, const char* path, float** d_xyz, int64_t* n);
 
 /* Deterministic synthetic scenes; used by tests and bench. */
 int fccf_synth_scene(int64_t n, double Lx, double Ly, double Lz, uint64_t seed,
