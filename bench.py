@@ -213,6 +213,29 @@ def probe_pass(ctx, reg, kernel, steps):
     return ms, n, b
 
 
+def rccl_shard_pass(F, ctx, dist, ws, rank, src, tar, leaf, T_ref, steps):
+    """SURVEY.md §8(e) row K5, informational: every rank registers the SAME pair with
+    the correspondence search sharded over an RCCL group (source-pair blocks, rank-
+    ordered candidate gather over xGMI); the result must equal the unsharded T.  The
+    group's id travels over the gloo process group."""
+    ids = [F.group_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(ids, src=0)
+    g = F.Group(ctx, ids[0], ws, rank)
+    try:
+        ctx.register(src, tar, leaf)  # warm (graphs, communicator buffers)
+        barrier(dist)
+        a = time.perf_counter()
+        for _ in range(steps):
+            T, st = ctx.register(src, tar, leaf)
+        dt = allmax(dist, time.perf_counter() - a)
+    finally:
+        g.close()
+    assert np.array_equal(T.view(np.uint32), np.asarray(T_ref).view(np.uint32)), "sharded result differs"
+    return {"ranks": ws, "ms_per_registration": dt / steps * 1e3, "K": int(st.K), "K_pass": int(st.K_pass),
+            "note": "one pair registered collectively by all ranks (strong scaling of the search); "
+                    "host-array inputs; bit-identical to the unsharded T"}
+
+
 def ingest_pass(F, ctx, src, tar, leaf, T_ref, reps=3):
     """f2, informational: the reference's PLY -> T path
     (FCCF.cpp:1655-1685) with the clouds streamed from PLY files into HBM
@@ -261,6 +284,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--selftest", action="store_true", help="CPU stub registration (tests only)")
     ap.add_argument("--probe-kernel", default="auto", help="kernel for the roofline object (auto = dominant)")
+    ap.add_argument("--rccl-shard", action="store_true",
+                    help="N>1, informational: also time registrations of ONE pair by all ranks with the "
+                         "correspondence search sharded over an RCCL group (fccf_group_create)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="time K sequential fccf_register_device calls instead of one pipelined batch of K")
     args = ap.parse_args()
@@ -357,6 +383,8 @@ def main():
     if not args.selftest:
         assert np.array_equal(T2.view(np.uint32), np.asarray(T).view(np.uint32)), "host-input result differs"
     ingest = None if args.selftest or rank != 0 else ingest_pass(F, ctx, src, tar, leaf, T)
+    sharded = rccl_shard_pass(F, ctx, dist, ws, rank, src, tar, leaf, T, args.steps) \
+        if args.rccl_shard and ws > 1 and not args.selftest else None
     roofline = None
     if probe:
         # Probe window right after the timed region, same inputs: every launch of
@@ -411,6 +439,8 @@ def main():
         }
         if ingest is not None:
             out["ingest"] = ingest
+        if sharded is not None:
+            out["rccl_sharded_search"] = sharded
         if roofline is not None:
             roofline["stage"] = stage_rl
             out["roofline"] = roofline

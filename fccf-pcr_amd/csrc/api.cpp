@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "ctx.h"
+#include "group.h"
 #include "host_stages.h"
 #include "kernels.h"
 #include "match.h"
@@ -463,14 +464,17 @@ static_assert(sizeof(fccf_plane) == sizeof(MPlane) && sizeof(fccf_base) == sizeo
 
 // K5 alone (match.hip) over the b1 range; the same kernels registration runs, without
 // the pinned mailbox (K_pass is counted from the per-test candidate counts here).
-extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
-                                const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2, int b1_lo, int b1_hi,
-                                const fccf_params* params, float* const cand[3], const int64_t cap[3],
-                                int64_t n_cand[3], int64_t* k_pass) {
+namespace {
+// fccf_stage_match, and with a group (G) the sharded search: G's block of source
+// pairs, then the rank-ordered gather of every rank's lists (group.cpp).
+int stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1, const fccf_plane* F2,
+                int nF2, const fccf_base* B2, int nB2, int b1_lo, int b1_hi, const fccf_params* params,
+                float* const cand[3], const int64_t cap[3], int64_t n_cand[3], int64_t* k_pass, Group* G) {
   if (!c || !n_cand || nF1 < 0 || nF2 < 0 || nB1 < 0 || nB2 < 0 || nF1 > MAX_PLANES || nF2 > MAX_PLANES ||
       nB1 > MAX_BASES || nB2 > MAX_BASES || (nF1 && !F1) || (nF2 && !F2) || (nB1 && !B1) || (nB2 && !B2))
     return FCCF_E_ARG;
   if (b1_hi < 0) b1_hi = nB1;
+  if (G) shard_range(nB1, G->rank, G->n, &b1_lo, &b1_hi);
   if (b1_lo < 0 || b1_lo > b1_hi || b1_hi > nB1) return FCCF_E_ARG;
   // every pair must name planes of its own table: the kernels index F by i1, i2
   for (int i = 0; i < nB1; ++i)
@@ -496,11 +500,11 @@ extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, cons
     M.ang_same = P.included_angle_same_threshold;
     M.third_thr = P.third_plane_threshold;
     M.third_cut = make_cut(P.third_plane_normal_threshold);
-    const int K = nb * nB2;
+    const int K = nb * nB2, Kall = nB1 * nB2;
     const size_t per = (size_t)std::max(1, std::max(0, nF1 - 2) * std::max(0, nF2 - 2));
-    const size_t ccap = std::max<size_t>(1, (size_t)K * per);
-    c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + 3 * ccap * (sizeof(MCand) + sizeof(QTd)) +
-                     (1 << 16));
+    const size_t ccap = std::max<size_t>(1, (size_t)(G ? Kall : K) * per);
+    c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) +
+                     3 * ccap * (sizeof(MCand) + sizeof(QTd)) * (G ? 2 : 1) + (1 << 16));
     c->arena2.reset();
     MatchIn* dM = c->arena2.take_n<MatchIn>(1);
     uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
@@ -524,9 +528,22 @@ extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, cons
     HIP_CHECK(hipStreamSynchronize(st));
     int64_t kp = 0;
     for (int k = 0; k < K; ++k) kp += cnt[k] > 0;
+    if (!K) tot[0] = tot[1] = tot[2] = 0;
+    if (G) {
+      MCand* ca[3];
+      QTd* qa[3];
+      for (int t = 0; t < 3; ++t) {
+        ca[t] = c->arena2.take_n<MCand>(ccap);
+        qa[t] = c->arena2.take_n<QTd>(ccap);
+      }
+      uint32_t* dta = c->arena2.take_n<uint32_t>(4);
+      uint32_t tl[3] = {tot[0], tot[1], tot[2]};
+      group_gather_candidates(G, dq, dc, tl, kp, qa, ca, ccap, tot, dta, &kp, st);
+      for (int t = 0; t < 3; ++t) dc[t] = ca[t];
+    }
     if (k_pass) *k_pass = kp;
     for (int t = 0; t < 3; ++t) {
-      n_cand[t] = K ? tot[t] : 0;
+      n_cand[t] = (G ? Kall : K) ? tot[t] : 0;
       const int64_t nc = std::min<int64_t>(n_cand[t], cand && cap && cand[t] ? cap[t] : 0);
       if (nc <= 0) continue;
       std::vector<MCand> v((size_t)nc);
@@ -543,6 +560,23 @@ extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, cons
       }
     }
   });
+}
+}  // namespace
+
+extern "C" int fccf_stage_match(fccf_ctx* c, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
+                                const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2, int b1_lo, int b1_hi,
+                                const fccf_params* params, float* const cand[3], const int64_t cap[3],
+                                int64_t n_cand[3], int64_t* k_pass) {
+  return stage_match(c, F1, nF1, B1, nB1, F2, nF2, B2, nB2, b1_lo, b1_hi, params, cand, cap, n_cand, k_pass, nullptr);
+}
+
+extern "C" int fccf_group_stage_match(fccf_group* g, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
+                                      const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2,
+                                      const fccf_params* params, float* const cand[3], const int64_t cap[3],
+                                      int64_t n_cand[3], int64_t* k_pass) {
+  Group* G = group_of(g);
+  if (!G) return FCCF_E_ARG;
+  return stage_match(G->ctx, F1, nF1, B1, nB1, F2, nF2, B2, nB2, 0, -1, params, cand, cap, n_cand, k_pass, G);
 }
 
 extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int cluster_num,

@@ -20,6 +20,8 @@
 
 namespace fccf {
 
+struct Group;
+
 struct Error : std::runtime_error {
   int code;
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
@@ -246,6 +248,7 @@ struct fccf_ctx {
   fccf::AsyncTask enq;  // pipelined batch: enqueues the next pair's cloud stage
   fccf::Probe probe;
   fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)
+  fccf::Group* group = nullptr;  // RCCL rank of a sharded registration (group.cpp), or none
   bool debug = false;
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   std::map<std::string, std::vector<uint8_t>> dbg;

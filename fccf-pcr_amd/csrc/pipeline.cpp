@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "group.h"
 #include "host_stages.h"
 #include "kernels.h"
 #include "match.h"
@@ -608,10 +609,20 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   M.ang_same = P.included_angle_same_threshold;
   M.third_thr = P.third_plane_threshold;
   M.third_cut = make_cut(P.third_plane_normal_threshold);
+  // Sharded search (group.cpp): this rank tests its contiguous block of source pairs;
+  // the lists of all ranks are gathered in rank order after the kernels.
+  Group* G = c->group;
+  if (G) {
+    int lo = 0, hi = 0;
+    shard_range(M.nB1, G->rank, G->n, &lo, &hi);
+    if (lo) std::memmove(M.B1, M.B1 + lo, sizeof(MBase) * (size_t)(hi - lo));
+    M.nB1 = hi - lo;
+  }
+  const int Kloc = M.nB1 * M.nB2;
   const size_t per = (size_t)std::max(1, std::max(0, M.nF1 - 2) * std::max(0, M.nF2 - 2));
   const size_t ccap = std::max<size_t>(1, (size_t)K * per);
-  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + 3 * ccap * (sizeof(MCand) + sizeof(QTd)) +
-                   (1 << 16));
+  const size_t lists = 3 * ccap * (sizeof(MCand) + sizeof(QTd));
+  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + lists * (G ? 2 : 1) + (1 << 16));
   c->arena2.reset();
   MatchIn* dM = c->arena2.take_n<MatchIn>(1);
   uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
@@ -627,18 +638,42 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   uint32_t tot[4] = {0, 0, 0, 0};
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
   HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
-  match_candidates(dM, K, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
+  match_candidates(dM, Kloc, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
   // transform_cluster's radius search for all three lists on the device (k_cluster_bits)
   const char* cbe = std::getenv("FCCF_CLUSTER_BITS");  // "0": host radius search (tests both paths)
   const bool cbits_on = !(cbe && cbe[0] == '0');
   const float cr2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
-  if (cbits_on && K > 0)
+  if (cbits_on && K > 0 && !G)
     cluster_bits(dq, dtot, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(st0));  // totals, K_pass and candidate lists are in the mailbox
   std::vector<QTd> qraw[3];
   int64_t kpass = 0;
-  if (K > 0) {
+  if (G && K > 0) {
+    uint32_t tl[3] = {0, 0, 0};
+    int64_t kl = 0;
+    if (Kloc > 0) {
+      std::memcpy(tl, mm.tot, 12);
+      kl = mm.kpass;
+    }
+    MCand* ca[3];
+    QTd* qa[3];
+    for (int t = 0; t < 3; ++t) {
+      ca[t] = c->arena2.take_n<MCand>(ccap);
+      qa[t] = c->arena2.take_n<QTd>(ccap);
+    }
+    uint32_t* dtot_all = c->arena2.take_n<uint32_t>(4);
+    group_gather_candidates(G, dq, dc, tl, kl, qa, ca, ccap, tot, dtot_all, &kpass, st0);
+    for (int t = 0; t < 3; ++t) {
+      dc[t] = ca[t];
+      dq[t] = qa[t];
+    }
+    if (cbits_on)
+      cluster_bits(dq, dtot_all, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0);
+    HIP_CHECK(hipGetLastError());
+    for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
+    HIP_CHECK(hipStreamSynchronize(st0));
+  } else if (K > 0) {
     std::memcpy(tot, mm.tot, 12);
     kpass = mm.kpass;
     bool over = false;

@@ -107,6 +107,12 @@ _sig("fccf_ply_write", ctypes.c_int, ctypes.c_char_p, _P, _I64, ctypes.c_int)
 _sig("fccf_free", None, _P)
 _sig("fccf_ply_load_device", ctypes.c_int, _P, ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_I64))
 _sig("fccf_device_download", ctypes.c_int, _P, _P, _I64, _P)
+_sig("fccf_group_unique_id", ctypes.c_int, _P)
+_sig("fccf_group_create", ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P))
+_sig("fccf_group_destroy", ctypes.c_int, _P)
+_sig("fccf_group_info", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+_sig("fccf_group_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
+     ctypes.POINTER(Params), ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
      ctypes.c_double, _P)
 _sig("fccf_synth_pair", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P, _P, _P)
@@ -382,6 +388,64 @@ class Ctx:
         buf = np.zeros(n.value // np.dtype(dtype).itemsize, dtype)
         _check(_lib.fccf_debug_get(self._h, name.encode(), buf.ctypes.data, n.value, ctypes.byref(n)), "debug")
         return buf
+
+
+GROUP_ID_BYTES = 128
+
+
+def group_unique_id() -> bytes:
+    """An RCCL unique id (rank 0 makes it; every rank of the group needs the same bytes)."""
+    buf = (ctypes.c_uint8 * GROUP_ID_BYTES)()
+    _check(_lib.fccf_group_unique_id(buf), "fccf_group_unique_id")
+    return bytes(buf)
+
+
+class Group:
+    """One rank of an RCCL group attached to a Ctx (fccf_group_create): while it is
+    open, the ctx's registrations shard the correspondence search across the ranks."""
+
+    def __init__(self, ctx: "Ctx", uid: bytes, n_ranks: int, rank: int):
+        if len(uid) != GROUP_ID_BYTES:
+            raise ValueError("group id must be 128 bytes")
+        self.ctx = ctx
+        self._h = _P()
+        buf = (ctypes.c_uint8 * GROUP_ID_BYTES).from_buffer_copy(uid)
+        _check(_lib.fccf_group_create(ctx._h, buf, int(n_ranks), int(rank), ctypes.byref(self._h)),
+               "fccf_group_create", ctx._h)
+
+    def info(self):
+        n, r = ctypes.c_int(), ctypes.c_int()
+        _check(_lib.fccf_group_info(self._h, ctypes.byref(n), ctypes.byref(r)), "fccf_group_info")
+        return n.value, r.value
+
+    def match(self, F1, B1, F2, B2, params: Params | None = None):
+        """The sharded search (fccf_group_stage_match): same result as Ctx.match over
+        all source pairs, on every rank."""
+        F1, F2 = np.ascontiguousarray(F1, PLANE_DTYPE), np.ascontiguousarray(F2, PLANE_DTYPE)
+        B1, B2 = np.ascontiguousarray(B1, BASE_DTYPE), np.ascontiguousarray(B2, BASE_DTYPE)
+        p = params if params is not None else default_params()
+        ncand, kp = (_I64 * 3)(), _I64()
+        args = [self._h, F1.ctypes.data, len(F1), B1.ctypes.data, len(B1), F2.ctypes.data, len(F2),
+                B2.ctypes.data, len(B2), ctypes.byref(p)]
+        _check(_lib.fccf_group_stage_match(*args, None, None, ncand, ctypes.byref(kp)), "fccf_group_stage_match",
+               self.ctx._h)
+        out = [np.zeros((max(int(n), 1), 4, 4), np.float32) for n in ncand]
+        ptrs = (_P * 3)(*[o.ctypes.data for o in out])
+        caps = (_I64 * 3)(*[int(n) for n in ncand])
+        _check(_lib.fccf_group_stage_match(*args, ptrs, caps, ncand, ctypes.byref(kp)), "fccf_group_stage_match",
+               self.ctx._h)
+        return [o[: int(n)] for o, n in zip(out, ncand)], kp.value
+
+    def close(self):
+        if self._h:
+            _lib.fccf_group_destroy(self._h)
+            self._h = _P()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def strerror(code: int) -> str:
