@@ -103,6 +103,12 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   return FCCF_OK;
 }
 
+extern "C" int fccf_ctx_set_grow_device(fccf_ctx* c, int on) {
+  if (!c) return FCCF_E_ARG;
+  c->grow_device = on != 0;
+  return FCCF_OK;
+}
+
 extern "C" int fccf_ctx_set_debug(fccf_ctx* c, int on) {
   if (!c) return FCCF_E_ARG;
   c->debug = on != 0;
@@ -449,7 +455,27 @@ extern "C" int fccf_stage_grow(fccf_ctx* c, const fccf_voxel* vox, int64_t nv, i
   return guarded(c, [&] {
     std::vector<VoxRec> v((size_t)nv);
     if (nv) std::memcpy(v.data(), vox, sizeof(VoxRec) * (size_t)nv);
-    const GrowOut g = grow_and_select(v.data(), (int)nv, P);
+    GrowOut g;
+    if (c->grow_device && nv <= (int64_t)GROW_CAP) {  // K4 on the device (grow.hip)
+      hipStream_t st = c->sb;
+      VoxRec* d = nullptr;
+      if (hipMalloc((void**)&d, sizeof(VoxRec) * (size_t)std::max<int64_t>(nv, 1)) != hipSuccess)
+        throw Error(FCCF_E_OOM, "hipMalloc");
+      try {
+        if (nv) HIP_CHECK(hipMemcpyAsync(d, v.data(), sizeof(VoxRec) * (size_t)nv, hipMemcpyHostToDevice, st));
+        const VoxRec* dv[2] = {d, d};
+        const uint32_t n2[2] = {(uint32_t)nv, 0u};
+        std::vector<GroupOut> gg[2];
+        grow_groups_device(c, dv, n2, P, st, gg);
+        g = select_groups(gg[0], v.data(), P);
+      } catch (...) {
+        (void)hipFree(d);
+        throw;
+      }
+      HIP_CHECK(hipFree(d));
+    } else {
+      g = grow_and_select(v.data(), (int)nv, P);
+    }
     const std::vector<Base> b = select_base(g.planes, g.theta, P, side);
     *n_planes = (int)g.planes.size();
     *n_bases = (int)b.size();

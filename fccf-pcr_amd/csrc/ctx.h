@@ -250,6 +250,7 @@ struct fccf_ctx {
   fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)
   fccf::Group* group = nullptr;  // RCCL rank of a sharded registration (group.cpp), or none
   bool debug = false;
+  bool grow_device = false;  // K4 region growing on the GPU (grow.hip) instead of the host
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;

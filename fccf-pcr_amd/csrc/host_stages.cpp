@@ -58,7 +58,7 @@ static inline void angle_skip8(const float* __restrict__ nx, const float* __rest
   }
 }
 
-GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
+std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& P) {
   // compare_normal(...) == !(theta > thr) == !angle_gt(cos, cut): no acos in the O(V^2) loops
   const AngleCut cut1 = make_cut(P.normal_vector_threshold1), cut2 = make_cut(P.normal_vector_threshold2);
   std::vector<char> va(nv, 0);
@@ -145,6 +145,18 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
       }
     }
   }
+  std::vector<GroupOut> out(G.size());
+  for (size_t i = 0; i < G.size(); ++i) {
+    std::memcpy(out[i].ac, G[i].ac, 12);
+    std::memcpy(out[i].an, G[i].an, 12);
+    out[i].fps = G[i].fps;
+    out[i].alloc = G[i].alloc;
+    out[i].mem = std::move(G[i].mem);
+  }
+  return out;
+}
+
+GrowOut select_groups(const std::vector<GroupOut>& G, const VoxRec* vox, const fccf_params& P) {
   // range_face (:409-427): exchange sort on voxel counts, emulated on indices
   const auto t_sel = std::chrono::steady_clock::now();  // range_face + selection from here
   std::vector<int> ord(G.size());
@@ -154,7 +166,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
       if (G[ord[i]].mem.size() < G[ord[j]].mem.size()) std::swap(ord[i], ord[j]);
   GrowOut out;
   for (int k : ord) {
-    const Group& g = G[k];
+    const GroupOut& g = G[k];
     Plane p;
     std::memcpy(p.c, g.ac, 12);
     std::memcpy(p.n, g.an, 12);
@@ -165,7 +177,7 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
   }
   int cur = 0;
   for (size_t r = 0; r < ord.size(); ++r) {
-    const Group& g = G[ord[r]];
+    const GroupOut& g = G[ord[r]];
     if (!g.alloc) {
       out.planes.push_back(out.groups[r]);
       double sum = 0;
@@ -181,6 +193,10 @@ GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
   }
   out.ms_select = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sel).count();
   return out;
+}
+
+GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P) {
+  return select_groups(grow_groups(vox, nv, P), vox, P);
 }
 
 std::vector<Base> select_base(const std::vector<Plane>& F, const std::vector<double>& th, const fccf_params& P,

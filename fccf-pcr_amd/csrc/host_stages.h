@@ -35,7 +35,17 @@ struct GrowOut {
   double ms_select = 0.0;        // host time of range_face + selection
 };
 
-// face_extrate region growing (:536-648), range_face (:409-427), selection (:650-677).
+// A growth group after stage 2 (a facenode of voxel_vector_groth, :595-648).
+struct GroupOut {
+  float ac[3], an[3], fps;
+  bool alloc;
+  std::vector<int> mem;  // member voxels in voxelgrothnode order
+};
+// face_extrate region growing, stages 1 and 2 (:536-648), on the host.
+std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& P);
+// range_face (:409-427) and the plane selection with roughness (:650-677).
+GrowOut select_groups(const std::vector<GroupOut>& G, const VoxRec* vox, const fccf_params& P);
+// both of the above
 GrowOut grow_and_select(const VoxRec* vox, int nv, const fccf_params& P);
 // select_base (:429-468); `side` picks the out-of-range type sentinel (-1 / -2).
 std::vector<Base> select_base(const std::vector<Plane>& F, const std::vector<double>& theta, const fccf_params& P,

@@ -126,6 +126,28 @@ struct VoxRec {  // one occupied octree leaf, Morton order
   float curvature;
 };
 
+// ------------------------------------------------ K4: region growing (FCCF.cpp:536-648), grow.hip
+constexpr uint32_t GROW_CAP = 3072;  // voxels per cloud held in LDS (larger clouds grow on the host)
+struct GrowIn {
+  const VoxRec* vox;  // planar voxel records of one cloud, Morton order
+  uint32_t nv;        // <= GROW_CAP
+};
+struct GrowDev {      // per group (<= nv), creation (seed) order; plus the member lists
+  float* gac;         // 3 per group: average centre
+  float* gan;         // 3 per group: average normal
+  float* gfps;        // face_point_size
+  float* gsum;        // 7 per group: running sums s, sc[3], sn[3] after stage 1
+  double* gna;        // norm3d(an)
+  uint32_t *ghead, *gtail, *gnmem, *galloc;
+  uint32_t* next;     // nv: next member of the same group (0xFFFFFFFF at a tail)
+  uint32_t* ng;       // number of groups
+};
+struct GrowParams {
+  AngleCut cut1, cut2;  // normal_vector_threshold1/2 as cosine cuts
+  float l1, k1, l2, k2;
+};
+void grow_device(const GrowIn in[2], const GrowDev out[2], const GrowParams& P, hipStream_t st);
+
 struct FaceBufs {
   uint64_t *c0, *c1;       // codes, cap each
   uint32_t *v0, *v1;       // cap each

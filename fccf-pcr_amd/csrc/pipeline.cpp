@@ -549,8 +549,16 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   GrowOut g[2];
   std::vector<Base> base[2];
   double sel_ms[2] = {0.0, 0.0};
+  // K4 on the device (grow.hip) when the ctx asks for it and both clouds fit its LDS
+  const bool gdev = c->grow_device && fsc[0][2] <= GROW_CAP && fsc[1][2] <= GROW_CAP;
+  std::vector<GroupOut> gg[2];
+  if (gdev) {
+    const VoxRec* dv[2] = {w[0].planar, w[1].planar};
+    const uint32_t nvv[2] = {fsc[0][2], fsc[1][2]};
+    grow_groups_device(c, dv, nvv, P, st0, gg);
+  }
   c->pool.parallel_for(2, [&](int k) {  // the two clouds are independent
-    g[k] = grow_and_select(vox[k].data(), (int)vox[k].size(), P);
+    g[k] = gdev ? select_groups(gg[k], vox[k].data(), P) : grow_and_select(vox[k].data(), (int)vox[k].size(), P);
     const auto tb = clk::now();
     base[k] = select_base(g[k].planes, g[k].theta, P, k + 1);
     sel_ms[k] = g[k].ms_select + ms_since(tb);
@@ -964,6 +972,75 @@ struct ProbeGuard {
 };
 
 }  // namespace
+
+void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t nv[2], const fccf_params& P,
+                        hipStream_t st, std::vector<GroupOut> out[2]) {
+  // one contiguous block per cloud: the D2H of a block brings every output back
+  const auto block_words = [](uint32_t n) { return (size_t)n * 22 + 64; };  // 4-byte words
+  const size_t w0 = block_words(std::max(nv[0], 1u)), w1 = block_words(std::max(nv[1], 1u));
+  c->arena2.ensure(4 * (w0 + w1) + 1024);
+  c->arena2.reset();
+  uint32_t* blk[2] = {c->arena2.take_n<uint32_t>(w0), c->arena2.take_n<uint32_t>(w1)};
+  GrowIn in[2];
+  GrowDev od[2];
+  auto carve = [](uint32_t* b, uint32_t n, GrowDev& d) {
+    n = std::max(n, 1u);
+    d.gna = (double*)b;  // 8-byte aligned first
+    uint32_t* q = b + 2 * (size_t)n;
+    d.gac = (float*)q; q += 3 * (size_t)n;
+    d.gan = (float*)q; q += 3 * (size_t)n;
+    d.gfps = (float*)q; q += n;
+    d.gsum = (float*)q; q += 7 * (size_t)n;
+    d.ghead = q; q += n;
+    d.gtail = q; q += n;
+    d.gnmem = q; q += n;
+    d.galloc = q; q += n;
+    d.next = q; q += n;
+    d.ng = q;
+  };
+  for (int k = 0; k < 2; ++k) {
+    in[k] = {dvox[k], nv[k]};
+    carve(blk[k], nv[k], od[k]);
+  }
+  GrowParams gp;
+  gp.cut1 = make_cut(P.normal_vector_threshold1);
+  gp.cut2 = make_cut(P.normal_vector_threshold2);
+  gp.l1 = P.parameter_l1;
+  gp.k1 = P.parameter_k1;
+  gp.l2 = P.parameter_l2;
+  gp.k2 = P.parameter_k2;
+  grow_device(in, od, gp, st);
+  HIP_CHECK(hipGetLastError());
+  uint32_t* h = (uint32_t*)c->pinned.get(4 * (w0 + w1));
+  HIP_CHECK(hipMemcpyAsync(h, blk[0], 4 * w0, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(h + w0, blk[1], 4 * w1, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  for (int k = 0; k < 2; ++k) {
+    GrowDev hd;
+    carve(h + (k ? w0 : 0), nv[k], hd);
+    const uint32_t G = nv[k] ? *hd.ng : 0u;
+    if (G > nv[k]) throw Error(FCCF_E_INTERNAL, "k_grow: group count out of range");
+    out[k].assign(G, GroupOut());
+    for (uint32_t g = 0; g < G; ++g) {
+      GroupOut& o = out[k][g];
+      std::memcpy(o.ac, hd.gac + 3 * (size_t)g, 12);
+      std::memcpy(o.an, hd.gan + 3 * (size_t)g, 12);
+      o.fps = hd.gfps[g];
+      o.alloc = hd.galloc[g] != 0;
+      // a group's members are the first gnmem nodes of the list from its head: a group
+      // merged into another keeps its tail, which the absorbing group extends later
+      const uint32_t nm = hd.gnmem[g];
+      if (nm == 0 || nm > nv[k]) throw Error(FCCF_E_INTERNAL, "k_grow: member count out of range");
+      o.mem.resize(nm);
+      uint32_t m = hd.ghead[g];
+      for (uint32_t q = 0; q < nm; ++q) {
+        if (m >= nv[k]) throw Error(FCCF_E_INTERNAL, "k_grow: member list corrupt");
+        o.mem[q] = (int)m;
+        m = hd.next[m];
+      }
+    }
+  }
+}
 
 void pipeline_release(fccf_ctx* c) {
   for (auto& cs : c->cs) {

@@ -1,6 +1,7 @@
 // pipeline.h — workspace layout helpers shared by api.cpp and pipeline.cpp.
 #pragma once
 #include "ctx.h"
+#include "host_stages.h"
 #include "kernels.h"
 
 namespace fccf {
@@ -58,6 +59,12 @@ inline FaceBufs face_bufs_carve(Arena& a, uint32_t cap) {
   f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
   return f;
 }
+
+// K4 (grow.hip): region growing stages 1-2 of both clouds on the device.  dvox: the
+// clouds' planar voxel records in HBM, nv their counts (each <= GROW_CAP, else the
+// caller grows on the host).  Uses arena2 and c->pinned; synchronises st.
+void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t nv[2], const fccf_params& P,
+                        hipStream_t st, std::vector<GroupOut> out[2]);
 
 // Releases the per-CloudSet pipeline state (fccf_ctx_destroy).
 void pipeline_release(fccf_ctx* c);

@@ -71,6 +71,7 @@ _sig("fccf_strerror", ctypes.c_char_p, ctypes.c_int)
 _sig("fccf_ctx_create", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int)
 _sig("fccf_ctx_destroy", ctypes.c_int, _P)
 _sig("fccf_ctx_set_debug", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_ctx_set_grow_device", ctypes.c_int, _P, ctypes.c_int)
 _sig("fccf_ctx_last_error", ctypes.c_char_p, _P)
 _sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
      ctypes.POINTER(Stats))
@@ -170,6 +171,10 @@ class Ctx:
         _check(_lib.fccf_ctx_create(ctypes.byref(self._h), int(device)), "fccf_ctx_create")
         if debug:
             _check(_lib.fccf_ctx_set_debug(self._h, 1), "fccf_ctx_set_debug", self._h)
+
+    def set_grow_device(self, on: bool = True):
+        """Region growing (FCCF.cpp:536-648) on the GPU (K4) instead of the host."""
+        _check(_lib.fccf_ctx_set_grow_device(self._h, int(bool(on))), "fccf_ctx_set_grow_device", self._h)
 
     def close(self):
         if self._h:

@@ -100,6 +100,11 @@ int fccf_ctx_create(fccf_ctx** ctx, int device);
 int fccf_ctx_destroy(fccf_ctx* ctx);
 /* Message of the last failing call on ctx ("" if none); valid until the next call. */
 const char* fccf_ctx_last_error(fccf_ctx* ctx);
+/* Region growing (FCCF.cpp:536-648) on the GPU (K4, one wave
+ * per cloud with LDS-resident voxels, bit-identical) instead of the host: applies to
+ * fccf_register* and fccf_stage_grow on this ctx; clouds with more planar voxels than
+ * the kernel's LDS holds still grow on the host.  Off by default. */
+int fccf_ctx_set_grow_device(fccf_ctx* ctx, int on);
 /* Keep per-stage intermediates for fccf_debug_get (tests). Off by default. */
 int fccf_ctx_set_debug(fccf_ctx* ctx, int on);
 
@@ -246,6 +251,28 @@ int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
  * releasing the waiter, [2] the wait's error code, [3] 1 if it returned after the
  * capture ended.  Test hook. */
 int fccf_debug_capture_race(fccf_ctx* ctx, int hold_ms, int guard, double out[4]);
+
+/* Multi-GPU over RCCL: one process per GPU, one group per
+ * ctx.  Rank 0 makes an id with fccf_group_unique_id and the caller hands it to every
+ * rank out of band; each rank calls fccf_group_create with its ctx (collective over
+ * the n ranks).  While a group is attached, fccf_register* on that ctx is a
+ * collective: every rank passes the same clouds, the coplane-pair correspondence
+ * search (FCCF.cpp:1410-1428) is sharded by contiguous source-pair blocks and the
+ * candidate lists are gathered in rank order over RCCL; every rank returns the same T,
+ * bit-identical to the unsharded registration.  fccf_group_destroy detaches it. */
+#define FCCF_GROUP_ID_BYTES 128
+typedef struct fccf_group fccf_group;
+int fccf_group_unique_id(uint8_t id[FCCF_GROUP_ID_BYTES]);
+int fccf_group_create(fccf_ctx* ctx, const uint8_t id[FCCF_GROUP_ID_BYTES], int n_ranks, int rank,
+                      fccf_group** group);
+int fccf_group_destroy(fccf_group* group);
+int fccf_group_info(const fccf_group* group, int* n_ranks, int* rank);
+/* Stage export of the sharded search: fccf_stage_match's arguments without the
+ * range; this rank searches its block, and every rank receives the whole lists. */
+int fccf_group_stage_match(fccf_group* group, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,
+                           const fccf_plane* F2, int nF2, const fccf_base* B2, int nB2,
+                           const fccf_params* params, float* const cand[3], const int64_t cap[3],
+                           int64_t n_cand[3], int64_t* k_pass);
 
 /* PLY I/O (the reference's pcl::io::loadPLYFile<PointXYZ> surface, FCCF.cpp:1655-1665):
  * ascii / binary_little_endian / binary_big_endian, float x,y,z (double converted).

@@ -1,0 +1,37 @@
+"""Dev probe: K4 growth on the host vs on the GPU (fccf_ctx_set_grow_device) at a
+config: median grow-stage ms, single-registration ms and pipelined ms per registration.
+Usage: python tools/grow_ab.py [config] [reps]"""
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fccf-pcr_amd"))
+import fccf_amd as F  # noqa: E402
+
+cfg = F.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
+ctx = F.Ctx(0)
+ds, dt = ctx.upload(src), ctx.upload(tar)
+ref = None
+for mode in (False, True, False, True):
+    ctx.set_grow_device(mode)
+    for _ in range(3):
+        ctx.register_device(ds, len(src), dt, len(tar), cfg["leaf"])
+    g, e = [], []
+    for _ in range(reps):
+        a = time.perf_counter()
+        T, st = ctx.register_device(ds, len(src), dt, len(tar), cfg["leaf"])
+        e.append((time.perf_counter() - a) * 1e3)
+        g.append(st.ms[2])
+    ref = T if ref is None else ref
+    assert np.array_equal(T.view(np.uint32), ref.view(np.uint32))
+    a = time.perf_counter()
+    ctx.register_batch([((ds, len(src)), (dt, len(tar)))] * reps, cfg["leaf"], on_device=True)
+    pb = (time.perf_counter() - a) / reps * 1e3
+    print(f"grow_device={mode}: vox {st.vox1}/{st.vox2} grow {statistics.median(g):.4f} ms  "
+          f"e2e {statistics.median(e):.3f} ms  pipelined {pb:.3f} ms/reg", flush=True)
