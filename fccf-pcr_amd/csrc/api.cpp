@@ -109,6 +109,12 @@ extern "C" int fccf_ctx_set_grow_device(fccf_ctx* c, int on) {
   return FCCF_OK;
 }
 
+extern "C" int fccf_ctx_set_lm_device(fccf_ctx* c, int on) {
+  if (!c) return FCCF_E_ARG;
+  c->lm_device = on != 0;
+  return FCCF_OK;
+}
+
 extern "C" int fccf_ctx_set_debug(fccf_ctx* c, int on) {
   if (!c) return FCCF_E_ARG;
   c->debug = on != 0;
@@ -487,6 +493,75 @@ extern "C" int fccf_stage_grow(fccf_ctx* c, const fccf_voxel* vox, int64_t nv, i
 }
 
 static_assert(sizeof(fccf_plane) == sizeof(MPlane) && sizeof(fccf_base) == sizeof(MBase), "table layouts");
+
+extern "C" int fccf_debug_sincos(fccf_ctx* c, const double* x, int64_t n, double* s, double* co, uint32_t* ok) {
+  if (!c || n < 0 || n > (1 << 24) || (n && (!x || !s || !co || !ok))) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    if (!n) return;
+    hipStream_t st = c->sb;
+    c->arena2.ensure(28 * (size_t)n + 1024);
+    c->arena2.reset();
+    double* dx = c->arena2.take_n<double>(n);
+    double* ds = c->arena2.take_n<double>(n);
+    double* dc = c->arena2.take_n<double>(n);
+    uint32_t* dk = c->arena2.take_n<uint32_t>(n);
+    HIP_CHECK(hipMemcpyAsync(dx, x, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+    sincos_probe(dx, (int)n, ds, dc, dk, st);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(s, ds, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(co, dc, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(ok, dk, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
+extern "C" int fccf_stage_verify(fccf_ctx* c, const fccf_plane* F1, int nF1, const fccf_plane* F2, int nF2,
+                                 const float* qt, int64_t n, const fccf_params* params, float* T_out, float* score,
+                                 int32_t* npairs) {
+  if (!c || nF1 < 0 || nF2 < 0 || nF1 > MAX_PLANES || nF2 > MAX_PLANES || (nF1 && !F1) || (nF2 && !F2) || n < 0 ||
+      n > (1 << 24) || (n && (!qt || !T_out || !score || !npairs)))
+    return FCCF_E_ARG;
+  fccf_params P;
+  if (params) P = *params;
+  else fccf_params_default(&P);
+  return guarded(c, [&] {
+    std::vector<Plane> A((size_t)nF1), B((size_t)nF2);
+    if (nF1) std::memcpy(A.data(), F1, sizeof(Plane) * (size_t)nF1);
+    if (nF2) std::memcpy(B.data(), F2, sizeof(Plane) * (size_t)nF2);
+    std::vector<QT> qs((size_t)n);
+    for (int64_t k = 0; k < n; ++k) {
+      const float* a = qt + 8 * k;
+      qs[(size_t)k] = {a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7] != 0.f ? 1u : 0u};
+    }
+    std::vector<m44> T((size_t)n);
+    std::vector<float> sc((size_t)n);
+    std::vector<int> np((size_t)n);
+    if (c->lm_device) {
+      hipStream_t st = c->sb;
+      MatchIn M;
+      std::memset(&M, 0, sizeof M);
+      if (nF1) std::memcpy(M.F1, F1, sizeof(MPlane) * nF1);
+      if (nF2) std::memcpy(M.F2, F2, sizeof(MPlane) * nF2);
+      M.nF1 = nF1;
+      M.nF2 = nF2;
+      c->arena2.ensure(sizeof(MatchIn) + 1024);
+      c->arena2.reset();
+      MatchIn* dM = c->arena2.take_n<MatchIn>(1);
+      HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st));
+      verify_items_device(c, qs, A, B, dM, P, st, T, sc, np);
+    } else {
+      c->pool.parallel_for((int)n, [&](int k) {
+        T[(size_t)k] = T_from_qt(qs[(size_t)k]);
+        sc[(size_t)k] = quick_verify(T[(size_t)k], A, B, P, &np[(size_t)k]);
+      });
+    }
+    for (int64_t k = 0; k < n; ++k) {
+      std::memcpy(T_out + 16 * k, &T[(size_t)k].m[0][0], 64);
+      score[k] = sc[(size_t)k];
+      npairs[k] = np[(size_t)k];
+    }
+  });
+}
 
 // K5 alone (match.hip) over the b1 range; the same kernels registration runs, without
 // the pinned mailbox (K_pass is counted from the per-test candidate counts here).

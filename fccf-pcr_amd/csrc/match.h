@@ -31,6 +31,25 @@ struct MatchMail;
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
                       MCand* c[3], QTd* q[3], hipStream_t st, MatchMail* mail = nullptr);
 
+// ------------------------------------------------ f1: quick_verify + LM on the device (verify.hip)
+struct VerifyIn {
+  const QTd* q;           // candidate transforms as quaternion records, all types concatenated
+  const MatchIn* planes;  // F1, F2 and their counts (the matching table)
+  int32_t fs12;           // fs1 + fs2, quick_verify's face-point sums (FCCF.cpp:688-697)
+  AngleCut qcut;          // quick_verify_angel_threshold
+  float dist_thr;         // quick_verify_distance_threshold
+  float required;         // required_optimize_plane
+};
+struct VerifyOut {
+  float* T;          // 16 per candidate, row-major, refined
+  float* score;
+  int32_t* npairs;
+  uint32_t* status;  // 1: a sin/cos argument outside the device reduction (host redoes it)
+};
+void verify_device(const VerifyIn& in, int n, const VerifyOut& out, hipStream_t st);
+// test hook: the device's correctly rounded double sin/cos of x[0..n)
+void sincos_probe(const double* x, int n, double* s, double* c, uint32_t* ok, hipStream_t st);
+
 // ------------------------------------------------ K7: fine_verify (FCCF.cpp:785-839)
 constexpr int MAX_EVAL = 16;
 struct FineBufs {

@@ -754,13 +754,29 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     npairs[t].resize(fine[t].size());
     for (size_t i = 0; i < fine[t].size(); ++i) items.push_back({t, (int)i});
   }
-  c->pool.parallel_for((int)items.size(), [&](int k) {  // independent per candidate
-    const int t = items[k].first, i = items[k].second;
-    TS& r = res[t][i];
-    r.T = T_from_qt(fine[t][i]);
-    r.score = quick_verify(r.T, g[0].planes, g[1].planes, P, &npairs[t][i]);
-    r.score2 = 0.f;
-  });
+  if (c->lm_device && !items.empty()) {  // f1: every candidate's quick_verify + LM on the device
+    std::vector<QT> qs(items.size());
+    for (size_t k = 0; k < items.size(); ++k) qs[k] = fine[items[k].first][(size_t)items[k].second];
+    std::vector<m44> Ts(items.size());
+    std::vector<float> scs(items.size());
+    std::vector<int> nps(items.size());
+    verify_items_device(c, qs, g[0].planes, g[1].planes, dM, P, st0, Ts, scs, nps);
+    for (size_t k = 0; k < items.size(); ++k) {
+      TS& r = res[items[k].first][(size_t)items[k].second];
+      r.T = Ts[k];
+      r.score = scs[k];
+      r.score2 = 0.f;
+      npairs[items[k].first][(size_t)items[k].second] = nps[k];
+    }
+  } else {
+    c->pool.parallel_for((int)items.size(), [&](int k) {  // independent per candidate
+      const int t = items[k].first, i = items[k].second;
+      TS& r = res[t][i];
+      r.T = T_from_qt(fine[t][i]);
+      r.score = quick_verify(r.T, g[0].planes, g[1].planes, P, &npairs[t][i]);
+      r.score2 = 0.f;
+    });
+  }
   for (int t = 0; t < 3; ++t) {
     std::vector<float> fdump, qdump;
     for (size_t i = 0; i < fine[t].size(); ++i) {
@@ -1039,6 +1055,58 @@ void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t
         m = hd.next[m];
       }
     }
+  }
+}
+
+void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vector<Plane>& F1,
+                         const std::vector<Plane>& F2, const MatchIn* dM, const fccf_params& P, hipStream_t st,
+                         std::vector<m44>& T, std::vector<float>& score, std::vector<int>& npairs) {
+  const int n = (int)qs.size();
+  if (n == 0) return;
+  const size_t in_b = sizeof(QTd) * (size_t)n, out_b = (16 * 4 + 4 + 4 + 4) * (size_t)n;
+  c->arena_v.ensure(in_b + out_b + 8 * 256);  // (each take is 256-byte aligned)
+  c->arena_v.reset();
+  QTd* dq = c->arena_v.take_n<QTd>(n);
+  VerifyOut o;
+  o.T = c->arena_v.take_n<float>(16 * (size_t)n);
+  o.score = c->arena_v.take_n<float>(n);
+  o.npairs = c->arena_v.take_n<int32_t>(n);
+  o.status = c->arena_v.take_n<uint32_t>(n);
+  uint8_t* h = (uint8_t*)c->pinned.get(in_b + out_b);
+  QTd* hq = (QTd*)h;
+  for (int k = 0; k < n; ++k) hq[k] = {qs[k].qw, qs[k].qx, qs[k].qy, qs[k].qz, qs[k].tx, qs[k].ty, qs[k].tz, qs[k].alloc};
+  HIP_CHECK(hipMemcpyAsync(dq, hq, in_b, hipMemcpyHostToDevice, st));
+  // quick_verify's face-point sums (FCCF.cpp:688-697): float accumulation, int each step
+  int fs1 = 0, fs2 = 0;
+  for (const Plane& f : F1) fs1 = (int)((float)fs1 + f.fps);
+  for (const Plane& f : F2) fs2 = (int)((float)fs2 + f.fps);
+  VerifyIn in;
+  in.q = dq;
+  in.planes = dM;
+  in.fs12 = fs1 + fs2;
+  in.qcut = make_cut(P.quick_verify_angel_threshold);
+  in.dist_thr = P.quick_verify_distance_threshold;
+  in.required = P.required_optimize_plane;
+  verify_device(in, n, o, st);
+  HIP_CHECK(hipGetLastError());
+  float* hT = (float*)(h + in_b);
+  float* hs = hT + 16 * (size_t)n;
+  int32_t* hn = (int32_t*)(hs + n);
+  uint32_t* hst = (uint32_t*)(hn + n);
+  HIP_CHECK(hipMemcpyAsync(hT, o.T, 64 * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(hs, o.score, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(hn, o.npairs, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(hst, o.status, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  for (int k = 0; k < n; ++k) {
+    if (hst[k]) {  // an argument beyond the device reduction: this candidate on the host
+      T[k] = T_from_qt(qs[k]);
+      score[k] = quick_verify(T[k], F1, F2, P, &npairs[k]);
+      continue;
+    }
+    std::memcpy(&T[k].m[0][0], hT + 16 * (size_t)k, 64);
+    score[k] = hs[k];
+    npairs[k] = hn[k];
   }
 }
 

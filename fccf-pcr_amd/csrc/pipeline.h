@@ -3,6 +3,7 @@
 #include "ctx.h"
 #include "host_stages.h"
 #include "kernels.h"
+#include "match.h"
 
 namespace fccf {
 
@@ -65,6 +66,13 @@ inline FaceBufs face_bufs_carve(Arena& a, uint32_t cap) {
 // caller grows on the host).  Uses arena2 and c->pinned; synchronises st.
 void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t nv[2], const fccf_params& P,
                         hipStream_t st, std::vector<GroupOut> out[2]);
+
+// f1 (verify.hip): quick_verify + LM of the candidates qs on the device; dM holds the
+// F1/F2 tables (MatchIn, device).  Outputs per candidate: refined T, score, pairs.
+// Uses arena_v and c->pinned; synchronises st.
+void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vector<Plane>& F1,
+                         const std::vector<Plane>& F2, const MatchIn* dM, const fccf_params& P, hipStream_t st,
+                         std::vector<m44>& T, std::vector<float>& score, std::vector<int>& npairs);
 
 // Releases the per-CloudSet pipeline state (fccf_ctx_destroy).
 void pipeline_release(fccf_ctx* c);

@@ -72,6 +72,9 @@ _sig("fccf_ctx_create", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int)
 _sig("fccf_ctx_destroy", ctypes.c_int, _P)
 _sig("fccf_ctx_set_debug", ctypes.c_int, _P, ctypes.c_int)
 _sig("fccf_ctx_set_grow_device", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_ctx_set_lm_device", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_debug_sincos", ctypes.c_int, _P, _P, _I64, _P, _P, _P)
+_sig("fccf_stage_verify", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, _I64, ctypes.POINTER(Params), _P, _P, _P)
 _sig("fccf_ctx_last_error", ctypes.c_char_p, _P)
 _sig("fccf_register", ctypes.c_int, _P, _P, _I64, _P, _I64, ctypes.c_float, ctypes.POINTER(Params), _P,
      ctypes.POINTER(Stats))
@@ -175,6 +178,33 @@ class Ctx:
     def set_grow_device(self, on: bool = True):
         """Region growing (FCCF.cpp:536-648) on the GPU (K4) instead of the host."""
         _check(_lib.fccf_ctx_set_grow_device(self._h, int(bool(on))), "fccf_ctx_set_grow_device", self._h)
+
+    def sincos(self, x):
+        """Test hook: the device LM's correctly rounded sin/cos of float64 x: (s, c, ok)."""
+        a = np.ascontiguousarray(x, np.float64).reshape(-1)
+        s, c, ok = np.zeros(max(a.size, 1)), np.zeros(max(a.size, 1)), np.zeros(max(a.size, 1), np.uint32)
+        _check(_lib.fccf_debug_sincos(self._h, a.ctypes.data, a.size, s.ctypes.data, c.ctypes.data, ok.ctypes.data),
+               "fccf_debug_sincos", self._h)
+        return s[:a.size], c[:a.size], ok[:a.size].astype(bool)
+
+    def set_lm_device(self, on: bool = True):
+        """quick_verify + LM (FCCF.cpp:680-783, :210-249) on the GPU instead of the host."""
+        _check(_lib.fccf_ctx_set_lm_device(self._h, int(bool(on))), "fccf_ctx_set_lm_device", self._h)
+
+    def verify(self, F1, F2, qt, params: Params | None = None):
+        """quick_verify + LM of clustered candidates qt[n, 8] (fccf_stage_verify):
+        (T float32[n, 4, 4], score float32[n], npairs int32[n])."""
+        F1, F2 = np.ascontiguousarray(F1, PLANE_DTYPE), np.ascontiguousarray(F2, PLANE_DTYPE)
+        q = np.ascontiguousarray(np.asarray(qt, np.float32).reshape(-1, 8))
+        n = len(q)
+        T = np.zeros((max(n, 1), 16), np.float32)
+        sc = np.zeros(max(n, 1), np.float32)
+        npr = np.zeros(max(n, 1), np.int32)
+        p = params if params is not None else default_params()
+        _check(_lib.fccf_stage_verify(self._h, F1.ctypes.data, len(F1), F2.ctypes.data, len(F2), q.ctypes.data, n,
+                                      ctypes.byref(p), T.ctypes.data, sc.ctypes.data, npr.ctypes.data),
+               "fccf_stage_verify", self._h)
+        return T[:n].reshape(-1, 4, 4), sc[:n], npr[:n]
 
     def close(self):
         if self._h:

@@ -105,6 +105,11 @@ const char* fccf_ctx_last_error(fccf_ctx* ctx);
  * fccf_register* and fccf_stage_grow on this ctx; clouds with more planar voxels than
  * the kernel's LDS holds still grow on the host.  Off by default. */
 int fccf_ctx_set_grow_device(fccf_ctx* ctx, int on);
+/* quick_verify with its Ceres-style LM refinement (FCCF.cpp:680-783, :210-249; SURVEY
+ * §8(f) f1) on the GPU, one wave per candidate, all candidates in one launch, instead
+ * of the host pool: applies to fccf_register* and fccf_stage_verify on this ctx.  Off
+ * by default. */
+int fccf_ctx_set_lm_device(fccf_ctx* ctx, int on);
 /* Keep per-stage intermediates for fccf_debug_get (tests). Off by default. */
 int fccf_ctx_set_debug(fccf_ctx* ctx, int on);
 
@@ -219,6 +224,11 @@ int fccf_stage_cluster(fccf_ctx* ctx, const float* cand_rowmajor, int64_t n, int
  * scores[e] = score of S2 transformed by T_e against S1 over the fine_verify_voxel
  * octree (the voxel argument).  s1/s2: residual clouds (xyz float32, n1, n2 >= 1);
  * T_rowmajor: 16*E floats.  Bit-identical to the sequential reference arithmetic. */
+/* quick_verify + LM of n clustered candidates (8 floats each: qw qx qy qz tx ty tz
+ * allocated, as fccf_stage_cluster returns them) against the selected planes F1/F2:
+ * refined T (row-major, 16 per candidate), score and plane-pair count per candidate. */
+int fccf_stage_verify(fccf_ctx* ctx, const fccf_plane* F1, int nF1, const fccf_plane* F2, int nF2, const float* qt,
+                      int64_t n, const fccf_params* params, float* T_out, float* score, int32_t* npairs);
 int fccf_stage_fine_verify(fccf_ctx* ctx, const float* s1_xyz, int64_t n1, const float* s2_xyz, int64_t n2,
                            const float* T_rowmajor, int E, float voxel, float* scores);
 
@@ -243,6 +253,9 @@ int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exa
 /* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags,
  * [3] global partitions, [4] LDS segments, [5] workgroup partitions, [6] wave
  * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks. */
+/* Test hook: the device LM's correctly rounded double sin/cos (verify.hip); ok[i] = 0
+ * where |x| is beyond its argument reduction. */
+int fccf_debug_sincos(fccf_ctx* ctx, const double* x, int64_t n, double* s, double* c, uint32_t* ok);
 int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
 /* Forces a graph capture on one stream concurrent with another thread's wait on
  * an event last recorded on that stream (the pipelined batch's hazard, guarded by

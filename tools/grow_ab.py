@@ -1,5 +1,6 @@
-"""Dev probe: K4 growth on the host vs on the GPU (fccf_ctx_set_grow_device) at a
-config: median grow-stage ms, single-registration ms and pipelined ms per registration.
+"""Dev probe: host vs GPU forms of the serial stages at a config -- K4 growth
+(fccf_ctx_set_grow_device) and quick_verify + LM (fccf_ctx_set_lm_device): median
+grow / verify stage ms, single-registration ms and pipelined ms per registration.
 Usage: python tools/grow_ab.py [config] [reps]"""
 import os
 import statistics
@@ -18,20 +19,24 @@ src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
 ctx = F.Ctx(0)
 ds, dt = ctx.upload(src), ctx.upload(tar)
 ref = None
-for mode in (False, True, False, True):
-    ctx.set_grow_device(mode)
+MODES = [("host", False, False), ("grow_dev", True, False), ("lm_dev", False, True)] * 2
+for name, gdev, ldev in MODES:
+    ctx.set_grow_device(gdev)
+    ctx.set_lm_device(ldev)
     for _ in range(3):
         ctx.register_device(ds, len(src), dt, len(tar), cfg["leaf"])
-    g, e = [], []
+    g, e, v = [], [], []
     for _ in range(reps):
         a = time.perf_counter()
         T, st = ctx.register_device(ds, len(src), dt, len(tar), cfg["leaf"])
         e.append((time.perf_counter() - a) * 1e3)
         g.append(st.ms[2])
+        v.append(st.ms[6])
     ref = T if ref is None else ref
     assert np.array_equal(T.view(np.uint32), ref.view(np.uint32))
     a = time.perf_counter()
     ctx.register_batch([((ds, len(src)), (dt, len(tar)))] * reps, cfg["leaf"], on_device=True)
     pb = (time.perf_counter() - a) / reps * 1e3
-    print(f"grow_device={mode}: vox {st.vox1}/{st.vox2} grow {statistics.median(g):.4f} ms  "
+    print(f"{name:9s}: vox {st.vox1}/{st.vox2} lm {st.lm_solves} grow {statistics.median(g):.4f} ms  "
+          f"verify {statistics.median(v):.4f} ms  "
           f"e2e {statistics.median(e):.3f} ms  pipelined {pb:.3f} ms/reg", flush=True)
