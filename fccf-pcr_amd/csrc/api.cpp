@@ -246,8 +246,36 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
       HIP_CHECK(hipHostGetDevicePointer((void**)&dprog, prog, 0));
       b.is.prog = dprog;
     }
+    // FCCF_IS_TRACE_OUT=<path> (dev): per block item / wave task timestamps (IsBufs::trace)
+    static const char* tpath = std::getenv("FCCF_IS_TRACE_OUT");
+    unsigned long long* dtr = nullptr;
+    if (tpath) {
+      HIP_CHECK(hipMalloc((void**)&dtr, 64 * (size_t)b.is.taskmax));
+      HIP_CHECK(hipMemsetAsync(dtr, 0, 64 * (size_t)b.is.taskmax, st));
+      b.is.trace = dtr;
+    }
+    const auto tsort = std::chrono::steady_clock::now();
     introsort_u32(b.k0, b.v0, b.k1, b.v1, B2<const uint32_t*>(d_sc), B2<const VGParams*>(b.params), cap, b.is, st, 1,
                   exact_gate != 0);
+    if (tpath) {
+      std::vector<unsigned long long> h(8 * (size_t)b.is.taskmax);
+      uint32_t ctl[32];
+      HIP_CHECK(hipMemcpyAsync(h.data(), dtr, 64 * (size_t)b.is.taskmax, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipMemcpyAsync(ctl, b.is.ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+      (void)tsort;
+      if (FILE* f = std::fopen(tpath, "w")) {
+        std::fprintf(f, "kind start end size who\n");
+        for (uint32_t i = 0; i < std::min(ctl[24], b.is.taskmax); ++i)
+          std::fprintf(f, "B %llu %llu %llu %llu\n", h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]);
+        for (uint32_t i = 0; i < std::min(ctl[25], b.is.taskmax); ++i) {
+          const unsigned long long* r = &h[4 * ((size_t)b.is.taskmax + i)];
+          std::fprintf(f, "W %llu %llu %llu %llu\n", r[0], r[1], r[2], r[3]);
+        }
+        std::fclose(f);
+      }
+      (void)hipFree(dtr);
+    }
     HIP_CHECK(hipGetLastError());
     if (watch > 0) {
       const auto t0 = std::chrono::steady_clock::now();

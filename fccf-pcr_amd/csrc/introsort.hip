@@ -45,7 +45,10 @@ constexpr uint32_t IS_TILE = 2048;   // elements per round tile
 constexpr int IS_TT = 256;           // round kernels: threads per block
 constexpr int IS_TC = IS_TILE / IS_TT;  // 8 elements per thread
 constexpr uint32_t IS_LCAP = 8192;   // largest segment a block kernel workgroup holds in LDS
-constexpr int IS_OT = 1024;          // block kernel: threads per block (16 waves, one block per CU)
+#ifndef IS_OT_VAL
+#define IS_OT_VAL 1024
+#endif
+constexpr int IS_OT = IS_OT_VAL;     // block kernel: threads per block (16 waves, one block per CU)
 constexpr int IS_OW = IS_OT / 64;    // block kernel: waves
 constexpr int IS_OC = IS_LCAP / IS_OT;  // 8 elements per thread in a workgroup partition
 constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a workgroup partition
@@ -1172,6 +1175,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       buf = o.buf;
     }
     if (l <= f) continue;
+    const unsigned long long t_item = W.trace ? wall_clock64() : 0ull;
     uint32_t* K = buf ? K1 : K0;  // selects: a dynamically indexed local array lives in scratch
     uint32_t* V = buf ? V1 : V0;
     if (threadIdx.x == 0) {
@@ -1224,6 +1228,16 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
         __syncthreads();
       }
     }
+    if (W.trace && threadIdx.x == 0) {  // dev: item timestamps (fccf_debug_sort_keys, FCCF_IS_TRACE_OUT)
+      const uint32_t slot = atomicAdd(&W.ctl[24], 1u);
+      if (slot < W.taskmax) {
+        unsigned long long* r = W.trace + 4 * (size_t)slot;
+        r[0] = t_item;
+        r[1] = wall_clock64();
+        r[2] = l - f;
+        r[3] = blockIdx.x;
+      }
+    }
   }
   if (threadIdx.x == 0 && units) atomicAdd(&W.ctl[20], units);
 }
@@ -1265,6 +1279,7 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
     }
     if (lane < IS_WCAP / 32) S.heads[lane] = 0;
     wsync();
+    const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
     wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
     wsync();
 #pragma unroll
@@ -1292,6 +1307,16 @@ __global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_
       V[f + a + rank] = S.v[p];
     }
     wsync();
+    if (W.trace && lane == 0) {
+      const uint32_t slot = atomicAdd(&W.ctl[25], 1u);
+      if (slot < W.taskmax) {
+        unsigned long long* r = W.trace + 4 * ((size_t)W.taskmax + slot);
+        r[0] = t_task;
+        r[1] = wall_clock64();
+        r[2] = n;
+        r[3] = blockIdx.x * (IS_WT / 64) + w;
+      }
+    }
   }
   if (S.son && lane == 0) {
     atomicAdd(&W.ctl[6], S.lstat[2]);
@@ -1359,6 +1384,7 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.taskmax = cap / 16 + 64;
   b.tasks = (uint4*)take(sizeof(uint4) * (size_t)b.taskmax);
   b.prog = nullptr;
+  b.trace = nullptr;
   b.tier = introsort_tier();
   b.stats = 0;
   return b;

@@ -58,6 +58,8 @@ struct IsBufs {
   IsOwn* own;           // ownmax
   uint4* tasks;         // wave tasks {f, n, depth, -} (count in ctl[16])
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
+  unsigned long long* trace;  // dev (null = off): per block item / wave task {start, end, size, who},
+                              // block records from 0 (count in ctl[24]), wave records from taskmax (ctl[25])
   uint32_t segmax, maxtiles, ownmax, taskmax;
   uint32_t tier;        // rounds split segments longer than this (<= the owner's LDS capacity)
   uint32_t stats;       // path counters in ctl[3..15] (debug sorts; each costs a global atomic)

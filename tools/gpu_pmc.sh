@@ -11,5 +11,5 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d $OUT/fet
 echo "fetch pass ok"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d $OUT/write -o run -- python3 -u bench.py --no-cpu-baseline --steps 5 --warmup 2 > $OUT/write.json 2> $OUT/write.err
 echo "write pass ok"
-python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json && python3 -c "import json,sys; p=sys.argv[1]; d=json.load(open(p)); d[\"config\"]=\"c3\"; json.dump(d,open(p,\"w\"),indent=1)" $OUT/pmc_traffic.json
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json ${PMC_MIN_FRAC:-0.05} && python3 -c "import json,sys; p=sys.argv[1]; d=json.load(open(p)); d[\"config\"]=\"c3\"; json.dump(d,open(p,\"w\"),indent=1)" $OUT/pmc_traffic.json
 cat $OUT/pmc_traffic.json
