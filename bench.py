@@ -375,11 +375,13 @@ def main():
         assert np.array_equal(T1.view(np.uint32), np.asarray(T).view(np.uint32)), "pipelined result differs"
     # PCIe-inclusive latency: the same registration from host arrays (fccf_register);
     # informational, never `value`
-    per_host = []
+    per_host, h2d = [], []
     for _ in range(min(args.steps, 5)):
         a = time.perf_counter()
-        T2, _ = ctx.register(src, tar, leaf)
+        T2, st2 = ctx.register(src, tar, leaf)
         per_host.append(time.perf_counter() - a)
+        if not args.selftest:
+            h2d.append(st2.as_dict()["ms"]["h2d"])
     if not args.selftest:
         assert np.array_equal(T2.view(np.uint32), np.asarray(T).view(np.uint32)), "host-input result differs"
     ingest = None if args.selftest or rank != 0 else ingest_pass(F, ctx, src, tar, leaf, T)
@@ -427,6 +429,7 @@ def main():
                        "host_threads_per_rank": int(os.environ.get("FCCF_HOST_THREADS", "0")) or None},
             "e2e_ms_median": statistics.median(per) * 1e3,  # one registration alone (latency)
             "e2e_host_input_ms_median": statistics.median(per_host) * 1e3,  # incl. H2D of both clouds
+            "h2d_ms_median": statistics.median(h2d) if h2d else None,  # that copy alone (copy-stream events)
             "ref_window_ms_median": statistics.median(ref_win) if ref_win else None,
             "device_ms": {k: round(v, 4) for k, v in st1.as_dict()["dev_ms"].items()} if not args.selftest else None,
             "K_per_registration": int(st.K),

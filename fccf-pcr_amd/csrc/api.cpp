@@ -70,7 +70,7 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   for (auto& cs : c->cs) {
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (auto& e : cs.tev) ok = ok && hipEventCreate(&e) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&cs.ev_in, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreate(&cs.ev_in0) == hipSuccess && hipEventCreate(&cs.ev_in) == hipSuccess;
   }
   if (!ok) {
     fccf_ctx_destroy(c);
@@ -95,6 +95,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
     for (auto& e : cs.tev)
       if (e) (void)hipEventDestroy(e);
     if (cs.ev_in) (void)hipEventDestroy(cs.ev_in);
+    if (cs.ev_in0) (void)hipEventDestroy(cs.ev_in0);
   }
   for (auto& s : c->sa)
     if (s) (void)hipStreamDestroy(s);

@@ -227,7 +227,7 @@ struct fccf_ctx {
     fccf::Arena arena;
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
     fccf::Arena inarena;             // staged host inputs of the pair on this set (copy stream)
-    hipEvent_t ev_in = nullptr;      // their copies done
+    hipEvent_t ev_in0 = nullptr, ev_in = nullptr;  // their copies started / done (timing: fccf_stats h2d)
     hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
                                      // [4] clouds done, [5] S1 replay done
     hipEvent_t tev[6] = {};          // timing: cloud start, pass 1 done, pass 2 done, faces done,

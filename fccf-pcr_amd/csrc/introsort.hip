@@ -945,9 +945,7 @@ __device__ __forceinline__ uint32_t block_partition(BlockLds& S, uint32_t f, uin
   __syncthreads();
   if (w == 0) block_chunk_scan(S, 0u, 0u);
   __syncthreads();
-  if (threadIdx.x == 0) S.bc[5] = S.pl[IS_OE - 1] + S.cl[IS_OE - 1];
-  __syncthreads();
-  const uint32_t le_tot = S.bc[5];
+  const uint32_t le_tot = S.pl[IS_OE - 1] + S.cl[IS_OE - 1];  // read by every thread after the scan's barrier
   uint32_t cut = IS_NONE;
   uint32_t sw[C];  // swap rank as >= (low 16 bits) / as <= (high 16), later the <= destination
 #pragma unroll
@@ -986,9 +984,9 @@ __device__ __forceinline__ uint32_t block_partition(BlockLds& S, uint32_t f, uin
     }
   }
   __syncthreads();
-  const uint32_t r = min(max(S.bc[4], f + 1), l - 1);
-  __syncthreads();
-  return r;
+  // (S.bc[4] is reset only by the next partition's thread 0, after the caller's
+  // barrier that follows its stack update, so no barrier is needed after this read)
+  return min(max(S.bc[4], f + 1), l - 1);
 }
 
 // The segment [f, f+len) (len <= IS_LCAP, depth d) from (Ki, Vi): workgroup
@@ -1015,8 +1013,9 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
       S.bc[0] = 1;
     }
   }
-  __syncthreads();
-  for (;;) {
+  // thread 0 pops the stack until it finds a subtree to partition (leaves, heap
+  // ranges and wave tasks are settled on the way); S.bc[3] = found
+  auto pop = [&]() {
     if (threadIdx.x == 0) {
       uint32_t go = 0;
       while (S.bc[0] > 0 && !go) {
@@ -1050,7 +1049,10 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
       }
       S.bc[3] = go;
     }
-    __syncthreads();
+  };
+  pop();
+  __syncthreads();
+  for (;;) {
     if (!S.bc[3]) break;
     const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
     const int dd = (int)(S.bc[7] >> 16);
@@ -1060,11 +1062,12 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     else if (n <= 4 * IS_OT) c = block_partition<4>(S, off, off + n);
     else if (n <= 8 * IS_OT) c = block_partition<8>(S, off, off + n);
     else c = block_partition<IS_OC>(S, off, off + n);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // push both children, then pop the next subtree: one barrier
       const uint32_t nd = (uint32_t)(dd - 1) << 16;
       S.wstk[S.bc[0]++] = make_uint2(c, (off + n - c) | nd);
       S.wstk[S.bc[0]++] = make_uint2(off, (c - off) | nd);
     }
+    pop();
     __syncthreads();
   }
   // the segment's wave tasks into the global list: one slot reservation per class

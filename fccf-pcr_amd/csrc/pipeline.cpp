@@ -333,6 +333,7 @@ struct PipeSet {
   float* cen = nullptr;  // both cloud centroids: cloud k at cen[3k .. 3k+2]
   XsBufs xs;             // their exact-sum scratch (6 rows)
   VGEntry entry;         // arguments of pass 1's entry kernel, patched into g_seg[0] per call
+  bool staged = false;   // host inputs copied by stage_inputs (ev_in0 .. ev_in time the H2D)
   clk::time_point t_enq;
 };
 
@@ -359,6 +360,7 @@ Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   float* ds = cs.inarena.take_n<float>(3 * (size_t)n_src);
   hipStream_t su = c->ingest.su;
   guarded_stream_wait(su, cs.ev[0]);
+  HIP_CHECK(hipEventRecord(cs.ev_in0, su));
   if (n_tar) HIP_CHECK(hipMemcpyAsync(dt, tar, 12 * (size_t)n_tar, hipMemcpyHostToDevice, su));
   if (n_src) HIP_CHECK(hipMemcpyAsync(ds, src, 12 * (size_t)n_src, hipMemcpyHostToDevice, su));
   HIP_CHECK(hipEventRecord(cs.ev_in, su));
@@ -402,6 +404,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     xin[k] = hin[k];
   }
   // host inputs: staged by stage_inputs() into cs.inarena on the copy stream
+  ps.staged = staged;
   if (staged) HIP_CHECK(hipStreamWaitEvent(st0, cs.ev_in, 0));
   struct {
     const void* base;
@@ -489,6 +492,9 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     for (int i = 0; i < 3; ++i) S.dev_ms[i] = d[i];
     S.ms[FCCF_T_DOWNSAMPLE] = d[0] + d[1];
     S.ms[FCCF_T_VOXELFIT] = d[2];
+    float h = 0.f;  // the staged host inputs' copy (complete before pass 1 started)
+    if (ps.staged) HIP_CHECK(hipEventElapsedTime(&h, c->cs[s].ev_in0, c->cs[s].ev_in));
+    S.ms[FCCF_T_H2D] = h;
   }
   S.m1_tar = sc[0][1];
   S.m1_src = sc[1][1];

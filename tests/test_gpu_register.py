@@ -240,3 +240,18 @@ def test_nonfinite_points_through_overflow_passthrough(ctx, oracle, fccf):
     T, _ = ctx.register(src2, tar, 0.1)
     compare_all(ctx, run)
     np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
+
+
+def test_stats_time_the_host_input_copy(ctx, fccf):
+    """fccf_stats.ms[h2d] is the staged copy of host inputs (0 for device-resident clouds)."""
+    src, tar, _ = fccf.synth_pair(200_000)
+    _, st = ctx.register(src, tar, 0.1)
+    d = st.as_dict()["ms"]
+    assert d["h2d"] > 0 and d["voxelfit"] > 0 and d["select"] > 0
+    ds, dt = ctx.upload(src), ctx.upload(tar)
+    try:
+        _, st2 = ctx.register_device(ds, len(src), dt, len(tar), 0.1)
+    finally:
+        ctx.free(ds)
+        ctx.free(dt)
+    assert st2.as_dict()["ms"]["h2d"] == 0.0
