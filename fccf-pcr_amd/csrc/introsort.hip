@@ -1339,7 +1339,10 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
 
 // Every wave takes its share of the wave tasks: the subtree in its LDS slice,
 // finished and stably leaf-sorted, written back in place in buffer 0.
-__global__ void __launch_bounds__(IS_WT) k_is_wave(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<IsBufs> W2) {
+#ifndef IS_WAVE_LB
+#define IS_WAVE_LB 4  // 4 waves per SIMD: 128 VGPRs, no spill (1.19 vs 1.21 ms pipelined, profiles/r02j)
+#endif
+__global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<IsBufs> W2) {
   KT();
   __shared__ WaveLds WL[IS_WT / 64];
   const int e = blockIdx.y;
