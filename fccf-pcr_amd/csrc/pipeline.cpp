@@ -475,8 +475,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
   c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
-  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));  // (no enqueue is in flight on the helper here)
-  HIP_CHECK(hipStreamWaitEvent(st0, c->cs[s].ev[4], 0));
+  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+  guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
   std::memcpy(fsc, cm.fsc, sizeof fsc);
