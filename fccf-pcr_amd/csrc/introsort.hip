@@ -228,75 +228,14 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
 }
 
 // ---------------------------------------------------------------- rounds
-// k_is_plan (one block per cloud): this round's large segments -- the children of the
-// previous round's, or the root -- with their pivots (__move_median_to_first applied
-// to the round's input), tile ranges and the tile -> segment map; small children go
-// to the owned list.  The tile kernels then read one descriptor each instead of
-// rebuilding the table (their dependent-load chains set the round's latency).
-// Dynamic LDS: 4 * segmax u32.
-__global__ void __launch_bounds__(1024) k_is_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2, B2<IsBufs> W2, int r) {
-  KT();
-  extern __shared__ uint32_t dyn[];
-  __shared__ uint32_t sh[16];
-  const int e = blockIdx.y;
-  const IsBufs W = W2[e];
-  const uint32_t nsort = W.ctl[0];
-  uint32_t* tf = dyn;
-  uint32_t* tl = tf + W.segmax;
-  int32_t* td = (int32_t*)(tl + W.segmax);
-  uint32_t* t0 = (uint32_t*)(td + W.segmax);
-  const uint32_t nch = nchildren(W, r);
-  const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
-  uint32_t nseg = 0, ntiles = 0, nown = 0;
-  for (uint32_t b = 0; b < nch; b += blockDim.x) {
-    const uint32_t i = b + threadIdx.x;
-    Child c = {0u, 0u, 0};
-    if (i < nch) c = child_of(W, r, nsort, i);
-    const bool lg = i < nch && is_large(c, W.tier);
-    const bool ow = i < nch && !lg && c.l > c.f;
-    const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
-    uint32_t s_lg, s_nt, s_ow;
-    const uint32_t p_lg = block_excl_scan(lg ? 1u : 0u, sh, &s_lg);
-    const uint32_t p_nt = block_excl_scan(nt, sh, &s_nt);
-    const uint32_t p_ow = block_excl_scan(ow ? 1u : 0u, sh, &s_ow);
-    if (lg) {
-      tf[nseg + p_lg] = c.f;
-      tl[nseg + p_lg] = c.l;
-      td[nseg + p_lg] = c.d;
-      t0[nseg + p_lg] = ntiles + p_nt;
-    }
-    if (ow) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
-    nseg += s_lg;
-    ntiles += s_nt;
-    nown += s_ow;
-  }
-  __syncthreads();
-  const uint32_t* __restrict__ K = K2[e];
-  const uint32_t* __restrict__ V = V2[e];
-  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) {
-    const uint32_t f = tf[j], l = tl[j];
-    const uint32_t m = median_pos(K, f, l);
-    W.segs[(size_t)r * W.segmax + j] = IsSeg{f, l, td[j], t0[j], m, K[m], K[f], V[f], V[m]};
-    W.cuts[(size_t)r * W.segmax + j] = l;
-  }
-  for (uint32_t t = threadIdx.x; t < W.maxtiles; t += blockDim.x)
-    W.tseg[t] = t < ntiles ? upper_index(t0, nseg, t) : IS_NONE;
-  uint32_t ne = 0;  // elements partitioned this round (the scatter probe's unit count)
-  for (uint32_t j = threadIdx.x; j < nseg; j += blockDim.x) ne += tl[j] - tf[j];
-  uint32_t ne_tot;
-  (void)block_excl_scan(ne, sh, &ne_tot);
-  if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, ne_tot};
-}
-
-// Per-tile ge/le counts against the segment's pivot and the tile-local position
-// lists (offsets from the tile start, in position order).  With the plan folded in
-// (k_is_count_plan), every workgroup first derives the round's segment table itself
+// k_is_count_plan: the round's plan, then per-tile ge/le counts against the segment's
+// pivot and the tile-local position lists (offsets from the tile start, in position
+// order).  Every workgroup first derives the round's segment table itself
 // from the previous round's segments and cuts (a few hundred entries, in LDS): the
 // workgroup of a segment's first tile publishes its IsSeg and initial cut, every
-// workgroup its tile's tseg entry, workgroup 0 the owned list and the IsRound; the
-// scatter reads them after the kernel boundary.  This removes the single-workgroup
-// plan kernel (and its dependent launch) from every round.
-template <bool PLAN>
+// workgroup its tile's descriptor (IsTile), workgroup 0 the owned list of small
+// children and the IsRound; the scatter reads them after the kernel boundary.  (A
+// separate single-workgroup plan kernel per round cost 0.07 ms per registration.)
 __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
                                               const IsBufs& W, int r, uint32_t* dyn) {
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
@@ -304,7 +243,7 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
   const uint32_t t = blockIdx.x;
   uint32_t j, f, l, m, P, kf;
   uint32_t tile0;
-  if (PLAN) {
+  {
     const uint32_t nsort = W.ctl[0];
     uint32_t* tf = dyn;
     uint32_t* tl = tf + W.segmax;
@@ -344,7 +283,10 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
       if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, ne_tot};
     }
     if (t >= ntiles) {
-      if (threadIdx.x == 0 && t < W.maxtiles) W.tseg[t] = IS_NONE;
+      if (threadIdx.x == 0 && t < W.maxtiles) {
+        W.tseg[t] = IS_NONE;
+        W.tdesc[t].j = IS_NONE;
+      }
       return;
     }
     j = upper_index(t0, nseg, t);
@@ -356,9 +298,11 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
       bsh[0] = m;
       bsh[1] = K[m];
       bsh[2] = K[f];
+      const IsSeg rec{f, l, td[j], tile0, m, bsh[1], bsh[2], V[f], V[m]};
       W.tseg[t] = j;
+      W.tdesc[t] = IsTile{j, rec};  // the scatter's one-load view of this tile's segment
       if (t == tile0) {  // the segment's record, once
-        W.segs[(size_t)r * W.segmax + j] = IsSeg{f, l, td[j], tile0, m, bsh[1], bsh[2], V[f], V[m]};
+        W.segs[(size_t)r * W.segmax + j] = rec;
         W.cuts[(size_t)r * W.segmax + j] = l;
       }
     }
@@ -366,16 +310,6 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
     m = bsh[0];
     P = bsh[1];
     kf = bsh[2];
-  } else {
-    j = W.tseg[t];
-    if (j == IS_NONE) return;
-    const IsSeg sg = W.segs[(size_t)r * W.segmax + j];
-    f = sg.f;
-    l = sg.l;
-    m = sg.m;
-    P = sg.P;
-    kf = sg.kf;
-    tile0 = sg.tile0;
   }
   const uint32_t i = t - tile0;
   const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
@@ -426,19 +360,13 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
   }
 }
 
-__global__ void __launch_bounds__(IS_TT) k_is_count(B2<const uint32_t*> K2, B2<IsBufs> W2, int r) {
-  KT();
-  const int e = blockIdx.y;
-  is_count_body<false>(K2[e], nullptr, W2[e], r, nullptr);
-}
-
 // Dynamic LDS: 4 * segmax u32 (the round's segment table).
 __global__ void __launch_bounds__(IS_TT) k_is_count_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
                                                          B2<IsBufs> W2, int r) {
   KT();
   extern __shared__ uint32_t dyn[];
   const int e = blockIdx.y;
-  is_count_body<true>(K2[e], V2[e], W2[e], r, dyn);
+  is_count_body(K2[e], V2[e], W2[e], r, dyn);
 }
 
 // Every element of the round's large segments to its place after the partition,
@@ -453,9 +381,10 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
   const uint32_t t = blockIdx.x;
-  const uint32_t j = W.tseg[t];
+  const IsTile td = W.tdesc[t];
+  const uint32_t j = td.j;
   if (j == IS_NONE) return;
-  const IsSeg s = W.segs[(size_t)r * W.segmax + j];
+  const IsSeg s = td.s;
   const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0, m = s.m, P = s.P;
   uint32_t* preg = dyn;
   uint32_t* prel = preg + W.maxtiles;
@@ -1455,7 +1384,7 @@ int introsort_rounds(uint32_t cap) {
 size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
-  return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
+  return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + sizeof(IsTile) * mt + 256 + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
          (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 8 * 256;
 }
 
@@ -1473,6 +1402,7 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.ctl = (uint32_t*)take(256);
   b.cnt = (uint32_t*)take(8 * (size_t)b.maxtiles);
   b.tseg = (uint32_t*)take(4 * (size_t)b.maxtiles);
+  b.tdesc = (IsTile*)take(sizeof(IsTile) * (size_t)b.maxtiles);
   b.gel = (uint16_t*)take(2 * ((size_t)cap + 64));
   b.lel = (uint16_t*)take(2 * ((size_t)cap + 64));
   b.rounds = (IsRound*)take(sizeof(IsRound) * IS_RMAX);
@@ -1504,18 +1434,8 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   for (int r = 0; r < R; ++r) {
     const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
-    static const bool sep_plan = [] {  // dev: FCCF_IS_PLAN=1 keeps the separate plan kernel (A/B)
-      const char* e = std::getenv("FCCF_IS_PLAN");
-      return e && e[0] == '1';
-    }();
-    if (sep_plan) {
-      k_is_plan<<<dim3(1, nbatch), 1024, lds_plan, st>>>(B2<const uint32_t*>(ki), B2<const uint32_t*>(vi), b, r);
-      step("plan", r);
-      k_is_count<<<dim3(maxtiles, nbatch), IS_TT, 0, st>>>(B2<const uint32_t*>(ki), b, r);
-    } else {
-      k_is_count_plan<<<dim3(maxtiles, nbatch), IS_TT, lds_plan, st>>>(B2<const uint32_t*>(ki),
-                                                                      B2<const uint32_t*>(vi), b, r);
-    }
+    k_is_count_plan<<<dim3(maxtiles, nbatch), IS_TT, lds_plan, st>>>(B2<const uint32_t*>(ki),
+                                                                    B2<const uint32_t*>(vi), b, r);
     step("count", r);
     // algorithmic bytes: key + value read and written, plus a 2-byte list entry
     FCCF_LAUNCH("k_is_scatter",

@@ -40,6 +40,10 @@ struct IsSeg {
   uint32_t tile0;
   uint32_t m, P, kf, vf, vm;  // median position, pivot key, the first element, the median's value
 };
+struct IsTile {  // a round tile's segment (j = IS_NONE past the round's tiles): one load for the scatter
+  uint32_t j;
+  IsSeg s;
+};
 struct IsOwn {
   uint32_t f, l;
   int32_t depth;
@@ -51,6 +55,7 @@ struct IsBufs {
                         // (stored from the end), [19]/[20] wave/block probe unit counts
   uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
   uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles)
+  IsTile* tdesc;        // per round tile: its segment and the segment's record (the scatter's input)
   uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
   IsRound* rounds;      // IS_RMAX
   IsSeg* segs;          // IS_RMAX x segmax
