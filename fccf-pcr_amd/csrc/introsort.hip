@@ -52,7 +52,10 @@ constexpr int IS_OT = IS_OT_VAL;     // block kernel: threads per block (16 wave
 constexpr int IS_OW = IS_OT / 64;    // block kernel: waves
 constexpr int IS_OC = IS_LCAP / IS_OT;  // 8 elements per thread in a workgroup partition
 constexpr uint32_t IS_OE = IS_OC * IS_OW;  // (chunk, wave) count entries of a workgroup partition
-constexpr uint32_t IS_WCAP = 512;    // largest subtree finished by one wave (wave kernel)
+#ifndef IS_WCAP_VAL
+#define IS_WCAP_VAL 512
+#endif
+constexpr uint32_t IS_WCAP = IS_WCAP_VAL;  // largest subtree finished by one wave (wave kernel)
 constexpr int IS_WC = IS_WCAP / 64;  // 8 elements per lane
 constexpr int IS_WT = 256;           // wave kernel: threads per block
 constexpr uint32_t IS_TASK_BIG = 128;  // wave tasks above this are dequeued first
@@ -524,13 +527,13 @@ struct BlockLds {
   uint32_t sh[16];
   uint32_t* stat;                   // IsBufs::ctl
   uint32_t son;                     // path counters on (IS_STATS && IsBufs::stats)
-  // wave tasks of the current segment, packed off | n << 13 | depth << 23, handed
+  // wave tasks of the current segment, packed off | n << 13 | depth << 24, handed
   // to the global list with one atomic per class when the segment is done
   uint32_t tb[IS_LCAP / (IS_TASK_BIG + 1) + 1];  // > IS_TASK_BIG elements
   uint32_t ts[IS_LCAP / (IS_THRESHOLD + 1) + 1];  // the rest
   uint32_t ntb, nts, units;
 };
-static_assert(IS_LCAP <= 8192 && IS_WCAP < 1024, "task packing: 13-bit offsets, 10-bit sizes");
+static_assert(IS_LCAP <= 8192 && IS_WCAP <= 1024, "task packing: 13-bit offsets, 11-bit sizes, 8-bit depths");
 
 // One wave's slice of the wave kernel
 struct WaveLds {
@@ -832,6 +835,7 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
     uint32_t c;
     if (n <= 128) c = wave_partition<2, SL>(S, f, f + n, xch);
     else if (n <= 256) c = wave_partition<4, SL>(S, f, f + n, xch);
+    else if (IS_WC <= 8 || n <= 512) c = wave_partition<(IS_WC < 8 ? IS_WC : 8), SL>(S, f, f + n, xch);
     else c = wave_partition<IS_WC, SL>(S, f, f + n, xch);
     stk[sp++] = wpack(c, f + n - c, dd - 1);
     stk[sp++] = wpack(f, c - f, dd - 1);
@@ -959,7 +963,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
           for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
         } else if (n <= IS_WCAP) {  // a wave task: large ones from the front, small from the back
           S.units += n;  // the wave probe's unit count
-          const uint32_t pk = off | (n << 13) | ((uint32_t)dd << 23);
+          const uint32_t pk = off | (n << 13) | ((uint32_t)dd << 24);
           if (n > IS_TASK_BIG) S.tb[S.ntb++] = pk;
           else S.ts[S.nts++] = pk;
           for (uint32_t q = off; q < off + n; q += 32 - (q & 31)) {
@@ -1009,7 +1013,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
   for (uint32_t i = threadIdx.x; i < S.ntb + S.nts; i += IS_OT) {
     const bool big = i < S.ntb;
     const uint32_t pk = big ? S.tb[i] : S.ts[i - S.ntb];
-    const uint4 t = make_uint4(f + (pk & 0x1FFFu), (pk >> 13) & 0x3FFu, pk >> 23, 0u);
+    const uint4 t = make_uint4(f + (pk & 0x1FFFu), (pk >> 13) & 0x7FFu, pk >> 24, 0u);
     if (big) W.tasks[S.bc[1] + i] = t;
     else W.tasks[W.taskmax - 1u - (S.bc[2] + i - S.ntb)] = t;
   }
