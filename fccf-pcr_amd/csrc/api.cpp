@@ -14,6 +14,7 @@
 #include "host_stages.h"
 #include "kernels.h"
 #include "match.h"
+#include "mail.h"
 #include "pipeline.h"
 
 using namespace fccf;
@@ -113,6 +114,12 @@ extern "C" int fccf_ctx_set_grow_device(fccf_ctx* c, int on) {
 extern "C" int fccf_ctx_set_lm_device(fccf_ctx* c, int on) {
   if (!c) return FCCF_E_ARG;
   c->lm_device = on != 0;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_ctx_set_cluster_device(fccf_ctx* c, int on) {
+  if (!c) return FCCF_E_ARG;
+  c->cluster_device = on != 0;
   return FCCF_OK;
 }
 
@@ -726,7 +733,40 @@ extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int
       in[i].alloc = 0;
     }
     int64_t ncl = 0;
-    transform_cluster(in, out, cluster_num, P, &ncl, &c->pool, nullptr);
+    bool done = false;
+    if (c->cluster_device && n > 0) {  // f3: radius search, seeds, sort and averaging on the device
+      hipStream_t st = c->sb;
+      MatchMail* mm = match_mail(c);
+      const size_t nn = (size_t)n;
+      c->arena2.ensure(sizeof(QTd) * nn + sizeof(uint64_t) * MatchMail::CB_CAP + 15 * 4 * nn + (1 << 16));
+      c->arena2.reset();
+      QTd* dq0 = c->arena2.take_n<QTd>(nn);
+      uint32_t* dtot = c->arena2.take_n<uint32_t>(4);
+      uint64_t* drows = c->arena2.take_n<uint64_t>(MatchMail::CB_CAP);
+      QTd* const dq[3] = {dq0, dq0, dq0};
+      uint8_t* h = (uint8_t*)c->pinned.get(sizeof(QTd) * nn + 16);
+      QTd* hq = (QTd*)h;
+      for (size_t i = 0; i < nn; ++i) hq[i] = {in[i].qw, in[i].qx, in[i].qy, in[i].qz, in[i].tx, in[i].ty, in[i].tz, 0u};
+      uint32_t* ht = (uint32_t*)(h + sizeof(QTd) * nn);
+      ht[0] = (uint32_t)n;
+      ht[1] = ht[2] = ht[3] = 0;
+      HIP_CHECK(hipMemcpyAsync(dq0, hq, sizeof(QTd) * nn, hipMemcpyHostToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(dtot, ht, 16, hipMemcpyHostToDevice, st));
+      const float r2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
+      cluster_bits(dq, dtot, r2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, mm, st, drows);
+      cluster_launch(c, dq, dtot, drows, nn, P, mm, st, &cluster_num);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipStreamSynchronize(st));
+      if (mm->cl_stat[0][0] == 0) {
+        out = cluster_results(*mm, 0);
+        ncl = (int64_t)mm->cl_stat[0][1];
+        done = true;
+      } else if (nn * ((nn + 63) / 64) <= MatchMail::CB_CAP && !((float)n <= P.cluster_number_threshold)) {
+        transform_cluster(in, out, cluster_num, P, &ncl, &c->pool, mm->cbits);  // past the kernels' capacities
+        done = true;
+      }
+    }
+    if (!done) transform_cluster(in, out, cluster_num, P, &ncl, &c->pool, nullptr);
     *n_fine = (int64_t)out.size();
     if (n_clusters) *n_clusters = ncl;
     for (int64_t i = 0; i < std::min(*n_fine, cap); ++i) {

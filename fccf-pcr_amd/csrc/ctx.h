@@ -252,6 +252,7 @@ struct fccf_ctx {
   bool debug = false;
   bool grow_device = false;  // K4 region growing on the GPU (grow.hip) instead of the host
   bool lm_device = false;    // quick_verify + LM on the GPU (verify.hip) instead of the host pool
+  bool cluster_device = false;  // transform_cluster's seeds, sort and averaging on the GPU (cluster.hip)
   fccf::Arena arena_v;       // device quick_verify batch (candidates in, refined T / scores out)
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   std::map<std::string, std::vector<uint8_t>> dbg;

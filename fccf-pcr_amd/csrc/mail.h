@@ -32,6 +32,11 @@ struct MatchMail {
   // (W_t = ceil(n_t / 64)) at word offset sum_{t' < t} n_t' W_t'; written only when
   // all types fit CB_CAP and cbits_on.
   uint64_t cbits[CB_CAP];
+  // device clustering (cluster.hip): per type status, clusters, emitted, cluster_num;
+  // the averaged clusters in emission order
+  static constexpr uint32_t CL_FCAP = 1024;
+  uint32_t cl_stat[3][4];
+  QTd cl_fine[3][CL_FCAP];
 };
 
 struct FineMail {

@@ -31,6 +31,32 @@ struct MatchMail;
 void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, uint32_t* off, uint32_t* totals,
                       MCand* c[3], QTd* q[3], hipStream_t st, MatchMail* mail = nullptr);
 
+// ------------------------------------------------ f3: transform_cluster on the device (cluster.hip)
+// Everything is derived on the device from the totals, so the launches go into the
+// match stage's stream before its one host sync.  Results land in the mailbox
+// (MatchMail::cl_stat / cl_fine); a type whose status is not 0 is redone by the host.
+struct ClusterIn {
+  const QTd* q[3];           // candidates per type
+  const uint64_t* rows;      // k_cluster_bits's neighbour rows in HBM (MatchMail::cbits layout)
+  const uint32_t* totals;    // candidates per type
+  uint32_t cb_cap;           // row words present only when all types fit (MatchMail::CB_CAP)
+  float min_n;               // cluster_number_threshold: n <= min_n is not clustered (host)
+  float sel;                 // seclct_cluster_number (cluster_num, :1458)
+  int32_t cnum_given;        // has_cnum: every type's cluster_num is this instead (fccf_stage_cluster)
+  uint32_t has_cnum;
+};
+struct ClusterOut {
+  uint32_t *cseed[3], *csize[3];  // clusters in creation order
+  uint32_t *bx[3], *bid[3];       // range_cluster's working array
+  uint32_t* emit[3];              // averaged clusters in emission order
+  uint32_t cap;                   // entries of each of those per type (>= the type's candidates)
+  uint32_t* stat;                 // 4 per type: status, clusters, emitted, cluster_num
+  QTd* fine;                      // fcap per type: the averages in emission order
+  uint32_t fcap;
+  uint32_t egrid;                 // averaging waves launched per type (<= fcap); cluster_num + 1 must fit
+};
+void cluster_device(const ClusterIn& in, const ClusterOut& out, hipStream_t st);
+
 // ------------------------------------------------ f1: quick_verify + LM on the device (verify.hip)
 struct VerifyIn {
   const QTd* q;           // candidate transforms as quaternion records, all types concatenated
@@ -72,9 +98,10 @@ struct FineBufs {
 };
 // s1_state: octree bounds after inserting S1 alone (octree_replay, run ahead of time).
 // transform_cluster neighbour bitmasks of the three candidate lists into mail->cbits
-// (layout in mail.h); types with <= min_n candidates are skipped (not clustered).
+// (layout in mail.h) and, when dev_rows is not null, the same words into dev_rows
+// (device clustering); types with <= min_n candidates are skipped (not clustered).
 void cluster_bits(QTd* const q[3], const uint32_t* totals, float r2, AngleCut ccut, float min_n, MatchMail* mail,
-                  hipStream_t st);
+                  hipStream_t st, uint64_t* dev_rows = nullptr);
 
 // mail (may be null): pinned mailbox receiving the E scores and the error word (mail.h)
 struct FineMail;

@@ -276,7 +276,8 @@ __global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ 
 // out empty (d2 is NaN or inf), as in the host path.
 __global__ void __launch_bounds__(256) k_cluster_bits(const QTd* __restrict__ q0, const QTd* __restrict__ q1,
                                                       const QTd* __restrict__ q2, const uint32_t* __restrict__ totals,
-                                                      float r2, AngleCut ccut, float min_n, uint64_t* __restrict__ out) {
+                                                      float r2, AngleCut ccut, float min_n, uint64_t* __restrict__ out,
+                                                      uint64_t* __restrict__ dout) {
   KT();
   const int t = blockIdx.y;
   const QTd* __restrict__ q = t == 0 ? q0 : (t == 1 ? q1 : q2);
@@ -311,7 +312,10 @@ __global__ void __launch_bounds__(256) k_cluster_bits(const QTd* __restrict__ q0
       }
     }
     const uint64_t m = __ballot(nb);
-    if (lane == 0) out[off + g] = m;
+    if (lane == 0) {
+      out[off + g] = m;
+      if (dout) dout[off + g] = m;
+    }
   }
 }
 
@@ -327,8 +331,8 @@ void match_candidates(const MatchIn* d_in, int K, uint32_t* cnt, int32_t* type, 
 }
 
 void cluster_bits(QTd* const q[3], const uint32_t* totals, float r2, AngleCut ccut, float min_n, MatchMail* mail,
-                  hipStream_t st) {
-  k_cluster_bits<<<dim3(512, 3), 256, 0, st>>>(q[0], q[1], q[2], totals, r2, ccut, min_n, mail->cbits);
+                  hipStream_t st, uint64_t* dev_rows) {
+  k_cluster_bits<<<dim3(512, 3), 256, 0, st>>>(q[0], q[1], q[2], totals, r2, ccut, min_n, mail->cbits, dev_rows);
 }
 
 }  // namespace fccf

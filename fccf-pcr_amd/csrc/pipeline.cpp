@@ -636,7 +636,12 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   const size_t per = (size_t)std::max(1, std::max(0, M.nF1 - 2) * std::max(0, M.nF2 - 2));
   const size_t ccap = std::max<size_t>(1, (size_t)K * per);
   const size_t lists = 3 * ccap * (sizeof(MCand) + sizeof(QTd));
-  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + lists * (G ? 2 : 1) + (1 << 16));
+  // transform_cluster's radius search for all three lists on the device (k_cluster_bits)
+  const char* cbe = std::getenv("FCCF_CLUSTER_BITS");  // "0": host radius search (tests both paths)
+  const bool cbits_on = !(cbe && cbe[0] == '0');
+  const bool cdev = c->cluster_device && cbits_on && K > 0;  // f3 on the device (cluster.hip)
+  const size_t cl_bytes = cdev ? sizeof(uint64_t) * MatchMail::CB_CAP + 15 * 4 * ccap + 4096 : 0;
+  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + lists * (G ? 2 : 1) + cl_bytes + (1 << 16));
   c->arena2.reset();
   MatchIn* dM = c->arena2.take_n<MatchIn>(1);
   uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
@@ -652,13 +657,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   uint32_t tot[4] = {0, 0, 0, 0};
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
   HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
+  uint64_t* drows = cdev ? c->arena2.take_n<uint64_t>(MatchMail::CB_CAP) : nullptr;
   match_candidates(dM, Kloc, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
-  // transform_cluster's radius search for all three lists on the device (k_cluster_bits)
-  const char* cbe = std::getenv("FCCF_CLUSTER_BITS");  // "0": host radius search (tests both paths)
-  const bool cbits_on = !(cbe && cbe[0] == '0');
   const float cr2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
-  if (cbits_on && K > 0 && !G)
-    cluster_bits(dq, dtot, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0);
+  if (cbits_on && K > 0 && !G) {
+    cluster_bits(dq, dtot, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0, drows);
+    if (cdev) cluster_launch(c, dq, dtot, drows, ccap, P, &mm, st0);
+  }
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(st0));  // totals, K_pass and candidate lists are in the mailbox
   std::vector<QTd> qraw[3];
@@ -682,8 +687,11 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       dc[t] = ca[t];
       dq[t] = qa[t];
     }
-    if (cbits_on)
-      cluster_bits(dq, dtot_all, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0);
+    if (cbits_on) {
+      cluster_bits(dq, dtot_all, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0,
+                   drows);
+      if (cdev) cluster_launch(c, dq, dtot_all, drows, ccap, P, &mm, st0);
+    }
     HIP_CHECK(hipGetLastError());
     for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
     HIP_CHECK(hipStreamSynchronize(st0));
@@ -744,6 +752,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     }
     const int cluster_num =
         transformation_num ? (int)(P.seclct_cluster_number * (float)qv.size() / (float)transformation_num) : 0;
+    if (cdev && mm.cl_stat[t][0] == 0) {  // clustered on the device (cluster_launch)
+      if ((int)mm.cl_stat[t][3] != cluster_num) throw Error(FCCF_E_INTERNAL, "device cluster_num differs");
+      fine[t] = cluster_results(mm, t);
+      counts.push_back((int64_t)mm.cl_stat[t][1]);
+      S.fine[t] = (int64_t)fine[t].size();
+      continue;
+    }
     int64_t ncl = 0;
     transform_cluster(qv, fine[t], cluster_num, P, &ncl, &c->pool, bits);
     counts.push_back(ncl);
@@ -1114,6 +1129,49 @@ void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vect
     score[k] = hs[k];
     npairs[k] = hn[k];
   }
+}
+
+void cluster_launch(fccf_ctx* c, QTd* const dq[3], const uint32_t* dtot, const uint64_t* drows, size_t ccap,
+                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num) {
+  ClusterIn in{};
+  ClusterOut out{};
+  for (int t = 0; t < 3; ++t) {
+    in.q[t] = dq[t];
+    out.cseed[t] = c->arena2.take_n<uint32_t>(ccap);
+    out.csize[t] = c->arena2.take_n<uint32_t>(ccap);
+    out.bx[t] = c->arena2.take_n<uint32_t>(ccap);
+    out.bid[t] = c->arena2.take_n<uint32_t>(ccap);
+    out.emit[t] = c->arena2.take_n<uint32_t>(ccap);
+  }
+  in.rows = drows;
+  in.totals = dtot;
+  in.cb_cap = MatchMail::CB_CAP;
+  in.min_n = P.cluster_number_threshold;
+  in.sel = P.seclct_cluster_number;
+  if (cluster_num) {
+    in.cnum_given = *cluster_num;
+    in.has_cnum = 1;
+  }
+  out.cap = (uint32_t)std::min<size_t>(ccap, 0xFFFFFFFFu);
+  out.stat = &mail->cl_stat[0][0];
+  out.fine = &mail->cl_fine[0][0];
+  out.fcap = MatchMail::CL_FCAP;
+  // cluster_num <= sel (n <= total), so sel + 2 averaging waves per type cover the
+  // emission loop (:1205-1229, at most cluster_num + 1); a type past them is the host's
+  const double cmax = cluster_num ? (double)*cluster_num : (double)P.seclct_cluster_number;
+  out.egrid = (uint32_t)std::clamp(cmax + 2.0, 2.0, (double)MatchMail::CL_FCAP);
+  cluster_device(in, out, st);
+}
+
+MatchMail* match_mail(fccf_ctx* c) { return &host_mail(c)->match; }
+
+std::vector<QT> cluster_results(const MatchMail& mm, int t) {
+  std::vector<QT> f(mm.cl_stat[t][2]);
+  for (size_t e = 0; e < f.size(); ++e) {
+    const QTd& a = mm.cl_fine[t][e];
+    f[e] = {a.qw, a.qx, a.qy, a.qz, a.tx, a.ty, a.tz, a.alloc};
+  }
+  return f;
 }
 
 void pipeline_release(fccf_ctx* c) {

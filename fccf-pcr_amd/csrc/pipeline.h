@@ -70,6 +70,14 @@ void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t
 // f1 (verify.hip): quick_verify + LM of the candidates qs on the device; dM holds the
 // F1/F2 tables (MatchIn, device).  Outputs per candidate: refined T, score, pairs.
 // Uses arena_v and c->pinned; synchronises st.
+// f3: transform_cluster after k_cluster_bits on the device (cluster.hip), the results
+// into the mailbox (MatchMail::cl_stat/cl_fine); scratch from c->arena2.  cluster_num
+// (may be null): one value for all types instead of the one derived from the totals.
+struct MatchMail;
+void cluster_launch(fccf_ctx* c, QTd* const dq[3], const uint32_t* dtot, const uint64_t* drows, size_t ccap,
+                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num = nullptr);
+std::vector<QT> cluster_results(const MatchMail& mm, int t);  // type t's averages (status 0)
+MatchMail* match_mail(fccf_ctx* c);
 void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vector<Plane>& F1,
                          const std::vector<Plane>& F2, const MatchIn* dM, const fccf_params& P, hipStream_t st,
                          std::vector<m44>& T, std::vector<float>& score, std::vector<int>& npairs);

@@ -73,6 +73,7 @@ _sig("fccf_ctx_destroy", ctypes.c_int, _P)
 _sig("fccf_ctx_set_debug", ctypes.c_int, _P, ctypes.c_int)
 _sig("fccf_ctx_set_grow_device", ctypes.c_int, _P, ctypes.c_int)
 _sig("fccf_ctx_set_lm_device", ctypes.c_int, _P, ctypes.c_int)
+_sig("fccf_ctx_set_cluster_device", ctypes.c_int, _P, ctypes.c_int)
 _sig("fccf_debug_sincos", ctypes.c_int, _P, _P, _I64, _P, _P, _P)
 _sig("fccf_stage_verify", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, _I64, ctypes.POINTER(Params), _P, _P, _P)
 _sig("fccf_ctx_last_error", ctypes.c_char_p, _P)
@@ -190,6 +191,10 @@ class Ctx:
     def set_lm_device(self, on: bool = True):
         """quick_verify + LM (FCCF.cpp:680-783, :210-249) on the GPU instead of the host."""
         _check(_lib.fccf_ctx_set_lm_device(self._h, int(bool(on))), "fccf_ctx_set_lm_device", self._h)
+
+    def set_cluster_device(self, on: bool = True):
+        """transform_cluster's seeds, sort and averaging (FCCF.cpp:1040-1231) on the GPU."""
+        _check(_lib.fccf_ctx_set_cluster_device(self._h, int(bool(on))), "fccf_ctx_set_cluster_device", self._h)
 
     def verify(self, F1, F2, qt, params: Params | None = None):
         """quick_verify + LM of clustered candidates qt[n, 8] (fccf_stage_verify):

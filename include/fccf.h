@@ -110,6 +110,12 @@ int fccf_ctx_set_grow_device(fccf_ctx* ctx, int on);
  * of the host pool: applies to fccf_register* and fccf_stage_verify on this ctx.  Off
  * by default. */
 int fccf_ctx_set_lm_device(fccf_ctx* ctx, int on);
+/* transform_cluster's seed pass, range_cluster's exchange sort and the cluster
+ * averaging (FCCF.cpp:1040-1231, :1020-1038) on the GPU, after the
+ * device radius search, bit-identical: applies to fccf_register* and
+ * fccf_stage_cluster on this ctx; a type past the kernels' capacities is clustered on
+ * the host.  Off by default. */
+int fccf_ctx_set_cluster_device(fccf_ctx* ctx, int on);
 /* Keep per-stage intermediates for fccf_debug_get (tests). Off by default. */
 int fccf_ctx_set_debug(fccf_ctx* ctx, int on);
 
