@@ -535,9 +535,19 @@ struct BlockLds {
 };
 static_assert(IS_LCAP <= 8192 && IS_WCAP <= 1024, "task packing: 13-bit offsets, 11-bit sizes, 8-bit depths");
 
+#ifndef IS_WLEVEL
+#define IS_WLEVEL 1  // wave tasks of > 64 elements partitioned level by level (wave_task_level)
+#endif
+
 // One wave's slice of the wave kernel
 struct WaveLds {
   uint32_t k[IS_WCAP], v[IS_WCAP];
+#if IS_WLEVEL
+  uint16_t lg[IS_WCAP], ll[IS_WCAP];   // a level's >= / <= positions, in position order
+  uint32_t cutv[IS_WCAP];              // per segment (at its first position): its cut, or its end
+  uint64_t bw[2][IS_WC + 1];           // the level's >= / <= ballots per chunk
+  uint32_t pc[2][IS_WC + 1];           // and their exclusive prefix counts
+#endif
   uint16_t xch[IS_WCAP / 2];
   uint32_t heads[IS_WCAP / 32];
   uint32_t stk[IS_STACK];
@@ -841,6 +851,176 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
     stk[sp++] = wpack(f, c - f, dd - 1);
   }
 }
+
+#if IS_WLEVEL
+// # of the level's >= (s = 0) / <= (s = 1) elements before position x (0 <= x <= 64 C)
+__device__ __forceinline__ uint32_t level_rank(const WaveLds& S, int s, uint32_t x) {
+  const uint32_t c = x >> 6, bit = x & 63u;
+  return S.pc[s][c] + (uint32_t)__popcll(S.bw[s][c] & ((1ull << bit) - 1ull));
+}
+
+// A whole wave task [f, f+n) (64 < n <= 64 C), in LDS, level by level: every segment
+// of a level is partitioned in the same pass, so the task's dependent chain is its
+// tree depth instead of its partition count (the <= 64 subtrees of wave_sort_regs
+// already work this way).  Position p = 64 c + lane stays with (chunk c, lane), whose
+// segment [a, b) is kept in registers.  Per level, for the segments longer than 16:
+// each lane takes its segment's median-of-3 pivot itself (three LDS reads), >= / <=
+// flags against it, ballots per chunk and their prefix counts (one LDS table), so
+// the segment-relative ranks are differences of whole-window ranks and the k-th
+// >= / <= element of a segment is read from the window's compacted position lists;
+// the swap rule and the cut are wave_partition's.  Depth 0 heap-sorts what is still
+// active (rare).  The leaves are then stably sorted by rank and written to K/V.
+template <int C>
+__device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict__ K, uint32_t* __restrict__ V,
+                                                uint32_t f, uint32_t n, int d) {
+  const uint32_t lane = lane_id();
+  uint32_t ab[C];  // a | b << 16
+#pragma unroll
+  for (int c = 0; c < C; ++c) ab[c] = n << 16;
+  for (int dd = d;; --dd) {
+    uint32_t actm = 0;  // bit c: chunk c's position lies in a segment still to partition
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const uint32_t p = c * 64 + lane, a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+      if (p < n && b - a > IS_THRESHOLD) actm |= 1u << c;
+    }
+    if (!__ballot(actm != 0u)) break;
+    if (dd == 0) {  // depth limit: heap sort every active segment (one lane; rare)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const uint32_t p = c * 64 + lane;
+        if (((actm >> c) & 1u) && p == (ab[c] & 0xFFFFu)) S.cutv[p] = ab[c] >> 16;
+      }
+      uint64_t hd[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) hd[c] = __ballot(((actm >> c) & 1u) && c * 64 + lane == (ab[c] & 0xFFFFu));
+      wsync();
+      if (lane == 0)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          for (uint64_t m = hd[c]; m; m &= m - 1) {
+            const uint32_t a = c * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+            heap_sort(S.k + a, S.v + a, (int64_t)(S.cutv[a] - a));
+          }
+      wsync();
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const uint32_t p = c * 64 + lane;
+        if ((actm >> c) & 1u) ab[c] = p | ((p + 1) << 16);  // sorted: every position its own leaf
+      }
+      break;
+    }
+    uint32_t kk[C], vv[C];
+    uint64_t bg[C], bl[C];
+    uint32_t moved = 0;  // bit c: chunk c's position is the segment's first or its median (rewritten in place)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const uint32_t p = c * 64 + lane, a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+      const bool act = (actm >> c) & 1u;
+      kk[c] = 0u;
+      vv[c] = 0u;
+      bool ge = false, le = false;
+      if (act) {  // (positions in finished segments are neither read nor written)
+        kk[c] = S.k[p];
+        vv[c] = S.v[p];
+        // __move_median_to_first(a, a+1, mid, b-1): a receives the pivot, m the old first
+        const uint32_t m = median_pos(S.k, a, b);
+        const uint32_t P = S.k[m];
+        if (p == a) {
+          kk[c] = P;
+          vv[c] = S.v[m];
+          S.cutv[a] = IS_NONE;
+          moved |= 1u << c;
+        } else {
+          if (p == m) {
+            kk[c] = S.k[a];
+            vv[c] = S.v[a];
+            moved |= 1u << c;
+          }
+          ge = kk[c] >= P;
+          le = kk[c] <= P;
+        }
+      }
+      bg[c] = __ballot(ge);
+      bl[c] = __ballot(le);
+    }
+    if (lane == 0) {
+      uint32_t rg = 0, rl = 0;
+#pragma unroll
+      for (int c = 0; c <= C; ++c) {
+        S.pc[0][c] = rg;
+        S.pc[1][c] = rl;
+        S.bw[0][c] = c < C ? bg[c] : 0ull;
+        S.bw[1][c] = c < C ? bl[c] : 0ull;
+        if (c < C) {
+          rg += (uint32_t)__popcll(bg[c]);
+          rl += (uint32_t)__popcll(bl[c]);
+        }
+      }
+    }
+    wsync();  // (every read of S.k above precedes every write below)
+    uint32_t li[C];  // 1 + index into S.ll (a swapped >=) or S.lg | 1 << 16 (a swapped <=), 0: stays
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      li[c] = 0;
+      if (!((actm >> c) & 1u)) continue;
+      const uint32_t p = c * 64 + lane, a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+      if (p == a) continue;
+      const bool ge = (bg[c] >> lane) & 1ull, le = (bl[c] >> lane) & 1ull;
+      const uint32_t g0 = level_rank(S, 0, a + 1), l0 = level_rank(S, 1, a + 1);
+      const uint32_t le_tot = level_rank(S, 1, b) - l0;
+      const uint32_t ga = S.pc[0][c] + mbcnt(bg[c]), la = S.pc[1][c] + mbcnt(bl[c]);
+      const uint32_t g = ga - g0, h = la - l0;  // # >= / # <= of the segment before p
+      const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
+      const bool sl = le && g >= le_tot - h;
+      if (ge) S.lg[ga] = (uint16_t)p;
+      if (le) S.ll[la] = (uint16_t)p;
+      if ((ge && !sg) || sl) atomicMin(&S.cutv[a], p);  // L[K+1] / R[K]
+      if (sg) li[c] = 1u + l0 + (le_tot - g - 1);        // R[g+1]
+      else if (sl) li[c] = (1u + g0 + (le_tot - h - 1)) | (1u << 16);  // L[kr]
+    }
+    wsync();
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (!((actm >> c) & 1u)) continue;
+      const uint32_t p = c * 64 + lane;
+      uint32_t dst = p;
+      if (li[c]) {
+        const uint32_t x = (li[c] & 0xFFFFu) - 1u;
+        dst = (li[c] >> 16) ? S.lg[x] : S.ll[x];
+      } else if (!((moved >> c) & 1u)) {
+        continue;  // stays in place
+      }
+      S.k[dst] = kk[c];
+      S.v[dst] = vv[c];
+    }
+    wsync();
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (!((actm >> c) & 1u)) continue;
+      const uint32_t p = c * 64 + lane, a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+      const uint32_t cut = min(max(S.cutv[a], a + 1), b - 1);
+      ab[c] = p >= cut ? (cut | (b << 16)) : (a | (cut << 16));
+    }
+    wsync();  // (the cut reads precede the next level's resets)
+  }
+  // stable sort of every leaf (<= 16 positions) by rank, straight to K/V
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const uint32_t p = c * 64 + lane;
+    if (p >= n) continue;
+    const uint32_t a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+    const uint32_t key = S.k[p];
+    uint32_t rank = 0;
+    for (uint32_t q = a; q < b; ++q) {
+      const uint32_t kq = S.k[q];
+      rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
+    }
+    K[f + a + rank] = key;
+    V[f + a + rank] = S.v[p];
+  }
+}
+#endif
 
 // One partition of [f, l) (IS_WCAP < l - f <= IS_OT * C) in LDS by the whole block.
 template <int C>
@@ -1311,6 +1491,15 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
     if (lane < IS_WCAP / 32) S.heads[lane] = 0;
     wsync();
     const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
+#if IS_WLEVEL
+    if (n > 64) {
+      if (n <= 128) wave_task_level<2>(S, K, V, f, n, d);
+      else if (n <= 256) wave_task_level<4>(S, K, V, f, n, d);
+      else wave_task_level<IS_WC>(S, K, V, f, n, d);
+      if (S.son && lane == 0) atomicAdd(&S.lstat[2], 1u);
+    } else
+#endif
+    {
     wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
     wsync();
 #pragma unroll
@@ -1336,6 +1525,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
       }
       K[f + a + rank] = key;
       V[f + a + rank] = S.v[p];
+    }
     }
     wsync();
     if (W.trace && lane == 0) {
