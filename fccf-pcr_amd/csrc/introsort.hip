@@ -163,6 +163,28 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   return wp + x - v;
 }
 
+// The same for packed 64-bit counters (several fields summed at once, no carries
+// between them by construction); sh >= 16 u64.
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* sh, uint64_t* total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint64_t wp = 0, tot = 0;
+  for (uint32_t w = 0; w < nw; ++w) {
+    wp += w < wave ? sh[w] : 0ull;
+    tot += sh[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
 struct Child {
   uint32_t f, l;
   int32_t d;
@@ -243,6 +265,7 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
                                               const IsBufs& W, int r, uint32_t* dyn) {
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
   __shared__ uint32_t sh[16], bsh[4];
+  __shared__ uint64_t sh64[16];
   const uint32_t t = blockIdx.x;
   uint32_t j, f, l, m, P, kf;
   uint32_t tile0;
@@ -262,10 +285,14 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
       const bool lg = i < nch && is_large(c, W.tier);
       const bool ow = i < nch && !lg && c.l > c.f;
       const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
-      uint32_t s_lg, s_nt, s_ow;
-      const uint32_t p_lg = block_excl_scan(lg ? 1u : 0u, sh, &s_lg);
-      const uint32_t p_nt = block_excl_scan(nt, sh, &s_nt);
-      const uint32_t p_ow = block_excl_scan(ow ? 1u : 0u, sh, &s_ow);
+      // one scan of the three counters packed: large (21 bits) | owned (21) | tiles (22)
+      uint64_t s_all;
+      const uint64_t p_all =
+          block_excl_scan64((lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)nt << 42), sh64, &s_all);
+      const uint32_t p_lg = (uint32_t)(p_all & 0x1FFFFFu), p_ow = (uint32_t)((p_all >> 21) & 0x1FFFFFu),
+                     p_nt = (uint32_t)(p_all >> 42);
+      const uint32_t s_lg = (uint32_t)(s_all & 0x1FFFFFu), s_ow = (uint32_t)((s_all >> 21) & 0x1FFFFFu),
+                     s_nt = (uint32_t)(s_all >> 42);
       if (lg) {
         tf[nseg + p_lg] = c.f;
         tl[nseg + p_lg] = c.l;
@@ -378,7 +405,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
                                                       B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
   KT();
   extern __shared__ uint32_t dyn[];
-  __shared__ uint32_t sh[16];
+  __shared__ uint64_t sh64[16];
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
   __shared__ uint32_t scut;
   const int e = blockIdx.y;
@@ -417,9 +444,9 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     const uint32_t u = u0 + threadIdx.x;
     const uint32_t g = u < nt ? W.cnt[2 * (size_t)(s.tile0 + u)] : 0u;
     const uint32_t q = u < nt ? W.cnt[2 * (size_t)(s.tile0 + u) + 1] : 0u;
-    uint32_t sg, sl;
-    const uint32_t xg = block_excl_scan(g, sh, &sg);
-    const uint32_t xl = block_excl_scan(q, sh, &sl);
+    uint64_t sx;  // >= counts (low 32 bits) and <= counts (high) in one scan: each sums to <= l - f
+    const uint64_t xx = block_excl_scan64((uint64_t)g | ((uint64_t)q << 32), sh64, &sx);
+    const uint32_t xg = (uint32_t)xx, xl = (uint32_t)(xx >> 32), sg = (uint32_t)sx, sl = (uint32_t)(sx >> 32);
     if (u < nt) {
       preg[u] = rg + xg;
       prel[u] = rl + xl;
