@@ -269,6 +269,7 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
   const uint32_t t = blockIdx.x;
   uint32_t j, f, l, m, P, kf;
   uint32_t tile0;
+  uint32_t kk[IS_TC];
   {
     const uint32_t nsort = W.ctl[0];
     uint32_t* tf = dyn;
@@ -323,6 +324,16 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
     f = tf[j];
     l = tl[j];
     tile0 = t0[j];
+    // the tile's keys are loaded before the pivot, so their latency overlaps thread 0's
+    // dependent median reads below
+    {
+      const uint32_t a0 = f + 1 + (t - tile0) * IS_TILE, b0 = min(l, a0 + IS_TILE);
+#pragma unroll
+      for (int c = 0; c < IS_TC; ++c) {
+        const uint32_t p = a0 + c * IS_TT + threadIdx.x;
+        kk[c] = p < b0 ? K[p] : 0u;
+      }
+    }
     if (threadIdx.x == 0) {
       m = median_pos(K, f, l);
       bsh[0] = m;
@@ -344,13 +355,9 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
   const uint32_t i = t - tile0;
   const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-  uint32_t kk[IS_TC];
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
-    const uint32_t p = a + c * IS_TT + threadIdx.x;
-    kk[c] = p < b ? K[p] : 0u;
-    if (p == m) kk[c] = kf;
-  }
+  for (int c = 0; c < IS_TC; ++c)
+    if (a + c * IS_TT + threadIdx.x == m) kk[c] = kf;  // the median-to-first swap
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const bool ok = a + c * IS_TT + threadIdx.x < b;
