@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
 __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
                                               const IsBufs& W, int r, uint32_t* dyn) {
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
-  __shared__ uint32_t sh[16], bsh[4];
+  __shared__ uint32_t bsh[4];
   __shared__ uint64_t sh64[16];
   const uint32_t t = blockIdx.x;
   uint32_t j, f, l, m, P, kf;
@@ -306,13 +306,9 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
       nown += s_ow;
     }
     __syncthreads();
-    if (t == 0) {
-      uint32_t ne = 0;  // elements partitioned this round (the scatter probe's unit count)
-      for (uint32_t q = threadIdx.x; q < nseg; q += blockDim.x) ne += tl[q] - tf[q];
-      uint32_t ne_tot;
-      (void)block_excl_scan(ne, sh, &ne_tot);
-      if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, ne_tot};
-    }
+    // (pad: elements partitioned this round, the scatter probe's unit count, summed by
+    // the scatter's first tiles)
+    if (t == 0 && threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
     if (t >= ntiles) {
       if (threadIdx.x == 0 && t < W.maxtiles) {
         W.tseg[t] = IS_NONE;
@@ -431,6 +427,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
   uint32_t* __restrict__ Vo = Vo2[e];
   const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  if (i == 0 && threadIdx.x == 0) atomicAdd(&W.rounds[r].pad, l - f);
   // the tile's elements are loaded first: their latency overlaps the prefix below
   uint32_t kk[IS_TC], vv[IS_TC];
 #pragma unroll
