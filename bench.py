@@ -37,7 +37,7 @@ PROBE_KERNELS = ["k_is_wave", "k_is_scatter", "k_is_block", "k_xs_chain", "k_xs_
 
 def stage_roofline(st):
     """algorithmic bytes of the N-proportional stages over their
-    device spans (HIP events between the cloud-stage graphs, fccf_stats.dev_ms), per
+    device spans (the cloud stage's kernel timestamps, fccf_stats.dev_ms), per
     stage and aggregated.  Per cloud c: D = 12 N_c + 12 M1_c + 12 M1_c + 12 M_c (both
     VoxelGrid passes), P = 12 M_c + 32 V_c (1 m voxel fit, V = occupied leaves),
     F = 12 (S1 + S2) per fine_verify evaluation."""

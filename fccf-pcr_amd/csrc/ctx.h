@@ -228,12 +228,12 @@ struct fccf_ctx {
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
     fccf::Arena inarena;             // staged host inputs of the pair on this set (copy stream)
     hipEvent_t ev_in0 = nullptr, ev_in = nullptr;  // their copies started / done (timing: fccf_stats h2d)
-    hipEvent_t ev[6] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
-                                     // [4] clouds done, [5] S1 replay done
-    hipEvent_t tev[6] = {};          // timing: cloud start, pass 1 done, pass 2 done, faces done,
-                                     // fine start, fine done (fccf_stats::dev_ms)
-    fccf::CachedGraph g_seg[3];      // both clouds batched: main's VoxelGrid, faces, the driver's pass
-    fccf::CachedGraph g_cen;         // both cloud centroids (one exact-sum launch set)
+    hipEvent_t ev[8] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
+                                     // [4] clouds done, [5] S1 replay done; [6]/[7] the centroid branch's
+                                     // fork/join inside the one-graph cloud stage (capture-internal)
+    hipEvent_t tev[6] = {};          // timing: [4] fine start, [5] fine done (fccf_stats::dev_ms[3]);
+                                     // the cloud stage's spans are device stamps (CloudMail::stamp)
+    fccf::CachedGraph g_seg[1];      // the cloud stage of both clouds (VoxelGrid passes, centroids, faces)
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing

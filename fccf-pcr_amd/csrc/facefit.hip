@@ -29,8 +29,11 @@ namespace {
 // Batched over blockIdx.y = sequence e.
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n0,
                                                     float* __restrict__ aggr0, SeqStrides sd,
-                                                    uint32_t nbc, OctState* __restrict__ reset0) {
+                                                    uint32_t nbc, OctState* __restrict__ reset0,
+                                                    uint64_t* __restrict__ stamp) {
   KT();
+  if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)  // the face stage starts
+    *stamp = __builtin_amdgcn_s_memrealtime();
   if (reset0 && blockIdx.x == 0 && threadIdx.x == 0) {  // empty octree for k_oct_sim (sequence blockIdx.y)
     OctState z;
     for (int a = 0; a < 3; ++a) z.min[a] = z.max[a] = 0.0;
@@ -442,6 +445,16 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
     if (threadIdx.x < 4) mail->sc[e][i] = sc2[e][i];
     else mail->fsc[e][i] = B.nleaf[i];
   }
+  // the cloud stage's device spans: the stamps of main's pass, the driver's pass and the
+  // face stage, and now (this last kernel of the stage, ~5 us, starts) into the mailbox.
+  // (A finished-block count to stamp the true end cost 8192 same-address atomics:
+  // ~70 us.)
+  if (mail && e == 0 && blockIdx.x == 0 && threadIdx.x == 0 && B.vgp) {
+    mail->stamp[3] = __builtin_amdgcn_s_memrealtime();
+    mail->stamp[0] = B.vgp->t_main;
+    mail->stamp[1] = B.vgp->t_driver;
+    mail->stamp[2] = *B.t_faces;
+  }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
     if (!planar[s]) continue;
     VoxRec r = recs[s];
@@ -464,9 +477,9 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
-                SeqStrides sd, OctState* reset_state) {
+                SeqStrides sd, OctState* reset_state, uint64_t* stamp) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap), reset_state);
+  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap), reset_state, stamp);
 }
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,
@@ -494,7 +507,7 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   sd.aggr = byte_stride(aggr, nbatch);
   sd.state = byte_stride(oct, nbatch);
   sd.n = byte_stride(d_n, nbatch);
-  block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd, oct[0]);  // also resets the octree states
+  block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd, oct[0], b[0].t_faces);  // also resets the octree states
   octree_sim(xyz[0], d_n[0], cap, res, aggr[0], oct[0], st, nbatch, sd);
   const B2<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
   const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });

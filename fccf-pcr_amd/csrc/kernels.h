@@ -22,6 +22,8 @@ struct VGParams {
   uint32_t chk_done;  // presorted check: blocks finished
   uint32_t nonfinite; // some output point is not finite (set by k_vg_centroid when it writes a copy)
   const float* src;   // the pass's input points (set by k_vg_bbox, read by the later kernels)
+  uint64_t t_main;    // s_memrealtime at the start of main's pass (k_vg_bbox<0>): stage spans
+  uint64_t t_driver;  // ... and of the driver's remove-NaN + second pass (k_finite_fix)
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
@@ -173,6 +175,8 @@ struct FaceBufs {
   uint32_t* nbits;
   uint32_t* nplanar;
   uint32_t* nresid;
+  uint64_t* t_faces;       // s_memrealtime at the start of the face stage (k_block_aggr)
+  const VGParams* vgp;     // the cloud's VoxelGrid parameters (their stage stamps), or null
   SortScratch ss;
 };
 
@@ -212,7 +216,8 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
 // reset_state (optional): block 0 of each sequence also writes an empty OctState
 // there (sequence e at reset_state + e * sd.state bytes) for the octree_sim that follows.
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
-                SeqStrides sd = SeqStrides(), OctState* reset_state = nullptr);
+                SeqStrides sd = SeqStrides(), OctState* reset_state = nullptr,
+                uint64_t* stamp = nullptr);  // stamp: the face stage's start (FaceBufs::t_faces)
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
 constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
 // aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per

@@ -48,6 +48,7 @@ __global__ void __launch_bounds__(1024) k_finite_fix(B2<const float*> xyz2, B2<c
                                                      B2<const VGParams*> P2, B2<float*> out2, B2<uint32_t*> d_m2) {
   KT();
   const int e = blockIdx.y;
+  if (threadIdx.x == 0) const_cast<VGParams*>(P2[e])->t_driver = __builtin_amdgcn_s_memrealtime();
   const uint32_t n = *d_n2[e];
   if (!P2[e]->nonfinite) {
     if (threadIdx.x == 0) *d_m2[e] = n;
@@ -178,6 +179,7 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool) {
   w.ds2 = a.take_n<float>(3 * (size_t)cap);
   w.vg = voxel_grid_carve(a, cap);
   w.fb = face_bufs_carve(a, cap);
+  w.fb.vgp = w.vg.params;  // stage stamps (k_compact_planar -> CloudMail::stamp)
   w.planar = a.take_n<VoxRec>(cap);
   w.resid = a.take_n<float>(3 * (size_t)cap);
   w.faggr = a.take_n<float>(aggr_floats(cap));
@@ -266,30 +268,6 @@ void dump_planes(fccf_ctx* c, const std::string& k, const std::vector<Plane>& F)
 }  // namespace
 
 namespace {
-
-// Development timing of the cloud-stage segments (FCCF_SEG_TIMING).
-struct SegTimer {
-  hipEvent_t ev[5] = {};
-  bool armed = false;
-};
-SegTimer& seg_timer(int s) {
-  static SegTimer t[2];
-  if (!t[s].ev[0])
-    for (auto& e : t[s].ev) HIP_CHECK(hipEventCreate(&e));
-  return t[s];
-}
-void seg_timer_print(int s) {
-  SegTimer& t = seg_timer(s);
-  if (!t.armed) return;
-  t.armed = false;
-  float v[5] = {};
-  for (int i = 0; i < 5; ++i) {
-    HIP_CHECK(hipEventSynchronize(t.ev[i]));
-    if (i) HIP_CHECK(hipEventElapsedTime(&v[i], t.ev[0], t.ev[i]));
-  }
-  std::fprintf(stderr, "seg us (from start): downsample ->%.0f faces ->%.0f centroids ->%.0f orient ->%.0f\n",
-               v[1] * 1e3, v[2] * 1e3, v[3] * 1e3, v[4] * 1e3);
-}
 
 struct TS { m44 T; float score, score2; };  // a verified candidate: T, quick score, fine score
 
@@ -413,39 +391,30 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     float leaf, fvs, vpt, ct, fine_res;
   } key = {cs.arena.base, cs.arena.cap, capmax, leaf, P.face_voxel_size, P.voxel_point_threshold,
            P.curvature_threshold, P.fine_verify_voxel_size};
-  // FCCF_SEG_TIMING=1 (development): timing events between the segment graphs,
-  // printed to stderr by register_finish.
-  static const bool seg_timing = std::getenv("FCCF_SEG_TIMING") != nullptr;
-  SegTimer& tm = seg_timer(s);
-  auto mark = [&](int i, hipStream_t q) {
-    if (seg_timing) HIP_CHECK(hipEventRecord(tm.ev[i], q));
-  };
-  mark(0, st0);
-  HIP_CHECK(hipEventRecord(cs.tev[0], st0));
   ps.entry.xyz = B2<const float*>(xin[0], xin[1]);
   ps.entry.n = B2<uint32_t>(nv[0], nv[1]);
   ps.entry.bind();
-  cs.g_seg[0].run(&key, sizeof key, st0, [&] { seg_pass1(w, xin, nv, leaf, st0, &ps.entry); }, vg_entry_kernel(),
-                  ps.entry.args);
-  HIP_CHECK(hipEventRecord(cs.tev[1], st0));
-  cs.g_seg[2].run(&key, sizeof key, st0, [&] { seg_downsample(w, leaf, st0); });
-  HIP_CHECK(hipEventRecord(cs.tev[2], st0));
-  mark(1, st0);
-  HIP_CHECK(hipEventRecord(cs.ev[0], st0));
-  HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[0], 0));
-  cs.g_cen.run(&key, sizeof key, ss, [&] {
+  // The whole cloud stage is ONE graph: both VoxelGrid passes, then the centroid sums
+  // forked onto ss beside the face voxels, joined before the orientation.  ROCm 7.2
+  // runs the two branches of a replay concurrently (tools/graph_fork_probe.hip).  The
+  // device spans come from s_memrealtime stamps the stage's kernels write (no timing
+  // events, which would split the graph: four graphs with events between them were
+  // 0.04 ms per registration slower).
+  CloudMail* cmail = &host_mail(c)->clouds[s];  // allocated on first use: never inside the capture
+  cs.g_seg[0].run(&key, sizeof key, st0, [&] {
+    seg_pass1(w, xin, nv, leaf, st0, &ps.entry);
+    seg_downsample(w, leaf, st0);
+    HIP_CHECK(hipEventRecord(cs.ev[6], st0));
+    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[6], 0));
     exact_sum2(w[0].ds2, w[0].sc + 3, w[1].ds2, w[1].sc + 3, 3, 3, ps.cen, true, ps.xs, ss);  // compute3DCentroid (:473)
-  });
-  mark(3, ss);
-  HIP_CHECK(hipEventRecord(cs.ev[2], ss));
-  cs.g_seg[1].run(&key, sizeof key, st0, [&] { seg_faces(w, P, st0); });
-  mark(2, st0);
-  HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[2], 0));
-  face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
-                     &host_mail(c)->clouds[s], B2<const uint32_t*>(w[0].sc, w[1].sc));
-  mark(4, st0);
-  tm.armed = seg_timing;
-  HIP_CHECK(hipEventRecord(cs.tev[3], st0));
+    HIP_CHECK(hipEventRecord(cs.ev[7], ss));
+    seg_faces(w, P, st0);
+    HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[7], 0));
+    face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
+                       cmail, B2<const uint32_t*>(w[0].sc, w[1].sc));
+  }, vg_entry_kernel(), ps.entry.args);
+  // external signal for stage_inputs (this set's inputs have been read): after the graph
+  HIP_CHECK(hipEventRecord(cs.ev[0], st0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
   cs.g_rep.run(&key, sizeof key, st0, [&] { seg_s1_replay(w, P, st0); });
   HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
@@ -486,9 +455,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     else vox[k] = d2h(w[k].planar, fsc[k][2], st0);  // past the mailbox: copy from HBM
   }
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
-  {  // device spans of the cloud stage (its events have completed with ev[4])
+  {  // device spans of the cloud stage: its kernels' s_memrealtime stamps (100 MHz)
     float d[3] = {};
-    for (int i = 0; i < 3; ++i) HIP_CHECK(hipEventElapsedTime(&d[i], c->cs[s].tev[i], c->cs[s].tev[i + 1]));
+    for (int i = 0; i < 3; ++i)
+      d[i] = cm.stamp[i + 1] > cm.stamp[i] ? (float)((double)(cm.stamp[i + 1] - cm.stamp[i]) * 1e-5) : 0.f;
     for (int i = 0; i < 3; ++i) S.dev_ms[i] = d[i];
     S.ms[FCCF_T_DOWNSAMPLE] = d[0] + d[1];
     S.ms[FCCF_T_VOXELFIT] = d[2];
@@ -503,7 +473,6 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   HostTrace ht;
   ht.t0 = ps.t_enq;
   ht.mark("clouds");
-  seg_timer_print(s);
   after_clouds();
   ht.mark("next_enq");
   t0 = clk::now();
@@ -975,7 +944,6 @@ void phase_b2(fccf_ctx* c, int s) {
   S.graph_captures = c->cs[s].g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
   S.graph_captures += c->cs[s].g_rep.captures;
-  S.graph_captures += c->cs[s].g_cen.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
   if (c->debug) {
@@ -996,7 +964,6 @@ void reset_capture_counts(fccf_ctx* c) {
     for (auto& g : cs.g_seg) g.captures = 0;
     cs.g_rep.captures = 0;
     cs.g_fine.captures = 0;
-    cs.g_cen.captures = 0;
   }
 }
 

@@ -57,6 +57,8 @@ inline FaceBufs face_bufs_carve(Arena& a, uint32_t cap) {
   f.nbits = s + 1;
   f.nplanar = s + 2;
   f.nresid = s + 3;
+  f.t_faces = reinterpret_cast<uint64_t*>(s + 4);
+  f.vgp = nullptr;
   f.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
   return f;
 }

@@ -30,6 +30,9 @@ __device__ __forceinline__ float wave_max(float v) {
 // The pass's entry kernel (VGEntry): block 0 also publishes the input pointer (and,
 // with set_n, the count) and clears the pass's flags (keys' order check, the
 // centroid kernel's non-finite flag) before any later kernel of the pass runs.
+// Tag: 0 = a first pass (the patched entry node), 1 = a presorted second pass, so the
+// two passes are distinct kernels when one graph holds both.
+template <int Tag>
 __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint32_t*> d_n2, B2<uint32_t> n2,
                                                  int set_n, B2<float*> part2, B2<VGParams*> P2) {
   KT();
@@ -38,6 +41,7 @@ __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint3
   const float* __restrict__ xyz = xyz2[e];
   const uint32_t n = set_n ? n2[e] : *d_n2[e];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (Tag == 0) P2[e]->t_main = __builtin_amdgcn_s_memrealtime();
     P2[e]->unsorted = 0;
     P2[e]->chk_done = 0;
     P2[e]->nonfinite = 0;
@@ -344,7 +348,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 }  // namespace
 
-const void* vg_entry_kernel() { return (const void*)k_vg_bbox; }
+const void* vg_entry_kernel() { return (const void*)k_vg_bbox<0>; }
 
 void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float leaf, B2<float*> out,
                 B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch, B2<float*> out_copy,
@@ -366,7 +370,10 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
   en.part = F([](const VGBufs& v) { return v.part; });
   en.P = P;
   en.bind();
-  k_vg_bbox<<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(en.xyz, en.d_n, en.n, en.set_n, en.part, en.P);
+  if (presorted)
+    k_vg_bbox<1><<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(en.xyz, en.d_n, en.n, en.set_n, en.part, en.P);
+  else
+    k_vg_bbox<0><<<dim3(VG_BBOX_BLOCKS, nbatch), 256, 0, st>>>(en.xyz, en.d_n, en.n, en.set_n, en.part, en.P);
   if (entry) {
     *entry = en;
     entry->bind();

@@ -87,7 +87,8 @@ typedef struct fccf_stats {
   int64_t leaves1, leaves2;      /* occupied 1 m octree leaves (driver source / target) */
   int64_t fine_evals;            /* fine_verify evaluations E                      */
   double dev_ms[4];              /* device spans: main's VoxelGrid pass, the driver's
-                                    remove-NaN + second pass, face voxels, fine verify */
+                                    remove-NaN + second pass, face voxels (s_memrealtime
+                                    stamps of the cloud stage's kernels), fine verify */
 } fccf_stats;
 
 typedef struct fccf_ctx fccf_ctx;
