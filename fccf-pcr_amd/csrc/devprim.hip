@@ -39,36 +39,43 @@ __device__ __forceinline__ uint32_t block_scan_256(uint32_t v, uint32_t* sh, uin
 
 __device__ __forceinline__ uint32_t passes_of(uint32_t nbits) { return (nbits + 7u) / 8u; }
 
-// Digit plan of the device-wide passes for an nbits-wide key: up to 27 bits, the
-// fewest passes of <= 9-bit digits (19..27 bits: three passes instead of four 8-bit
-// ones), wider keys 8-bit digits (the fast launches then cover 32 bits and the
-// single-workgroup tail the rest).  Every kernel of a sort derives the same plan
-// from the device-side nbits.
-constexpr int RS_MAXD = 512;  // buckets of the widest digit
+// Digit plan of the device-wide passes for an nbits-wide key: up to RS_MAXW * 3 bits,
+// the fewest passes of <= RS_MAXW-bit digits (19..27 bits: three 9-bit passes instead
+// of four 8-bit ones), wider keys 8-bit digits (the fast launches then cover 32 bits
+// and the single-workgroup tail the rest).  Every kernel of a sort derives the same
+// plan from the device-side nbits.  RS_MAXW 10 (two passes for the c3 face codes,
+// three for fine verification's keys) measured no faster: 1024-bucket tiles write
+// ~4-key digit runs.
+#ifndef RS_MAXW
+#define RS_MAXW 9
+#endif
+constexpr int RS_MAXD = 1 << RS_MAXW;  // buckets of the widest digit (<= SORT_THREADS)
+static_assert(RS_MAXD <= SORT_THREADS, "one digit bucket per sort thread");
 struct RsPlan {
   uint32_t passes, width;
 };
 __device__ __forceinline__ RsPlan rs_plan(uint32_t nbits) {
   if (nbits == 0) return {0u, 8u};
-  const uint32_t p = nbits <= 27u ? (nbits + 8u) / 9u : (nbits + 7u) / 8u;
+  const uint32_t p = nbits <= 3u * RS_MAXW ? (nbits + RS_MAXW - 1u) / RS_MAXW : (nbits + 7u) / 8u;
   return {p, (nbits + p - 1u) / p};
 }
 
-// Exclusive scan of v over the first 512 threads of an ST-thread block (threads
-// >= 512 pass 0 and get garbage); sh needs SW u32.  Every thread must call it.
-__device__ __forceinline__ uint32_t scan_512_of(uint32_t v, uint32_t* sh, uint32_t* total) {
+// Exclusive scan of v over the first RS_MAXD threads of an ST-thread block (threads
+// >= RS_MAXD pass 0 and get garbage); sh needs SW u32.  Every thread must call it.
+__device__ __forceinline__ uint32_t scan_digits_of(uint32_t v, uint32_t* sh, uint32_t* total) {
+  constexpr uint32_t NW = RS_MAXD / 64;  // waves holding digits
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  if (threadIdx.x >= 512) v = 0;
+  if (threadIdx.x >= (uint32_t)RS_MAXD) v = 0;
   uint32_t x = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o, 64);
     if (lane >= (uint32_t)o) x += y;
   }
-  if (lane == 63 && wave < 8) sh[wave] = x;
+  if (lane == 63 && wave < NW) sh[wave] = x;
   __syncthreads();
   uint32_t wp = 0, tot = 0;
-  for (uint32_t w = 0; w < 8; ++w) {
+  for (uint32_t w = 0; w < NW; ++w) {
     wp += w < wave ? sh[w] : 0u;
     tot += sh[w];
   }
@@ -212,7 +219,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
     uint32_t t;
     const uint32_t g = tid < nd ? tot[tid] : 0u;
     const uint32_t h = tid < nd ? hist[tid * nblocks + blockIdx.x] : 0u;
-    const uint32_t ex = scan_512_of(g, sh, &t);
+    const uint32_t ex = scan_digits_of(g, sh, &t);
     if (tid < nd) gofs[tid] = ex + h;
   }
   for (uint32_t j = tid; j < SW * RS_MAXD; j += ST) (&wcnt[0][0])[j] = 0;
@@ -244,7 +251,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
         acc += t;
       }
     uint32_t t;
-    const uint32_t ex = scan_512_of(acc, sh, &t);
+    const uint32_t ex = scan_digits_of(acc, sh, &t);
     if (tid < nd) tex[tid] = ex;
   }
   __syncthreads();
@@ -594,17 +601,20 @@ __global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<ui
 
 }  // namespace
 
+// hist: max(256 words per segment-kernel tile, RS_MAXD per radix tile)
+static size_t hist_words(uint32_t cap) {
+  return std::max<size_t>(256 * ((size_t)rs_blocks(cap) + 1), (size_t)RS_MAXD * ((size_t)sort_blocks(cap) + 1));
+}
 size_t sort_scratch_bytes(uint32_t cap) {
   const size_t nb = rs_blocks(cap) + 1;
-  return sizeof(uint32_t) * (256 * nb + RS_MAXD + nb + 1) + 256;
+  return sizeof(uint32_t) * (hist_words(cap) + RS_MAXD + nb + 1) + 256;
 }
 
 SortScratch sort_scratch_carve(void* base, uint32_t cap) {
-  const size_t nb = rs_blocks(cap) + 1;
   uint32_t* p = (uint32_t*)base;
   SortScratch s;
   s.hist = p;
-  s.tot = p + 256 * nb;  // 256 * (rs_blocks + 1) >= RS_MAXD * sort_blocks
+  s.tot = p + hist_words(cap);
   s.blk = s.tot + RS_MAXD;
   return s;
 }
