@@ -98,5 +98,10 @@ void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32
 // Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
 void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
                         B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch = 1);
+// Two such scans of the same length in the same two launches (the second's tile
+// totals use the scratch's radix histogram words, unused outside a sort).
+void exclusive_scan2_u32(B2<const uint32_t*> in_a, B2<uint32_t*> out_a, B2<uint32_t*> total_a,
+                         B2<const uint32_t*> in_b, B2<uint32_t*> out_b, B2<uint32_t*> total_b,
+                         B2<const uint32_t*> d_n, uint32_t cap, B2<SortScratch> s, hipStream_t st, int nbatch = 1);
 
 }  // namespace fccf

@@ -550,14 +550,18 @@ void segment_heads(B2<const K*> keys, B2<const uint32_t*> d_n, uint32_t cap, K i
   k_seg_write<K, HasInvalid><<<dim3(nb, nbatch), T, 0, st>>>(keys, d_n, invalid, s, starts, d_nseg, seg_of, run);
 }
 
-__global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<const uint32_t*> d_n2,
-                                                 B2<SortScratch> ss) {
+// Two independent scans may share the launches (gridDim.z = 2): z = 1 scans in2b into
+// out2b with its tile totals in the scratch's hist words (free outside a radix sort).
+__device__ __forceinline__ uint32_t* scan_blk(const SortScratch& s) { return blockIdx.z ? s.hist : s.blk; }
+
+__global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<const uint32_t*> in2b,
+                                                 B2<const uint32_t*> d_n2, B2<SortScratch> ss) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
   const uint32_t n = *d_n2[e];
   if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
-  const uint32_t* __restrict__ in = in2[e];
+  const uint32_t* __restrict__ in = blockIdx.z ? in2b[e] : in2[e];
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
   uint32_t v[RS_CHUNKS], c = 0;
 #pragma unroll
@@ -566,19 +570,21 @@ __global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<con
   for (int j = 0; j < RS_CHUNKS; ++j) c += (i0 + j < n) ? v[j] : 0u;
   uint32_t t;
   block_scan_256(c, sh, &t);
-  if (threadIdx.x == 0) ss[e].blk[blockIdx.x] = t;
+  if (threadIdx.x == 0) scan_blk(ss[e])[blockIdx.x] = t;
 }
 
-__global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<uint32_t*> out2,
-                                                  B2<const uint32_t*> d_n2, B2<SortScratch> ss,
-                                                  B2<uint32_t*> d_total2) {
+__global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<uint32_t*> out2, B2<uint32_t*> d_total2,
+                                                  B2<const uint32_t*> in2b, B2<uint32_t*> out2b,
+                                                  B2<uint32_t*> d_total2b, B2<const uint32_t*> d_n2,
+                                                  B2<SortScratch> ss) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
   const uint32_t n = *d_n2[e];
   if (blockIdx.x * RS_TILE >= n && blockIdx.x) return;
-  const uint32_t* __restrict__ in = in2[e];
-  uint32_t* __restrict__ out = out2[e];
+  const uint32_t* __restrict__ in = blockIdx.z ? in2b[e] : in2[e];
+  uint32_t* __restrict__ out = blockIdx.z ? out2b[e] : out2[e];
+  uint32_t* d_total = blockIdx.z ? d_total2b[e] : d_total2[e];
   const uint32_t i0 = blockIdx.x * RS_TILE + threadIdx.x * RS_CHUNKS;
   uint32_t v[RS_CHUNKS], c = 0;
 #pragma unroll
@@ -588,10 +594,10 @@ __global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<ui
     v[j] = (i0 + j < n) ? v[j] : 0u;
     c += v[j];
   }
-  const uint32_t before = tiles_before(ss[e].blk, sh);
+  const uint32_t before = tiles_before(scan_blk(ss[e]), sh);
   uint32_t t;
   uint32_t run = before + block_scan_256(c, sh, &t);
-  if (threadIdx.x == 0 && owns_last(n) && d_total2[e]) *d_total2[e] = before + t;
+  if (threadIdx.x == 0 && owns_last(n) && d_total) *d_total = before + t;
 #pragma unroll
   for (int j = 0; j < RS_CHUNKS; ++j) {
     if (i0 + j < n) out[i0 + j] = run;
@@ -642,8 +648,17 @@ void segment_heads_u64(B2<const uint64_t*> keys, B2<const uint32_t*> d_n, uint32
 void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
                         B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch) {
   const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
-  k_sum_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, d_n, s);
-  k_scan_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, out, d_n, s, d_total);
+  k_sum_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, in, d_n, s);
+  k_scan_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, out, d_total, in, out, d_total, d_n, s);
+}
+
+void exclusive_scan2_u32(B2<const uint32_t*> in_a, B2<uint32_t*> out_a, B2<uint32_t*> total_a,
+                         B2<const uint32_t*> in_b, B2<uint32_t*> out_b, B2<uint32_t*> total_b,
+                         B2<const uint32_t*> d_n, uint32_t cap, B2<SortScratch> s, hipStream_t st, int nbatch) {
+  const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
+  if ((size_t)nb > hist_words(cap)) throw Error(FCCF_E_INTERNAL, "exclusive_scan2_u32: scratch");
+  k_sum_tiles<<<dim3(nb, nbatch, 2), T, 0, st>>>(in_a, in_b, d_n, s);
+  k_scan_tiles<<<dim3(nb, nbatch, 2), T, 0, st>>>(in_a, out_a, total_a, in_b, out_b, total_b, d_n, s);
 }
 
 }  // namespace fccf

@@ -531,12 +531,12 @@ void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float vpt, float cth
   FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st, b, vpt, cthr);
   const B2<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
   const B2<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
-  exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
-                     pick(b, [](const FaceBufs& f) { return f.planar_off; }), nleaf, cap,
-                     pick(b, [](const FaceBufs& f) { return f.nplanar; }), ss, st, nbatch);
-  exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.resid_cnt; }),
-                     pick(b, [](const FaceBufs& f) { return f.resid_off; }), nleaf, cap,
-                     pick(b, [](const FaceBufs& f) { return f.nresid; }), ss, st, nbatch);
+  exclusive_scan2_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
+                      pick(b, [](const FaceBufs& f) { return f.planar_off; }),
+                      pick(b, [](const FaceBufs& f) { return f.nplanar; }),
+                      pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.resid_cnt; }),
+                      pick(b, [](const FaceBufs& f) { return f.resid_off; }),
+                      pick(b, [](const FaceBufs& f) { return f.nresid; }), nleaf, cap, ss, st, nbatch);
   k_compact_resid<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, d_n, resid_out);
 }
 
