@@ -54,6 +54,7 @@ struct B2 {
 // Stable LSD radix sort of (key, val) by the low *d_nbits bits of key (8-bit
 // digits).  The sorted result is always left in (k0, v0); (k1, v1) are temporaries.
 // If vals_iota, v0 is ignored on input and the values are the input positions.
+// Keys-only: v0 = v1 = null (no value traffic).
 // cap bounds every problem's count.  The first fast_bits (a multiple of 8) run as
 // device-wide passes (3 launches each, a pass past *d_nbits exits at once); any
 // higher bits run in one single-workgroup tail launch (k_rs_tail), which also

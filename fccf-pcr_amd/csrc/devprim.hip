@@ -209,11 +209,12 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
   K kk[SORT_CHUNKS];
   uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
   const uint32_t last = n - 1u;  // n > tile0 >= 0
+  const bool hv = vout != nullptr;  // keys-only sorts pass no value buffers
 #pragma unroll
   for (int c = 0; c < SORT_CHUNKS; ++c) {  // all loads in flight before the ranking
     const uint32_t i = min(base + c * 64 + lane, last);
     kk[c] = kin[i];
-    vv[c] = iota ? i : vin[i];
+    vv[c] = (iota || !hv) ? i : vin[i];
   }
   {
     uint32_t t;
@@ -261,7 +262,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
     if (d >= (uint32_t)RS_MAXD) continue;
     const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
     sk[lp] = kk[c];
-    sv[lp] = vv[c];
+    if (hv) sv[lp] = vv[c];
   }
   __syncthreads();
   const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
@@ -270,7 +271,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const u
     const uint32_t d = (uint32_t)(k >> shift) & mask;
     const uint32_t pos = gofs[d] + (j - tex[d]);
     kout[pos] = k;
-    vout[pos] = sv[j];
+    if (hv) vout[pos] = sv[j];
   }
 }
 
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
       for (int c = 0; c < SORT_CHUNKS; ++c) {
         const uint32_t i = min(base + c * 64 + lane, n - 1u);
         kk[c] = kin[i];
-        vv[c] = vin[i];
+        vv[c] = vin ? vin[i] : 0u;
       }
       for (uint32_t j = tid; j < SW * 256; j += ST) (&wcnt[0][0])[j] = 0;
       __syncthreads();
@@ -385,7 +386,7 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
         const uint32_t d = (uint32_t)(k >> shift) & 255u;
         const uint32_t pos = run_ofs[d] + (j - tex[d]);
         kout[pos] = k;
-        vout[pos] = sv[j];
+        if (vout) vout[pos] = sv[j];
       }
       __syncthreads();
       if (tid < 256) run_ofs[tid] += tcnt[tid];
@@ -396,7 +397,7 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
   if (src)
     for (uint32_t i = tid; i < n; i += ST) {
       kb[0][i] = kb[1][i];
-      vb[0][i] = vb[1][i];
+      if (vb[0]) vb[0][i] = vb[1][i];
     }
 }
 
@@ -414,7 +415,7 @@ __global__ void k_rs_copyback(B2<const K*> k12, B2<const uint32_t*> v12, B2<K*> 
   const uint32_t n = *d_n2[e];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     k0[i] = k1[i];
-    v0[i] = v1[i];
+    if (v0) v0[i] = v1[i];
   }
 }
 
@@ -425,6 +426,7 @@ void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<con
   const uint32_t nb = sort_blocks(cap);
   if (nb == 0) return;
   if (fast_bits == 0 && iota) throw Error(FCCF_E_INTERNAL, "radix_sort: a tail-only sort takes its values as input");
+  if ((v0[0] == nullptr) != (v1[0] == nullptr)) throw Error(FCCF_E_INTERNAL, "radix_sort: both or no value buffers");
   const int fast_passes = fast_bits / 8;
   B2<K*> kb[2] = {k0, k1};
   B2<uint32_t*> vb[2] = {v0, v1};
@@ -432,7 +434,8 @@ void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<con
     const int src = p & 1, dst = src ^ 1;
     k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(kb[src], d_n, d_nbits, p, s, nb);
     k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
-    FCCF_LAUNCH("k_rs_scatter", (d_n[0], 2.0 * (sizeof(K) + 4), nbatch > 1 ? d_n[1] : nullptr, 2.0 * (sizeof(K) + 4)), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
+    const double eb = 2.0 * (sizeof(K) + (v0[0] ? 4 : 0));  // algorithmic bytes per element
+    FCCF_LAUNCH("k_rs_scatter", (d_n[0], eb, nbatch > 1 ? d_n[1] : nullptr, eb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
   }
   if (fast_passes) {
     const uint32_t g = min(nb * 8u, 2048u);
