@@ -63,9 +63,12 @@ struct B2 {
 void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                     uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
                     hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));
+// (k2, v2) optional: a third buffer, so a sort of three active passes ends in (k0, v0)
+// without a copy-back.
 void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                     uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));
+                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr),
+                    B2<uint64_t*> k2 = B2<uint64_t*>(nullptr), B2<uint32_t*> v2 = B2<uint32_t*>(nullptr));
 
 // Run-length segmentation of sorted keys[0..*d_n): starts[s] = first index of
 // segment s, starts[S] = *d_n, *d_nseg = S.  Keys equal to `invalid` (which sort

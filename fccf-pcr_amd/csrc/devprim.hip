@@ -111,13 +111,46 @@ __device__ __forceinline__ uint32_t scan_256_of(uint32_t v, uint32_t* sh, uint32
   return wp + x - v;
 }
 
+// The buffers of one sort: k[0]/v[0] in and out, k[1]/v[1] ping-pong, k[2]/v[2] an
+// optional third buffer.  With it, a sort of exactly three active passes rotates
+// 0 -> 2 -> 1 -> 0 and ends in buffer 0 without the copy-back an odd pass count
+// otherwise needs; every kernel derives the same route from the device-side plan.
 template <class K>
-__global__ void __launch_bounds__(ST) k_rs_hist(B2<const K*> keys2, B2<const uint32_t*> d_n2,
+struct RsRing {
+  K* k[3];
+  uint32_t* v[3];
+};
+// buffer i of problem e, by selects only (no struct or array copy of the argument)
+template <class K>
+__device__ __forceinline__ K* ring_key(const B2<RsRing<K>>& R2, int e, int i) {
+  K* a = i == 0 ? R2.v[0].k[0] : (i == 1 ? R2.v[0].k[1] : R2.v[0].k[2]);
+  K* b = i == 0 ? R2.v[1].k[0] : (i == 1 ? R2.v[1].k[1] : R2.v[1].k[2]);
+  return e ? b : a;
+}
+template <class K>
+__device__ __forceinline__ uint32_t* ring_val(const B2<RsRing<K>>& R2, int e, int i) {
+  uint32_t* a = i == 0 ? R2.v[0].v[0] : (i == 1 ? R2.v[0].v[1] : R2.v[0].v[2]);
+  uint32_t* b = i == 0 ? R2.v[1].v[0] : (i == 1 ? R2.v[1].v[1] : R2.v[1].v[2]);
+  return e ? b : a;
+}
+__device__ __forceinline__ uint32_t rs_active(uint32_t nbits, int fast_passes) {
+  return min(rs_plan(nbits).passes, (uint32_t)fast_passes);
+}
+__device__ __forceinline__ int rs_src(int p, uint32_t P, bool three) {
+  return (three && P == 3u) ? (p == 0 ? 0 : (p == 1 ? 2 : 1)) : (p & 1);
+}
+__device__ __forceinline__ int rs_dst(int p, uint32_t P, bool three) {
+  return (three && P == 3u) ? (p == 0 ? 2 : (p == 1 ? 1 : 0)) : ((p & 1) ^ 1);
+}
+
+template <class K>
+__global__ void __launch_bounds__(ST) k_rs_hist(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2,
                                                 B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
-                                                uint32_t nblocks) {
+                                                uint32_t nblocks, int fast_passes) {
   KT();
   const int e = blockIdx.y;
-  const K* __restrict__ keys = keys2[e];
+  const bool three = ring_key(R2, e, 2) != nullptr;
+  const K* __restrict__ keys = ring_key(R2, e, rs_src(pass, rs_active(*d_nbits2[e], fast_passes), three));
   uint32_t* __restrict__ hist = ss[e].hist;
   const RsPlan pl = rs_plan(*d_nbits2[e]);
   if ((uint32_t)pass >= pl.passes) return;
@@ -178,16 +211,19 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t n
 // writes each digit run to its global slot with consecutive lanes on consecutive
 // addresses.  *active (probe, may be null) is cleared when the pass is skipped.
 template <class K>
-__global__ void __launch_bounds__(ST) k_rs_scatter(B2<const K*> kin2, B2<const uint32_t*> vin2, B2<K*> kout2,
-                                                   B2<uint32_t*> vout2, B2<const uint32_t*> d_n2,
+__global__ void __launch_bounds__(ST) k_rs_scatter(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2,
                                                    B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
-                                                   uint32_t nblocks, int iota, uint32_t* __restrict__ active) {
+                                                   uint32_t nblocks, int iota, uint32_t* __restrict__ active,
+                                                   int fast_passes) {
   KT();
   const int e = blockIdx.y;
-  const K* __restrict__ kin = kin2[e];
-  const uint32_t* __restrict__ vin = vin2[e];
-  K* __restrict__ kout = kout2[e];
-  uint32_t* __restrict__ vout = vout2[e];
+  const uint32_t P = rs_active(*d_nbits2[e], fast_passes);
+  const bool three = ring_key(R2, e, 2) != nullptr;
+  const int si = rs_src(pass, P, three), di = rs_dst(pass, P, three);
+  const K* __restrict__ kin = ring_key(R2, e, si);
+  const uint32_t* __restrict__ vin = ring_val(R2, e, si);
+  K* __restrict__ kout = ring_key(R2, e, di);
+  uint32_t* __restrict__ vout = ring_val(R2, e, di);
   const uint32_t* __restrict__ hist = ss[e].hist;
   const uint32_t* __restrict__ tot = ss[e].tot;
   const RsPlan pl = rs_plan(*d_nbits2[e]);
@@ -402,16 +438,16 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
 }
 
 template <class K>
-__global__ void k_rs_copyback(B2<const K*> k12, B2<const uint32_t*> v12, B2<K*> k02, B2<uint32_t*> v02,
-                              B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2, int max_passes) {
+__global__ void k_rs_copyback(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2,
+                              int max_passes) {
   KT();
   const int e = blockIdx.y;
-  const uint32_t p = min(rs_plan(*d_nbits2[e]).passes, (uint32_t)max_passes);
-  if ((p & 1u) == 0u) return;
-  const K* __restrict__ k1 = k12[e];
-  const uint32_t* __restrict__ v1 = v12[e];
-  K* __restrict__ k0 = k02[e];
-  uint32_t* __restrict__ v0 = v02[e];
+  const uint32_t p = rs_active(*d_nbits2[e], max_passes);
+  if ((p & 1u) == 0u || (p == 3u && ring_key(R2, e, 2) != nullptr)) return;  // even, or rotated home
+  const K* __restrict__ k1 = ring_key(R2, e, 1);
+  const uint32_t* __restrict__ v1 = ring_val(R2, e, 1);
+  K* __restrict__ k0 = ring_key(R2, e, 0);
+  uint32_t* __restrict__ v0 = ring_val(R2, e, 0);
   const uint32_t n = *d_n2[e];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     k0[i] = k1[i];
@@ -422,25 +458,25 @@ __global__ void k_rs_copyback(B2<const K*> k12, B2<const uint32_t*> v12, B2<K*> 
 template <class K>
 void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n, uint32_t cap,
                 B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s, hipStream_t st,
-                int nbatch, B2<const uint32_t*> tail_need) {
+                int nbatch, B2<const uint32_t*> tail_need, B2<K*> k2, B2<uint32_t*> v2) {
   const uint32_t nb = sort_blocks(cap);
   if (nb == 0) return;
   if (fast_bits == 0 && iota) throw Error(FCCF_E_INTERNAL, "radix_sort: a tail-only sort takes its values as input");
   if ((v0[0] == nullptr) != (v1[0] == nullptr)) throw Error(FCCF_E_INTERNAL, "radix_sort: both or no value buffers");
+  if ((k2[0] == nullptr) != (k2[nbatch > 1 ? 1 : 0] == nullptr) || (k2[0] && (v2[0] == nullptr) != (v0[0] == nullptr)))
+    throw Error(FCCF_E_INTERNAL, "radix_sort: third buffer on every problem, values with values");
   const int fast_passes = fast_bits / 8;
-  B2<K*> kb[2] = {k0, k1};
-  B2<uint32_t*> vb[2] = {v0, v1};
+  B2<RsRing<K>> R;
+  for (int e = 0; e < 2; ++e) R.v[e] = RsRing<K>{{k0[e], k1[e], k2[e]}, {v0[e], v1[e], v2[e]}};  // host side
   for (int p = 0; p < fast_passes; ++p) {  // pass p: digit p of the device-side plan (rs_plan)
-    const int src = p & 1, dst = src ^ 1;
-    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(kb[src], d_n, d_nbits, p, s, nb);
+    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(R, d_n, d_nbits, p, s, nb, fast_passes);
     k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
     const double eb = 2.0 * (sizeof(K) + (v0[0] ? 4 : 0));  // algorithmic bytes per element
-    FCCF_LAUNCH("k_rs_scatter", (d_n[0], eb, nbatch > 1 ? d_n[1] : nullptr, eb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, B2<const K*>(kb[src]), B2<const uint32_t*>(vb[src]), kb[dst], vb[dst], d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active());
+    FCCF_LAUNCH("k_rs_scatter", (d_n[0], eb, nbatch > 1 ? d_n[1] : nullptr, eb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
   }
   if (fast_passes) {
     const uint32_t g = min(nb * 8u, 2048u);
-    k_rs_copyback<K><<<dim3(g, nbatch), 256, 0, st>>>(B2<const K*>(k1), B2<const uint32_t*>(v1), k0, v0, d_n, d_nbits,
-                                                    fast_passes);
+    k_rs_copyback<K><<<dim3(g, nbatch), 256, 0, st>>>(R, d_n, d_nbits, fast_passes);
   }
   if (fast_bits < (int)(8 * sizeof(K)))
     k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_bits, tail_need);
@@ -631,12 +667,13 @@ SortScratch sort_scratch_carve(void* base, uint32_t cap) {
 void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                     uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
                     hipStream_t st, int nbatch, B2<const uint32_t*> tail_need) {
-  radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need);
+  radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need,
+                       B2<uint32_t*>(nullptr), B2<uint32_t*>(nullptr));
 }
 void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                     uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need) {
-  radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need);
+                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need, B2<uint64_t*> k2, B2<uint32_t*> v2) {
+  radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need, k2, v2);
 }
 void segment_heads_u32(B2<const uint32_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
                        B2<uint32_t*> starts, B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,

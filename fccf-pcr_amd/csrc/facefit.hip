@@ -516,7 +516,8 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   // codes are 3 bits per octree level (+1): 4 fast passes cover depth <= 10, i.e.
   // extents up to ~1000 x face_voxel_size; deeper trees finish in the tail launch
   radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 32, true,
-                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch);
+                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B2<const uint32_t*>(nullptr),
+                 pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
   segment_heads_u64(B2<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
                     pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
                     st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);

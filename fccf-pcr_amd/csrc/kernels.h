@@ -158,8 +158,8 @@ struct GrowParams {
 void grow_device(const GrowIn in[2], const GrowDev out[2], const GrowParams& P, hipStream_t st);
 
 struct FaceBufs {
-  uint64_t *c0, *c1;       // codes, cap each
-  uint32_t *v0, *v1;       // cap each
+  uint64_t *c0, *c1, *c2;  // codes, cap each (c2: the sort's third buffer)
+  uint32_t *v0, *v1, *v2;  // cap each
   uint32_t* starts;        // cap + 1
   float* aggr;             // octree-bounds aggregates, aggr_floats(cap) (see block_aggr)
   OctState* oct;

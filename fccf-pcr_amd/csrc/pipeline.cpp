@@ -161,7 +161,7 @@ size_t cloud_bytes(uint32_t cap, bool) {
   size_t b = 0;
   b += 12 * N * 3 + 64;                                        // ds1, ds1f, ds2
   b += voxel_grid_bytes(cap);                                  // K1
-  b += 2 * 8 * N + 2 * 4 * N + 4 * (N + 1);                    // codes, vals, starts
+  b += 3 * 8 * N + 3 * 4 * N + 4 * (N + 1);                    // codes, vals (3 buffers), starts
   b += 4 * aggr_floats(cap) + 256;                             // aggregates, state, centroid
   b += sizeof(VoxRec) * N + 4 * 4 * N + 64;                    // leaf records, flags, offsets
   b += 12 * N + 4 * N;                                         // sorted points, leaf of point

@@ -31,7 +31,7 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
 // null for the caller to point at its compute3DCentroid output.
 inline size_t face_bufs_bytes(uint32_t cap) {
   const size_t N = cap;
-  return 2 * 8 * N + 2 * 4 * N + 4 * (N + 1) + 4 * aggr_floats(cap) + 256 + sizeof(VoxRec) * N + 4 * 4 * N + 64 +
+  return 3 * 8 * N + 3 * 4 * N + 4 * (N + 1) + 4 * aggr_floats(cap) + 256 + sizeof(VoxRec) * N + 4 * 4 * N + 64 +
          12 * N + 4 * N + sort_scratch_bytes(cap) + 24 * 256;
 }
 
@@ -39,8 +39,10 @@ inline FaceBufs face_bufs_carve(Arena& a, uint32_t cap) {
   FaceBufs f;
   f.c0 = a.take_n<uint64_t>(cap);
   f.c1 = a.take_n<uint64_t>(cap);
+  f.c2 = a.take_n<uint64_t>(cap);
   f.v0 = a.take_n<uint32_t>(cap);
   f.v1 = a.take_n<uint32_t>(cap);
+  f.v2 = a.take_n<uint32_t>(cap);
   f.starts = a.take_n<uint32_t>((size_t)cap + 1);
   f.aggr = a.take_n<float>(aggr_floats(cap));
   f.oct = a.take_n<OctState>(1);
