@@ -55,11 +55,11 @@ struct B2 {
 // digits).  The sorted result is always left in (k0, v0); (k1, v1) are temporaries.
 // If vals_iota, v0 is ignored on input and the values are the input positions.
 // Keys-only: v0 = v1 = null (no value traffic).
-// cap bounds every problem's count.  The first fast_bits (a multiple of 8) run as
-// device-wide passes (3 launches each, a pass past *d_nbits exits at once); any
-// higher bits run in one single-workgroup tail launch (k_rs_tail), which also
-// exits at once unless needed.  tail_need (optional): the tail runs only where
-// *tail_need != 0 (fast_bits == 0: a sort of keys usually already in order).
+// cap bounds every problem's count.  fast_bits / 8 passes of the device-side digit
+// plan run as device-wide passes (3 launches each, a pass past the plan exits at
+// once); the bits they leave run in one single-workgroup tail launch (k_rs_tail),
+// which also exits at once unless needed.  tail_need (optional): the tail runs only
+// where *tail_need != 0 (fast_bits == 0: a sort of keys usually already in order).
 void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
                     uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
                     hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));

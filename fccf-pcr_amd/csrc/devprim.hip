@@ -314,17 +314,20 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<RsRing<K>> R2, B2<const ui
 // The high passes of a sort, for keys wider than the fast passes cover (octree
 // codes of very large extents), or the whole sort of keys that are normally already
 // in order (VoxelGrid's second pass; `need` = its "unsorted" flag): one workgroup per
-// problem runs the stable 8-bit LSD passes [lo_bit, nbits) over all tiles in order.
+// problem runs the stable 8-bit LSD passes [lo, nbits) over all tiles in order, lo =
+// the bits the fast_passes launched passes of the device plan covered.
 // Slow (one CU) but a single launch that exits at once in the common case, where
 // the launches of never-needed fast passes would each cost a kernel boundary.
 template <class K>
 __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B2<K*> k12, B2<uint32_t*> v12,
-                                                B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2, int lo_bit,
-                                                B2<const uint32_t*> need2) {
+                                                B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2,
+                                                int fast_passes, B2<const uint32_t*> need2) {
   KT();
   const int e = blockIdx.y;
   const uint32_t nbits = *d_nbits2[e], n = *d_n2[e];
-  if ((uint32_t)lo_bit >= nbits || n < 2) return;
+  const RsPlan pl = rs_plan(nbits);
+  const uint32_t lo_bit = pl.passes <= (uint32_t)fast_passes ? nbits : (uint32_t)fast_passes * pl.width;
+  if (lo_bit >= nbits || n < 2) return;
   if (need2[e] && *need2[e] == 0u) return;
   K* kb[2] = {k02[e], k12[e]};
   uint32_t* vb[2] = {v02[e], v12[e]};
@@ -335,7 +338,7 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
   __shared__ uint32_t sv[SORT_TILE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   int src = 0;
-  for (uint32_t shift = (uint32_t)lo_bit; shift < nbits; shift += 8) {
+  for (uint32_t shift = lo_bit; shift < nbits; shift += 8) {
     const K* __restrict__ kin = kb[src];
     const uint32_t* __restrict__ vin = vb[src];
     K* __restrict__ kout = kb[src ^ 1];
@@ -479,7 +482,7 @@ void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<con
     k_rs_copyback<K><<<dim3(g, nbatch), 256, 0, st>>>(R, d_n, d_nbits, fast_passes);
   }
   if (fast_bits < (int)(8 * sizeof(K)))
-    k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_bits, tail_need);
+    k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_passes, tail_need);
 }
 
 // ---------------------------------------------------------------- segments / scan

@@ -513,9 +513,12 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
   const B2<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
   k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B2<const OctState*>(oct), res, c0, nbits);
-  // codes are 3 bits per octree level (+1): 4 fast passes cover depth <= 10, i.e.
-  // extents up to ~1000 x face_voxel_size; deeper trees finish in the tail launch
-  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 32, true,
+  // codes are 3 bits per octree level (+1): 3 fast passes of <= 9-bit digits cover
+  // depth <= 8, i.e. extents up to ~256 x face_voxel_size (c3: depth 6, 19 bits);
+  // deeper trees finish in the tail launch.  (A fourth fast pass cost ~6 us of no-op
+  // launches per registration.)  With the third buffer a three-pass sort ends in
+  // (c0, v0) without a copy-back.
+  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 24, true,
                  pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B2<const uint32_t*>(nullptr),
                  pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
   segment_heads_u64(B2<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
