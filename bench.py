@@ -129,7 +129,7 @@ def cpu_baseline(src, tar, leaf, budget_s):
     the reference's std::sort) on the same workload, repeated within a time budget,
     pinned to one host core (taskset-style pinning, CPU model recorded)."""
     import oracle_py
-    times, K, stages, ref_win = [], None, None, []
+    times, K, stages, ref_win, T = [], None, None, [], None
     try:
         prev = os.sched_getaffinity(0)
         core = min(prev)
@@ -143,6 +143,7 @@ def cpu_baseline(src, tar, leaf, budget_s):
             run = oracle_py.Run(src, tar, leaf, oracle_py.INTROSORT)
             times.append(time.perf_counter() - t0)
             K = int(run.get("counts", np.int64)[0])
+            T = run.T.copy()
             stages = run.times()
             ref_win.append(times[-1] * 1e3 - float(run.get("main_vg_ms", np.float64)[0]))
             del run
@@ -151,14 +152,43 @@ def cpu_baseline(src, tar, leaf, budget_s):
             os.sched_setaffinity(0, prev)
     med = statistics.median(times)
     names = ["downsample", "voxelfit", "grow_select", "match", "cluster", "verify", "fine", "fuse", "total"]
-    return {"value": K / med, "unit": "correspondences/s", "cores": 1, "kind": "port",
-            "ms_per_registration": med * 1e3, "K": K, "pinned_cpu": core, "cpu_model": cpu_model(),
-            "host_nproc": os.cpu_count(),
-            "stage_ms_last": {n: round(float(v), 3) for n, v in zip(names, stages)} if stages is not None else None,
-            # the reference's own timer window (FCCF.cpp:1681-1685) excludes main's VoxelGrid
-            "ref_window_ms_median": statistics.median(ref_win),
-            "sample": f"{len(times)} full registrations of the same c3 pair (median), oracle/ C++ restatement, "
-                      f"introsort summation order, 1 thread pinned to CPU {core}"}
+    out = {"value": K / med, "unit": "correspondences/s", "cores": 1, "kind": "port",
+           "ms_per_registration": med * 1e3, "K": K, "pinned_cpu": core, "cpu_model": cpu_model(),
+           "host_nproc": os.cpu_count(),
+           "stage_ms_last": {n: round(float(v), 3) for n, v in zip(names, stages)} if stages is not None else None,
+           # the reference's own timer window (FCCF.cpp:1681-1685) excludes main's VoxelGrid
+           "ref_window_ms_median": statistics.median(ref_win),
+           "sample": f"{len(times)} full registrations of the same c3 pair (median), oracle/ C++ restatement, "
+                     f"introsort summation order, 1 thread pinned to CPU {core}"}
+    return out, T  # T: the oracle's transform (the parity check against the GPU's)
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a, np.float32).view(np.uint32),
+                          np.ascontiguousarray(b, np.float32).view(np.uint32))
+
+
+def parity_pass(F, ctx, configs):
+    """Parity of the product against the oracle (introsort order = the reference's
+    std::sort VoxelGrid), outside the timed region: per BASELINE config, one GPU
+    registration from host arrays (fccf_register) and one oracle registration of the
+    same synthetic pair; the 4x4 transforms must be equal bit for bit and the
+    correspondence test counts K (FCCF.cpp:1415-1427) equal.  Returns
+    {config: verdict}; any mismatch ends the bench without a JSON line."""
+    import oracle_py
+    out = {}
+    for name in configs:
+        cfg = F.CONFIGS[name]
+        src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
+        Tg, st = ctx.register(src, tar, cfg["leaf"])
+        run = oracle_py.Run(src, tar, cfg["leaf"], oracle_py.INTROSORT)
+        To, Ko = run.T.copy(), int(run.get("counts", np.int64)[0])
+        del run
+        if not same_bits(Tg, To) or int(st.K) != Ko:
+            raise SystemExit(f"bench.py: parity FAILED at {name}: GPU K {int(st.K)} T\n{Tg}\n"
+                             f"oracle K {Ko} T\n{To}")
+        out[name] = "bit-exact"
+    return out
 
 
 class _SelftestCtx:
@@ -287,6 +317,10 @@ def main():
     ap.add_argument("--rccl-shard", action="store_true",
                     help="N>1, informational: also time registrations of ONE pair by all ranks with the "
                          "correspondence search sharded over an RCCL group (fccf_group_create)")
+    ap.add_argument("--parity-configs", default=None,
+                    help="comma-separated BASELINE configs checked bit for bit against the oracle after the "
+                         "timed region (default c2,c4,c5 at N=1, none at N>1; the bench's own config is always "
+                         "checked on rank 0)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="time K sequential fccf_register_device calls instead of one pipelined batch of K")
     args = ap.parse_args()
@@ -400,6 +434,11 @@ def main():
                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe, args.config), "kernel": probe,
                         "avg_launch_us": avg_s * 1e6, "algorithmic_bytes_per_launch": pb / pn,
                         "launches_per_step": pn / args.steps}
+    # parity against the oracle, after every timed or probed run (other sizes re-capture graphs)
+    parity = None
+    if rank == 0 and not args.selftest:
+        pc = args.parity_configs if args.parity_configs is not None else ("c2,c4,c5" if ws == 1 else "")
+        parity = parity_pass(F, ctx, [c for c in pc.split(",") if c and c != args.config])
     elapsed = allmax(dist, elapsed)
     Ks_all = allsum(dist, float(Ks))
     ctx.free(d_src)
@@ -449,12 +488,21 @@ def main():
             out["roofline"] = roofline
             out["kernel_table"] = {k: {a: (round(b, 4) if isinstance(b, float) else b) for a, b in v.items()}
                                    for k, v in table.items()}
+        T_oracle = None
         if ws == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(src, tar, leaf, args.cpu_budget)
+            out["cpu_baseline"], T_oracle = cpu_baseline(src, tar, leaf, args.cpu_budget)
             # the CPU and GPU runs must do the same work (same plane pairs, same K)
             if out["cpu_baseline"]["K"] != out["K_per_registration"]:
                 raise SystemExit(f"bench.py: cpu_baseline K {out['cpu_baseline']['K']} != GPU K "
                                  f"{out['K_per_registration']}")
+        if parity is not None:
+            if T_oracle is None:  # no CPU baseline leg: one oracle registration of the bench's pair
+                import oracle_py
+                T_oracle = oracle_py.Run(src, tar, leaf, oracle_py.INTROSORT).T.copy()
+            # the timed registrations' T (every step returned the same bits, asserted above)
+            if not same_bits(T, T_oracle):
+                raise SystemExit(f"bench.py: parity FAILED at {args.config}: GPU T\n{T}\noracle T\n{T_oracle}")
+            out["parity"] = dict({args.config: "bit-exact"}, **parity)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

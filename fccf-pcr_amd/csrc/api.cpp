@@ -19,40 +19,6 @@
 
 using namespace fccf;
 
-extern "C" void fccf_params_default(fccf_params* p) {
-  if (!p) return;
-  // FCCF.cpp:126-175
-  p->parameter_l1 = 0.5f; p->parameter_l2 = 1.0f; p->parameter_k1 = 5.0f; p->parameter_k2 = 2.0f;
-  p->normal_vector_threshold1 = 5.0f; p->normal_vector_threshold2 = 8.0f;
-  p->face_voxel_size = 1.0f;
-  p->voxel_point_threshold = 5;
-  p->curvature_threshold = 0.05f;
-  p->select_plane_number = 15;
-  p->quick_verify_angel_threshold = 10.0f; p->quick_verify_distance_threshold = 2.0f;
-  p->required_optimize_plane = 4.0f;
-  p->fine_verify_voxel_size = 0.5f; p->fine_verify_number = 4;
-  p->included_angle_same_threshold = 5.0f; p->included_angle_min_threshold = 30.0f;
-  p->included_angle_max_threshold = 150.0f;
-  p->third_plane_threshold = 0.5f; p->third_plane_normal_threshold = 5.0f;
-  p->cluster_number_threshold = 10; p->cluster_angel_threshold = 2.0f; p->cluster_distance_threshold = 0.8f;
-  p->seclct_cluster_number = 200;
-  p->rough_threshold_gl = 2;
-}
-
-extern "C" const char* fccf_strerror(int code) {
-  switch (code) {
-    case FCCF_OK: return "ok";
-    case FCCF_E_ARG: return "invalid argument";
-    case FCCF_E_HIP: return "HIP runtime error";
-    case FCCF_E_RCCL: return "collective error";
-    case FCCF_E_OOM: return "out of memory";
-    case FCCF_E_IO: return "I/O error";
-    case FCCF_E_INTERNAL: return "internal error";
-    case FCCF_E_NODEVICE: return "no usable HIP device";
-    default: return "unknown error";
-  }
-}
-
 extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   if (!out) return FCCF_E_ARG;
   *out = nullptr;
@@ -68,6 +34,7 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   bool ok = true;
   for (auto& s : c->sa) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
   ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->d_flags, 256) == hipSuccess && hipMemset(c->d_flags, 0, 256) == hipSuccess;
   for (auto& cs : c->cs) {
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (auto& e : cs.tev) ok = ok && hipEventCreate(&e) == hipSuccess;
@@ -85,6 +52,12 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   if (!c) return FCCF_E_ARG;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
+  // a group still attached is detached, not destroyed: its handle stays the caller's,
+  // and fccf_group_destroy then only releases the communicator
+  if (c->group) {
+    c->group->ctx = nullptr;
+    c->group = nullptr;
+  }
   pipeline_release(c);
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.reset();
@@ -100,6 +73,7 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   for (auto& s : c->sa)
     if (s) (void)hipStreamDestroy(s);
   if (c->sb) (void)hipStreamDestroy(c->sb);
+  if (c->d_flags) (void)hipFree(c->d_flags);
   delete c;
   return FCCF_OK;
 }
@@ -187,14 +161,18 @@ int stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float
     uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
     VGBufs b = voxel_grid_carve(c->arena2, cap);
     b.is.stats = 1;  // path counters for fccf_debug_sort_stats
+    b.is.inject = c->d_flags;
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(&b.params->sort_err, 0, 4, st));  // (a presorted pass alone does not clear it)
     voxel_grid(d_in, d_sc, cap, leaf, d_out, d_sc + 1, b, st, presorted);
     HIP_CHECK(hipGetLastError());
-    uint32_t hm = 0;
+    uint32_t hm = 0, err = 0;
     HIP_CHECK(hipMemcpyAsync(&hm, d_sc + 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&err, &b.params->sort_err, 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    if (err) throw Error(FCCF_E_INTERNAL, "VoxelGrid: K1 sort invariant violated (flags " + std::to_string(err) + ")");
     HIP_CHECK(hipMemcpyAsync(out, d_out, 12 * (size_t)hm, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     *m = hm;
@@ -234,6 +212,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     uint32_t* d_sc = c->arena2.take_n<uint32_t>(64);
     VGBufs b = voxel_grid_carve(c->arena2, cap);
     b.is.stats = 1;  // path counters for fccf_debug_sort_stats
+    b.is.inject = c->d_flags;
     uint32_t hn = (uint32_t)n;
     HIP_CHECK(hipMemcpyAsync(d_sc, &hn, 4, hipMemcpyHostToDevice, st));
     if (n) HIP_CHECK(hipMemcpyAsync(b.k0, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
@@ -305,6 +284,16 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    if (c->sort_stats[2] & IS_FAULT_MASK)
+      throw Error(FCCF_E_INTERNAL, "K1 sort invariant violated (flags " + std::to_string(c->sort_stats[2]) + ")");
+  });
+}
+
+extern "C" int fccf_debug_inject_sort_fault(fccf_ctx* c, uint32_t bits) {
+  if (!c || (bits & ~IS_FAULT_MASK)) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    HIP_CHECK(hipDeviceSynchronize());  // no sort of this ctx in flight reads the word meanwhile
+    HIP_CHECK(hipMemcpy(c->d_flags, &bits, 4, hipMemcpyHostToDevice));
   });
 }
 

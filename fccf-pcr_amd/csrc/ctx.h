@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/fccf.h"
+#include "error.h"
 #include "ingest.h"
 #include "pool.h"
 #include "probe.h"
@@ -21,11 +22,6 @@
 namespace fccf {
 
 struct Group;
-
-struct Error : std::runtime_error {
-  int code;
-  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
 
 #define HIP_CHECK(x)                                                                          \
   do {                                                                                        \
@@ -255,6 +251,7 @@ struct fccf_ctx {
   bool cluster_device = false;  // transform_cluster's seeds, sort and averaging on the GPU (cluster.hip)
   fccf::Arena arena_v;       // device quick_verify batch (candidates in, refined T / scores out)
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
+  uint32_t* d_flags = nullptr;   // device words (zeroed at creation): [0] injected K1 sort faults (test hook)
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;
 

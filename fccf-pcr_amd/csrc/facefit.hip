@@ -443,6 +443,7 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
   if (mail && blockIdx.x == 0 && threadIdx.x < 8) {
     const uint32_t i = threadIdx.x & 3u;
     if (threadIdx.x < 4) mail->sc[e][i] = sc2[e][i];
+    else if (i == 1) mail->fsc[e][1] = B.vgp ? B.vgp->sort_err : 0u;  // both VoxelGrid passes' sort flags
     else mail->fsc[e][i] = B.nleaf[i];
   }
   // the cloud stage's device spans: the stamps of main's pass, the driver's pass and the
@@ -513,12 +514,14 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
   const B2<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
   k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B2<const OctState*>(oct), res, c0, nbits);
-  // codes are 3 bits per octree level (+1): 3 fast passes of <= 9-bit digits cover
-  // depth <= 8, i.e. extents up to ~256 x face_voxel_size (c3: depth 6, 19 bits);
-  // deeper trees finish in the tail launch.  (A fourth fast pass cost ~6 us of no-op
-  // launches per registration.)  With the third buffer a three-pass sort ends in
-  // (c0, v0) without a copy-back.
-  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 24, true,
+  // codes are 3 bits per octree level (+1): the device plan takes 3 passes of <= 9-bit
+  // digits up to depth 8 (extents up to ~256 x face_voxel_size; c3: depth 6, 19 bits)
+  // and 4 passes of 8 bits at depth 9-10 (~1 km at 1 m voxels, outdoor scans), so four
+  // fast passes are launched: at depth <= 8 the fourth exits at once (~6 us of no-op
+  // launches per registration), and only trees deeper than 10 levels reach the
+  // single-workgroup tail launch.  With the third buffer a three-pass sort ends in
+  // (c0, v0) without a copy-back; a four-pass sort ends there by ping-pong.
+  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 32, true,
                  pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B2<const uint32_t*>(nullptr),
                  pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
   segment_heads_u64(B2<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),

@@ -29,6 +29,23 @@ namespace fccf {
     if (r_ != ncclSuccess) throw ::fccf::Error(FCCF_E_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+// An open ncclGroupStart is always closed: a call that fails inside the group ends it
+// (ncclGroupEnd) before the error propagates, so the communicator stays usable.
+struct NcclGroup {
+  bool open = false;
+  NcclGroup() {
+    NCCL_CHECK(ncclGroupStart());
+    open = true;
+  }
+  void end() {
+    open = false;
+    NCCL_CHECK(ncclGroupEnd());
+  }
+  ~NcclGroup() {
+    if (open) (void)ncclGroupEnd();
+  }
+};
+
 void shard_range(int n, int rank, int world, int* lo, int* hi) {
   const int q = n / world, r = n % world;
   *lo = rank * q + std::min(rank, r);
@@ -64,18 +81,20 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
   }
   *kpass_all = kp;
   // all-gather-v: one broadcast per (root, type) inside one group; empty blocks skipped
-  NCCL_CHECK(ncclGroupStart());
-  for (int r = 0; r < n; ++r)
-    for (int t = 0; t < 3; ++t) {
-      const size_t cnt = h[4 + 4 * r + t];
-      if (!cnt) continue;
-      const size_t b = base[(size_t)r * 3 + t];
-      NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)q_loc[t] : (const void*)(q_all[t] + b), q_all[t] + b, cnt * sizeof(QTd),
-                               ncclUint8, r, g->comm, st));
-      NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)c_loc[t] : (const void*)(c_all[t] + b), c_all[t] + b, cnt * sizeof(MCand),
-                               ncclUint8, r, g->comm, st));
-    }
-  NCCL_CHECK(ncclGroupEnd());
+  {
+    NcclGroup grp;
+    for (int r = 0; r < n; ++r)
+      for (int t = 0; t < 3; ++t) {
+        const size_t cnt = h[4 + 4 * r + t];
+        if (!cnt) continue;
+        const size_t b = base[(size_t)r * 3 + t];
+        NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)q_loc[t] : (const void*)(q_all[t] + b), q_all[t] + b,
+                                 cnt * sizeof(QTd), ncclUint8, r, g->comm, st));
+        NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)c_loc[t] : (const void*)(c_all[t] + b), c_all[t] + b,
+                                 cnt * sizeof(MCand), ncclUint8, r, g->comm, st));
+      }
+    grp.end();
+  }
   h[0] = tot_all[0];
   h[1] = tot_all[1];
   h[2] = tot_all[2];

@@ -13,6 +13,61 @@
 
 namespace fccf {
 
+namespace {
+
+// ------------------------------------------------------------ exact angle cuts
+// theta(c) is monotone non-increasing on [-1,1]; find c* with theta(c) > thr <=> c < gt
+// and theta(c) < thr <=> c > lt, then verify the claim around the cut.
+uint32_t okey(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+float okey_inv(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+AngleCut make_cut_impl(float thr) {
+  auto first_true = [](uint32_t lo, uint32_t hi, auto pred) {  // pred monotone false..true on [lo,hi]
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (pred(mid)) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  const uint32_t lo = okey(-1.0f), hi = okey(1.0f);
+  const uint32_t kg = first_true(lo, hi + 1, [&](uint32_t k) { return !(theta_of_cos_host(okey_inv(k)) > thr); });
+  const uint32_t kl = first_true(lo, hi + 1, [&](uint32_t k) { return theta_of_cos_host(okey_inv(k)) < thr; });
+  AngleCut c;
+  c.gt = okey_inv(kg);
+  c.lt = okey_inv(kl - 1);
+  for (int64_t d = -4096; d <= 4096; ++d) {  // monotonicity check around both cuts
+    for (uint32_t base : {kg, kl}) {
+      const int64_t k = (int64_t)base + d;
+      if (k < (int64_t)lo || k > (int64_t)hi) continue;
+      const float v = okey_inv((uint32_t)k);
+      const float th = theta_of_cos_host(v);
+      if ((th > thr) != (v >= -1.0f && v < c.gt) || (th < thr) != (v > c.lt && v <= 1.0f))
+        throw Error(FCCF_E_INTERNAL, "angle cut not monotone");
+    }
+  }
+  return c;
+}
+
+}  // namespace
+
+AngleCut make_cut(float thr) {  // memoised per thread: thresholds are few and fixed per call
+  static thread_local std::vector<std::pair<float, AngleCut>> memo;
+  for (const auto& m : memo)
+    if (m.first == thr) return m.second;
+  const AngleCut c = make_cut_impl(thr);
+  memo.push_back({thr, c});
+  return c;
+}
+
 static inline float angle_deg(float x1, float y1, float z1, float x2, float y2, float z2) {
   return theta_of_cos_host(normal_cos(x1, y1, z1, x2, y2, z2));
 }

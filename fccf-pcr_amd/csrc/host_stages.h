@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "../../include/fccf.h"
+#include "error.h"
 #include "fccf_math.h"
 #include "kernels.h"
 #include "pool.h"

@@ -78,6 +78,20 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// An invariant violation (IS_FAULT_*, kernels.h): recorded in the sort's ctl[2] and in
+// the cloud's VGParams::sort_err, which the host turns into FCCF_E_INTERNAL.
+__device__ __forceinline__ void is_fault(uint32_t* ctl, uint32_t* err, uint32_t bits) {
+  atomicOr(&ctl[2], bits);
+  if (err) atomicOr(err, bits);
+}
+// Test hook: the injected flags of `bits` (fccf_debug_inject_sort_fault), raised by the
+// caller's one designated thread.
+__device__ __forceinline__ void is_inject(const IsBufs& W, uint32_t bits) {
+  if (!W.inject) return;
+  const uint32_t b = *W.inject & bits;
+  if (b) is_fault(W.ctl, W.err, b);
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
@@ -428,6 +442,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
   const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (i == 0 && threadIdx.x == 0) atomicAdd(&W.rounds[r].pad, l - f);
+  if (r == 0 && t == 0 && e == 0 && threadIdx.x == 0) is_inject(W, IS_FAULT_SCATTER);
   // the tile's elements are loaded first: their latency overlaps the prefix below
   uint32_t kk[IS_TC], vv[IS_TC];
 #pragma unroll
@@ -516,7 +531,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     const uint32_t d = dst[c];
     if (d == IS_NONE) continue;
     if (d <= f || d >= l) {  // cannot happen; never write outside the segment
-      W.ctl[2] |= 0x100u;
+      is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
       continue;
     }
     Ko[d] = kk[c];
@@ -557,6 +572,7 @@ struct BlockLds {
   uint32_t bc[8];                   // broadcasts
   uint32_t sh[16];
   uint32_t* stat;                   // IsBufs::ctl
+  uint32_t* err;                    // IsBufs::err
   uint32_t son;                     // path counters on (IS_STATS && IsBufs::stats)
   // wave tasks of the current segment, packed off | n << 13 | depth << 24, handed
   // to the global list with one atomic per class when the segment is done
@@ -584,6 +600,7 @@ struct WaveLds {
   uint32_t stk[IS_STACK];
   uint32_t lstat[4];
   uint32_t* stat;
+  uint32_t* err;
   uint32_t son;  // path counters on (IS_STATS && IsBufs::stats)
 };
 
@@ -849,7 +866,7 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
   stk[sp++] = packed;
   for (uint32_t guard = 0; sp > 0; ++guard) {
     if (guard > 4 * IS_WCAP || sp >= IS_STACK / 2) {  // cannot happen
-      if (lane == 0) S.stat[2] |= 0x400u;
+      if (lane == 0) is_fault(S.stat, S.err, IS_FAULT_WAVE);
       break;
     }
     const uint32_t it = __builtin_amdgcn_readfirstlane(stk[--sp]);
@@ -1188,7 +1205,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
         }
       }
       if (S.bc[0] >= IS_STACK / 2 - 2) {  // cannot happen
-        S.stat[2] |= 0x1000u;
+        is_fault(S.stat, S.err, IS_FAULT_POP);
         S.bc[0] = 0;
       }
       S.bc[3] = go;
@@ -1376,9 +1393,11 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
   const uint32_t nsort = W.ctl[0];
+  if (blockIdx.x == 0 && e == 0 && threadIdx.x == 0) is_inject(W, IS_FAULT_BLOCK | IS_FAULT_POP);
   if (nsort == 0) return;
   if (threadIdx.x == 0) {
     S.stat = W.ctl;
+    S.err = W.err;
     S.son = IS_STATS && W.stats;
   }
   const uint32_t nfin = nchildren(W, R);
@@ -1427,7 +1446,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       __syncthreads();
       if (sp == 0) break;
       if (guard > 4 * (l - f) || sp >= IS_STACK / 2 - 2) {  // cannot happen: every step shrinks a segment
-        if (threadIdx.x == 0) W.ctl[2] |= 0x200u;
+        if (threadIdx.x == 0) is_fault(W.ctl, W.err, IS_FAULT_BLOCK);
         break;
       }
       const uint4 it = S.gstk[sp - 1];
@@ -1495,9 +1514,11 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
   WaveLds& S = WL[w];
   if (lane == 0) {
     S.stat = W.ctl;
+    S.err = W.err;
     S.son = IS_STATS && W.stats;
     for (int i = 0; i < 4; ++i) S.lstat[i] = 0;
   }
+  if (blockIdx.x == 0 && e == 0 && threadIdx.x == 0) is_inject(W, IS_FAULT_WAVE);
   wsync();
   // Static assignment, no queue: wave g of the grid takes tasks g, g + NW, g + 2 NW ...
   // of the list, which holds the large tasks first, so the largest ones are spread
@@ -1640,6 +1661,8 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.trace = nullptr;
   b.tier = introsort_tier();
   b.stats = 0;
+  b.err = nullptr;
+  b.inject = nullptr;
   return b;
 }
 

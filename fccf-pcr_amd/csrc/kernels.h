@@ -24,6 +24,9 @@ struct VGParams {
   const float* src;   // the pass's input points (set by k_vg_bbox, read by the later kernels)
   uint64_t t_main;    // s_memrealtime at the start of main's pass (k_vg_bbox<0>): stage spans
   uint64_t t_driver;  // ... and of the driver's remove-NaN + second pass (k_finite_fix)
+  uint32_t sort_err;  // K1 sort invariant flags of this cloud's passes (IS_FAULT_*), cleared by main's pass
+                      // entry (k_vg_bbox<0>); copied to the cloud mailbox, where the host turns them into
+                      // FCCF_E_INTERNAL
 };
 
 constexpr int VG_BBOX_BLOCKS = 512;
@@ -70,7 +73,18 @@ struct IsBufs {
   uint32_t segmax, maxtiles, ownmax, taskmax;
   uint32_t tier;        // rounds split segments longer than this (<= the owner's LDS capacity)
   uint32_t stats;       // path counters in ctl[3..15] (debug sorts; each costs a global atomic)
+  uint32_t* err;        // VGParams::sort_err of the pass's cloud (null: ctl[2] only)
+  const uint32_t* inject;  // test hook (fccf_debug_inject_sort_fault): IS_FAULT_* bits raised once per
+                           // sort by a designated thread at the matching site (null: off)
 };
+// Invariant flags of the sort (IsBufs::ctl[2], VGParams::sort_err).  Each marks a
+// state the algorithm cannot reach; any of them makes fccf_register* fail with
+// FCCF_E_INTERNAL instead of returning a transform from a wrong order.
+constexpr uint32_t IS_FAULT_SCATTER = 0x100u;  // a round's scatter destination outside its segment
+constexpr uint32_t IS_FAULT_BLOCK = 0x200u;    // a block item's stack or step guard exceeded
+constexpr uint32_t IS_FAULT_WAVE = 0x400u;     // a wave task's stack or step guard exceeded
+constexpr uint32_t IS_FAULT_POP = 0x1000u;     // a block item's partition stack overran
+constexpr uint32_t IS_FAULT_MASK = IS_FAULT_SCATTER | IS_FAULT_BLOCK | IS_FAULT_WAVE | IS_FAULT_POP;
 size_t introsort_bytes(uint32_t cap);
 IsBufs introsort_carve(void* base, uint32_t cap);
 int introsort_rounds(uint32_t cap);

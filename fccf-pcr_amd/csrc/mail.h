@@ -16,7 +16,8 @@ namespace fccf {
 struct CloudMail {                     // one per cloud set (double-buffered pairs)
   static constexpr uint32_t REC_CAP = 16384;   // planar 1 m voxels per cloud
   uint32_t sc[2][4];                   // per cloud: n_in, M1, M1 finite, M2
-  uint32_t fsc[2][4];                  // per cloud: leaves, -, planar leaves, residual points
+  uint32_t fsc[2][4];                  // per cloud: leaves, K1 sort fault flags (VGParams::sort_err),
+                                       // planar leaves, residual points
   uint64_t stamp[4];                   // s_memrealtime (100 MHz) when main's pass, the driver's pass,
                                        // the face stage and its last kernel started (fccf_stats dev_ms)
   VoxRec rec[2][REC_CAP];              // oriented planar records, Morton order

@@ -88,58 +88,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
   return g < 1 ? 1 : (g > mx ? mx : g);
 }
 
-// ------------------------------------------------------------ exact angle cuts
-// theta(c) is monotone non-increasing on [-1,1]; find c* with theta(c) > thr <=> c < gt
-// and theta(c) < thr <=> c > lt, then verify the claim around the cut.
-uint32_t okey(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-float okey_inv(uint32_t k) {
-  const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-AngleCut make_cut_impl(float thr) {
-  auto first_true = [](uint32_t lo, uint32_t hi, auto pred) {  // pred monotone false..true on [lo,hi]
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo) / 2;
-      if (pred(mid)) hi = mid;
-      else lo = mid + 1;
-    }
-    return lo;
-  };
-  const uint32_t lo = okey(-1.0f), hi = okey(1.0f);
-  const uint32_t kg = first_true(lo, hi + 1, [&](uint32_t k) { return !(theta_of_cos_host(okey_inv(k)) > thr); });
-  const uint32_t kl = first_true(lo, hi + 1, [&](uint32_t k) { return theta_of_cos_host(okey_inv(k)) < thr; });
-  AngleCut c;
-  c.gt = okey_inv(kg);
-  c.lt = okey_inv(kl - 1);
-  for (int64_t d = -4096; d <= 4096; ++d) {  // monotonicity check around both cuts
-    for (uint32_t base : {kg, kl}) {
-      const int64_t k = (int64_t)base + d;
-      if (k < (int64_t)lo || k > (int64_t)hi) continue;
-      const float v = okey_inv((uint32_t)k);
-      const float th = theta_of_cos_host(v);
-      if ((th > thr) != (v >= -1.0f && v < c.gt) || (th < thr) != (v > c.lt && v <= 1.0f))
-        throw Error(FCCF_E_INTERNAL, "angle cut not monotone");
-    }
-  }
-  return c;
-}
-
 }  // namespace
-
-AngleCut make_cut(float thr) {  // memoised per thread: thresholds are few and fixed per call
-  static thread_local std::vector<std::pair<float, AngleCut>> memo;
-  for (const auto& m : memo)
-    if (m.first == thr) return m.second;
-  const AngleCut c = make_cut_impl(thr);
-  memo.push_back({thr, c});
-  return c;
-}
 
 namespace {
 
@@ -377,6 +326,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
     carve_cloud(cs.arena, w[k], capmax, false);
+    w[k].vg.is.inject = c->d_flags;     // (test hook; a constant pointer per ctx)
     w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
     nv[k] = (uint32_t)ps.nin[k];
     xin[k] = hin[k];
@@ -455,6 +405,11 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     else vox[k] = d2h(w[k].planar, fsc[k][2], st0);  // past the mailbox: copy from HBM
   }
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
+  // K1's sort checks its invariants on the device (IS_FAULT_*): a violation means the
+  // VoxelGrid order may not be std::sort's, so no transform is returned
+  if (fsc[0][1] | fsc[1][1])
+    throw Error(FCCF_E_INTERNAL, "VoxelGrid: K1 sort invariant violated (flags cloud 0: " + std::to_string(fsc[0][1]) +
+                                     ", cloud 1: " + std::to_string(fsc[1][1]) + ")");
   {  // device spans of the cloud stage: its kernels' s_memrealtime stamps (100 MHz)
     float d[3] = {};
     for (int i = 0; i < 3; ++i)
@@ -1168,6 +1123,21 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   if (n <= 0) return;
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
+  // On an error (an exception out of a pair's phase B) the helper thread may still be
+  // staging or enqueueing the next pair with references into this frame: join it, and
+  // let the device finish what was enqueued, before the frame unwinds.
+  struct JoinOnUnwind {
+    fccf_ctx* c;
+    bool armed = true;
+    ~JoinOnUnwind() {
+      if (!armed) return;
+      try {
+        c->enq.wait();
+      } catch (...) {
+      }
+      (void)hipDeviceSynchronize();
+    }
+  } join_guard{c};
   // Host inputs: pair i+1's clouds are staged on the copy stream at the start of
   // pair i (from the helper thread: the pageable copy blocks its caller), so the host
   // link works while pair i's cloud stage runs.
@@ -1206,6 +1176,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   }
   c->enq.wait();
   phase_b2(c, (n - 1) & 1);
+  join_guard.armed = false;
 }
 
 }  // namespace fccf

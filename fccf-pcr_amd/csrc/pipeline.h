@@ -24,6 +24,7 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
   b.nseg = a.take_n<uint32_t>(16);
   b.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
   b.is = introsort_carve(a.take(introsort_bytes(cap)), cap);
+  b.is.err = &b.params->sort_err;
   return b;
 }
 

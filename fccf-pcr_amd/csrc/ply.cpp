@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <new>
 #include <sstream>
 #include <thread>
 
@@ -71,9 +72,12 @@ float bin_value(const unsigned char* p, const std::string& t, bool swap) {
   std::memcpy(&v, b, 8);
   return (float)v;
 }
-int64_t bin_count(const unsigned char* p, const std::string& t, bool swap) {
-  return (int64_t)bin_value(p, t, swap);
-}
+// A list count: -1 (rejected) unless it is a whole number in [0, 2^31) -- a count
+// from the file is never converted to an integer it does not fit.
+int64_t count_of(float v) { return (v >= 0.f && v < 2147483648.f) ? (int64_t)v : -1; }
+int64_t bin_count(const unsigned char* p, const std::string& t, bool swap) { return count_of(bin_value(p, t, swap)); }
+
+constexpr int64_t MAX_COUNT = 2147483647;  // element counts beyond int32 are rejected (PCL indexes with int)
 
 bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r'; }
 
@@ -230,8 +234,12 @@ int open(const char* path, File& f, int threads) {
     else if (w[0] == "element" && w.size() > 2) {
       Elem el;
       el.name = w[1];
-      el.count = std::atoll(w[2].c_str());
-      if (el.count < 0) return FCCF_E_IO;
+      // a count is a plain decimal number of at most int32 range: no wrap-around of the
+      // size checks below (rec * count, 12 * count) for any header
+      const std::string& cs = w[2];
+      if (cs.empty() || cs.size() > 10 || cs.find_first_not_of("0123456789") != std::string::npos) return FCCF_E_IO;
+      el.count = std::atoll(cs.c_str());
+      if (el.count < 0 || el.count > MAX_COUNT) return FCCF_E_IO;
       f.elems.push_back(el);
     } else if (w[0] == "property") {
       if (f.elems.empty() || w.size() < 3) return FCCF_E_IO;
@@ -278,6 +286,8 @@ int open(const char* path, File& f, int threads) {
       body = index_rows(f.data, f.size, body, f.elems[(size_t)i].count, nullptr, threads);
       if (body == (size_t)-1) return FCCF_E_IO;
     }
+    // n rows need n - 1 newlines after the body start: check before the row index is allocated
+    if (f.n > 0 && (uint64_t)(f.n - 1) > (uint64_t)(f.size - body)) return FCCF_E_IO;
     if (index_rows(f.data, f.size, body, f.n, &f.rowoff, threads) == (size_t)-1) return FCCF_E_IO;
     return FCCF_OK;
   }
@@ -298,6 +308,7 @@ int open(const char* path, File& f, int threads) {
   };
   for (int i = 0; i < f.vi; ++i) {
     const Elem& el = f.elems[(size_t)i];
+    if (el.props.empty()) continue;  // zero-byte rows
     for (int64_t r = 0; r < el.count; ++r)
       if (!walk_row(el, body)) return FCCF_E_IO;
   }
@@ -311,10 +322,13 @@ int open(const char* path, File& f, int threads) {
     off += V.props[j].size;
   }
   f.rec = off;
+  // rec <= 8 bytes per property and n < 2^31: the products below cannot wrap in 64 bits
   if (f.fixed) {
-    if (f.vbase + (size_t)f.rec * (size_t)f.n > f.size) return FCCF_E_IO;
+    if ((uint64_t)f.rec * (uint64_t)f.n > (uint64_t)(f.size - f.vbase)) return FCCF_E_IO;
     return FCCF_OK;
   }
+  // a vertex row holds at least its x, y, z bytes: bound n by the data before allocating
+  if ((uint64_t)f.n * 3u > (uint64_t)(f.size - f.vbase)) return FCCF_E_IO;
   f.rowoff.resize((size_t)f.n);
   for (int64_t r = 0; r < f.n; ++r) {
     f.rowoff[(size_t)r] = body;
@@ -374,8 +388,8 @@ int decode(const File& f, int64_t r0, int64_t nr, float* out) {
       const Prop& pr = V.props[j];
       size_t len;
       const char* s = next_token(p, e, len);
-      if (pr.is_list) {
-        const int64_t c = (int64_t)std::max(0.f, ascii_value(s, len, pr.count_type));
+      if (pr.is_list) {  // (a row holds at most e - p more tokens)
+        const int64_t c = std::min<int64_t>(std::max<int64_t>(count_of(ascii_value(s, len, pr.count_type)), 0), e - p);
         for (int64_t k = 0; k < c; ++k) (void)next_token(p, e, len);
         continue;
       }
@@ -398,29 +412,47 @@ extern "C" int fccf_ply_read(const char* path, float** out, int64_t* nout) {
   if (!path || !out || !nout) return FCCF_E_ARG;
   *out = nullptr;
   *nout = 0;
-  const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  fccf::ply::File f;
-  if (int rc = fccf::ply::open(path, f, T)) return rc;
-  float* xyz = (float*)std::malloc(sizeof(float) * 3 * (size_t)(f.n ? f.n : 1));
-  if (!xyz) return FCCF_E_OOM;
-  // rows in T contiguous ranges on T threads
-  std::vector<int> rc(T, FCCF_OK);
-  std::vector<std::thread> th;
-  auto part = [&](int t) {
-    const int64_t a = f.n * t / T, b = f.n * (t + 1) / T;
-    rc[t] = fccf::ply::decode(f, a, b - a, xyz + 3 * a);
-  };
-  for (int t = 1; t < T; ++t) th.emplace_back(part, t);
-  part(0);
-  for (auto& x : th) x.join();
-  for (int t = 0; t < T; ++t)
-    if (rc[t]) {
-      std::free(xyz);
-      return rc[t];
-    }
-  *out = xyz;
-  *nout = f.n;
-  return FCCF_OK;
+  float* xyz = nullptr;
+  // no exception may cross the C ABI (allocation in the header parse or the row index,
+  // thread creation): each becomes a status code
+  try {
+    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    fccf::ply::File f;
+    if (int rc = fccf::ply::open(path, f, T)) return rc;
+    xyz = (float*)std::malloc(sizeof(float) * 3 * (size_t)(f.n ? f.n : 1));  // n < 2^31 (open)
+    if (!xyz) return FCCF_E_OOM;
+    // rows in T contiguous ranges on T threads
+    std::vector<int> rc(T, FCCF_OK);
+    auto part = [&](int t) {
+      const int64_t a = f.n * t / T, b = f.n * (t + 1) / T;
+      rc[t] = fccf::ply::decode(f, a, b - a, xyz + 3 * a);
+    };
+    std::vector<std::thread> th;
+    struct Join {  // destroyed before f and rc, also when a thread fails to start
+      std::vector<std::thread>& th;
+      ~Join() {
+        for (auto& x : th)
+          if (x.joinable()) x.join();
+      }
+    } join{th};
+    for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T; ++t)
+      if (rc[t]) {
+        std::free(xyz);
+        return rc[t];
+      }
+    *out = xyz;
+    *nout = f.n;
+    return FCCF_OK;
+  } catch (const std::bad_alloc&) {
+    std::free(xyz);
+    return FCCF_E_OOM;
+  } catch (...) {
+    std::free(xyz);
+    return FCCF_E_INTERNAL;
+  }
 }
 
 extern "C" int fccf_ply_write(const char* path, const float* xyz, int64_t n, int binary) {

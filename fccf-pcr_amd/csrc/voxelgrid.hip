@@ -41,7 +41,10 @@ __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint3
   const float* __restrict__ xyz = xyz2[e];
   const uint32_t n = set_n ? n2[e] : *d_n2[e];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (Tag == 0) P2[e]->t_main = __builtin_amdgcn_s_memrealtime();
+    if (Tag == 0) {
+      P2[e]->t_main = __builtin_amdgcn_s_memrealtime();
+      P2[e]->sort_err = 0;  // (the driver's pass adds its flags to main's)
+    }
     P2[e]->unsorted = 0;
     P2[e]->chk_done = 0;
     P2[e]->nonfinite = 0;

@@ -105,6 +105,7 @@ _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctype
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
 _sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
+_sig("fccf_debug_inject_sort_fault", ctypes.c_int, _P, ctypes.c_uint32)
 _sig("fccf_debug_capture_race", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P)
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
      ctypes.POINTER(_I64))
@@ -314,6 +315,10 @@ class Ctx:
                "fccf_debug_sort_keys", self._h)
         return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
 
+    def inject_sort_fault(self, bits: int):
+        """Test hook: later K1 sorts raise these invariant flags (0 switches it off)."""
+        _check(_lib.fccf_debug_inject_sort_fault(self._h, int(bits)), "fccf_debug_inject_sort_fault", self._h)
+
     def sort_stats(self) -> dict:
         a = np.zeros(32, np.uint32)
         _check(_lib.fccf_debug_sort_stats(self._h, a.ctypes.data), "fccf_debug_sort_stats", self._h)
@@ -477,9 +482,17 @@ class Group:
         return [o[: int(n)] for o, n in zip(out, ncand)], kp.value
 
     def close(self):
+        """Releases the communicator.  Safe in either order with Ctx.close: a ctx
+        destroyed first detaches its group (fccf_ctx_destroy)."""
         if self._h:
             _lib.fccf_group_destroy(self._h)
             self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def __enter__(self):
         return self

@@ -80,7 +80,9 @@ typedef struct fccf_stats {
   int32_t overflow_passthrough;  /* VoxelGrid int32 guard tripped (any pass)      */
   int32_t graph_captures;        /* device-stage graphs (re)captured by this call */
   double ms[FCCF_T_COUNT];       /* stage times: DOWNSAMPLE and VOXELFIT are device
-                                    spans (HIP events), the others host wall times  */
+                                    spans (s_memrealtime stamps written by the cloud
+                                    stage's own kernels, dev_ms below), H2D a HIP-event
+                                    span of the input copy, the others host wall times */
   double ms_total;               /* host arrays (or resident device arrays) -> T  */
   /* appended in round 2 (SURVEY.md §8(d) stage roofline inputs) */
   int64_t m1_src, m1_tar;        /* after main's VoxelGrid pass (FCCF.cpp:1668-1678) */
@@ -150,7 +152,10 @@ int fccf_device_download(fccf_ctx* ctx, const float* d_xyz, int64_t n, float* xy
 
 /* Stage export: PCL VoxelGrid<PointXYZ> (FCCF.cpp:1668-1678) on the GPU.
  * out_xyz capacity 3*n floats; *m receives the output count.  Output order is
- * ascending leaf index; points of one leaf are summed in ascending input order. */
+ * ascending leaf index; the points of one leaf are summed in the order libstdc++
+ * std::sort leaves PCL's (leaf, index) pairs (the reference's own order, introsort,
+ * unstable), bit-identical to the oracle's INTROSORT mode.  FCCF_E_INTERNAL if the
+ * sort's device invariant checks fail. */
 int fccf_stage_downsample(fccf_ctx* ctx, const float* xyz, int64_t n, float leaf, float* out_xyz,
                           int64_t* m);
 /* The same, as the driver's second pass runs it (FCCF.cpp:1377-1387 over main's
@@ -259,11 +264,17 @@ int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes
 int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm_out);
 /* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags,
  * [3] global partitions, [4] LDS segments, [5] workgroup partitions, [6] wave
- * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks. */
+ * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks.
+ * fccf_debug_sort_keys returns FCCF_E_INTERNAL when an invariant flag is set. */
 /* Test hook: the device LM's correctly rounded double sin/cos (verify.hip); ok[i] = 0
  * where |x| is beyond its argument reduction. */
 int fccf_debug_sincos(fccf_ctx* ctx, const double* x, int64_t n, double* s, double* c, uint32_t* ok);
 int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
+/* Test hook: every later sort of K1 on ctx raises the invariant flags in bits (0x100
+ * round scatter outside its segment, 0x200 block item guard, 0x400 wave task stack,
+ * 0x1000 block partition stack) as if the check had fired, until called with 0.
+ * fccf_register* then fails with FCCF_E_INTERNAL, as it does for a real violation. */
+int fccf_debug_inject_sort_fault(fccf_ctx* ctx, uint32_t bits);
 /* Forces a graph capture on one stream concurrent with another thread's wait on
  * an event last recorded on that stream (the pipelined batch's hazard, guarded by
  * the capture lock).  guard 1 = the product's guarded wait, 0 = an unguarded

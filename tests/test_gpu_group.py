@@ -89,3 +89,16 @@ def test_two_ranks_on_one_gpu(fccf, pair, tmp_path):
     for r in res:
         assert np.array_equal(np.array(r["T"], np.uint32), bits(T0).ravel())
         assert (r["K"], r["K_pass"], r["cand"]) == (s0.K, s0.K_pass, list(s0.cand))
+
+
+def test_ctx_destroyed_before_its_group(fccf):
+    """fccf_ctx_destroy detaches an attached group instead of leaving it pointing at
+    freed memory; destroying the group afterwards only releases the communicator."""
+    ctx = fccf.Ctx(0)
+    g = fccf.Group(ctx, fccf.group_unique_id(), 1, 0)
+    ctx.close()
+    assert g.info() == (1, 0)
+    g.close()
+    with fccf.Ctx(0) as ctx2:  # the device is still usable
+        g2 = fccf.Group(ctx2, fccf.group_unique_id(), 1, 0)
+        g2.close()

@@ -255,3 +255,45 @@ def test_stats_time_the_host_input_copy(ctx, fccf):
         ctx.free(ds)
         ctx.free(dt)
     assert st2.as_dict()["ms"]["h2d"] == 0.0
+
+
+@pytest.mark.parametrize("bit", [0x100, 0x200, 0x400, 0x1000])
+def test_sort_invariant_flag_fails_registration(ctx, oracle, fccf, bit):
+    """A K1 sort invariant flag (IS_FAULT_*, raised through the injection hook at its
+    kernel) makes every path fail with FCCF_E_INTERNAL instead of returning a
+    transform computed from a possibly wrong VoxelGrid order (FCCF.cpp:1668-1678);
+    with the hook off again the same ctx registers bit-exactly."""
+    src, tar, _ = fccf.synth_pair(100_000)
+    FCCF_E_INTERNAL = -6
+    ctx.inject_sort_fault(bit)
+    try:
+        with pytest.raises(fccf.FCCFError) as e:
+            ctx.register(src, tar, 0.1)
+        assert e.value.code == FCCF_E_INTERNAL and "sort invariant" in str(e.value)
+        with pytest.raises(fccf.FCCFError) as e:
+            ctx.register_batch([(src, tar)] * 3, 0.1)
+        assert e.value.code == FCCF_E_INTERNAL
+        with pytest.raises(fccf.FCCFError) as e:
+            ctx.downsample(src, 0.1)
+        assert e.value.code == FCCF_E_INTERNAL
+    finally:
+        ctx.inject_sort_fault(0)
+    T, _ = ctx.register(src, tar, 0.1)
+    np.testing.assert_array_equal(T.view(np.uint32), oracle.Run(src, tar, 0.1, oracle.INTROSORT).T.view(np.uint32))
+
+
+def test_outdoor_extent_face_sort_stays_on_fast_passes(ctx, oracle, fccf):
+    """A scene ~120 m across (the first-point-anchored 1 m octree grows to depth 9:
+    28-bit face codes, about 500 x face_voxel_size of root cell) is sorted by the four
+    device-wide radix passes, not the single-workgroup tail: bitwise parity, and the
+    face stage's device span stays well under a millisecond (the tail path over the
+    whole cloud would take several)."""
+    src, tar, _ = fccf.synth_pair(400_000, (120.0, 90.0, 8.0))
+    run = oracle.Run(src, tar, 0.1, oracle.INTROSORT)
+    assert run.get("oct1", np.float64)[3] == 9 and run.get("oct2", np.float64)[3] == 9  # depth
+    T, st = ctx.register(src, tar, 0.1)
+    compare_all(ctx, run)
+    np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
+    spans = [ctx.register(src, tar, 0.1)[1].dev_ms[2] for _ in range(3)]
+    print(f"face stage span at 400 m extent: {min(spans):.3f} ms")
+    assert min(spans) < 1.0
