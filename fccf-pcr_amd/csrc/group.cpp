@@ -1,21 +1,34 @@
-// group.cpp — multi-GPU inside libfccf over RCCL (SURVEY.md §8(b) fccf_group_create,
-// §8(e) row K5).  One process per GPU; every rank holds a communicator created from
-// one ncclUniqueId that rank 0 made and the caller distributed out of band.
+// group.cpp — multi-GPU inside libfccf (SURVEY.md §8(b) fccf_group_create, §8(e)).
+// One process per GPU; every rank holds communicators created from one
+// ncclUniqueId that rank 0 made and the caller distributed out of band.
 //
-// What is sharded: the coplane-pair correspondence search (FCCF.cpp:1410-1428).
-// Source pairs B1 are split into contiguous blocks (shard_range); each rank tests its
-// block against all target pairs on its GPU, then the per-type candidate lists are
-// gathered in rank order with RCCL over xGMI: the counts by one ncclAllGather, the
-// variable-length lists by one group of per-root ncclBroadcasts (an all-gather-v).
-// The reference's loop is b1-major, so the concatenation is the unsharded list.
+// What is sharded:
+//  * K5, the coplane-pair correspondence search (FCCF.cpp:1410-1428): source pairs B1
+//    in contiguous blocks (shard_range); each rank tests its block against all target
+//    pairs on its GPU, then the per-type candidate lists are gathered in rank order:
+//    the counts by one all-gather, the variable-length lists by an all-gather-v.  The
+//    reference's loop is b1-major, so the concatenation is the unsharded list.
+//  * F, fine_verify (:785-839): the <= 16 evaluations (the top fine_verify_number
+//    candidates of each type) in contiguous blocks; each rank scores its block on
+//    its GPU and the scores are all-gathered in rank order, so every rank fuses the
+//    same scores in the same order.
 // Everything else is replicated: every rank runs the cloud stage on the same inputs
 // (the VoxelGrid's std::sort order spans the whole cloud), growth,
 // selection, clustering and the LM are sequential and deterministic, so every rank
 // computes the same T with no further exchange.
+//
+// Transports: RCCL (RcclTransport: an all-gather-v is one ncclGroupStart/End of
+// per-root ncclBroadcasts), or virtual ranks (LocalTransport, test hook): n contexts
+// of one process on one device exchange through a shared device staging buffer under
+// host barriers -- the same gather logic with n > 1, where RCCL itself would refuse
+// two ranks on one GPU.
 #include "group.h"
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -46,6 +59,92 @@ struct NcclGroup {
   }
 };
 
+struct RcclTransport : Transport {
+  Group* g;
+  explicit RcclTransport(Group* g_) : g(g_) {}
+  void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
+                  hipStream_t st) override {
+    NcclGroup grp;
+    for (int r = 0; r < g->n; ++r) {
+      if (!counts[r]) continue;
+      char* dst = (char*)recv + offs[r];
+      NCCL_CHECK(ncclBroadcast(r == g->rank ? send : (const void*)dst, dst, counts[r], ncclUint8, r, g->comm[ch], st));
+    }
+    grp.end();
+  }
+  void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, g->comm[ch], st));
+  }
+};
+
+// Virtual ranks of one process on one device: every collective is host-synchronous.
+struct LocalHub {
+  int n;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  char* stage[CH_COUNT] = {nullptr, nullptr};
+  size_t cap[CH_COUNT] = {0, 0};
+  size_t need[CH_COUNT] = {0, 0};
+  explicit LocalHub(int n_) : n(n_) {}
+  ~LocalHub() {
+    for (char* p : stage)
+      if (p) (void)hipFree(p);
+  }
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const uint64_t my = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    // bounded: a rank that never arrives (its call failed) ends the wait with an error
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != my; }))
+      throw Error(FCCF_E_RCCL, "virtual-rank group: a rank did not reach the collective");
+  }
+};
+
+struct LocalTransport : Transport {
+  Group* g;
+  explicit LocalTransport(Group* g_) : g(g_) {}
+  void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
+                  hipStream_t st) override {
+    LocalHub& H = *g->hub;
+    size_t total = 0;
+    for (int r = 0; r < g->n; ++r) total = std::max(total, offs[r] + counts[r]);
+    HIP_CHECK(hipStreamSynchronize(st));  // this rank's send data is complete
+    {
+      std::lock_guard<std::mutex> lk(H.m);
+      H.need[ch] = std::max(H.need[ch], total);
+    }
+    H.barrier();
+    if (g->rank == 0 && H.need[ch] > H.cap[ch]) {  // one rank grows the staging, between barriers
+      if (H.stage[ch]) HIP_CHECK(hipFree(H.stage[ch]));
+      H.stage[ch] = nullptr;
+      H.cap[ch] = 0;
+      if (hipMalloc((void**)&H.stage[ch], H.need[ch]) != hipSuccess) throw Error(FCCF_E_OOM, "virtual-rank staging");
+      H.cap[ch] = H.need[ch];
+    }
+    H.barrier();
+    if (counts[g->rank]) {  // (on st: the legacy null stream would also wait for the other ranks' streams)
+      HIP_CHECK(hipMemcpyAsync(H.stage[ch] + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+    }
+    H.barrier();
+    if (total) HIP_CHECK(hipMemcpyAsync(recv, H.stage[ch], total, hipMemcpyDeviceToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    H.barrier();  // (the staging is rewritten by the next collective)
+  }
+  void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    std::vector<size_t> counts((size_t)g->n, bytes), offs((size_t)g->n);
+    for (int r = 0; r < g->n; ++r) offs[(size_t)r] = (size_t)r * bytes;
+    allgatherv(ch, send, recv, counts.data(), offs.data(), st);
+  }
+};
+
 void shard_range(int n, int rank, int world, int* lo, int* hi) {
   const int q = n / world, r = n % world;
   *lo = rank * q + std::min(rank, r);
@@ -62,7 +161,7 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
   h[2] = tot_loc[2];
   h[3] = (uint32_t)kpass_loc;
   HIP_CHECK(hipMemcpyAsync(g->d_cnt, h, 16, hipMemcpyHostToDevice, st));
-  NCCL_CHECK(ncclAllGather(g->d_cnt, g->d_cnt + 4, 4, ncclUint32, g->comm, st));
+  g->tr->allgather(CH_MATCH, g->d_cnt, g->d_cnt + 4, 16, st);
   HIP_CHECK(hipMemcpyAsync(h + 4, g->d_cnt + 4, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
   int64_t kp = 0;
@@ -80,20 +179,19 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
     tot_all[t] = (uint32_t)off[t];
   }
   *kpass_all = kp;
-  // all-gather-v: one broadcast per (root, type) inside one group; empty blocks skipped
-  {
-    NcclGroup grp;
-    for (int r = 0; r < n; ++r)
-      for (int t = 0; t < 3; ++t) {
-        const size_t cnt = h[4 + 4 * r + t];
-        if (!cnt) continue;
-        const size_t b = base[(size_t)r * 3 + t];
-        NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)q_loc[t] : (const void*)(q_all[t] + b), q_all[t] + b,
-                                 cnt * sizeof(QTd), ncclUint8, r, g->comm, st));
-        NCCL_CHECK(ncclBroadcast(r == g->rank ? (const void*)c_loc[t] : (const void*)(c_all[t] + b), c_all[t] + b,
-                                 cnt * sizeof(MCand), ncclUint8, r, g->comm, st));
-      }
-    grp.end();
+  // all-gather-v of each type's quaternion records and matrices, rank-ordered
+  std::vector<size_t> cnt((size_t)n), offs((size_t)n);
+  for (int t = 0; t < 3; ++t) {
+    for (int r = 0; r < n; ++r) {
+      cnt[(size_t)r] = (size_t)h[4 + 4 * r + t] * sizeof(QTd);
+      offs[(size_t)r] = base[(size_t)r * 3 + t] * sizeof(QTd);
+    }
+    g->tr->allgatherv(CH_MATCH, q_loc[t], q_all[t], cnt.data(), offs.data(), st);
+    for (int r = 0; r < n; ++r) {
+      cnt[(size_t)r] = (size_t)h[4 + 4 * r + t] * sizeof(MCand);
+      offs[(size_t)r] = base[(size_t)r * 3 + t] * sizeof(MCand);
+    }
+    g->tr->allgatherv(CH_MATCH, c_loc[t], c_all[t], cnt.data(), offs.data(), st);
   }
   h[0] = tot_all[0];
   h[1] = tot_all[1];
@@ -101,6 +199,31 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
   h[3] = 0;
   HIP_CHECK(hipMemcpyAsync(d_tot_all, h, 16, hipMemcpyHostToDevice, st));
   HIP_CHECK(hipStreamSynchronize(st));  // (h is reused by the next call)
+}
+
+void group_fine_gather(Group* g, int s, const float* d_scores, int E_loc, const uint32_t* d_err, hipStream_t st) {
+  float* snd = g->d_fsend[s];
+  HIP_CHECK(hipMemsetAsync(snd, 0, sizeof(float) * Group::FE_BLK, st));
+  if (E_loc > 0) {
+    HIP_CHECK(hipMemcpyAsync(snd, d_scores, sizeof(float) * (size_t)E_loc, hipMemcpyDeviceToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(snd + MAX_EVAL, d_err, 4, hipMemcpyDeviceToDevice, st));  // the error word's bits
+  }
+  g->tr->allgather(CH_FINE, snd, g->d_frecv[s], sizeof(float) * Group::FE_BLK, st);
+  HIP_CHECK(hipMemcpyAsync(g->h_frecv[s], g->d_frecv[s], sizeof(float) * Group::FE_BLK * (size_t)g->n,
+                           hipMemcpyDeviceToHost, st));
+}
+
+void group_fine_scores(const Group* g, int s, int E, float* scores, uint32_t* err) {
+  *err = 0;
+  for (int r = 0; r < g->n; ++r) {
+    int lo, hi;
+    shard_range(E, r, g->n, &lo, &hi);
+    const float* blk = g->h_frecv[s] + (size_t)r * Group::FE_BLK;
+    for (int e = lo; e < hi; ++e) scores[e] = blk[e - lo];
+    uint32_t w;
+    std::memcpy(&w, blk + MAX_EVAL, 4);
+    *err |= w;
+  }
 }
 
 }  // namespace fccf
@@ -112,6 +235,45 @@ struct fccf_group {
 };
 
 Group* fccf::group_of(fccf_group* g) { return g ? &g->g : nullptr; }
+
+namespace {
+
+// the buffers of a group, after its transport exists
+void group_alloc(Group& g) {
+  const size_t n = (size_t)g.n;
+  if (hipMalloc((void**)&g.d_cnt, 16 * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
+  if (hipHostMalloc((void**)&g.h_cnt, 16 * (n + 1), hipHostMallocDefault) != hipSuccess)
+    throw Error(FCCF_E_OOM, "hipHostMalloc");
+  for (int s = 0; s < 2; ++s) {
+    if (hipMalloc((void**)&g.d_fsend[s], sizeof(float) * Group::FE_BLK) != hipSuccess ||
+        hipMalloc((void**)&g.d_frecv[s], sizeof(float) * Group::FE_BLK * n) != hipSuccess)
+      throw Error(FCCF_E_OOM, "hipMalloc");
+    if (hipHostMalloc((void**)&g.h_frecv[s], sizeof(float) * Group::FE_BLK * n, hipHostMallocDefault) != hipSuccess)
+      throw Error(FCCF_E_OOM, "hipHostMalloc");
+  }
+}
+
+void group_free(Group& g) {
+  for (ncclComm_t& c : g.comm)
+    if (c) {
+      (void)ncclCommDestroy(c);
+      c = nullptr;
+    }
+  if (g.d_cnt) (void)hipFree(g.d_cnt);
+  if (g.h_cnt) (void)hipHostFree(g.h_cnt);
+  for (int s = 0; s < 2; ++s) {
+    if (g.d_fsend[s]) (void)hipFree(g.d_fsend[s]);
+    if (g.d_frecv[s]) (void)hipFree(g.d_frecv[s]);
+    if (g.h_frecv[s]) (void)hipHostFree(g.h_frecv[s]);
+    g.d_fsend[s] = g.d_frecv[s] = g.h_frecv[s] = nullptr;
+  }
+  g.d_cnt = nullptr;
+  g.h_cnt = nullptr;
+  g.tr.reset();
+  g.hub.reset();
+}
+
+}  // namespace
 
 extern "C" int fccf_group_unique_id(uint8_t id[FCCF_GROUP_ID_BYTES]) {
   if (!id) return FCCF_E_ARG;
@@ -131,23 +293,63 @@ extern "C" int fccf_group_create(fccf_ctx* c, const uint8_t id[FCCF_GROUP_ID_BYT
     HIP_CHECK(hipSetDevice(c->device));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    NCCL_CHECK(ncclCommInitRank(&G->g.comm, n_ranks, u, rank));
+    NCCL_CHECK(ncclCommInitRank(&G->g.comm[CH_MATCH], n_ranks, u, rank));
+    // the fine-verification channel: its own communicator, so collectives issued on the
+    // matching and fine streams never interleave on one communicator
+    NCCL_CHECK(ncclCommSplit(G->g.comm[CH_MATCH], 0, rank, &G->g.comm[CH_FINE], nullptr));
     G->g.ctx = c;
     G->g.n = n_ranks;
     G->g.rank = rank;
-    if (hipMalloc((void**)&G->g.d_cnt, 16 * (size_t)(n_ranks + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
-    if (hipHostMalloc((void**)&G->g.h_cnt, 16 * (size_t)(n_ranks + 1), hipHostMallocDefault) != hipSuccess)
-      throw Error(FCCF_E_OOM, "hipHostMalloc");
+    G->g.tr.reset(new RcclTransport(&G->g));
+    group_alloc(G->g);
     c->group = &G->g;
     *out = G;
     return FCCF_OK;
   } catch (const Error& e) {
     c->last_error = e.what();
-    if (G->g.comm) (void)ncclCommDestroy(G->g.comm);
-    if (G->g.d_cnt) (void)hipFree(G->g.d_cnt);
+    group_free(G->g);
     delete G;
     return e.code;
+  } catch (...) {
+    group_free(G->g);
+    delete G;
+    return FCCF_E_INTERNAL;
   }
+}
+
+extern "C" int fccf_group_create_local(fccf_ctx* const* ctxs, int n, fccf_group** out) {
+  if (!ctxs || !out || n < 1) return FCCF_E_ARG;
+  for (int r = 0; r < n; ++r)
+    if (!ctxs[r] || ctxs[r]->group || ctxs[r]->device != ctxs[0]->device) return FCCF_E_ARG;
+  for (int r = 0; r < n; ++r)
+    for (int q = 0; q < r; ++q)
+      if (ctxs[q] == ctxs[r]) return FCCF_E_ARG;
+  auto hub = std::make_shared<LocalHub>(n);
+  std::vector<fccf_group*> made;
+  try {
+    HIP_CHECK(hipSetDevice(ctxs[0]->device));
+    for (int r = 0; r < n; ++r) {
+      fccf_group* G = new fccf_group();
+      made.push_back(G);
+      G->g.ctx = ctxs[r];
+      G->g.n = n;
+      G->g.rank = r;
+      G->g.hub = hub;
+      G->g.tr.reset(new LocalTransport(&G->g));
+      group_alloc(G->g);
+    }
+  } catch (...) {
+    for (fccf_group* G : made) {
+      group_free(G->g);
+      delete G;
+    }
+    return FCCF_E_OOM;
+  }
+  for (int r = 0; r < n; ++r) {
+    ctxs[r]->group = &made[(size_t)r]->g;
+    out[r] = made[(size_t)r];
+  }
+  return FCCF_OK;
 }
 
 extern "C" int fccf_group_destroy(fccf_group* G) {
@@ -157,9 +359,7 @@ extern "C" int fccf_group_destroy(fccf_group* G) {
     (void)hipDeviceSynchronize();
     if (G->g.ctx->group == &G->g) G->g.ctx->group = nullptr;
   }
-  if (G->g.comm) (void)ncclCommDestroy(G->g.comm);
-  if (G->g.d_cnt) (void)hipFree(G->g.d_cnt);
-  if (G->g.h_cnt) (void)hipHostFree(G->g.h_cnt);
+  group_free(G->g);
   delete G;
   return FCCF_OK;
 }

@@ -1,10 +1,21 @@
-// group.h — RCCL communicator of one rank (one process per GPU) and the sharded
-// correspondence search's candidate gather (FCCF.cpp:1410-1428).
+// group.h — one rank of a multi-GPU registration group (one process per GPU) and
+// the exchange steps of the sharded stages:
+//   K5  the coplane-pair correspondence search (FCCF.cpp:1410-1428): source pairs in
+//       contiguous blocks, the candidate lists gathered in rank order;
+//   F   fine_verify (:785-839): the <= 16 evaluations in contiguous blocks, the
+//       scores gathered in rank order.
+// The collectives go through a Transport: RCCL over xGMI in the product (two
+// communicators, one per stream that issues collectives, so the matching stream and
+// the fine-verification stream never interleave operations on one communicator), or
+// an in-process hub of virtual ranks on one device (fccf_group_create_local, a test
+// hook that runs the same host-side exchange logic with n > 1 ranks on one GPU).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstddef>
 #include <cstdint>
+#include <memory>
 
 #include "match.h"
 
@@ -13,19 +24,43 @@ struct fccf_group;
 
 namespace fccf {
 
+// Collective channels: each is used from one stream only (stream order = issue order).
+enum { CH_MATCH = 0, CH_FINE = 1, CH_COUNT = 2 };
+
+struct Transport {
+  virtual ~Transport() = default;
+  // Rank-ordered all-gather-v on channel ch, in the order of stream st: rank r's
+  // counts[r] bytes (its `send`) land at recv + offs[r] on every rank.  Buffers are
+  // device memory of the rank's device.
+  virtual void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
+                          hipStream_t st) = 0;
+  // The same with equal blocks of `bytes`, rank r's at recv + r * bytes.
+  virtual void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
+};
+
+struct LocalHub;  // group.cpp
+
 struct Group {
   fccf_ctx* ctx = nullptr;
-  ncclComm_t comm = nullptr;
   int n = 1, rank = 0;
+  ncclComm_t comm[CH_COUNT] = {nullptr, nullptr};  // RCCL groups
+  std::shared_ptr<LocalHub> hub;                   // virtual-rank groups
+  std::unique_ptr<Transport> tr;
   uint32_t* d_cnt = nullptr;  // device: this rank's 4 counts, then all ranks' (n x 4)
   uint32_t* h_cnt = nullptr;  // pinned copy of all ranks' counts
+  // sharded fine verification, per cloud set s (the pipelined batch overlaps two pairs):
+  // this rank's block of scores + its error word (FE_BLK floats), all ranks' blocks
+  static constexpr int FE_BLK = MAX_EVAL + 1;
+  float* d_fsend[2] = {nullptr, nullptr};
+  float* d_frecv[2] = {nullptr, nullptr};  // n x FE_BLK
+  float* h_frecv[2] = {nullptr, nullptr};  // pinned copies
 };
 
 // the Group inside a C-ABI handle (null for null)
 Group* group_of(fccf_group* g);
 
-// Contiguous block [lo, hi) of n source pairs for `rank` (sizes differ by at most
-// one, lower ranks larger; shard.py's shard_range).
+// Contiguous block [lo, hi) of n items for `rank` (sizes differ by at most one,
+// lower ranks larger; shard.py's shard_range).
 void shard_range(int n, int rank, int world, int* lo, int* hi);
 
 // The rank-ordered concatenation of every rank's candidate lists (q: quaternion
@@ -37,5 +72,15 @@ void shard_range(int n, int rank, int world, int* lo, int* hi);
 void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3], const uint32_t tot_loc[3],
                              int64_t kpass_loc, QTd* const q_all[3], MCand* const c_all[3], size_t cap,
                              uint32_t tot_all[3], uint32_t* d_tot_all, int64_t* kpass_all, hipStream_t st);
+
+// Sharded fine verification (row F): this rank evaluated the block [lo, hi) of the E
+// transforms (shard_range), its E_loc = hi - lo scores at d_scores and its error word
+// at d_err.  Enqueues on st (the fine stream): the block and the error word into the
+// send slot of cloud set s, the all-gather, and the copy of every rank's block into
+// g->h_frecv[s], complete when st reaches that point.
+void group_fine_gather(Group* g, int s, const float* d_scores, int E_loc, const uint32_t* d_err, hipStream_t st);
+// After st has passed group_fine_gather: the E scores in evaluation order and the
+// OR of every rank's error word.
+void group_fine_scores(const Group* g, int s, int E, float* scores, uint32_t* err);
 
 }  // namespace fccf

@@ -244,7 +244,7 @@ struct PhaseB {
   fccf_stats S;
   std::vector<TS> ctv[3];
   std::vector<int64_t> counts;
-  int E = 0, analyse_max = 0;
+  int E = 0, E_loc = 0, analyse_max = 0;  // E_loc: this rank's block of the E fine evaluations
   float* T_out = nullptr;
   fccf_stats* stats = nullptr;
   clk::time_point t_all, t_fine;
@@ -756,10 +756,17 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) evals.push_back(ctv[t][i].T);
   const int E = (int)evals.size();
   if (E > MAX_EVAL) throw Error(FCCF_E_INTERNAL, "too many fine-verify evaluations");
-  if (E > 0) {
-    hipStream_t sf = c->sa[1];
+  // Sharded fine verification (group.cpp, row F): this rank scores its contiguous block
+  // [flo, fhi) of the E evaluations; the blocks are all-gathered in rank order.
+  Group* const FG = (c->group && c->group->n > 1) ? c->group : nullptr;
+  int flo = 0, fhi = E;
+  if (FG) shard_range(E, FG->rank, FG->n, &flo, &fhi);
+  const int El = fhi - flo;
+  hipStream_t sf = c->sa[1];
+  if (El > 0) {
     fccf::Arena& a3 = c->cs[s].arena3;
     const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
+    const int E = El;  // this rank's evaluations: evals[flo, fhi)
     const size_t nk = (size_t)E * (n1 + n2);
     const size_t af2 = aggr_floats(n2);
     const size_t need = 12 * (size_t)E * n2 + 4 * E * af2 + sizeof(OctState) * (E + 1) +
@@ -789,7 +796,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
                                (uint32_t)std::max<size_t>(nk, 1));
     fb.xs = exact_sum_carve(a3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
     FineMail& fm = host_mail(c)->fine[s];
-    std::memcpy(fm.T, evals.data(), sizeof(m44) * E);  // pinned staging: async H2D
+    std::memcpy(fm.T, evals.data() + flo, sizeof(m44) * E);  // pinned staging: async H2D
     HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, sf));
     struct {
       const void* base;
@@ -809,13 +816,18 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
+    if (FG) group_fine_gather(FG, s, fb.scores, El, fb.scal + 7, sf);
     HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));  // fine verification of this set's pair done
     ht.mark("fine_launched");
+  } else if (E > 0 && FG) {  // no evaluation in this rank's block: it still takes part in the gather
+    group_fine_gather(FG, s, nullptr, 0, nullptr, sf);
+    HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));
   }
   pb.S = S;
   for (int t = 0; t < 3; ++t) pb.ctv[t] = std::move(ctv[t]);
   pb.counts = std::move(counts);
   pb.E = E;
+  pb.E_loc = El;
   pb.analyse_max = analyse_max;
   pb.T_out = T_out;
   pb.stats = stats;
@@ -837,12 +849,20 @@ void phase_b2(fccf_ctx* c, int s) {
   if (E > 0) {
     // (ev[3]'s stream is captured only by this thread)
     HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));  // scores and the error word are in the mailbox
-    const FineMail& fm = host_mail(c)->fine[s];
-    std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
-    if (fm.err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
-    float d = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
-    S.dev_ms[3] = d;
+    uint32_t err = 0;
+    if (c->group && c->group->n > 1) {  // every rank's block, gathered in rank order
+      group_fine_scores(c->group, s, E, scores.data(), &err);
+    } else {
+      const FineMail& fm = host_mail(c)->fine[s];
+      std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
+      err = fm.err;
+    }
+    if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
+    if (pb.E_loc > 0) {
+      float d = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
+      S.dev_ms[3] = d;
+    }
   }
   S.fine_evals = E;
   S.ms[FCCF_T_FINE] = ms_since(pb.t_fine);

@@ -115,6 +115,7 @@ _sig("fccf_ply_load_device", ctypes.c_int, _P, ctypes.c_char_p, ctypes.POINTER(_
 _sig("fccf_device_download", ctypes.c_int, _P, _P, _I64, _P)
 _sig("fccf_group_unique_id", ctypes.c_int, _P)
 _sig("fccf_group_create", ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P))
+_sig("fccf_group_create_local", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P))
 _sig("fccf_group_destroy", ctypes.c_int, _P)
 _sig("fccf_group_info", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
 _sig("fccf_group_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
@@ -322,9 +323,8 @@ class Ctx:
     def sort_stats(self) -> dict:
         a = np.zeros(32, np.uint32)
         _check(_lib.fccf_debug_sort_stats(self._h, a.ctypes.data), "fccf_debug_sort_stats", self._h)
-        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_segments=int(a[4]),
-                    block_parts=int(a[5]), wave_parts=int(a[6]), heaps=int(a[7]), reg_subtrees=int(a[12]),
-                    wave_tasks=int(a[16]))
+        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_items=int(a[4]),
+                    lds_levels=int(a[5]), heaps=int(a[7]), raw=a)
 
     def capture_race(self, hold_ms: int = 200, guard: bool = True) -> dict:
         """Test hook: a graph capture held for hold_ms concurrent with another thread's
@@ -458,6 +458,13 @@ class Group:
         _check(_lib.fccf_group_create(ctx._h, buf, int(n_ranks), int(rank), ctypes.byref(self._h)),
                "fccf_group_create", ctx._h)
 
+    @classmethod
+    def _wrap(cls, ctx: "Ctx", h) -> "Group":
+        g = cls.__new__(cls)
+        g.ctx = ctx
+        g._h = h
+        return g
+
     def info(self):
         n, r = ctypes.c_int(), ctypes.c_int()
         _check(_lib.fccf_group_info(self._h, ctypes.byref(n), ctypes.byref(r)), "fccf_group_info")
@@ -499,6 +506,18 @@ class Group:
 
     def __exit__(self, *a):
         self.close()
+
+
+def local_groups(ctxs) -> list:
+    """Virtual ranks (fccf_group_create_local, a test hook): one Group per Ctx, all on
+    one device, exchanging through host barriers instead of RCCL.  Rank r's calls must
+    run on their own thread, concurrently with the other ranks' (ctypes releases the
+    GIL inside the library), exactly as one process per GPU would."""
+    n = len(ctxs)
+    hs = (_P * n)(*[c._h for c in ctxs])
+    out = (_P * n)()
+    _check(_lib.fccf_group_create_local(hs, n, out), "fccf_group_create_local")
+    return [Group._wrap(c, _P(out[i])) for i, c in enumerate(ctxs)]
 
 
 def strerror(code: int) -> str:

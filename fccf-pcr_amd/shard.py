@@ -94,6 +94,28 @@ def match_sharded(ctx, F1, B1, F2, B2, rank: int, world: int, gather, params=Non
     return combine(gather(pack(cands, k_pass)))
 
 
+# ---------------------------------------------------------------- fine_verify (row F)
+# SURVEY.md §8(e) row F.  The <= 16 evaluations (the top fine_verify_number candidates
+# of each type, FCCF.cpp:1526-1536) are independent: each rank scores a contiguous
+# block (shard_range) on its GPU, the scores are gathered in rank order, and every rank
+# fuses the same E scores.  Inside libfccf the same split runs over the group's own
+# fine-verification communicator (group.cpp, group_fine_gather); this is its mirror for
+# callers that drive the stages themselves.
+
+
+def fine_verify_sharded(ctx, s1, s2, T, voxel: float, rank: int, world: int, gather):
+    """This rank's block of fine_verify(s1, s2, T[e]) on its GPU, then the ordered gather.
+    Every rank returns the E float32 scores, identical to ctx.fine_verify(s1, s2, T, voxel)."""
+    T = np.ascontiguousarray(T, np.float32).reshape(-1, 4, 4)
+    lo, hi = shard_range(len(T), rank, world)
+    mine = ctx.fine_verify(s1, s2, T[lo:hi], voxel) if hi > lo else np.zeros(0, np.float32)
+    parts = gather(np.asarray(mine, np.float32))
+    out = np.concatenate([np.asarray(p, np.float32).reshape(-1) for p in parts])
+    if out.size != len(T):
+        raise ValueError(f"fine_verify gather: {out.size} scores for {len(T)} evaluations")
+    return out
+
+
 # ---------------------------------------------------------------- VoxelGrid (row D)
 # SURVEY.md §8(e) row D.  Helpers shared with the tests' CPU stand-in: PCL's leaf
 # coordinates floor(p * (1/leaf)) in float32 and its int32 overflow guard

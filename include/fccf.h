@@ -297,6 +297,12 @@ int fccf_group_unique_id(uint8_t id[FCCF_GROUP_ID_BYTES]);
 int fccf_group_create(fccf_ctx* ctx, const uint8_t id[FCCF_GROUP_ID_BYTES], int n_ranks, int rank,
                       fccf_group** group);
 int fccf_group_destroy(fccf_group* group);
+/* Test hook: n "virtual ranks" of one process on one device, one group per ctx
+ * (distinct ctxs of the same device), exchanging through a shared device buffer
+ * under host barriers instead of RCCL: the sharded paths' host-side exchange logic
+ * with n > 1 ranks on one GPU (RCCL refuses two ranks on one device).  Each rank's
+ * calls must come from its own host thread, all ranks calling the same sequence. */
+int fccf_group_create_local(fccf_ctx* const* ctxs, int n, fccf_group** groups);
 int fccf_group_info(const fccf_group* group, int* n_ranks, int* rank);
 /* Stage export of the sharded search: fccf_stage_match's arguments without the
  * range; this rank searches its block, and every rank receives the whole lists. */

@@ -102,3 +102,103 @@ def test_ctx_destroyed_before_its_group(fccf):
     with fccf.Ctx(0) as ctx2:  # the device is still usable
         g2 = fccf.Group(ctx2, fccf.group_unique_id(), 1, 0)
         g2.close()
+
+
+def _on_threads(fn, n):
+    """fn(r) on n threads at once (virtual ranks block in each other's collectives)."""
+    import threading
+    res, errs = [None] * n, []
+
+    def run(r):
+        try:
+            res[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 (re-raised below)
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a virtual rank did not finish"
+    if errs:
+        raise errs[0]
+    return res
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_virtual_ranks_shard_search_and_fine_verify(fccf, pair, n):
+    """n virtual ranks on the one GPU (fccf_group_create_local): the K5 search and the
+    F evaluations are split into rank blocks and gathered through the same host-side
+    exchange code as the RCCL path; every rank's registration (single and pipelined
+    batch) equals the unsharded one bit for bit."""
+    src, tar, leaf = pair
+    with fccf.Ctx(0) as ctx:
+        T0, s0 = ctx.register(src, tar, leaf)
+    assert s0.fine_evals >= n  # every rank scores a non-empty block
+    ctxs = [fccf.Ctx(0) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+        assert [g.info() for g in groups] == [(n, r) for r in range(n)]
+
+        def work(r):
+            T, s = ctxs[r].register(src, tar, leaf)
+            Tb, _ = ctxs[r].register_batch([(src, tar)] * 3, leaf)
+            return T, s, Tb
+
+        out = _on_threads(work, n)
+        for g in groups:
+            g.close()
+    finally:
+        for c in ctxs:
+            c.close()
+    for T, s, Tb in out:
+        np.testing.assert_array_equal(bits(T), bits(T0))
+        for Tx in Tb:
+            np.testing.assert_array_equal(bits(Tx), bits(T0))
+        assert (s.K, s.K_pass, list(s.cand), s.fine_evals) == (s0.K, s0.K_pass, list(s0.cand), s0.fine_evals)
+
+
+def test_virtual_ranks_stage_match(fccf, oracle, pair):
+    src, tar, leaf = pair
+    run = oracle.Run(src, tar, leaf, oracle.INTROSORT)
+    F1, B1 = fccf.planes_from_dump(run.get("planes1")), fccf.bases_from_dump(run.get("bases1", np.int32))
+    F2, B2 = fccf.planes_from_dump(run.get("planes2")), fccf.bases_from_dump(run.get("bases2", np.int32))
+    ctxs = [fccf.Ctx(0) for _ in range(3)]
+    try:
+        groups = fccf.local_groups(ctxs)
+        out = _on_threads(lambda r: groups[r].match(F1, B1, F2, B2), 3)
+        for g in groups:
+            g.close()
+    finally:
+        for c in ctxs:
+            c.close()
+    for got, kp in out:
+        for t in range(3):
+            np.testing.assert_array_equal(bits(got[t]), bits(run.get(f"cand{t}").reshape(-1, 4, 4)))
+
+
+def test_fine_verify_sharded_host_mirror(fccf, pair):
+    """shard.fine_verify_sharded (row F for callers that drive the stages): blocks of the
+    evaluations scored on the GPU by three rank threads, gathered in rank order, equal
+    to one unsharded fccf_stage_fine_verify bit for bit."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "fccf-pcr_amd"))
+    sys.path.insert(0, HERE)
+    import shard
+    import test_shard
+    src, tar, leaf = pair
+    rng = np.random.default_rng(5)
+    T = np.tile(np.eye(4, dtype=np.float32), (7, 1, 1))
+    T[:, :3, 3] = rng.normal(0, 0.05, (7, 3)).astype(np.float32)
+    with fccf.Ctx(0) as ctx:
+        s1, s2 = ctx.downsample(src, leaf), ctx.downsample(tar, leaf)
+        want = ctx.fine_verify(s1, s2, T, 0.5)
+    ctxs = [fccf.Ctx(0) for _ in range(3)]  # one per rank thread, as one per process
+    try:
+        gs = test_shard.thread_gathers(3)
+        got = _on_threads(lambda r: shard.fine_verify_sharded(ctxs[r], s1, s2, T, 0.5, r, 3, gs[r]), 3)
+    finally:
+        for c in ctxs:
+            c.close()
+    for g in got:
+        np.testing.assert_array_equal(g.view(np.uint32), np.asarray(want, np.float32).view(np.uint32))

@@ -1,6 +1,6 @@
-"""CPU checks of the sharded correspondence search's host logic (fccf-pcr_amd/shard.py):
-block ranges, the message format, rank-ordered concatenation, and the gloo gather with
-world_size 2.  The GPU search itself is stubbed by a deterministic b1-major generator;
+"""CPU checks of the sharded stages' host logic (fccf-pcr_amd/shard.py): block ranges,
+the message format, rank-ordered concatenation (K5 search, F fine verification, D
+VoxelGrid), and the gloo gather with world_size 2.  The GPU search itself is stubbed by a deterministic b1-major generator;
 the real one is tested in tests/test_gpu_stages.py."""
 import os
 import subprocess
@@ -88,6 +88,9 @@ full, kp0 = ctx.match(None, B1, None, B2)
 assert kp == kp0, (kp, kp0)
 for a, b in zip(got, full):
     assert np.array_equal(a, b)
+T = test_shard.evals(7)
+sc = shard.fine_verify_sharded(test_shard.StubFineCtx(), None, None, T, 0.5, r, w, shard.torch_gather())
+assert np.array_equal(sc.view(np.uint32), test_shard.StubFineCtx().fine_verify(None, None, T, 0.5).view(np.uint32))
 xyz = test_shard.cloud(3000, 11)
 lo, hi = shard.shard_range(len(xyz), r, w)
 vctx = test_shard.StubVoxelCtx()
@@ -96,6 +99,41 @@ assert np.array_equal(got.view(np.uint32), vctx.downsample(xyz, 0.25).view(np.ui
 dist.barrier(); dist.destroy_process_group()
 print("ok", r)
 '''
+
+
+class StubFineCtx:
+    """ctx.fine_verify stand-in: a score per transform that depends on that transform only."""
+
+    def fine_verify(self, s1, s2, T, voxel):
+        T = np.asarray(T, np.float32).reshape(-1, 4, 4)
+        return (T[:, :3, 3].sum(axis=1) * np.float32(voxel) + np.float32(1)).astype(np.float32)
+
+
+def evals(E, seed=3):
+    rng = np.random.default_rng(seed)
+    T = np.tile(np.eye(4, dtype=np.float32), (E, 1, 1))
+    T[:, :3, 3] = rng.random((E, 3), np.float32)
+    return T
+
+
+@pytest.mark.parametrize("E,world", [(0, 2), (1, 3), (5, 2), (16, 3), (15, 8), (3, 16)])
+def test_fine_verify_sharded_equals_whole(E, world):
+    """Row F's exchange: blocks of the E evaluations, gathered in rank order (ranks past
+    E contribute empty blocks)."""
+    T = evals(E)
+    want = StubFineCtx().fine_verify(None, None, T, 0.5)
+    import threading
+    gs, res = thread_gathers(world), [None] * world
+
+    def work(r):
+        res[r] = shard.fine_verify_sharded(StubFineCtx(), None, None, T, 0.5, r, world, gs[r])
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for got in res:
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
 def cloud(n, seed, nan=True):

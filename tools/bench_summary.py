@@ -6,6 +6,7 @@ import sys
 d = json.load(open(sys.argv[1]))
 print("value %.4g %s  ms/step %.4f  e2e %.4f" % (d["value"], d["unit"], d["ms_per_step"], d.get("e2e_ms_median", 0)))
 print("stage_ms", d.get("stage_ms"))
+print("device_ms", d.get("device_ms"), "parity", d.get("parity"))
 print("in_batch", d.get("stage_ms_in_batch"))
 r = d.get("roofline") or {}
 print("roofline", r.get("kernel"), "frac %.4f achieved %.1f GB/s" % (r.get("frac", 0), r.get("achieved", 0)))
