@@ -92,6 +92,21 @@ __device__ __forceinline__ void is_inject(const IsBufs& W, uint32_t bits) {
   if (b) is_fault(W.ctl, W.err, b);
 }
 
+// The fence before a workgroup barrier that hands global-memory data between the waves
+// of one workgroup (k_is_block's global phase).  Every sort kernel runs with TG_SPLIT = 0
+// (COMPUTE_PGM_RSRC3 bit 16; checked in tools/check_tgsplit.py), so all waves of a
+// workgroup share one CU and its vector L1, and the segment a workgroup works on is
+// touched by no other workgroup during the kernel: a workgroup-scope fence is enough by
+// the memory model.  The agent-scope fence is kept as the product default (measured
+// cost: DESIGN.md, "Sort edge behaviour"); -DIS_WG_FENCE builds the workgroup form.
+__device__ __forceinline__ void hand_off_fence() {
+#ifdef IS_WG_FENCE
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#else
+  __threadfence();
+#endif
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
@@ -154,6 +169,23 @@ __device__ __forceinline__ void heap_sort(KP K, VP V, int64_t len) {  // std::__
     V[last] = V[0];
     adjust_heap(K, V, 0, last, vk, vv);
   }
+}
+
+// The depth-limit step of std::sort is std::__partial_sort(first, last, last), a heap
+// sort, whose only freedom is the order of equal keys.  With pairwise distinct keys the
+// sorted order is unique, so the heap sort's result puts every element at its segment
+// start + #smaller keys: the parallel forms below rank each element against its
+// segment (reporting in dup whether another element has the same key), and only a
+// segment with a repeated key keeps the sequential heap sort for its tie order.
+__device__ __forceinline__ uint32_t rank_in_segment(const uint32_t* k, uint32_t a, uint32_t b, uint32_t p, uint32_t key,
+                                                    bool& dup) {
+  uint32_t r = 0;
+  for (uint32_t q = a; q < b; ++q) {
+    const uint32_t kq = k[q];
+    r += kq < key ? 1u : 0u;
+    dup |= kq == key && q != p;
+  }
+  return r;
 }
 
 // Exclusive scan over the whole block (blockDim a multiple of 64, <= 1024); sh >= 16 u32.
@@ -876,11 +908,33 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
       if (lane == 0 && n) mark_leaf(S, f);
       continue;
     }
-    if (dd == 0) {
-      if (lane == 0) {
-        heap_sort(S.k + f, S.v + f, (int64_t)n);
-        for (uint32_t q = 0; q < n; ++q) mark_leaf(S, f + q);
+    if (dd == 0) {  // depth limit: rank_in_segment (heap sort on ties)
+      uint32_t kd[IS_WC], vd[IS_WC], rd[IS_WC];
+      bool dup = false;
+#pragma unroll
+      for (int c = 0; c < IS_WC; ++c) {
+        const uint32_t q = c * 64 + lane;
+        kd[c] = vd[c] = rd[c] = 0u;
+        if (q < n) {
+          kd[c] = S.k[f + q];
+          vd[c] = S.v[f + q];
+          rd[c] = f + rank_in_segment(S.k, f, f + n, f + q, kd[c], dup);
+        }
       }
+      const bool ties = __ballot(dup) != 0ull;
+      wsync();
+      if (!ties) {
+#pragma unroll
+        for (int c = 0; c < IS_WC; ++c)
+          if (c * 64 + lane < n) {
+            S.k[rd[c]] = kd[c];
+            S.v[rd[c]] = vd[c];
+          }
+      } else if (lane == 0) {
+        heap_sort(S.k + f, S.v + f, (int64_t)n);
+      }
+      wsync();
+      for (uint32_t q = lane; q < n; q += 64) mark_leaf(S, f + q);
       wsync();
       continue;
     }
@@ -933,7 +987,38 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       if (p < n && b - a > IS_THRESHOLD) actm |= 1u << c;
     }
     if (!__ballot(actm != 0u)) break;
-    if (dd == 0) {  // depth limit: heap sort every active segment (one lane; rare)
+    if (dd == 0) {  // depth limit: every active segment sorted (rank_in_segment; heap sort on ties)
+      {
+        uint32_t kd[C], vd[C], rd[C];
+        bool dup = false;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const uint32_t p = c * 64 + lane;
+          kd[c] = vd[c] = rd[c] = 0u;
+          if ((actm >> c) & 1u) {
+            kd[c] = S.k[p];
+            vd[c] = S.v[p];
+            rd[c] = (ab[c] & 0xFFFFu) + rank_in_segment(S.k, ab[c] & 0xFFFFu, ab[c] >> 16, p, kd[c], dup);
+          }
+        }
+        if (!__ballot(dup)) {
+          wsync();
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            if ((actm >> c) & 1u) {
+              S.k[rd[c]] = kd[c];
+              S.v[rd[c]] = vd[c];
+            }
+          wsync();
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const uint32_t p = c * 64 + lane;
+            if ((actm >> c) & 1u) ab[c] = p | ((p + 1) << 16);  // sorted: every position its own leaf
+          }
+          if (S.son && lane == 0) atomicAdd(&S.stat[9], 1u);
+          break;
+        }
+      }
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const uint32_t p = c * 64 + lane;
@@ -1185,10 +1270,10 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
         const int dd = (int)(it.y >> 16);
         if (n <= IS_THRESHOLD) {
           if (n) mark_leaf(S, off);
-        } else if (dd == 0) {
-          heap_sort(S.k + off, S.v + off, (int64_t)n);
-          if (S.son) atomicAdd(&S.stat[7], 1u);
-          for (uint32_t q = 0; q < n; ++q) mark_leaf(S, off + q);
+        } else if (dd == 0) {  // depth limit: the whole workgroup sorts it (below)
+          S.bc[6] = off;
+          S.bc[7] = it.y;
+          go = 2;
         } else if (n <= IS_WCAP) {  // a wave task: large ones from the front, small from the back
           S.units += n;  // the wave probe's unit count
           const uint32_t pk = off | (n << 13) | ((uint32_t)dd << 24);
@@ -1217,6 +1302,41 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     if (!S.bc[3]) break;
     const uint32_t off = S.bc[6], n = S.bc[7] & 0xFFFFu;
     const int dd = (int)(S.bc[7] >> 16);
+    if (S.bc[3] == 2) {  // depth limit: rank_in_segment by the workgroup (heap sort on ties)
+      uint32_t kd[IS_OC], vd[IS_OC], rd[IS_OC];
+      bool dup = false;
+#pragma unroll
+      for (int c = 0; c < IS_OC; ++c) {
+        const uint32_t q = c * IS_OT + threadIdx.x;
+        kd[c] = vd[c] = rd[c] = 0u;
+        if (q < n) {
+          kd[c] = S.k[off + q];
+          vd[c] = S.v[off + q];
+          rd[c] = off + rank_in_segment(S.k, off, off + n, off + q, kd[c], dup);
+        }
+      }
+      if (threadIdx.x == 0) S.bc[5] = 0;
+      __syncthreads();
+      if (dup) S.bc[5] = 1;
+      __syncthreads();
+      if (S.bc[5] == 0) {
+#pragma unroll
+        for (int c = 0; c < IS_OC; ++c)
+          if (c * IS_OT + threadIdx.x < n) {
+            S.k[rd[c]] = kd[c];
+            S.v[rd[c]] = vd[c];
+          }
+        if (S.son && threadIdx.x == 0) atomicAdd(&S.stat[9], 1u);
+      } else if (threadIdx.x == 0) {
+        heap_sort(S.k + off, S.v + off, (int64_t)n);
+        if (S.son) atomicAdd(&S.stat[7], 1u);
+      }
+      __syncthreads();
+      for (uint32_t q = threadIdx.x; q < n; q += IS_OT) mark_leaf(S, off + q);
+      pop();
+      __syncthreads();
+      continue;
+    }
     if (S.son && threadIdx.x == 0) atomicAdd(&S.stat[5], 1u);
     uint32_t c;
     if (n <= 2 * IS_OT) c = block_partition<2>(S, off, off + n);
@@ -1284,11 +1404,30 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
 
 // One partition of [f, l) (l - f > IS_LCAP) in global memory by the whole block,
 // in place in (K, V); (SK, SV) at the same positions is scratch.  Returns the cut.
+// (free != 0: a segment known to hold pairwise distinct keys, whose sorted order is
+// unique: the median of three pseudo-random positions instead of std::sort's first+1 /
+// mid / last-1, so that an input built against that rule does not stay quadratic.)
 __device__ __forceinline__ uint32_t global_partition(BlockLds& S, uint32_t* K, uint32_t* V, uint32_t* SK, uint32_t* SV, uint32_t f,
-                                     uint32_t l) {
+                                     uint32_t l, uint32_t free = 0) {
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
-    const uint32_t m = median_pos(K, f, l);
+    uint32_t m;
+    if (free) {
+      uint32_t x = f * 0x9E3779B9u ^ l * 0x85EBCA6Bu;
+      uint32_t r[3];
+      for (int i = 0; i < 3; ++i) {
+        x ^= x >> 16;
+        x *= 0x7FEB352Du;
+        x ^= x >> 15;
+        x *= 0x846CA68Bu;
+        x ^= x >> 16;
+        r[i] = f + 1 + x % (l - f - 1);
+      }
+      const uint32_t a = K[r[0]], b = K[r[1]], c = K[r[2]];
+      m = (a < b) ? (b < c ? r[1] : (a < c ? r[2] : r[0])) : (a < c ? r[0] : (b < c ? r[2] : r[1]));
+    } else {
+      m = median_pos(K, f, l);
+    }
     const uint32_t tk = K[f], tv = V[f];
     K[f] = K[m];
     V[f] = V[m];
@@ -1298,7 +1437,7 @@ __device__ __forceinline__ uint32_t global_partition(BlockLds& S, uint32_t* K, u
     S.bc[0] = 0;  // running >= count
     S.bc[1] = 0;  // running <= count
   }
-  __threadfence();
+  hand_off_fence();
   __syncthreads();
   const uint32_t P = K[f];
   const uint32_t n = l - f - 1, H = (l - f) / 2;
@@ -1372,13 +1511,46 @@ __device__ __forceinline__ uint32_t global_partition(BlockLds& S, uint32_t* K, u
       }
       __syncthreads();  // superchunks are independent within a pass
     }
-    __threadfence();  // pass 0's scratch (or pass 1's in-place writes) visible to every wave
+    hand_off_fence();  // pass 0's scratch (or pass 1's in-place writes) visible to every wave
     __syncthreads();
   }
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&S.bc[4], cut);
   __syncthreads();
   const uint32_t r = min(max(S.bc[4], f + 1), l - 1);
+  __syncthreads();
+  return r;
+}
+
+// Whether the len keys at K are pairwise distinct (one workgroup): an open-addressing
+// table of 2 len slots in the scratch arrays T0[0, len) and T1[0, len) (the other
+// buffer at the segment's positions), filled by atomicCAS.  For the depth limit on a
+// segment beyond the LDS (see rank_in_segment).
+__device__ bool distinct_keys(BlockLds& S, const uint32_t* K, uint32_t* T0, uint32_t* T1, uint32_t len) {
+  for (uint32_t q = threadIdx.x; q < len; q += IS_OT) T0[q] = T1[q] = IS_NONE;
+  if (threadIdx.x == 0) S.bc[5] = 0;
+  hand_off_fence();  // (the table's initial values before any wave's atomics)
+  __syncthreads();
+  const uint32_t nsl = 2 * len;
+  bool dup = false;
+  for (uint32_t q = threadIdx.x; q < len && !dup; q += IS_OT) {
+    const uint32_t key = K[q];
+    uint32_t h = key * 0x9E3779B1u;
+    h = (uint32_t)(((uint64_t)(h ^ (h >> 15)) * nsl) >> 32);
+    for (uint32_t probe = 0; probe < nsl; ++probe) {
+      uint32_t* slot = h < len ? &T0[h] : &T1[h - len];
+      const uint32_t old = atomicCAS(slot, IS_NONE, key);
+      if (old == IS_NONE) break;
+      if (old == key) {
+        dup = true;
+        break;
+      }
+      h = h + 1 == nsl ? 0u : h + 1;
+    }
+  }
+  if (dup) S.bc[5] = 1;
+  __syncthreads();
+  const bool r = S.bc[5] == 0;
   __syncthreads();
   return r;
 }
@@ -1452,19 +1624,31 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       const uint4 it = S.gstk[sp - 1];
       const uint32_t gf = it.x, gl = it.y, len = gl - gf;
       const int gd = (int)it.z;
+      const uint32_t gfree = it.w;  // 1: distinct keys, any exact sort (global_partition's free pivots)
       __syncthreads();
       if (threadIdx.x == 0) S.gsp = sp - 1;
       __syncthreads();
       if (len <= IS_LCAP) {
         if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[4], 1u);
         units += len;
-        lds_block(S, W, K, V, K0, V0, gf, len, gd);
-      } else if (gd == 0) {  // depth exhausted on a large segment: heap sort in place (slow, adversarial only)
+        // (free: std::sort's depth bounds the LDS stacks; its depth limit there is the
+        // parallel rank sort, exact for distinct keys)
+        lds_block(S, W, K, V, K0, V0, gf, len, gfree ? depth0(len) : gd);
+      } else if (gd == 0 && distinct_keys(S, K + gf, (buf ? K0 : K1) + gf, (buf ? V0 : V1) + gf, len)) {
+        // depth exhausted, distinct keys: the order is unique; go on with free pivots
+        if (threadIdx.x == 0) {
+          W.ctl[2] |= 4u;
+          if (S.son) atomicAdd(&W.ctl[9], 1u);
+          S.gstk[S.gsp++] = make_uint4(gf, gl, 60u, 1u);
+        }
+        __syncthreads();
+      } else if (gd == 0) {  // depth exhausted, a repeated key: heap sort in place (slow; adversarial only)
         if (threadIdx.x == 0) {
           heap_sort(K + gf, V + gf, (int64_t)len);
           W.ctl[2] |= 2u;
+          if (S.son) atomicAdd(&W.ctl[7], 1u);
         }
-        __threadfence();
+        hand_off_fence();
         __syncthreads();
         if (buf != 0)
           for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
@@ -1474,15 +1658,20 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
         __syncthreads();
       } else {
         if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
-        const uint32_t c = global_partition(S, K, V, buf ? K0 : K1, buf ? V0 : V1, gf, gl);
+        const uint32_t c = global_partition(S, K, V, buf ? K0 : K1, buf ? V0 : V1, gf, gl, gfree);
         if (threadIdx.x == 0) {
           W.ctl[2] |= 1u;
           uint32_t s = S.gsp;
-          S.gstk[s++] = make_uint4(c, gl, (uint32_t)(gd - 1), 0u);
-          S.gstk[s++] = make_uint4(gf, c, (uint32_t)(gd - 1), 0u);
+          const uint32_t cd = gfree ? 60u : (uint32_t)(gd - 1);  // (free: depth is irrelevant)
+          // the larger child below the smaller (the segments are disjoint, so the order
+          // is free): the smaller is done first and the stack stays O(log n) deep
+          const uint4 lo = make_uint4(gf, c, cd, gfree), hi = make_uint4(c, gl, cd, gfree);
+          const bool lo_small = c - gf <= gl - c;
+          S.gstk[s++] = lo_small ? hi : lo;
+          S.gstk[s++] = lo_small ? lo : hi;
           S.gsp = s;
         }
-        __threadfence();
+        hand_off_fence();
         __syncthreads();
       }
     }

@@ -323,8 +323,10 @@ class Ctx:
     def sort_stats(self) -> dict:
         a = np.zeros(32, np.uint32)
         _check(_lib.fccf_debug_sort_stats(self._h, a.ctypes.data), "fccf_debug_sort_stats", self._h)
-        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_items=int(a[4]),
-                    lds_levels=int(a[5]), heaps=int(a[7]), raw=a)
+        # (include/fccf.h, fccf_debug_sort_keys' path counters)
+        return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_segments=int(a[4]),
+                    block_parts=int(a[5]), wave_parts=int(a[6]), heaps=int(a[7]), depth0_distinct=int(a[9]),
+                    wave_tasks=int(a[16]) + int(a[18]), raw=a)
 
     def capture_race(self, hold_ms: int = 200, guard: bool = True) -> dict:
         """Test hook: a graph capture held for hold_ms concurrent with another thread's

@@ -262,9 +262,12 @@ int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes
  * order; perm_out[0..n) receives the values in sorted order (the finite ones first).
  * exact_gate != 0 runs the presorted second pass's single-workgroup form. */
 int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm_out);
-/* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags,
- * [3] global partitions, [4] LDS segments, [5] workgroup partitions, [6] wave
- * partitions, [7] heap sorts, [12] register-resident subtrees, [16] wave tasks.
+/* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags
+ * (1 global partitions, 2 a sequential heap sort beyond the LDS, 4 a depth-limit segment
+ * beyond the LDS with distinct keys), [3] global partitions, [4] LDS segments, [5]
+ * workgroup partitions, [6] wave partitions, [7] sequential heap sorts (depth limit,
+ * repeated keys), [9] depth-limit segments with pairwise distinct keys (sorted in
+ * parallel: their order is unique), [12] register-resident subtrees, [16] wave tasks.
  * fccf_debug_sort_keys returns FCCF_E_INTERNAL when an invariant flag is set. */
 /* Test hook: the device LM's correctly rounded double sin/cos (verify.hip); ok[i] = 0
  * where |x| is beyond its argument reduction. */

@@ -34,9 +34,13 @@ def _keys_cases(fccf, oracle):
     k[rng.integers(0, k.size, 500)] = INVALID  # non-finite points: PCL skips them
     cases["room_200k_nan"] = k
     cases["all_invalid_100"] = np.full(100, INVALID, np.uint32)
-    # depth-limit (heap sort) paths: McIlroy adversaries against this std::sort
-    for n in (200, 5000, 20_000):
+    # depth-limit (heap sort) paths: McIlroy adversaries against this std::sort.  Their
+    # keys are pairwise distinct (the parallel depth-limit paths: wave, workgroup, and
+    # beyond the LDS); halved, every key repeats (the sequential heap sort, tie order)
+    for n in (200, 5000, 20_000, 65_536):
         cases[f"adversary_{n}"] = oracle.sort_adversary(n)
+    for n in (200, 5000, 20_000):
+        cases[f"adversary_ties_{n}"] = (oracle.sort_adversary(n) // 2).astype(np.uint32)
     return cases
 
 
