@@ -30,7 +30,7 @@ METRIC = "coplane-pair correspondences/sec + end-to-end registration ms, 1M-pt p
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM"); every kernel here is HBM/latency bound
 # Kernels with a probe site (fccf-pcr_amd/csrc, FCCF_PROBED) and their algorithmic bytes per launch
 # ("Measurement").  The roofline reports the one with the most GPU time per step.
-PROBE_KERNELS = ["k_is_wave", "k_is_scatter", "k_is_block", "k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter",
+PROBE_KERNELS = ["k_is_count_plan", "k_is_wave", "k_is_scatter", "k_is_block", "k_xs_chain", "k_xs_chunk", "k_oct_sim", "k_rs_scatter",
                  "k_vg_keys", "k_vg_centroid", "k_gather", "k_voxel_fit", "k_fv_counts", "k_match_count",
                  "k_match_emit"]
 

@@ -42,6 +42,9 @@ namespace fccf {
 namespace {
 
 constexpr uint32_t IS_TILE = 2048;   // elements per round tile
+constexpr uint32_t IS_LARGE_MIN = 1u << 21;  // clouds from this size plan each round once (k_is_count_plan)
+constexpr int IS_NSH = 64;                       // round kernels: completion counter shards (last_block)
+constexpr int IS_DONE_WORDS = (IS_NSH + 1) * 32;  // u32 per launch: shards + top, 128 B apart
 constexpr int IS_TT = 256;           // round kernels: threads per block
 constexpr int IS_TC = IS_TILE / IS_TT;  // 8 elements per thread
 constexpr uint32_t IS_LCAP = 8192;   // largest segment a block kernel workgroup holds in LDS
@@ -258,11 +261,25 @@ __device__ __forceinline__ uint32_t upper_index(const uint32_t* pre, uint32_t n,
   }
   return lo;
 }
+// the same over a segment's tile prefixes in global memory (component 0: >=, 1: <=)
+__device__ __forceinline__ uint32_t upper_index_g(const uint2* pre, uint32_t n, uint32_t x, int comp) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint2 v = pre[mid];
+    if ((comp ? v.y : v.x) <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh64);
 
 // ---------------------------------------------------------------- k_is_prep
 // PCL pushes only finite points into its index vector, in input order: compact the
 // (key, index) pairs of finite points (rare: only when some point is not finite) and
-// mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_block's dequeue head.
+// mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_block's dequeue head;
+// the rounds' completion counters zeroed and round 0 planned (plan_round).
 // exact_gate (the driver's presorted second pass): sort only when the order check failed.
 __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*> V2, B2<const uint32_t*> d_n2,
                                                    B2<const VGParams*> P2, B2<IsBufs> W2, int exact_gate) {
@@ -277,37 +294,496 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
     W.ctl[0] = ns;
     for (int i = 1; i < 32; ++i) W.ctl[i] = 0;
   }
-  if (ns == 0 || ns >= n) return;
-  uint32_t* K = K2[e];
-  uint32_t* V = V2[e];
-  __shared__ uint32_t sh[16];
-  uint32_t out = 0;
-  for (uint32_t b = 0; b < n; b += 1024) {
-    const uint32_t i = b + threadIdx.x;
-    const uint32_t k = i < n ? K[i] : IS_NONE, v = i < n ? V[i] : 0u;
-    const uint32_t keep = k != IS_NONE;
-    uint32_t tot;
-    const uint32_t o = block_excl_scan(keep, sh, &tot);  // its barriers order these reads before the writes
-    if (keep) {
-      K[out + o] = k;
-      V[out + o] = v;
+  for (int i = threadIdx.x; i < 2 * IS_RMAX * IS_DONE_WORDS; i += 1024) W.done[i] = 0;
+  if (ns > 0 && ns < n) {
+    uint32_t* K = K2[e];
+    uint32_t* V = V2[e];
+    __shared__ uint32_t sh[16];
+    uint32_t out = 0;
+    for (uint32_t b = 0; b < n; b += 1024) {
+      const uint32_t i = b + threadIdx.x;
+      const uint32_t k = i < n ? K[i] : IS_NONE, v = i < n ? V[i] : 0u;
+      const uint32_t keep = k != IS_NONE;
+      uint32_t tot;
+      const uint32_t o = block_excl_scan(keep, sh, &tot);  // its barriers order these reads before the writes
+      if (keep) {
+        K[out + o] = k;
+        V[out + o] = v;
+      }
+      out += tot;
+      __syncthreads();
     }
-    out += tot;
-    __syncthreads();
+    for (uint32_t i = ns + threadIdx.x; i < n; i += 1024) K[i] = IS_NONE;
   }
-  for (uint32_t i = ns + threadIdx.x; i < n; i += 1024) K[i] = IS_NONE;
+  __shared__ uint64_t sh64[16];
+  plan_round(W, 0, ns, sh64);
 }
 
 // ---------------------------------------------------------------- rounds
-// k_is_count_plan: the round's plan, then per-tile ge/le counts against the segment's
+// Per round r, two launches over maxtiles workgroups (one 2048-element tile each):
+//  k_is_count_plan  the tile's ge/le counts against its segment's pivot and the
+//                   tile-local position lists; the LAST workgroup to finish turns all
+//                   tiles' counts into each segment's exclusive tile prefix (pre) and
+//                   its <= total (letot), once for the round;
+//  k_is_scatter     ranks from that prefix, every element to its place after the
+//                   partition in the other buffer, the cut by atomicMin; the LAST
+//                   workgroup plans round r+1 (plan_round).
+// Round 0 is planned by k_is_prep.  (Before, every workgroup re-derived the round's
+// segment table and re-scanned its whole segment's tile counts: at c5 that was ~10K
+// workgroups x up to ~5K entries of block scans per launch, most of the rounds' time.)
+//
+// Hand-offs inside one launch (to its last workgroup): written with agent-scope
+// atomics (performed at the coherence point), read with atomic read-modify-writes
+// after an agent-scope acquire, so no stale L1 or L2 copy on another XCD is read
+// (MI355X_MICROARCH.md, inter-workgroup visibility); every storing wave drains
+// (s_waitcnt vmcnt(0)) before the barrier that precedes its workgroup's counter add.
+// Everything else is consumed by a later launch.
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t coherent_load(uint32_t* p) { return atomicAdd(p, 0u); }
+
+// Whether this workgroup is the last of its grid row to get here.  done: the launch's
+// IS_DONE_WORDS counters (zeroed by k_is_prep): IS_NSH shard counters and a top one,
+// each on its own 128-byte line -- same-address atomics serialise (~18 ns each), so one
+// counter for thousands of workgroups cost ~0.1 ms per launch at c5.  The last of a
+// shard adds to the top counter; the last there is the grid's last.  Every thread of
+// every workgroup must call it; the last workgroup returns true (in all threads) after
+// an agent-scope acquire.
+__device__ bool last_block(uint32_t* done, uint32_t* sflag) {
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t sh = blockIdx.x % IS_NSH, nsh = min((uint32_t)IS_NSH, gridDim.x);
+    const uint32_t members = (gridDim.x - sh + IS_NSH - 1) / IS_NSH;
+    bool last = false;
+    if (atomicAdd(&done[sh * 32], 1u) == members - 1u) last = atomicAdd(&done[IS_NSH * 32], 1u) == nsh - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_vm();
+    }
+    *sflag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return *sflag != 0u;
+}
+
+// child_of, reading round r-1's cut with an atomic (it was set by the atomicMin of
+// workgroups of the same launch: the planner in k_is_scatter's last workgroup)
+__device__ __forceinline__ Child child_coherent(const IsBufs& W, int r, uint32_t nsort, uint32_t i) {
+  if (r == 0) return {0u, nsort, depth0(nsort)};
+  const IsSeg s = W.segs[(size_t)(r - 1) * W.segmax + i / 2];
+  const uint32_t c = min(max(coherent_load(&W.cuts[(size_t)(r - 1) * W.segmax + i / 2]), s.f + 1), s.l - 1);
+  return (i & 1) ? Child{c, s.l, s.depth - 1} : Child{s.f, c, s.depth - 1};
+}
+
+// Largest u < n with key(u) <= x, by one wave (key(0) <= x and key ascending): a
+// 64-ary search, one load per lane and a ballot per step, ~log64(n) dependent loads.
+template <class KeyAt>
+__device__ __forceinline__ uint32_t wave_upper_index(KeyAt key, uint32_t n, uint32_t x) {
+  const uint32_t lane = lane_id();
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi), key(lo) <= x
+  while (hi - lo > 1) {
+    const uint32_t stride = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + lane * stride;
+    const uint64_t m = __ballot(idx < hi && key(idx) <= x);  // bit 0 set: key(lo) <= x
+    const uint32_t nlo = lo + (63u - (uint32_t)__clzll((long long)m)) * stride;
+    hi = min(hi, nlo + stride);
+    lo = nlo;
+    if (stride == 1) break;
+  }
+  return lo;
+}
+
+// The plan of round r, by one workgroup: the children of round r-1's segments (the
+// root for r = 0) longer than the tier become the round's segments (ptab: f, l, depth,
+// first tile), the shorter non-empty children go to the owned list, and the IsRound
+// record.  PL children per thread per step (their cut loads in flight together).
+constexpr int PL = 8;
+__device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh64) {
+  const uint32_t nch = nchildren(W, r);
+  const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
+  uint32_t nseg = 0, ntiles = 0, nown = 0;
+  for (uint32_t b0 = 0; b0 < nch; b0 += blockDim.x * PL) {
+    const uint32_t i0 = b0 + threadIdx.x * PL;  // this thread's PL consecutive children (PL/2 parents)
+    uint32_t cut[PL / 2];
+    IsSeg sg[PL / 2];
+#pragma unroll
+    for (int k = 0; k < PL / 2; ++k) {
+      const uint32_t i = i0 + 2 * k;
+      cut[k] = 0u;
+      sg[k] = IsSeg{};
+      if (r > 0 && i < nch) {
+        sg[k] = W.segs[(size_t)(r - 1) * W.segmax + i / 2];
+        cut[k] = coherent_load(&W.cuts[(size_t)(r - 1) * W.segmax + i / 2]);
+      }
+    }
+    Child ch[PL];
+    uint64_t tot_t = 0;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const uint32_t i = i0 + k;
+      Child c = {0u, 0u, 0};
+      if (i < nch) {
+        if (r == 0) {
+          c = Child{0u, nsort, depth0(nsort)};
+        } else {
+          const IsSeg& q = sg[k / 2];
+          const uint32_t cc = min(max(cut[k / 2], q.f + 1), q.l - 1);
+          c = (k & 1) ? Child{cc, q.l, q.depth - 1} : Child{q.f, cc, q.depth - 1};
+        }
+      }
+      ch[k] = c;
+      const bool lg = i < nch && is_large(c, W.tier), ow = i < nch && !lg && c.l > c.f;
+      // packed counters: large (21 bits) | owned (21) | tiles (22)
+      tot_t += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of(c.l - c.f) : 0u) << 42);
+    }
+    uint64_t s_all;
+    uint64_t run = block_excl_scan64(tot_t, sh64, &s_all);
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const uint32_t i = i0 + k;
+      const Child c = ch[k];
+      const bool lg = i < nch && is_large(c, W.tier), ow = i < nch && !lg && c.l > c.f;
+      const uint32_t p_lg = (uint32_t)(run & 0x1FFFFFu), p_ow = (uint32_t)((run >> 21) & 0x1FFFFFu),
+                     p_nt = (uint32_t)(run >> 42);
+      if (lg) W.ptab[nseg + p_lg] = make_uint4(c.f, c.l, (uint32_t)c.d, ntiles + p_nt);
+      if (ow) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
+      run += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of(c.l - c.f) : 0u) << 42);
+    }
+    nseg += (uint32_t)(s_all & 0x1FFFFFu);
+    nown += (uint32_t)((s_all >> 21) & 0x1FFFFFu);
+    ntiles += (uint32_t)(s_all >> 42);
+  }
+  // (pad: elements partitioned this round, the scatter probe's unit count, summed by
+  // the scatter's first tiles)
+  if (threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
+}
+
+// Tile t of segment j: pivot (its first tile publishes the segment record and the
+// initial cut), counts and its segment (atomics: read by this launch's last
+// workgroup), lists.
+__device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
+                                           const IsBufs& W, int r, uint32_t t, uint32_t j) {
+  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  __shared__ uint32_t bsh[4];
+  const uint4 pt = W.ptab[j];
+  const uint32_t f = pt.x, l = pt.y, tile0 = pt.w;
+  const uint32_t i = t - tile0;
+  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+  uint32_t kk[IS_TC];
+  // the tile's keys are loaded before the pivot, so their latency overlaps thread 0's
+  // dependent median reads below
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    kk[c] = p < b ? K[p] : 0u;
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t m = median_pos(K, f, l);
+    bsh[0] = m;
+    bsh[1] = K[m];
+    bsh[2] = K[f];
+    const IsSeg rec{f, l, (int32_t)pt.z, tile0, m, bsh[1], bsh[2], V[f], V[m]};
+    W.tdesc[t] = IsTile{j, rec};  // the scatter's one-load view of this tile's segment
+    atomicExch(&W.tseg[t], j);
+    if (t == tile0) {  // the segment's record, once
+      W.segs[(size_t)r * W.segmax + j] = rec;
+      W.cuts[(size_t)r * W.segmax + j] = l;
+    }
+  }
+  __syncthreads();
+  const uint32_t m = bsh[0], P = bsh[1], kf = bsh[2];
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c)
+    if (a + c * IS_TT + threadIdx.x == m) kk[c] = kf;  // the median-to-first swap
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const bool ok = a + c * IS_TT + threadIdx.x < b;
+    const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+    if (lane == 0) {
+      cg[c * 4 + w] = (uint32_t)__popcll(bg);
+      cl[c * 4 + w] = (uint32_t)__popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
+    const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+    uint32_t xg = xg0, xl = xl0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+      if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+    }
+    if (lane < IS_TC * 4) {
+      pg[lane] = xg - xg0;
+      pl[lane] = xl - xl0;
+    }
+    if (lane == IS_TC * 4 - 1) {
+      atomicExch(&W.cnt[2 * (size_t)t], xg);
+      atomicExch(&W.cnt[2 * (size_t)t + 1], xl);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < IS_TC; ++c) {
+    const uint32_t p = a + c * IS_TT + threadIdx.x;
+    const bool ok = p < b;
+    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    if (ge) W.gel[a + pg[c * 4 + w] + mbcnt(bg)] = (uint16_t)(p - a);
+    if (le) W.lel[a + pl[c * 4 + w] + mbcnt(bl)] = (uint16_t)(p - a);
+  }
+}
+
+// The round's tile prefixes, by its last count workgroup: per tile the exclusive
+// (>=, <=) prefix within its segment (pre), per segment the <= total (letot).  TP
+// consecutive tiles per thread per step (their atomic loads in flight together).
+// base: LDS scratch of 2 x segmax u32 (the running prefix at each segment's first tile).
+constexpr int TP = 16;
+__device__ void tile_prefix(const IsBufs& W, int r, uint32_t* base, uint64_t* sh64) {
+  const uint32_t ntiles = W.rounds[r].ntiles;
+  uint32_t* bg = base;
+  uint32_t* bl = base + W.segmax;
+  uint64_t run = 0;
+  for (uint32_t b0 = 0; b0 < ntiles; b0 += blockDim.x * TP) {
+    const uint32_t t0 = b0 + threadIdx.x * TP;
+    uint32_t g[TP], q[TP], js[TP];
+#pragma unroll
+    for (int k = 0; k < TP; ++k) {
+      const uint32_t t = t0 + k;
+      g[k] = q[k] = js[k] = 0u;
+      if (t < ntiles) {
+        g[k] = coherent_load(&W.cnt[2 * (size_t)t]);
+        q[k] = coherent_load(&W.cnt[2 * (size_t)t + 1]);
+        js[k] = coherent_load(&W.tseg[t]);
+      }
+    }
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < TP; ++k) sum += (uint64_t)g[k] | ((uint64_t)q[k] << 32);
+    uint64_t tot;  // >= counts (low 32 bits) and <= counts (high): each sums to <= the sort length
+    uint64_t x = run + block_excl_scan64(sum, sh64, &tot);
+    uint64_t xs[TP];
+#pragma unroll
+    for (int k = 0; k < TP; ++k) {
+      const uint32_t t = t0 + k;
+      xs[k] = x;
+      if (t < ntiles && t == W.ptab[js[k]].w) {
+        bg[js[k]] = (uint32_t)x;
+        bl[js[k]] = (uint32_t)(x >> 32);
+      }
+      x += (uint64_t)g[k] | ((uint64_t)q[k] << 32);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TP; ++k) {
+      const uint32_t t = t0 + k;
+      if (t >= ntiles) continue;
+      const uint32_t j = js[k];
+      W.pre[2 * (size_t)t] = (uint32_t)xs[k] - bg[j];
+      W.pre[2 * (size_t)t + 1] = (uint32_t)(xs[k] >> 32) - bl[j];
+      const uint4 pt = W.ptab[j];
+      if (t == pt.w + tiles_of(pt.y - pt.x) - 1u) W.letot[j] = (uint32_t)(xs[k] >> 32) + q[k] - bl[j];
+    }
+    run += tot;
+    __syncthreads();
+  }
+}
+
+// Dynamic LDS: 2 * segmax u32 (tile_prefix).
+__global__ void __launch_bounds__(IS_TT) k_is_count_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
+                                                         B2<IsBufs> W2, int r) {
+  KT();
+  extern __shared__ uint32_t dyn[];
+  __shared__ uint64_t sh64[16];
+  __shared__ uint32_t sflag, sj;
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t t = blockIdx.x;
+  const IsRound rd = W.rounds[r];
+  if (t < rd.ntiles) {
+    if (threadIdx.x < 64) {  // the tile's segment: the last with first tile <= t
+      const uint32_t j = wave_upper_index([&](uint32_t u) { return W.ptab[u].w; }, rd.nseg, t);
+      if (threadIdx.x == 0) sj = j;
+    }
+    __syncthreads();
+    count_tile(K2[e], V2[e], W, r, t, sj);
+  }
+  if (!last_block(W.done + (size_t)(2 * r) * IS_DONE_WORDS, &sflag)) return;
+  tile_prefix(W, r, dyn, sh64);
+}
+
+// Every element of the round's large segments to its place after the partition,
+// written to the other buffer; the cut by atomicMin; the last workgroup plans round
+// r + 1 (if r + 1 < R).  The partners of a tile's swapped elements have contiguous
+// ranks in the other list, so each workgroup locates that window of its segment's
+// tile prefix once (wave_upper_index over global memory) and keeps it in LDS.
+constexpr uint32_t IS_WIN = 256;  // prefix window in LDS (larger windows: binary search in global memory)
+__global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
+                                                      B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r,
+                                                      int R) {
+  KT();
+  __shared__ uint64_t sh64[16];
+  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  __shared__ uint32_t wing[IS_WIN], winl[IS_WIN];  // windows of the >= / <= prefixes
+  __shared__ uint32_t stot[2], swin[4];            // the tile's totals; window bounds
+  __shared__ uint32_t scut, sflag;
+  const int e = blockIdx.y;
+  const IsBufs W = W2[e];
+  const uint32_t t = blockIdx.x;
+  if (r == 0 && t == 0 && e == 0 && threadIdx.x == 0) is_inject(W, IS_FAULT_SCATTER);
+  if (t < W.rounds[r].ntiles) {
+    const IsTile td = W.tdesc[t];
+    const uint32_t j = td.j;
+    const IsSeg s = td.s;
+    const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0, m = s.m, P = s.P;
+    const uint32_t* __restrict__ K = Ki2[e];
+    const uint32_t* __restrict__ V = Vi2[e];
+    uint32_t* __restrict__ Ko = Ko2[e];
+    uint32_t* __restrict__ Vo = Vo2[e];
+    const uint2* pre = reinterpret_cast<const uint2*>(W.pre) + s.tile0;  // the segment's tile prefixes
+    const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    if (i == 0 && threadIdx.x == 0) atomicAdd(&W.rounds[r].pad, l - f);
+    // the tile's elements are loaded first: their latency overlaps the window searches
+    uint32_t kk[IS_TC], vv[IS_TC];
+#pragma unroll
+    for (int c = 0; c < IS_TC; ++c) {
+      const uint32_t p = a + c * IS_TT + threadIdx.x;
+      const bool ok = p < b;
+      kk[c] = ok ? K[p] : 0u;
+      vv[c] = ok ? V[p] : 0u;
+      if (p == m) {
+        kk[c] = s.kf;
+        vv[c] = s.vf;
+      }
+    }
+    if (threadIdx.x == 0) scut = IS_NONE;
+    const uint2 own = pre[i];
+    const uint32_t le_tot = W.letot[j];
+#pragma unroll
+    for (int c = 0; c < IS_TC; ++c) {
+      const bool ok = a + c * IS_TT + threadIdx.x < b;
+      const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+      if (lane == 0) {
+        cg[c * 4 + w] = (uint32_t)__popcll(bg);
+        cl[c * 4 + w] = (uint32_t)__popcll(bl);
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+      uint32_t xg = xg0, xl = xl0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+        if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+      }
+      if (lane < IS_TC * 4) {
+        pg[lane] = xg - xg0 + own.x;
+        pl[lane] = xl - xl0 + own.y;
+      }
+      if (lane == IS_TC * 4 - 1) {
+        stot[0] = xg;
+        stot[1] = xl;
+      }
+    }
+    __syncthreads();
+    // Partner windows.  A swapped >= element of rank gx in [own.x, own.x + cg) takes
+    // R[gx + 1], the <= element of rank le_tot - gx - 1; a swapped <= element of rank
+    // lx in [own.y, own.y + cl) takes L[le_tot - lx], the >= element of rank
+    // le_tot - lx - 1.  Each rank range spans a window of tiles of the other list.
+    const uint32_t cgt = stot[0], clt = stot[1];
+    const bool lw_any = cgt > 0 && le_tot > own.x;  // the <= window (partners of swapped >=)
+    const uint32_t xl_hi = lw_any ? le_tot - own.x - 1 : 0u;
+    const uint32_t xl_lo = lw_any ? (le_tot >= own.x + cgt ? le_tot - own.x - cgt : 0u) : 0u;
+    const bool gw_any = clt > 0 && le_tot > own.y;  // the >= window (partners of swapped <=)
+    const uint32_t xg_hi = gw_any ? le_tot - own.y - 1 : 0u;
+    const uint32_t xg_lo = gw_any ? (le_tot >= own.y + clt ? le_tot - own.y - clt : 0u) : 0u;
+    if (w < 4) {
+      uint32_t u = 0;
+      if (w == 0 && lw_any) u = wave_upper_index([&](uint32_t k) { return pre[k].y; }, nt, xl_lo);
+      if (w == 1 && lw_any) u = wave_upper_index([&](uint32_t k) { return pre[k].y; }, nt, xl_hi);
+      if (w == 2 && gw_any) u = wave_upper_index([&](uint32_t k) { return pre[k].x; }, nt, xg_lo);
+      if (w == 3 && gw_any) u = wave_upper_index([&](uint32_t k) { return pre[k].x; }, nt, xg_hi);
+      if (lane == 0) swin[w] = u;
+    }
+    __syncthreads();
+    const uint32_t wl_lo = swin[0], wl_n = lw_any ? swin[1] - swin[0] + 1 : 0u;
+    const uint32_t wg_lo = swin[2], wg_n = gw_any ? swin[3] - swin[2] + 1 : 0u;
+    for (uint32_t k = threadIdx.x; k < IS_WIN; k += IS_TT) {
+      if (k < wl_n) winl[k] = pre[wl_lo + k].y;
+      if (k < wg_n) wing[k] = pre[wg_lo + k].x;
+    }
+    __syncthreads();
+    // destinations: the swapped elements' partner positions come from the lists (all
+    // list loads issued before any store)
+    uint32_t cut = IS_NONE;
+    uint32_t dst[IS_TC];
+#pragma unroll
+    for (int c = 0; c < IS_TC; ++c) {
+      const uint32_t p = a + c * IS_TT + threadIdx.x;
+      const bool ok = p < b;
+      const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+      const uint64_t bg = __ballot(ge), bl = __ballot(le);
+      const uint32_t gx = pg[c * 4 + w] + mbcnt(bg);  // # >= P before p in the segment
+      const uint32_t lx = pl[c * 4 + w] + mbcnt(bl);  // # <= P before p
+      const bool sg = ge && le_tot - lx - (le ? 1u : 0u) >= gx + 1;
+      const bool sl = le && gx >= le_tot - lx;
+      if ((ge && !sg) || sl) cut = min(cut, p);  // L[K+1] / R[K]
+      dst[c] = ok ? p : IS_NONE;
+      if (sg) {  // R[gx+1]: the (le_tot-gx-1)-th <= P from the left
+        const uint32_t x = le_tot - gx - 1;
+        const uint32_t u = wl_n <= IS_WIN ? wl_lo + upper_index(winl, wl_n, x) : upper_index_g(pre, nt, x, 1);
+        const uint32_t au = f + 1 + u * IS_TILE;
+        dst[c] = au + W.lel[au + (x - (wl_n <= IS_WIN ? winl[u - wl_lo] : pre[u].y))];
+      } else if (sl) {  // L[kr]: the (kr-1)-th >= P from the left
+        const uint32_t x = le_tot - lx - 1;
+        const uint32_t u = wg_n <= IS_WIN ? wg_lo + upper_index(wing, wg_n, x) : upper_index_g(pre, nt, x, 0);
+        const uint32_t au = f + 1 + u * IS_TILE;
+        dst[c] = au + W.gel[au + (x - (wg_n <= IS_WIN ? wing[u - wg_lo] : pre[u].x))];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < IS_TC; ++c) {
+      const uint32_t d = dst[c];
+      if (d == IS_NONE) continue;
+      if (d <= f || d >= l) {  // cannot happen; never write outside the segment
+        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
+        continue;
+      }
+      Ko[d] = kk[c];
+      Vo[d] = vv[c];
+    }
+    cut = wave_min_u32(cut);
+    if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (scut != IS_NONE) atomicMin(&W.cuts[(size_t)r * W.segmax + j], scut);
+      if (i == 0) {
+        Ko[f] = P;
+        Vo[f] = s.vm;
+      }
+    }
+  }
+  if (r + 1 >= R) return;  // (uniform: no planner after the last round)
+  if (!last_block(W.done + (size_t)(2 * r + 1) * IS_DONE_WORDS, &sflag)) return;
+  plan_round(W, r + 1, W.ctl[0], sh64);
+}
+
+// ---------------------------------------------------------------- rounds, small clouds
+// Below IS_LARGE_MIN points the round plan is derived by every workgroup itself (the
+// segment table from the previous round's segments and cuts, a few hundred entries)
+// and every scatter workgroup scans its segment's tile counts itself: at ~700
+// workgroups per launch that costs less than the large form's per-round serial steps
+// (last-workgroup hand-offs; c3: 0.76 vs 0.96 ms main VoxelGrid).
+//
+// k_is_count_plan_s: the round's plan, then per-tile ge/le counts against the segment's
 // pivot and the tile-local position lists (offsets from the tile start, in position
-// order).  Every workgroup first derives the round's segment table itself
-// from the previous round's segments and cuts (a few hundred entries, in LDS): the
-// workgroup of a segment's first tile publishes its IsSeg and initial cut, every
-// workgroup its tile's descriptor (IsTile), workgroup 0 the owned list of small
-// children and the IsRound; the scatter reads them after the kernel boundary.  (A
-// separate single-workgroup plan kernel per round cost 0.07 ms per registration.)
-__device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
+// order).  The workgroup of a segment's first tile publishes its IsSeg and initial
+// cut, every workgroup its tile's descriptor (IsTile), workgroup 0 the owned list of
+// small children and the IsRound; the scatter reads them after the kernel boundary.
+__device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
                                               const IsBufs& W, int r, uint32_t* dyn) {
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
   __shared__ uint32_t bsh[4];
@@ -440,17 +916,17 @@ __device__ __forceinline__ void is_count_body(const uint32_t* __restrict__ K, co
 }
 
 // Dynamic LDS: 4 * segmax u32 (the round's segment table).
-__global__ void __launch_bounds__(IS_TT) k_is_count_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
+__global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
                                                          B2<IsBufs> W2, int r) {
   KT();
   extern __shared__ uint32_t dyn[];
   const int e = blockIdx.y;
-  is_count_body(K2[e], V2[e], W2[e], r, dyn);
+  is_count_body_s(K2[e], V2[e], W2[e], r, dyn);
 }
 
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
-__global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
+__global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
                                                       B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
   KT();
   extern __shared__ uint32_t dyn[];
@@ -580,6 +1056,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     }
   }
 }
+
 
 // ---------------------------------------------------------------- finish: block + wave kernels
 // After the rounds every segment is at most IS_LCAP long (leftovers beyond it are
@@ -1820,7 +2297,7 @@ size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
   return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + sizeof(IsTile) * mt + 256 + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
-         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 8 * 256;
+         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 12 * 256;
 }
 
 IsBufs introsort_carve(void* base, uint32_t cap) {
@@ -1846,6 +2323,10 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
   b.taskmax = cap / 16 + 64;
   b.tasks = (uint4*)take(sizeof(uint4) * (size_t)b.taskmax);
+  b.ptab = (uint4*)take(sizeof(uint4) * (size_t)b.segmax);
+  b.pre = (uint32_t*)take(8 * (size_t)b.maxtiles);
+  b.letot = (uint32_t*)take(4 * (size_t)b.segmax);
+  b.done = (uint32_t*)take(4 * 2 * (size_t)IS_RMAX * IS_DONE_WORDS);
   b.prog = nullptr;
   b.trace = nullptr;
   b.tier = introsort_tier();
@@ -1867,18 +2348,36 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   k_is_prep<<<dim3(1, nbatch), 1024, 0, st>>>(k0, v0, d_n, P, b, exact_gate ? 1 : 0);
   step("prep", 0);
   const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap);
-  const size_t lds_plan = 16 * (size_t)segmax, lds_scatter = 8 * (size_t)maxtiles;
+  // the round plan's form: once per round (large clouds) or per workgroup (small ones);
+  // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
+  const char* pm = std::getenv("FCCF_IS_PLAN");
+  const bool large = pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN);
   for (int r = 0; r < R; ++r) {
     const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
-    k_is_count_plan<<<dim3(maxtiles, nbatch), IS_TT, lds_plan, st>>>(B2<const uint32_t*>(ki),
-                                                                    B2<const uint32_t*>(vi), b, r);
-    step("count", r);
-    // algorithmic bytes: key + value read and written, plus a 2-byte list entry
-    FCCF_LAUNCH("k_is_scatter",
-                (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
-                k_is_scatter, dim3(maxtiles, nbatch), IS_TT, lds_scatter, st, B2<const uint32_t*>(ki),
-                B2<const uint32_t*>(vi), ko, vo, b, r);
+    if (large) {
+      // algorithmic bytes: the key read, a 2-byte list entry written (x2: >= and <= lists share a unit)
+      FCCF_LAUNCH("k_is_count_plan",
+                  (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
+                  k_is_count_plan, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)segmax, st, B2<const uint32_t*>(ki),
+                  B2<const uint32_t*>(vi), b, r);
+      step("count", r);
+      // algorithmic bytes: key + value read and written, plus a 2-byte list entry
+      FCCF_LAUNCH("k_is_scatter",
+                  (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
+                  k_is_scatter, dim3(maxtiles, nbatch), IS_TT, 0, st, B2<const uint32_t*>(ki),
+                  B2<const uint32_t*>(vi), ko, vo, b, r, R);
+    } else {
+      FCCF_LAUNCH("k_is_count_plan",
+                  (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
+                  k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B2<const uint32_t*>(ki),
+                  B2<const uint32_t*>(vi), b, r);
+      step("count", r);
+      FCCF_LAUNCH("k_is_scatter",
+                  (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
+                  k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)maxtiles, st, B2<const uint32_t*>(ki),
+                  B2<const uint32_t*>(vi), ko, vo, b, r);
+    }
     step("scatter", r);
   }
   // algorithmic bytes: each element's key and value read once and written once

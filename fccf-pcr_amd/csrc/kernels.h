@@ -58,8 +58,8 @@ struct IsBufs {
   uint32_t* ctl;        // [0] sort length, [1] block dequeue head, [2] slow paths taken (1 global partition,
                         // 2 heap), [3..15] counters, [16] large wave tasks, [18] small wave tasks
                         // (stored from the end), [19]/[20] wave/block probe unit counts
-  uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot)
-  uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles)
+  uint32_t* cnt;        // per round tile: (#>= pivot, #<= pivot), written with atomics
+  uint32_t* tseg;       // per round tile: its segment (0xFFFFFFFF past the round's tiles; plan_round)
   IsTile* tdesc;        // per round tile: its segment and the segment's record (the scatter's input)
   uint16_t *gel, *lel;  // tile-local positions of the >= / <= elements, indexed from the tile start
   IsRound* rounds;      // IS_RMAX
@@ -67,6 +67,10 @@ struct IsBufs {
   uint32_t* cuts;       // IS_RMAX x segmax
   IsOwn* own;           // ownmax
   uint4* tasks;         // wave tasks {f, n, depth, -} (count in ctl[16])
+  uint4* ptab;          // the current round's plan: per segment {f, l, depth, first tile} (plan_round)
+  uint32_t* pre;        // per round tile: exclusive (>=, <=) prefix within its segment (k_is_count_plan's last workgroup)
+  uint32_t* letot;      // per segment of the round: its <= count
+  uint32_t* done;       // per round, count and scatter: sharded completion counters (last-workgroup hand-offs)
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   unsigned long long* trace;  // dev (null = off): per block item / wave task {start, end, size, who},
                               // block records from 0 (count in ctl[24]), wave records from taskmax (ctl[25])

@@ -106,3 +106,25 @@ def test_downsample_equals_reference_order(ctx, fccf, oracle, n, leaf, seed):
     ref, _ = oracle.voxel_grid(pts, leaf, oracle.INTROSORT)
     assert out.shape == ref.shape
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["large", "small"])
+def test_round_plan_forms_equal_std_sort(ctx, fccf, oracle, plan, monkeypatch):
+    """Both forms of the rounds' plan (FCCF_IS_PLAN: once per round by the last
+    workgroups, the default from 2M points; or derived by every workgroup, below it)
+    on every case and on the c3 keys, against the oracle's std::sort."""
+    monkeypatch.setenv("FCCF_IS_PLAN", plan)
+    cases = _keys_cases(fccf, oracle)
+    c = fccf.CONFIGS["c3"]
+    src, _, _ = fccf.synth_pair(c["n"], c["room"])
+    inv = np.float32(1.0) / np.float32(c["leaf"])
+    minb = np.floor(src.min(0) * inv).astype(np.int64)
+    div = np.floor(src.max(0) * inv).astype(np.int64) - minb + 1
+    ijk = (np.floor(src * inv) - minb.astype(np.float32)).astype(np.int64)
+    cases["c3_src"] = (ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]).astype(np.uint32)
+    bad = [name for name, k in cases.items() if not np.array_equal(ctx.sort_keys(k), oracle.sort_pairs(k))]
+    assert not bad, bad
+    out = ctx.downsample(src, c["leaf"])
+    ref, _ = oracle.voxel_grid(src, c["leaf"], oracle.INTROSORT)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
