@@ -240,9 +240,25 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
       HIP_CHECK(hipMemsetAsync(dtr, 0, 64 * (size_t)b.is.taskmax, st));
       b.is.trace = dtr;
     }
+    // FCCF_SHARD_D_SIM=<r>/<N> (dev, row D): sort as rank r of N would -- its range only,
+    // no gather (sort_stats[28..29] = the range); the other positions are left unsorted
+    if (const char* sim = std::getenv("FCCF_SHARD_D_SIM")) {
+      int r = 0, nr = 1;
+      if (std::sscanf(sim, "%d/%d", &r, &nr) == 2 && nr > 1 && nr <= IS_SHARD_MAX && r >= 0 && r < nr) {
+        b.is.shard_n = (uint32_t)nr;
+        b.is.shard_rank = (uint32_t)r;
+        b.is.shard_r0 = (uint32_t)shard_sort_r0(nr);
+      }
+    }
     const auto tsort = std::chrono::steady_clock::now();
+    uint32_t sort_ns = 0;
+    hipEvent_t ev0, ev1;  // device time of the sort alone (sort_stats[31], ns)
+    HIP_CHECK(hipEventCreate(&ev0));
+    HIP_CHECK(hipEventCreate(&ev1));
+    HIP_CHECK(hipEventRecord(ev0, st));
     introsort_u32(b.k0, b.v0, b.k1, b.v1, B2<const uint32_t*>(d_sc), B2<const VGParams*>(b.params), cap, b.is, st, 1,
                   exact_gate != 0);
+    HIP_CHECK(hipEventRecord(ev1, st));
     if (tpath) {
       std::vector<unsigned long long> h(8 * (size_t)b.is.taskmax);
       uint32_t ctl[32];
@@ -283,7 +299,16 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     }
     if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
+    {
+      float ms = 0.f;
+      HIP_CHECK(hipEventSynchronize(ev1));
+      HIP_CHECK(hipEventElapsedTime(&ms, ev0, ev1));
+      (void)hipEventDestroy(ev0);
+      (void)hipEventDestroy(ev1);
+      sort_ns = (uint32_t)std::min(4.0e9, (double)ms * 1e6);
+    }
     HIP_CHECK(hipStreamSynchronize(st));
+    c->sort_stats[31] = sort_ns;
     if (c->sort_stats[2] & IS_FAULT_MASK)
       throw Error(FCCF_E_INTERNAL, "K1 sort invariant violated (flags " + std::to_string(c->sort_stats[2]) + ")");
   });

@@ -133,13 +133,16 @@ struct CachedGraph {
   ~CachedGraph() { reset(); }
   // body enqueues the work; pfunc/pargs (optional): the patched kernel and its
   // current arguments (kernelParams layout: one pointer per argument).
+  // eager: launch the body directly this call (work with a host step inside, e.g. the
+  // sharded sort's gather)
   template <class F>
-  void run(const void* k, size_t kn, hipStream_t st, F body, const void* pfunc = nullptr, void** pargs = nullptr) {
+  void run(const void* k, size_t kn, hipStream_t st, F body, const void* pfunc = nullptr, void** pargs = nullptr,
+           bool eager = false) {
     static const bool enabled = [] {
       const char* e = std::getenv("FCCF_GRAPHS");
       return !(e && e[0] == '0');
     }();
-    if (!enabled || (g_probe && g_probe->on())) {  // probed calls launch eagerly (probe.h)
+    if (!enabled || eager || (g_probe && g_probe->on())) {  // probed calls launch eagerly (probe.h)
       body();
       return;
     }

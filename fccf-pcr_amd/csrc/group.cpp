@@ -27,12 +27,14 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "ctx.h"
+#include "kernels.h"
 
 namespace fccf {
 
@@ -78,31 +80,35 @@ struct RcclTransport : Transport {
 };
 
 // Virtual ranks of one process on one device: every collective is host-synchronous.
+// Each channel has its own barrier and staging (channels are driven from different
+// host threads of a rank, like the separate communicators of the RCCL form).
 struct LocalHub {
   int n;
-  std::mutex m;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  char* stage[CH_COUNT] = {nullptr, nullptr};
-  size_t cap[CH_COUNT] = {0, 0};
-  size_t need[CH_COUNT] = {0, 0};
+  struct Chan {
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    char* stage = nullptr;
+    size_t cap = 0, need = 0;
+  } ch[CH_COUNT];
   explicit LocalHub(int n_) : n(n_) {}
   ~LocalHub() {
-    for (char* p : stage)
-      if (p) (void)hipFree(p);
+    for (Chan& c : ch)
+      if (c.stage) (void)hipFree(c.stage);
   }
-  void barrier() {
-    std::unique_lock<std::mutex> lk(m);
-    const uint64_t my = gen;
-    if (++arrived == n) {
-      arrived = 0;
-      ++gen;
-      cv.notify_all();
+  void barrier(int k) {
+    Chan& c = ch[k];
+    std::unique_lock<std::mutex> lk(c.m);
+    const uint64_t my = c.gen;
+    if (++c.arrived == n) {
+      c.arrived = 0;
+      ++c.gen;
+      c.cv.notify_all();
       return;
     }
     // bounded: a rank that never arrives (its call failed) ends the wait with an error
-    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != my; }))
+    if (!c.cv.wait_for(lk, std::chrono::seconds(60), [&] { return c.gen != my; }))
       throw Error(FCCF_E_RCCL, "virtual-rank group: a rank did not reach the collective");
   }
 };
@@ -112,31 +118,36 @@ struct LocalTransport : Transport {
   explicit LocalTransport(Group* g_) : g(g_) {}
   void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
                   hipStream_t st) override {
-    LocalHub& H = *g->hub;
+    LocalHub::Chan& C = g->hub->ch[ch];
     size_t total = 0;
     for (int r = 0; r < g->n; ++r) total = std::max(total, offs[r] + counts[r]);
     HIP_CHECK(hipStreamSynchronize(st));  // this rank's send data is complete
     {
-      std::lock_guard<std::mutex> lk(H.m);
-      H.need[ch] = std::max(H.need[ch], total);
+      std::lock_guard<std::mutex> lk(C.m);
+      C.need = std::max(C.need, total);
     }
-    H.barrier();
-    if (g->rank == 0 && H.need[ch] > H.cap[ch]) {  // one rank grows the staging, between barriers
-      if (H.stage[ch]) HIP_CHECK(hipFree(H.stage[ch]));
-      H.stage[ch] = nullptr;
-      H.cap[ch] = 0;
-      if (hipMalloc((void**)&H.stage[ch], H.need[ch]) != hipSuccess) throw Error(FCCF_E_OOM, "virtual-rank staging");
-      H.cap[ch] = H.need[ch];
+    g->hub->barrier(ch);
+    if (g->rank == 0 && C.need > C.cap) {  // one rank grows the staging, between barriers
+      if (C.stage) HIP_CHECK(hipFree(C.stage));
+      C.stage = nullptr;
+      C.cap = 0;
+      if (hipMalloc((void**)&C.stage, C.need) != hipSuccess) throw Error(FCCF_E_OOM, "virtual-rank staging");
+      C.cap = C.need;
     }
-    H.barrier();
+    g->hub->barrier(ch);
     if (counts[g->rank]) {  // (on st: the legacy null stream would also wait for the other ranks' streams)
-      HIP_CHECK(hipMemcpyAsync(H.stage[ch] + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(C.stage + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
       HIP_CHECK(hipStreamSynchronize(st));
     }
-    H.barrier();
-    if (total) HIP_CHECK(hipMemcpyAsync(recv, H.stage[ch], total, hipMemcpyDeviceToDevice, st));
+    g->hub->barrier(ch);
+    // every rank's part except its own (in place: an all-gather-v may send from its recv buffer)
+    for (int r = 0; r < g->n; ++r)
+      if (r != g->rank && counts[r])
+        HIP_CHECK(hipMemcpyAsync((char*)recv + offs[r], C.stage + offs[r], counts[r], hipMemcpyDeviceToDevice, st));
+    if (counts[g->rank] && (const char*)send != (const char*)recv + offs[g->rank])
+      HIP_CHECK(hipMemcpyAsync((char*)recv + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    H.barrier();  // (the staging is rewritten by the next collective)
+    g->hub->barrier(ch);  // (the staging is rewritten by the next collective)
   }
   void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
     std::vector<size_t> counts((size_t)g->n, bytes), offs((size_t)g->n);
@@ -226,6 +237,44 @@ void group_fine_scores(const Group* g, int s, int E, float* scores, uint32_t* er
   }
 }
 
+bool shard_sort_enabled(const Group* g, uint32_t cap, int rounds) {
+  if (!g || g->n < 2 || g->n > IS_SHARD_MAX) return false;
+  // FCCF_SHARD_D_MIN: the smallest cloud whose sort is sharded (default 2M points: below
+  // it the sort is ~0.4 ms per cloud and the bounds read-back + gather do not pay)
+  const char* e = std::getenv("FCCF_SHARD_D_MIN");
+  const uint32_t mn = e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 21);
+  return cap >= mn && rounds > shard_sort_r0(g->n);
+}
+
+int shard_sort_r0(int n_ranks) {
+  // replicated rounds: enough that round r0's children (2^r0 at most) can split into
+  // n_ranks blocks of similar size
+  int lg = 0;
+  while ((1 << lg) < n_ranks) ++lg;
+  return lg + 3;
+}
+
+void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
+                         int nbatch, hipStream_t st) {
+  const int n = g->n;
+  for (int e = 0; e < nbatch; ++e)
+    HIP_CHECK(hipMemcpyAsync(g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1), bounds[e], 4 * (size_t)(n + 1),
+                             hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  std::vector<size_t> cnt((size_t)n), off((size_t)n);
+  for (int e = 0; e < nbatch; ++e) {
+    const uint32_t* b = g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1);
+    for (int r = 0; r < n; ++r) {
+      if (b[r + 1] < b[r]) throw Error(FCCF_E_INTERNAL, "sharded sort: rank bounds out of order");
+      cnt[(size_t)r] = 4 * (size_t)(b[r + 1] - b[r]);
+      off[(size_t)r] = 4 * (size_t)b[r];
+    }
+    const size_t me = 4 * (size_t)b[g->rank];
+    g->tr->allgatherv(CH_CLOUD, (const char*)k0[e] + me, k0[e], cnt.data(), off.data(), st);
+    g->tr->allgatherv(CH_CLOUD, (const char*)v0[e] + me, v0[e], cnt.data(), off.data(), st);
+  }
+}
+
 }  // namespace fccf
 
 using namespace fccf;
@@ -243,6 +292,8 @@ void group_alloc(Group& g) {
   const size_t n = (size_t)g.n;
   if (hipMalloc((void**)&g.d_cnt, 16 * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
   if (hipHostMalloc((void**)&g.h_cnt, 16 * (n + 1), hipHostMallocDefault) != hipSuccess)
+    throw Error(FCCF_E_OOM, "hipHostMalloc");
+  if (hipHostMalloc((void**)&g.h_bounds, 4 * 2 * (IS_SHARD_MAX + 1), hipHostMallocDefault) != hipSuccess)
     throw Error(FCCF_E_OOM, "hipHostMalloc");
   for (int s = 0; s < 2; ++s) {
     if (hipMalloc((void**)&g.d_fsend[s], sizeof(float) * Group::FE_BLK) != hipSuccess ||
@@ -267,6 +318,8 @@ void group_free(Group& g) {
     if (g.h_frecv[s]) (void)hipHostFree(g.h_frecv[s]);
     g.d_fsend[s] = g.d_frecv[s] = g.h_frecv[s] = nullptr;
   }
+  if (g.h_bounds) (void)hipHostFree(g.h_bounds);
+  g.h_bounds = nullptr;
   g.d_cnt = nullptr;
   g.h_cnt = nullptr;
   g.tr.reset();
@@ -297,6 +350,7 @@ extern "C" int fccf_group_create(fccf_ctx* c, const uint8_t id[FCCF_GROUP_ID_BYT
     // the fine-verification channel: its own communicator, so collectives issued on the
     // matching and fine streams never interleave on one communicator
     NCCL_CHECK(ncclCommSplit(G->g.comm[CH_MATCH], 0, rank, &G->g.comm[CH_FINE], nullptr));
+    NCCL_CHECK(ncclCommSplit(G->g.comm[CH_MATCH], 0, rank, &G->g.comm[CH_CLOUD], nullptr));
     G->g.ctx = c;
     G->g.n = n_ranks;
     G->g.rank = rank;

@@ -24,8 +24,11 @@ struct fccf_group;
 
 namespace fccf {
 
-// Collective channels: each is used from one stream only (stream order = issue order).
-enum { CH_MATCH = 0, CH_FINE = 1, CH_COUNT = 2 };
+// Collective channels: each is used from one stream only (stream order = issue order):
+// CH_MATCH the candidate gather (phase B), CH_FINE the fine scores (fine stream),
+// CH_CLOUD the sharded sort's slices (the cloud stage, possibly on the batch's helper
+// thread).
+enum { CH_MATCH = 0, CH_FINE = 1, CH_CLOUD = 2, CH_COUNT = 3 };
 
 struct Transport {
   virtual ~Transport() = default;
@@ -43,7 +46,7 @@ struct LocalHub;  // group.cpp
 struct Group {
   fccf_ctx* ctx = nullptr;
   int n = 1, rank = 0;
-  ncclComm_t comm[CH_COUNT] = {nullptr, nullptr};  // RCCL groups
+  ncclComm_t comm[CH_COUNT] = {nullptr, nullptr, nullptr};  // RCCL groups
   std::shared_ptr<LocalHub> hub;                   // virtual-rank groups
   std::unique_ptr<Transport> tr;
   uint32_t* d_cnt = nullptr;  // device: this rank's 4 counts, then all ranks' (n x 4)
@@ -54,7 +57,18 @@ struct Group {
   float* d_fsend[2] = {nullptr, nullptr};
   float* d_frecv[2] = {nullptr, nullptr};  // n x FE_BLK
   float* h_frecv[2] = {nullptr, nullptr};  // pinned copies
+  uint32_t* h_bounds = nullptr;             // pinned: the sharded sort's rank bounds, per cloud (row D)
 };
+
+// Row D (K1's sort sharded after its first rounds, introsort.hip): whether the cloud
+// stage of clouds of cap points shards its sort over g, and the round it starts at.
+bool shard_sort_enabled(const Group* g, uint32_t cap, int rounds);
+int shard_sort_r0(int n_ranks);
+// After a sharded sort: every rank's sorted slice [bounds[r], bounds[r+1]) of (k0, v0)
+// of each cloud, gathered in rank order into every rank's arrays.  bounds[e]: the
+// device copy of cloud e's bounds (IsBufs::bounds).  Synchronises st (the bounds).
+void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
+                         int nbatch, hipStream_t st);
 
 // the Group inside a C-ABI handle (null for null)
 Group* group_of(fccf_group* g);

@@ -402,6 +402,32 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
   const uint32_t nch = nchildren(W, r);
   const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
   uint32_t nseg = 0, ntiles = 0, nown = 0;
+  // Row D: from round shard_r0 on only the children starting in this rank's range.  At
+  // shard_r0 the bounds are set here: bound j = the first child start >= j * nsort / N
+  // (a child's start is always a segment boundary: the owned segments of earlier rounds
+  // lie between the children), so every later segment lies within one rank's range.
+  const bool shard = W.shard_n > 1 && r >= (int)W.shard_r0;
+  __shared__ uint32_t sbound[IS_SHARD_MAX + 1];
+  if (shard && r == (int)W.shard_r0) {
+    const uint32_t N = W.shard_n;
+    for (uint32_t jb = threadIdx.x; jb <= N; jb += blockDim.x) sbound[jb] = jb == 0 ? 0u : nsort;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nch; i += blockDim.x) {
+      const uint32_t fi = W.segs[(size_t)(r - 1) * W.segmax + i / 2].f;  // left child: the parent's start
+      const uint32_t f = (i & 1) ? min(max(coherent_load(&W.cuts[(size_t)(r - 1) * W.segmax + i / 2]),
+                                           fi + 1), W.segs[(size_t)(r - 1) * W.segmax + i / 2].l - 1)
+                                 : fi;
+      for (uint32_t jb = 1; jb < N; ++jb)
+        if ((uint64_t)f * N >= (uint64_t)jb * nsort) atomicMin(&sbound[jb], f);
+    }
+    __syncthreads();
+    for (uint32_t jb = threadIdx.x; jb <= N; jb += blockDim.x) W.bounds[jb] = sbound[jb];
+    __syncthreads();
+  } else if (shard) {
+    for (uint32_t jb = threadIdx.x; jb <= W.shard_n; jb += blockDim.x) sbound[jb] = W.bounds[jb];
+    __syncthreads();
+  }
+  const uint32_t lo = shard ? sbound[W.shard_rank] : 0u, hi = shard ? sbound[W.shard_rank + 1] : 0xFFFFFFFFu;
   for (uint32_t b0 = 0; b0 < nch; b0 += blockDim.x * PL) {
     const uint32_t i0 = b0 + threadIdx.x * PL;  // this thread's PL consecutive children (PL/2 parents)
     uint32_t cut[PL / 2];
@@ -431,6 +457,7 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
           c = (k & 1) ? Child{cc, q.l, q.depth - 1} : Child{q.f, cc, q.depth - 1};
         }
       }
+      if (c.f < lo || c.f >= hi) c = Child{0u, 0u, 0};  // another rank's (row D)
       ch[k] = c;
       const bool lg = i < nch && is_large(c, W.tier), ow = i < nch && !lg && c.l > c.f;
       // packed counters: large (21 bits) | owned (21) | tiles (22)
@@ -2051,6 +2078,12 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
   }
   const uint32_t nfin = nchildren(W, R);
   const uint32_t nown = R ? W.rounds[R - 1].nown : 0u;
+  const bool shard_on = W.shard_n > 1 && R > (int)W.shard_r0;
+  const uint32_t shard_lo = shard_on ? W.bounds[W.shard_rank] : 0u, shard_hi = shard_on ? W.bounds[W.shard_rank + 1] : 0u;
+  if (shard_on && blockIdx.x == 0 && threadIdx.x == 0) {  // (debug counters: this rank's range)
+    W.ctl[28] = shard_lo;
+    W.ctl[29] = shard_hi;
+  }
   uint32_t* const K0 = K02[e];
   uint32_t* const V0 = V02[e];
   uint32_t* const K1 = K12[e];
@@ -2080,6 +2113,9 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       l = o.l;
       d = o.depth;
       buf = o.buf;
+      // row D: the replicated rounds' owned segments belong to the rank whose range
+      // holds their start (the later rounds list only this rank's)
+      if (shard_on && (f < shard_lo || f >= shard_hi)) continue;
     }
     if (l <= f) continue;
     const unsigned long long t_item = W.trace ? wall_clock64() : 0ull;
@@ -2297,7 +2333,7 @@ size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
   return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + sizeof(IsTile) * mt + 256 + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
-         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 12 * 256;
+         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 4 * (IS_SHARD_MAX + 1) + 13 * 256;
 }
 
 IsBufs introsort_carve(void* base, uint32_t cap) {
@@ -2327,6 +2363,11 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.pre = (uint32_t*)take(8 * (size_t)b.maxtiles);
   b.letot = (uint32_t*)take(4 * (size_t)b.segmax);
   b.done = (uint32_t*)take(4 * 2 * (size_t)IS_RMAX * IS_DONE_WORDS);
+  b.bounds = (uint32_t*)take(4 * (IS_SHARD_MAX + 1));
+  b.shard_n = 1;
+  b.shard_rank = 0;
+  b.shard_r0 = 0;
+  b.shard_group = nullptr;
   b.prog = nullptr;
   b.trace = nullptr;
   b.tier = introsort_tier();
@@ -2351,7 +2392,7 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   // the round plan's form: once per round (large clouds) or per workgroup (small ones);
   // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
   const char* pm = std::getenv("FCCF_IS_PLAN");
-  const bool large = pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN);
+  const bool large = b[0].shard_n > 1 || (pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN));
   for (int r = 0; r < R; ++r) {
     const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;

@@ -36,6 +36,7 @@ constexpr int VG_KEY_BLOCKS = 512;
 constexpr int IS_RMAX = 24;          // most partition rounds before the owner kernel
 constexpr int IS_OWN_BLOCKS = 256;   // block-kernel workgroups per cloud (one per CU)
 constexpr int IS_WAVE_BLOCKS = 512;  // wave-kernel workgroups per cloud (4 waves each)
+constexpr int IS_SHARD_MAX = 64;     // most ranks of a sharded sort (row D)
 struct IsRound {
   uint32_t nseg, ntiles, nown, pad;  // large segments, their tiles, owned entries so far
 };
@@ -71,6 +72,12 @@ struct IsBufs {
   uint32_t* pre;        // per round tile: exclusive (>=, <=) prefix within its segment (k_is_count_plan's last workgroup)
   uint32_t* letot;      // per segment of the round: its <= count
   uint32_t* done;       // per round, count and scatter: sharded completion counters (last-workgroup hand-offs)
+  // Row D sharding (group.cpp): from round shard_r0 on, this rank partitions and finishes
+  // only the segments starting in its range [bounds[shard_rank], bounds[shard_rank + 1]);
+  // plan_round of round shard_r0 writes the shard_n + 1 bounds.  shard_n = 1: off.
+  uint32_t shard_n, shard_rank, shard_r0;
+  uint32_t* bounds;     // IS_SHARD_MAX + 1
+  void* shard_group;    // host only: the Group whose ranks gather the sorted slices
   uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   unsigned long long* trace;  // dev (null = off): per block item / wave task {start, end, size, who},
                               // block records from 0 (count in ctl[24]), wave records from taskmax (ctl[25])

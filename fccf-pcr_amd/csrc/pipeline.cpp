@@ -323,10 +323,20 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   uint32_t nv[2] = {0, 0};
   ps.cen = cs.arena.take_n<float>(8);
   ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
+  // Row D: with a group, large clouds shard their K1 sort after its first rounds
+  // (introsort.hip, group.cpp); the stage then runs eagerly (a host step between the
+  // sort and the gather of the sorted slices)
+  Group* const DG = shard_sort_enabled(c->group, capmax, introsort_rounds(capmax)) ? c->group : nullptr;
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
     carve_cloud(cs.arena, w[k], capmax, false);
     w[k].vg.is.inject = c->d_flags;     // (test hook; a constant pointer per ctx)
+    if (DG) {
+      w[k].vg.is.shard_n = (uint32_t)DG->n;
+      w[k].vg.is.shard_rank = (uint32_t)DG->rank;
+      w[k].vg.is.shard_r0 = (uint32_t)shard_sort_r0(DG->n);
+      w[k].vg.is.shard_group = DG;
+    }
     w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
     nv[k] = (uint32_t)ps.nin[k];
     xin[k] = hin[k];
@@ -362,7 +372,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[7], 0));
     face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
                        cmail, B2<const uint32_t*>(w[0].sc, w[1].sc));
-  }, vg_entry_kernel(), ps.entry.args);
+  }, vg_entry_kernel(), ps.entry.args, DG != nullptr);
   // external signal for stage_inputs (this set's inputs have been read): after the graph
   HIP_CHECK(hipEventRecord(cs.ev[0], st0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done

@@ -13,6 +13,7 @@
 #define KT_TU 2  // ktrace.h source tag
 #include "probe.h"
 #include "kernels.h"
+#include "group.h"
 
 namespace fccf {
 namespace {
@@ -392,6 +393,12 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
   const B2<const VGParams*> Pc(P[0], P[1]);
   if (!presorted) {
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, false);
+    if (b[0].is.shard_n > 1) {  // row D: every rank's sorted slice, gathered in rank order
+      uint32_t* const kk[2] = {k0[0], k0[1]};
+      uint32_t* const vv[2] = {v0[0], v0[1]};
+      const uint32_t* const bb[2] = {b[0].is.bounds, b[1].is.bounds};
+      shard_gather_sorted((Group*)b[0].is.shard_group, kk, vv, bb, nbatch, st);
+    }
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch);
   } else {  // usually already in leaf order: a sort and segmentation that run only if not

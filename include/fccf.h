@@ -267,7 +267,9 @@ int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exa
  * beyond the LDS with distinct keys), [3] global partitions, [4] LDS segments, [5]
  * workgroup partitions, [6] wave partitions, [7] sequential heap sorts (depth limit,
  * repeated keys), [9] depth-limit segments with pairwise distinct keys (sorted in
- * parallel: their order is unique), [12] register-resident subtrees, [16] wave tasks.
+ * parallel: their order is unique), [12] register-resident subtrees, [16] wave tasks,
+ * [28..29] the rank range of a row-D simulated sort (FCCF_SHARD_D_SIM=r/N, environment),
+ * [31] the sort's device time in ns.
  * fccf_debug_sort_keys returns FCCF_E_INTERNAL when an invariant flag is set. */
 /* Test hook: the device LM's correctly rounded double sin/cos (verify.hip); ok[i] = 0
  * where |x| is beyond its argument reduction. */

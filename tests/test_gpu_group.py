@@ -159,6 +159,40 @@ def test_virtual_ranks_shard_search_and_fine_verify(fccf, pair, n):
         assert (s.K, s.K_pass, list(s.cand), s.fine_evals) == (s0.K, s0.K_pass, list(s0.cand), s0.fine_evals)
 
 
+@pytest.mark.parametrize("n,cfg", [(2, "c2"), (3, "c2"), (2, "c3")])
+def test_virtual_ranks_shard_the_sort(fccf, n, cfg, monkeypatch):
+    """Row D: with FCCF_SHARD_D_MIN=0 every virtual rank sorts only its range of K1's
+    std::sort order after the first rounds and the sorted slices are gathered in rank
+    order (group.cpp shard_gather_sorted) -- every rank's registration equals the
+    unsharded one bit for bit (single and pipelined batch)."""
+    c = fccf.CONFIGS[cfg]
+    src, tar, _ = fccf.synth_pair(c["n"], c["room"])
+    leaf = c["leaf"]
+    with fccf.Ctx(0) as ctx:
+        T0, s0 = ctx.register(src, tar, leaf)
+    monkeypatch.setenv("FCCF_SHARD_D_MIN", "0")
+    ctxs = [fccf.Ctx(0) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+
+        def work(r):
+            T, s = ctxs[r].register(src, tar, leaf)
+            Tb, _ = ctxs[r].register_batch([(src, tar)] * 2, leaf)
+            return T, s, Tb
+
+        out = _on_threads(work, n)
+        for g in groups:
+            g.close()
+    finally:
+        for cx in ctxs:
+            cx.close()
+    for T, s, Tb in out:
+        np.testing.assert_array_equal(bits(T), bits(T0))
+        for Tx in Tb:
+            np.testing.assert_array_equal(bits(Tx), bits(T0))
+        assert (s.K, s.K_pass, list(s.cand), s.vox1, s.vox2) == (s0.K, s0.K_pass, list(s0.cand), s0.vox1, s0.vox2)
+
+
 def test_virtual_ranks_stage_match(fccf, oracle, pair):
     src, tar, leaf = pair
     run = oracle.Run(src, tar, leaf, oracle.INTROSORT)

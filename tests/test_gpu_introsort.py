@@ -128,3 +128,34 @@ def test_round_plan_forms_equal_std_sort(ctx, fccf, oracle, plan, monkeypatch):
     out = ctx.downsample(src, c["leaf"])
     ref, _ = oracle.voxel_grid(src, c["leaf"], oracle.INTROSORT)
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_sort_rank_ranges(ctx, fccf, oracle, world, monkeypatch):
+    """Row D on the device: the sort run as rank r of N (FCCF_SHARD_D_SIM; the ranks'
+    exchange itself is covered by the virtual-rank registrations in test_gpu_group.py)
+    sorts exactly its range [lo, hi) of the std::sort order, and the ranges tile the
+    whole sort."""
+    rng = np.random.default_rng(11)
+    c = fccf.CONFIGS["c3"]
+    src, _, _ = fccf.synth_pair(c["n"], c["room"])
+    inv = np.float32(1.0) / np.float32(c["leaf"])
+    minb = np.floor(src.min(0) * inv).astype(np.int64)
+    div = np.floor(src.max(0) * inv).astype(np.int64) - minb + 1
+    ijk = (np.floor(src * inv) - minb.astype(np.float32)).astype(np.int64)
+    cases = {"c3_src": (ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]).astype(np.uint32),
+             "dups_300k": rng.integers(0, 60_000, 300_000).astype(np.uint32)}
+    for name, k in cases.items():
+        ref = oracle.sort_pairs(k)
+        prev = 0
+        for r in range(world):
+            monkeypatch.setenv("FCCF_SHARD_D_SIM", f"{r}/{world}")
+            got = ctx.sort_keys(k)
+            raw = ctx.sort_stats()["raw"]
+            lo, hi = int(raw[28]), int(raw[29])
+            assert lo == prev and hi >= lo, (name, r, lo, hi)
+            assert np.array_equal(got[lo:hi], ref[lo:hi]), (name, r)
+            prev = hi
+        assert prev == ref.size, name
+        monkeypatch.delenv("FCCF_SHARD_D_SIM")

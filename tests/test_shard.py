@@ -1,6 +1,7 @@
 """CPU checks of the sharded stages' host logic (fccf-pcr_amd/shard.py): block ranges,
 the message format, rank-ordered concatenation (K5 search, F fine verification, D
-VoxelGrid), and the gloo gather with world_size 2.  The GPU search itself is stubbed by a deterministic b1-major generator;
+VoxelGrid, and the K1 sort's row-D split via tests/introsort_model.py), and the gloo
+gather with world_size 2.  The GPU search itself is stubbed by a deterministic b1-major generator;
 the real one is tested in tests/test_gpu_stages.py."""
 import os
 import subprocess
@@ -91,6 +92,11 @@ for a, b in zip(got, full):
 T = test_shard.evals(7)
 sc = shard.fine_verify_sharded(test_shard.StubFineCtx(), None, None, T, 0.5, r, w, shard.torch_gather())
 assert np.array_equal(sc.view(np.uint32), test_shard.StubFineCtx().fine_verify(None, None, T, 0.5).view(np.uint32))
+import introsort_model as IM
+keys = test_shard.sort_case(2500, 5)
+(lo, hi), part = IM.sharded_rank(keys, r, w, 64, 4)
+whole = np.concatenate(shard.torch_gather()(np.asarray(part, np.float64))).astype(np.int64)
+assert whole.tolist() == IM.std_sort(keys), "sharded sort differs"
 xyz = test_shard.cloud(3000, 11)
 lo, hi = shard.shard_range(len(xyz), r, w)
 vctx = test_shard.StubVoxelCtx()
@@ -134,6 +140,34 @@ def test_fine_verify_sharded_equals_whole(E, world):
         t.join()
     for got in res:
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def sort_case(n, seed):
+    """VoxelGrid-like keys: many duplicates, a few invalid (non-finite) points."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, max(1, n // 4), n).astype(np.uint32)
+    k[rng.integers(0, n, 5)] = 0xFFFFFFFF
+    return k
+
+
+@pytest.mark.parametrize("n,world,seed", [(3000, 2, 1), (5000, 3, 2), (4000, 8, 3), (700, 4, 4)])
+def test_sharded_sort_model_equals_std_sort(oracle, n, world, seed):
+    """Row D's decomposition of K1's sort (csrc/introsort.hip plan_round / k_is_block):
+    levels < r0 replicated, then each rank finishes the segments starting in its
+    range; the rank-ordered concatenation equals std::sort (the oracle's) exactly."""
+    import introsort_model as IM
+    keys = sort_case(n, seed)
+    ref = oracle.sort_pairs(keys).tolist()
+    assert IM.std_sort(keys) == ref
+    r0 = (world - 1).bit_length() + 3
+    parts = [IM.sharded_rank(keys, r, world, 64, r0) for r in range(world)]
+    assert parts[0][0][0] == 0 and parts[-1][0][1] == len(ref)
+    for (a, b), _ in parts:
+        assert a <= b
+    for ((_, b), _), ((c, _), _) in zip(parts, parts[1:]):
+        assert b == c
+    assert [i for _, p in parts for i in p] == ref
+    assert sum(1 for (a, b), _ in parts if b > a) > 1  # the work is actually split
 
 
 def cloud(n, seed, nan=True):
