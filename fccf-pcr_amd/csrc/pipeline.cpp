@@ -590,7 +590,9 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   }
   uint32_t tot[4] = {0, 0, 0, 0};
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
-  HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
+  // (k_match_scan writes the totals whenever there are tests: only an empty search
+  // needs them zeroed -- one runtime fill kernel fewer on the dependent chain)
+  if (Kloc <= 0) HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
   uint64_t* drows = cdev ? c->arena2.take_n<uint64_t>(MatchMail::CB_CAP) : nullptr;
   match_candidates(dM, Kloc, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
   const float cr2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
