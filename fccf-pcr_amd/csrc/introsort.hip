@@ -41,7 +41,8 @@
 namespace fccf {
 namespace {
 
-constexpr uint32_t IS_TILE = 2048;   // elements per round tile
+constexpr uint32_t IS_TILE = 2048;   // elements per round tile (small clouds)
+constexpr uint32_t IS_TILE_L = 4096;  // elements per round tile (large clouds: fewer workgroup latency chains)
 constexpr uint32_t IS_LARGE_MIN = 1u << 21;  // clouds from this size plan each round once (k_is_count_plan)
 constexpr int IS_NSH = 64;                       // round kernels: completion counter shards (last_block)
 constexpr int IS_DONE_WORDS = (IS_NSH + 1) * 32;  // u32 per launch: shards + top, 128 B apart
@@ -250,6 +251,8 @@ __device__ __forceinline__ Child child_of(const IsBufs& W, int r, uint32_t nsort
 __device__ __forceinline__ uint32_t nchildren(const IsBufs& W, int r) { return r == 0 ? 1u : 2u * W.rounds[r - 1].nseg; }
 __device__ __forceinline__ bool is_large(const Child& c, uint32_t tier) { return c.l - c.f > tier && c.d > 0; }
 __device__ __forceinline__ uint32_t tiles_of(uint32_t len) { return (len - 1 + IS_TILE - 1) / IS_TILE; }
+constexpr int IS_TC_L = IS_TILE_L / IS_TT;  // 16 elements per thread (large-cloud rounds)
+__device__ __forceinline__ uint32_t tiles_of_l(uint32_t len) { return (len - 1 + IS_TILE_L - 1) / IS_TILE_L; }
 
 // largest u < n with pre[u] <= x (pre ascending, pre[0] = 0)
 __device__ __forceinline__ uint32_t upper_index(const uint32_t* pre, uint32_t n, uint32_t x) {
@@ -461,7 +464,7 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
       ch[k] = c;
       const bool lg = i < nch && is_large(c, W.tier), ow = i < nch && !lg && c.l > c.f;
       // packed counters: large (21 bits) | owned (21) | tiles (22)
-      tot_t += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of(c.l - c.f) : 0u) << 42);
+      tot_t += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of_l(c.l - c.f) : 0u) << 42);
     }
     uint64_t s_all;
     uint64_t run = block_excl_scan64(tot_t, sh64, &s_all);
@@ -474,7 +477,7 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
                      p_nt = (uint32_t)(run >> 42);
       if (lg) W.ptab[nseg + p_lg] = make_uint4(c.f, c.l, (uint32_t)c.d, ntiles + p_nt);
       if (ow) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
-      run += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of(c.l - c.f) : 0u) << 42);
+      run += (lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)(lg ? tiles_of_l(c.l - c.f) : 0u) << 42);
     }
     nseg += (uint32_t)(s_all & 0x1FFFFFu);
     nown += (uint32_t)((s_all >> 21) & 0x1FFFFFu);
@@ -490,17 +493,17 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
 // workgroup), lists.
 __device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
                                            const IsBufs& W, int r, uint32_t t, uint32_t j) {
-  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  __shared__ uint32_t cg[IS_TC_L * 4], cl[IS_TC_L * 4], pg[IS_TC_L * 4], pl[IS_TC_L * 4];
   __shared__ uint32_t bsh[4];
   const uint4 pt = W.ptab[j];
   const uint32_t f = pt.x, l = pt.y, tile0 = pt.w;
   const uint32_t i = t - tile0;
-  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
-  uint32_t kk[IS_TC];
+  const uint32_t a = f + 1 + i * IS_TILE_L, b = min(l, a + IS_TILE_L);
+  uint32_t kk[IS_TC_L];
   // the tile's keys are loaded before the pivot, so their latency overlaps thread 0's
   // dependent median reads below
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
+  for (int c = 0; c < IS_TC_L; ++c) {
     const uint32_t p = a + c * IS_TT + threadIdx.x;
     kk[c] = p < b ? K[p] : 0u;
   }
@@ -521,10 +524,10 @@ __device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const
   const uint32_t m = bsh[0], P = bsh[1], kf = bsh[2];
   const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c)
+  for (int c = 0; c < IS_TC_L; ++c)
     if (a + c * IS_TT + threadIdx.x == m) kk[c] = kf;  // the median-to-first swap
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
+  for (int c = 0; c < IS_TC_L; ++c) {
     const bool ok = a + c * IS_TT + threadIdx.x < b;
     const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
     if (lane == 0) {
@@ -533,26 +536,26 @@ __device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const
     }
   }
   __syncthreads();
-  if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
-    const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+  if (w == 0) {  // IS_TC_L * 4 (chunk, wave) entries in position order
+    const uint32_t xg0 = lane < IS_TC_L * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC_L * 4 ? cl[lane] : 0u;
     uint32_t xg = xg0, xl = xl0;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
       if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
     }
-    if (lane < IS_TC * 4) {
+    if (lane < IS_TC_L * 4) {
       pg[lane] = xg - xg0;
       pl[lane] = xl - xl0;
     }
-    if (lane == IS_TC * 4 - 1) {
+    if (lane == IS_TC_L * 4 - 1) {
       atomicExch(&W.cnt[2 * (size_t)t], xg);
       atomicExch(&W.cnt[2 * (size_t)t + 1], xl);
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
+  for (int c = 0; c < IS_TC_L; ++c) {
     const uint32_t p = a + c * IS_TT + threadIdx.x;
     const bool ok = p < b;
     const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
@@ -610,7 +613,7 @@ __device__ void tile_prefix(const IsBufs& W, int r, uint32_t* base, uint64_t* sh
       W.pre[2 * (size_t)t] = (uint32_t)xs[k] - bg[j];
       W.pre[2 * (size_t)t + 1] = (uint32_t)(xs[k] >> 32) - bl[j];
       const uint4 pt = W.ptab[j];
-      if (t == pt.w + tiles_of(pt.y - pt.x) - 1u) W.letot[j] = (uint32_t)(xs[k] >> 32) + q[k] - bl[j];
+      if (t == pt.w + tiles_of_l(pt.y - pt.x) - 1u) W.letot[j] = (uint32_t)(xs[k] >> 32) + q[k] - bl[j];
     }
     run += tot;
     __syncthreads();
@@ -651,7 +654,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
                                                       int R) {
   KT();
   __shared__ uint64_t sh64[16];
-  __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
+  __shared__ uint32_t cg[IS_TC_L * 4], cl[IS_TC_L * 4], pg[IS_TC_L * 4], pl[IS_TC_L * 4];
   __shared__ uint32_t wing[IS_WIN], winl[IS_WIN];  // windows of the >= / <= prefixes
   __shared__ uint32_t stot[2], swin[4];            // the tile's totals; window bounds
   __shared__ uint32_t scut, sflag;
@@ -663,19 +666,19 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     const IsTile td = W.tdesc[t];
     const uint32_t j = td.j;
     const IsSeg s = td.s;
-    const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0, m = s.m, P = s.P;
+    const uint32_t f = s.f, l = s.l, nt = tiles_of_l(l - f), i = t - s.tile0, m = s.m, P = s.P;
     const uint32_t* __restrict__ K = Ki2[e];
     const uint32_t* __restrict__ V = Vi2[e];
     uint32_t* __restrict__ Ko = Ko2[e];
     uint32_t* __restrict__ Vo = Vo2[e];
     const uint2* pre = reinterpret_cast<const uint2*>(W.pre) + s.tile0;  // the segment's tile prefixes
-    const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
+    const uint32_t a = f + 1 + i * IS_TILE_L, b = min(l, a + IS_TILE_L);
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     if (i == 0 && threadIdx.x == 0) atomicAdd(&W.rounds[r].pad, l - f);
     // the tile's elements are loaded first: their latency overlaps the window searches
-    uint32_t kk[IS_TC], vv[IS_TC];
+    uint32_t kk[IS_TC_L], vv[IS_TC_L];
 #pragma unroll
-    for (int c = 0; c < IS_TC; ++c) {
+    for (int c = 0; c < IS_TC_L; ++c) {
       const uint32_t p = a + c * IS_TT + threadIdx.x;
       const bool ok = p < b;
       kk[c] = ok ? K[p] : 0u;
@@ -689,7 +692,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     const uint2 own = pre[i];
     const uint32_t le_tot = W.letot[j];
 #pragma unroll
-    for (int c = 0; c < IS_TC; ++c) {
+    for (int c = 0; c < IS_TC_L; ++c) {
       const bool ok = a + c * IS_TT + threadIdx.x < b;
       const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
       if (lane == 0) {
@@ -699,18 +702,18 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     }
     __syncthreads();
     if (w == 0) {
-      const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+      const uint32_t xg0 = lane < IS_TC_L * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC_L * 4 ? cl[lane] : 0u;
       uint32_t xg = xg0, xl = xl0;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
         if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
       }
-      if (lane < IS_TC * 4) {
+      if (lane < IS_TC_L * 4) {
         pg[lane] = xg - xg0 + own.x;
         pl[lane] = xl - xl0 + own.y;
       }
-      if (lane == IS_TC * 4 - 1) {
+      if (lane == IS_TC_L * 4 - 1) {
         stot[0] = xg;
         stot[1] = xl;
       }
@@ -746,9 +749,9 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
     // destinations: the swapped elements' partner positions come from the lists (all
     // list loads issued before any store)
     uint32_t cut = IS_NONE;
-    uint32_t dst[IS_TC];
+    uint32_t dst[IS_TC_L];
 #pragma unroll
-    for (int c = 0; c < IS_TC; ++c) {
+    for (int c = 0; c < IS_TC_L; ++c) {
       const uint32_t p = a + c * IS_TT + threadIdx.x;
       const bool ok = p < b;
       const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
@@ -762,17 +765,17 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B
       if (sg) {  // R[gx+1]: the (le_tot-gx-1)-th <= P from the left
         const uint32_t x = le_tot - gx - 1;
         const uint32_t u = wl_n <= IS_WIN ? wl_lo + upper_index(winl, wl_n, x) : upper_index_g(pre, nt, x, 1);
-        const uint32_t au = f + 1 + u * IS_TILE;
+        const uint32_t au = f + 1 + u * IS_TILE_L;
         dst[c] = au + W.lel[au + (x - (wl_n <= IS_WIN ? winl[u - wl_lo] : pre[u].y))];
       } else if (sl) {  // L[kr]: the (kr-1)-th >= P from the left
         const uint32_t x = le_tot - lx - 1;
         const uint32_t u = wg_n <= IS_WIN ? wg_lo + upper_index(wing, wg_n, x) : upper_index_g(pre, nt, x, 0);
-        const uint32_t au = f + 1 + u * IS_TILE;
+        const uint32_t au = f + 1 + u * IS_TILE_L;
         dst[c] = au + W.gel[au + (x - (wg_n <= IS_WIN ? wing[u - wg_lo] : pre[u].x))];
       }
     }
 #pragma unroll
-    for (int c = 0; c < IS_TC; ++c) {
+    for (int c = 0; c < IS_TC_L; ++c) {
       const uint32_t d = dst[c];
       if (d == IS_NONE) continue;
       if (d <= f || d >= l) {  // cannot happen; never write outside the segment
@@ -2311,6 +2314,7 @@ uint32_t introsort_tier() {
 }
 uint32_t introsort_segmax(uint32_t cap) { return cap / introsort_tier() + 2; }
 uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
+uint32_t introsort_maxtiles_l(uint32_t cap) { return cap / IS_TILE_L + introsort_segmax(cap) + 1; }
 
 int introsort_rounds(uint32_t cap) {
   static const int env = [] {
@@ -2388,7 +2392,8 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   };
   k_is_prep<<<dim3(1, nbatch), 1024, 0, st>>>(k0, v0, d_n, P, b, exact_gate ? 1 : 0);
   step("prep", 0);
-  const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap);
+  const uint32_t segmax = introsort_segmax(cap), maxtiles = introsort_maxtiles(cap),
+                 maxtiles_l = introsort_maxtiles_l(cap);
   // the round plan's form: once per round (large clouds) or per workgroup (small ones);
   // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
   const char* pm = std::getenv("FCCF_IS_PLAN");
@@ -2400,13 +2405,13 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
       // algorithmic bytes: the key read, a 2-byte list entry written (x2: >= and <= lists share a unit)
       FCCF_LAUNCH("k_is_count_plan",
                   (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
-                  k_is_count_plan, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)segmax, st, B2<const uint32_t*>(ki),
+                  k_is_count_plan, dim3(maxtiles_l, nbatch), IS_TT, 8 * (size_t)segmax, st, B2<const uint32_t*>(ki),
                   B2<const uint32_t*>(vi), b, r);
       step("count", r);
       // algorithmic bytes: key + value read and written, plus a 2-byte list entry
       FCCF_LAUNCH("k_is_scatter",
                   (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
-                  k_is_scatter, dim3(maxtiles, nbatch), IS_TT, 0, st, B2<const uint32_t*>(ki),
+                  k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st, B2<const uint32_t*>(ki),
                   B2<const uint32_t*>(vi), ko, vo, b, r, R);
     } else {
       FCCF_LAUNCH("k_is_count_plan",
