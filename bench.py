@@ -228,8 +228,11 @@ def pmc_traffic(kernel, config):
             continue
         if d.get("config", "c3") != config:
             continue
-        if kernel in d.get("kernels", {}):
-            return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        # (the probe label names the kernel family: the sort's round kernels have a small-
+        # and a large-cloud form, k_is_scatter_s / k_is_scatter, by symbol)
+        for name in (kernel, kernel + "_s"):
+            if name in d.get("kernels", {}):
+                return d["kernels"][name]["hbm_bytes_per_launch"]
     return None
 
 
