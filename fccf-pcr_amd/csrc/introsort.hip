@@ -567,9 +567,22 @@ __device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const
 
 // The round's tile prefixes, by its last count workgroup: per tile the exclusive
 // (>=, <=) prefix within its segment (pre), per segment the <= total (letot).  TP
-// consecutive tiles per thread per step (their atomic loads in flight together).
+// consecutive tiles per thread per step (their atomic loads in flight together).  A
+// tile's two counts (<= IS_TILE_L each) travel packed in one u32 and are re-summed in
+// the second pass instead of kept per tile.  The last workgroup's registers set the
+// whole kernel's occupancy: 16 tiles per thread took 150 VGPRs (3 waves per SIMD), 4
+// take 65 (7 waves per SIMD; c5: 68 -> 38.5 us per count launch, 8.53 -> 7.97 ms per
+// registration, profiles/r03i).
 // base: LDS scratch of 2 x segmax u32 (the running prefix at each segment's first tile).
-constexpr int TP = 16;
+#ifndef IS_TP_VAL
+#define IS_TP_VAL 4
+#endif
+constexpr int TP = IS_TP_VAL;
+static_assert(IS_TILE_L < 65536, "tile counts packed in 16 bits");
+__device__ __forceinline__ uint64_t coherent_load64(uint32_t* p) {
+  return atomicAdd(reinterpret_cast<unsigned long long*>(p), 0ull);
+}
+__device__ __forceinline__ uint64_t unpack_gq(uint32_t gq) { return (uint64_t)(gq & 0xFFFFu) | ((uint64_t)(gq >> 16) << 32); }
 __device__ void tile_prefix(const IsBufs& W, int r, uint32_t* base, uint64_t* sh64) {
   const uint32_t ntiles = W.rounds[r].ntiles;
   uint32_t* bg = base;
@@ -577,43 +590,44 @@ __device__ void tile_prefix(const IsBufs& W, int r, uint32_t* base, uint64_t* sh
   uint64_t run = 0;
   for (uint32_t b0 = 0; b0 < ntiles; b0 += blockDim.x * TP) {
     const uint32_t t0 = b0 + threadIdx.x * TP;
-    uint32_t g[TP], q[TP], js[TP];
+    uint32_t gq[TP], js[TP];
 #pragma unroll
     for (int k = 0; k < TP; ++k) {
       const uint32_t t = t0 + k;
-      g[k] = q[k] = js[k] = 0u;
+      gq[k] = js[k] = 0u;
       if (t < ntiles) {
-        g[k] = coherent_load(&W.cnt[2 * (size_t)t]);
-        q[k] = coherent_load(&W.cnt[2 * (size_t)t + 1]);
+        const uint64_t c = coherent_load64(&W.cnt[2 * (size_t)t]);  // (>=, <=) of tile t
+        gq[k] = (uint32_t)c | ((uint32_t)(c >> 32) << 16);
         js[k] = coherent_load(&W.tseg[t]);
       }
     }
     uint64_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < TP; ++k) sum += (uint64_t)g[k] | ((uint64_t)q[k] << 32);
+    for (int k = 0; k < TP; ++k) sum += unpack_gq(gq[k]);
     uint64_t tot;  // >= counts (low 32 bits) and <= counts (high): each sums to <= the sort length
-    uint64_t x = run + block_excl_scan64(sum, sh64, &tot);
-    uint64_t xs[TP];
+    const uint64_t x0 = run + block_excl_scan64(sum, sh64, &tot);
+    uint64_t x = x0;
 #pragma unroll
     for (int k = 0; k < TP; ++k) {
       const uint32_t t = t0 + k;
-      xs[k] = x;
       if (t < ntiles && t == W.ptab[js[k]].w) {
         bg[js[k]] = (uint32_t)x;
         bl[js[k]] = (uint32_t)(x >> 32);
       }
-      x += (uint64_t)g[k] | ((uint64_t)q[k] << 32);
+      x += unpack_gq(gq[k]);
     }
     __syncthreads();
+    x = x0;
 #pragma unroll
     for (int k = 0; k < TP; ++k) {
       const uint32_t t = t0 + k;
       if (t >= ntiles) continue;
       const uint32_t j = js[k];
-      W.pre[2 * (size_t)t] = (uint32_t)xs[k] - bg[j];
-      W.pre[2 * (size_t)t + 1] = (uint32_t)(xs[k] >> 32) - bl[j];
+      W.pre[2 * (size_t)t] = (uint32_t)x - bg[j];
+      W.pre[2 * (size_t)t + 1] = (uint32_t)(x >> 32) - bl[j];
+      x += unpack_gq(gq[k]);
       const uint4 pt = W.ptab[j];
-      if (t == pt.w + tiles_of_l(pt.y - pt.x) - 1u) W.letot[j] = (uint32_t)(xs[k] >> 32) + q[k] - bl[j];
+      if (t == pt.w + tiles_of_l(pt.y - pt.x) - 1u) W.letot[j] = (uint32_t)(x >> 32) - bl[j];
     }
     run += tot;
     __syncthreads();
@@ -649,7 +663,11 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan(B2<const uint32_t*> K2,
 // ranks in the other list, so each workgroup locates that window of its segment's
 // tile prefix once (wave_upper_index over global memory) and keeps it in LDS.
 constexpr uint32_t IS_WIN = 256;  // prefix window in LDS (larger windows: binary search in global memory)
-__global__ void __launch_bounds__(IS_TT) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
+
+#ifndef IS_SCATTER_MINB
+#define IS_SCATTER_MINB 1
+#endif
+__global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
                                                       B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r,
                                                       int R) {
   KT();
