@@ -315,7 +315,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
 }
 
 extern "C" int fccf_debug_inject_sort_fault(fccf_ctx* c, uint32_t bits) {
-  if (!c || (bits & ~IS_FAULT_MASK)) return FCCF_E_ARG;
+  if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO))) return FCCF_E_ARG;
   return guarded(c, [&] {
     HIP_CHECK(hipDeviceSynchronize());  // no sort of this ctx in flight reads the word meanwhile
     HIP_CHECK(hipMemcpy(c->d_flags, &bits, 4, hipMemcpyHostToDevice));

@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
   if (mail && blockIdx.x == 0 && threadIdx.x < 8) {
     const uint32_t i = threadIdx.x & 3u;
     if (threadIdx.x < 4) mail->sc[e][i] = sc2[e][i];
-    else if (i == 1) mail->fsc[e][1] = B.vgp ? B.vgp->sort_err : 0u;  // both VoxelGrid passes' sort flags
+    else if (i == 1) mail->fsc[e][1] = B.vgp ? B.vgp->sort_err | (B.vgp->redo ? VG_REDO : 0u) : 0u;  // both passes' sort flags, redo
     else mail->fsc[e][i] = B.nleaf[i];
   }
   // the cloud stage's device spans: the stamps of main's pass, the driver's pass and the

@@ -24,6 +24,7 @@ struct VGParams {
   const float* src;   // the pass's input points (set by k_vg_bbox, read by the later kernels)
   uint64_t t_main;    // s_memrealtime at the start of main's pass (k_vg_bbox<0>): stage spans
   uint64_t t_driver;  // ... and of the driver's remove-NaN + second pass (k_finite_fix)
+  uint32_t redo;      // VG_OPTIMISTIC pass not in leaf order (output empty): cleared by k_vg_bbox
   uint32_t sort_err;  // K1 sort invariant flags of this cloud's passes (IS_FAULT_*), cleared by main's pass
                       // entry (k_vg_bbox<0>); copied to the cloud mailbox, where the host turns them into
                       // FCCF_E_INTERNAL
@@ -147,8 +148,16 @@ struct VGEntry {
 const void* vg_entry_kernel();
 // One VoxelGrid pass per batch entry.  n_in (optional): the counts by value (see
 // VGEntry.set_n), stored to d_n; entry (optional): receives the entry kernel's arguments.
+// presorted: VG_GENERAL; VG_PRESORTED (the driver's second pass over main's output:
+// usually every leaf holds one point in order, else the device sorts it exactly);
+// VG_OPTIMISTIC (the same without the sort and segmentation launches of the fallback:
+// an input that is not in leaf order yields an empty output and sets VGParams::redo,
+// and the caller redoes the pass with VG_PRESORTED).
+enum { VG_GENERAL = 0, VG_PRESORTED = 1, VG_OPTIMISTIC = 2 };
+constexpr uint32_t VG_REDO = 0x80000000u;       // CloudMail::fsc[k][1]: the optimistic pass must be redone
+constexpr uint32_t VG_FORCE_REDO = 0x10000u;    // test hook bit (fccf_debug_inject_sort_fault)
 void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted = false, int nbatch = 1,
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, int presorted = VG_GENERAL, int nbatch = 1,
                 B2<float*> out_copy = B2<float*>(nullptr), const uint32_t* n_in = nullptr,
                 VGEntry* entry = nullptr);
 

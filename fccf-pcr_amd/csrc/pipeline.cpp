@@ -155,8 +155,10 @@ void seg_pass1(CloudWS* w, const float* const xin[2], const uint32_t n[2], float
   voxel_grid(B2<const float*>(xin[0], xin[1]), sc(0), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds1; }),
              sc(1), vg, st, false, 2, both<float*>(w, [](const CloudWS& c) { return c.ds1f; }), n, entry);
 }
-// the driver's remove-NaN and second VoxelGrid pass (:1374-1387)
-void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
+// the driver's remove-NaN and second VoxelGrid pass (:1374-1387); mode VG_OPTIMISTIC
+// (the pipeline's default: no fallback sort launches, the host redoes a pass that was
+// not in leaf order) or VG_PRESORTED (the redo)
+void seg_downsample(CloudWS* w, float leaf, hipStream_t st, int mode) {
   const uint32_t cap = w[0].cap;
   auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
   const B2<VGBufs> vg(w[0].vg, w[1].vg);
@@ -166,7 +168,7 @@ void seg_downsample(CloudWS* w, float leaf, hipStream_t st) {
                                             B2<const VGParams*>(w[0].vg.params, w[1].vg.params), ds1f,
                                             sc(2));  // driver :1374-1375
   voxel_grid(B2<const float*>(ds1f), sc(2), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds2; }), sc(3),
-             vg, st, true, 2);  // driver :1377-1387
+             vg, st, mode, 2);  // driver :1377-1387
 }
 void seg_faces(CloudWS* w, const fccf_params& P, hipStream_t st) {
   const uint32_t cap = w[0].cap;
@@ -262,6 +264,10 @@ struct PipeSet {
   VGEntry entry;         // arguments of pass 1's entry kernel, patched into g_seg[0] per call
   bool staged = false;   // host inputs copied by stage_inputs (ev_in0 .. ev_in time the H2D)
   clk::time_point t_enq;
+  // the pair's device inputs and leaf, for a redo of the stage (VG_REDO)
+  const float *in_src = nullptr, *in_tar = nullptr;
+  int64_t in_nsrc = 0, in_ntar = 0;
+  float leaf = 0.f;
 };
 
 PipeSet& pset(fccf_ctx* c, int s) {
@@ -297,11 +303,18 @@ Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
 // Phase A: enqueue the cloud device stage of one pair on CloudSet s (returns at
 // once).  src/tar are device clouds (staged ones wait for ev_in).  cloud 0 = driver
 // source = TAR file; cloud 1 = driver target = SRC file (:1683).
+// exact2: the driver's pass as VG_PRESORTED, eagerly (the redo of a stage whose
+// optimistic second pass found its input out of leaf order; rare).
 void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
-                    bool staged, float leaf, const fccf_params& P) {
+                    bool staged, float leaf, const fccf_params& P, bool exact2 = false) {
   auto& cs = c->cs[s];
   PipeSet& ps = pset(c, s);
   ps.t_enq = clk::now();
+  ps.in_src = src;
+  ps.in_tar = tar;
+  ps.in_nsrc = n_src;
+  ps.in_ntar = n_tar;
+  ps.leaf = leaf;
   CloudWS* w = ps.w;
   ps.nin[0] = n_tar;
   ps.nin[1] = n_src;
@@ -363,7 +376,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   CloudMail* cmail = &host_mail(c)->clouds[s];  // allocated on first use: never inside the capture
   cs.g_seg[0].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, xin, nv, leaf, st0, &ps.entry);
-    seg_downsample(w, leaf, st0);
+    seg_downsample(w, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
     HIP_CHECK(hipEventRecord(cs.ev[6], st0));
     HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[6], 0));
     exact_sum2(w[0].ds2, w[0].sc + 3, w[1].ds2, w[1].sc + 3, 3, 3, ps.cen, true, ps.xs, ss);  // compute3DCentroid (:473)
@@ -372,7 +385,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
     HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[7], 0));
     face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
                        cmail, B2<const uint32_t*>(w[0].sc, w[1].sc));
-  }, vg_entry_kernel(), ps.entry.args, DG != nullptr);
+  }, vg_entry_kernel(), ps.entry.args, DG != nullptr || exact2);
   // external signal for stage_inputs (this set's inputs have been read): after the graph
   HIP_CHECK(hipEventRecord(cs.ev[0], st0));
   HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
@@ -405,10 +418,19 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   CloudMail& cm = host_mail(c)->clouds[s];
   c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
   HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
-  guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
   std::memcpy(fsc, cm.fsc, sizeof fsc);
+  if ((fsc[0][1] | fsc[1][1]) & VG_REDO) {
+    // the driver's pass found main's output out of leaf order (optimistic mode ran no
+    // sort): the stage again with the exact second pass, before the next pair is enqueued
+    clouds_enqueue(c, s, ps.in_src, ps.in_nsrc, ps.in_tar, ps.in_ntar, ps.staged, ps.leaf, P, true);
+    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+    std::memcpy(sc, cm.sc, sizeof sc);
+    std::memcpy(fsc, cm.fsc, sizeof fsc);
+    ++S.stage_redos;
+  }
+  guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
   std::vector<VoxRec> vox[2];
   for (int k = 0; k < 2; ++k) {
     if (fsc[k][2] <= CloudMail::REC_CAP) vox[k].assign(cm.rec[k], cm.rec[k] + fsc[k][2]);
@@ -417,7 +439,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
   // K1's sort checks its invariants on the device (IS_FAULT_*): a violation means the
   // VoxelGrid order may not be std::sort's, so no transform is returned
-  if (fsc[0][1] | fsc[1][1])
+  if ((fsc[0][1] | fsc[1][1]) & ~VG_REDO)
     throw Error(FCCF_E_INTERNAL, "VoxelGrid: K1 sort invariant violated (flags cloud 0: " + std::to_string(fsc[0][1]) +
                                      ", cloud 1: " + std::to_string(fsc[1][1]) + ")");
   {  // device spans of the cloud stage: its kernels' s_memrealtime stamps (100 MHz)

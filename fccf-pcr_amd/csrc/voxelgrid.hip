@@ -47,6 +47,7 @@ __global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint3
       P2[e]->sort_err = 0;  // (the driver's pass adds its flags to main's)
     }
     P2[e]->unsorted = 0;
+    P2[e]->redo = 0;
     P2[e]->chk_done = 0;
     P2[e]->nonfinite = 0;
     P2[e]->src = xyz;
@@ -255,7 +256,7 @@ constexpr int CL = 4;
 __global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B2<VGParams*> P2, B2<const uint32_t*> vals2,
                                                      B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
                                                      B2<float*> out2, B2<uint32_t*> d_m2, int presorted,
-                                                     B2<float*> copy2) {
+                                                     B2<float*> copy2, B2<const uint32_t*> inject2) {
   KT();
   const int e = blockIdx.y;
   const VGParams q = *P2[e];
@@ -269,6 +270,18 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B
   uint32_t* __restrict__ d_m = d_m2[e];
   const uint32_t n = *d_n2[e];
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
+  // VG_OPTIMISTIC: no sort or segmentation ran; an input out of leaf order is left to
+  // the caller's redo (nothing is output, the flag goes to the cloud mailbox)
+  if (presorted == VG_OPTIMISTIC && !q.overflow && n) {
+    const uint32_t* inj = inject2[e];
+    if (q.unsorted || (inj && (*inj & VG_FORCE_REDO))) {
+      if (gid == 0) {
+        *d_m = 0u;
+        P2[e]->redo = 1u;
+      }
+      return;
+    }
+  }
   // "Integer indices would overflow": output = *input_; presorted with every leaf
   // holding one finite point: the centroid of one point is the point (p / 1.f == p)
   if (q.overflow || (presorted && q.unsorted == 0u && n && q.nfinite == n)) {
@@ -355,7 +368,7 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 const void* vg_entry_kernel() { return (const void*)k_vg_bbox<0>; }
 
 void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, bool presorted, int nbatch, B2<float*> out_copy,
+                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, int presorted, int nbatch, B2<float*> out_copy,
                 const uint32_t* n_in, VGEntry* entry) {
   const B2<const uint32_t*> d_n(d_nw[0], d_nw[1]);
   auto F = [&](auto get) { return B2<decltype(get(b[0]))>(get(b[0]), get(b[1])); };
@@ -401,12 +414,13 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
     }
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch);
-  } else {  // usually already in leaf order: a sort and segmentation that run only if not
+  } else if (presorted == VG_PRESORTED) {  // usually already in leaf order: a sort and segmentation that run only if not
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, true);
     segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
                       nbatch, unsorted);
   }
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted ? 1 : 0, out_copy);
+  const B2<const uint32_t*> inj(b[0].is.inject, b[1].is.inject);
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj);
 }
 
 }  // namespace fccf

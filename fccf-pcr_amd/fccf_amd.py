@@ -48,7 +48,7 @@ class Stats(ctypes.Structure):
         ("overflow_passthrough", ctypes.c_int32), ("graph_captures", ctypes.c_int32),
         ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double),
         ("m1_src", ctypes.c_int64), ("m1_tar", ctypes.c_int64), ("leaves1", ctypes.c_int64), ("leaves2", ctypes.c_int64),
-        ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4)]
+        ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4), ("stage_redos", ctypes.c_int64)]
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "dev_ms")}

@@ -91,6 +91,9 @@ typedef struct fccf_stats {
   double dev_ms[4];              /* device spans: main's VoxelGrid pass, the driver's
                                     remove-NaN + second pass, face voxels (s_memrealtime
                                     stamps of the cloud stage's kernels), fine verify */
+  /* appended in round 3 */
+  int64_t stage_redos;           /* cloud stages redone because the driver's VoxelGrid
+                                    input was not in leaf order */
 } fccf_stats;
 
 typedef struct fccf_ctx fccf_ctx;
@@ -278,7 +281,10 @@ int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
 /* Test hook: every later sort of K1 on ctx raises the invariant flags in bits (0x100
  * round scatter outside its segment, 0x200 block item guard, 0x400 wave task stack,
  * 0x1000 block partition stack) as if the check had fired, until called with 0.
- * fccf_register* then fails with FCCF_E_INTERNAL, as it does for a real violation. */
+ * fccf_register* then fails with FCCF_E_INTERNAL, as it does for a real violation.
+ * Bit 0x10000 instead makes the pipeline's optimistic driver VoxelGrid pass report its
+ * input as out of leaf order, so the registration redoes its cloud stage with the
+ * exact second pass (fccf_stats.stage_redos; the result is unchanged). */
 int fccf_debug_inject_sort_fault(fccf_ctx* ctx, uint32_t bits);
 /* Forces a graph capture on one stream concurrent with another thread's wait on
  * an event last recorded on that stream (the pipelined batch's hazard, guarded by

@@ -297,3 +297,27 @@ def test_outdoor_extent_face_sort_stays_on_fast_passes(ctx, oracle, fccf):
     spans = [ctx.register(src, tar, 0.1)[1].dev_ms[2] for _ in range(3)]
     print(f"face stage span at 400 m extent: {min(spans):.3f} ms")
     assert min(spans) < 1.0
+
+
+def test_optimistic_driver_pass_redo(ctx, oracle, fccf):
+    """The pipeline's driver pass (FCCF.cpp:1377-1387 over main's output) runs without
+    the fallback sort and segmentation launches (VG_OPTIMISTIC); a pass whose input is
+    not in leaf order outputs nothing and sets VG_REDO, and the host redoes the stage
+    with the exact second pass.  Forced through the test hook (VG_FORCE_REDO): T stays
+    bit-exact against the oracle, and the stats count the redo, single and batched."""
+    src, tar, _ = fccf.synth_pair(100_000)
+    ref = oracle.Run(src, tar, 0.1, oracle.INTROSORT).T
+    T0, st0 = ctx.register(src, tar, 0.1)
+    assert st0.stage_redos == 0
+    ctx.inject_sort_fault(0x10000)
+    try:
+        T1, st1 = ctx.register(src, tar, 0.1)
+        Tb, stb = ctx.register_batch([(src, tar)] * 3, 0.1)
+    finally:
+        ctx.inject_sort_fault(0)
+    assert st1.stage_redos == 1 and all(x.stage_redos == 1 for x in stb)
+    for T in (T0, T1, *Tb):
+        np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    T2, st2 = ctx.register(src, tar, 0.1)  # the cached graphs are intact afterwards
+    assert st2.stage_redos == 0
+    np.testing.assert_array_equal(T2.view(np.uint32), ref.view(np.uint32))
