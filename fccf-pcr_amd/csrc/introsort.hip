@@ -43,7 +43,10 @@ namespace {
 
 constexpr uint32_t IS_TILE = 2048;   // elements per round tile (small clouds)
 constexpr uint32_t IS_TILE_L = 4096;  // elements per round tile (large clouds: fewer workgroup latency chains)
-constexpr uint32_t IS_LARGE_MIN = 1u << 21;  // clouds from this size plan each round once (k_is_count_plan)
+// clouds from this size plan each round once (k_is_count_plan; sharded sorts always):
+// c5 (10M) 7.93 ms per registration with it vs 10.6 without, c4 (5M) 3.98 vs 3.85
+// (profiles/r03l), so the crossover lies between
+constexpr uint32_t IS_LARGE_MIN = 1u << 23;
 constexpr int IS_NSH = 64;                       // round kernels: completion counter shards (last_block)
 constexpr int IS_DONE_WORDS = (IS_NSH + 1) * 32;  // u32 per launch: shards + top, 128 B apart
 constexpr int IS_TT = 256;           // round kernels: threads per block
