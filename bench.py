@@ -158,8 +158,9 @@ def cpu_baseline(src, tar, leaf, budget_s):
            "stage_ms_last": {n: round(float(v), 3) for n, v in zip(names, stages)} if stages is not None else None,
            # the reference's own timer window (FCCF.cpp:1681-1685) excludes main's VoxelGrid
            "ref_window_ms_median": statistics.median(ref_win),
-           "sample": f"{len(times)} full registrations of the same c3 pair (median), oracle/ C++ restatement, "
-                     f"introsort summation order, 1 thread pinned to CPU {core}"}
+           "sample": f"{len(times)} full registrations of the same c3 pair (median), oracle/ C++ restatement "
+                     f"with PCL's structures (std::sort VoxelGrid, pointer octrees with per-leaf index "
+                     f"vectors), 1 thread pinned to CPU {core}"}
     return out, T  # T: the oracle's transform (the parity check against the GPU's)
 
 

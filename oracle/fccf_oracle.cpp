@@ -424,11 +424,63 @@ static inline bool finite3(const float* p) {
   return std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]);
 }
 
+// PCL's OctreePointCloudSearch structure (octree_base.hpp / octree_pointcloud.hpp):
+// branch nodes with eight child pointers, leaf containers holding the point indices in
+// insertion order, a DFS over the children in index order (x bit most significant) for
+// the occupied leaves.  The oracle's result does not depend on the structure (the
+// Morton stable sort below yields the same leaves, checked in test_oracle_kat.py); it
+// is kept so that the CPU baseline times PCL's algorithm (pointer chasing, one heap
+// vector per leaf), SURVEY.md §8(d).  orc_set_octree_mode(0) selects the sort.
+struct PclOctNode {
+  PclOctNode* child[8] = {};
+  std::vector<uint32_t>* leaf = nullptr;  // a leaf node's container
+  ~PclOctNode() {
+    for (PclOctNode* c : child) delete c;
+    delete leaf;
+  }
+};
+static int g_octree_mode = 1;  // 1: PCL pointer octree, 0: Morton stable sort
+
+static void pcl_dfs(const PclOctNode* nd, uint64_t code, unsigned level, unsigned depth, Leaves& L) {
+  if (level == depth) {
+    L.code.push_back(code);
+    L.start.push_back((uint32_t)L.idx.size());
+    L.idx.insert(L.idx.end(), nd->leaf->begin(), nd->leaf->end());
+    return;
+  }
+  for (unsigned c = 0; c < 8; ++c)
+    if (nd->child[c]) pcl_dfs(nd->child[c], (code << 3) | c, level + 1, depth, L);
+}
+
 // addPointsFromInputCloud skips non-finite points (isFinite), so they belong to no leaf.
 static Leaves octree_leaves(const float* xyz, size_t n, double res) {
   Leaves L;
   for (size_t i = 0; i < n; ++i)
     if (finite3(&xyz[3 * i])) oct_adopt(L.b, res, &xyz[3 * i]);
+  if (g_octree_mode == 1) {
+    PclOctNode root;
+    const unsigned depth = L.b.depth;
+    for (size_t i = 0; i < n; ++i) {
+      if (!finite3(&xyz[3 * i])) continue;
+      uint32_t k[3];
+      for (int a = 0; a < 3; ++a) k[a] = (uint32_t)(((double)xyz[3 * i + a] - L.b.min[a]) / res);
+      PclOctNode* nd = &root;
+      for (int bit = (int)depth - 1; bit >= 0; --bit) {  // createLeafRecursive
+        const unsigned c = (((k[0] >> bit) & 1u) << 2) | (((k[1] >> bit) & 1u) << 1) | ((k[2] >> bit) & 1u);
+        if (!nd->child[c]) nd->child[c] = new PclOctNode();
+        nd = nd->child[c];
+      }
+      if (!nd->leaf) nd->leaf = new std::vector<uint32_t>();
+      nd->leaf->push_back((uint32_t)i);
+    }
+    if (depth == 0) {
+      if (root.leaf) pcl_dfs(&root, 0, 0, 0, L);
+    } else {
+      pcl_dfs(&root, 0, 0, depth, L);
+    }
+    L.start.push_back((uint32_t)L.idx.size());
+    return L;
+  }
   std::vector<std::pair<uint64_t, uint32_t>> kv;
   kv.reserve(n);
   for (size_t i = 0; i < n; ++i) {
@@ -1687,6 +1739,12 @@ extern "C" void orc_eigen33(const float cov[9], float* ev, float vec[3]) {
 extern "C" float orc_normal_angle(float x1, float y1, float z1, float x2, float y2, float z2) {
   return compute_normal_angel(x1, y1, z1, x2, y2, z2);
 }
+extern "C" int orc_set_octree_mode(int mode) {
+  const int prev = g_octree_mode;
+  if (mode == 0 || mode == 1) g_octree_mode = mode;
+  return prev;
+}
+
 extern "C" int orc_set_acos_mode(int mode) {
   const int prev = g_acos_mode;
   if (mode >= 0 && mode < ACOS_MODES) g_acos_mode = mode;

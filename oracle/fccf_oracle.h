@@ -54,6 +54,10 @@ float orc_normal_angle(float x1, float y1, float z1, float x2, float y2, float z
  * correctly rounded acosf — default; 1 = this host's glibc acosf; 2 = C's
  * double acos).  Returns the previous mode; out-of-range modes are ignored. */
 int orc_set_acos_mode(int mode);
+/* Octree structure of face_extrate / fine_verify: 1 = PCL's pointer octree (default,
+ * the CPU baseline's algorithm), 0 = a Morton stable sort (same leaves).  Returns the
+ * previous mode. */
+int orc_set_octree_mode(int mode);
 /* Per-site decision audit since the last reset, 8 sites (grow, merge, rough,
  * base, third, cluster, verify, pair): out[0..7] evaluations, out[8..15]
  * decision inputs whose bits differ between the conventions, out[16..23]

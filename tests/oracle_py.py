@@ -37,6 +37,8 @@ def _load():
     lib.orc_rot_from_quat.argtypes = [P, P]
     lib.orc_set_acos_mode.restype = ctypes.c_int
     lib.orc_set_acos_mode.argtypes = [ctypes.c_int]
+    lib.orc_set_octree_mode.restype = ctypes.c_int
+    lib.orc_set_octree_mode.argtypes = [ctypes.c_int]
     lib.orc_acos_audit.argtypes = [P, ctypes.c_int]
     lib.orc_lm_refine.restype = ctypes.c_int
     lib.orc_lm_refine.argtypes = [P, ctypes.c_int, P, P]
@@ -116,6 +118,11 @@ def normal_angle(a, b):
 # acos conventions of FCCF.cpp:374 (see oracle/fccf_oracle.cpp theta_of_cos)
 ACOS_CR_FLOAT, ACOS_LIBM_FLOAT, ACOS_DOUBLE = 0, 1, 2
 AUDIT_SITES = ("grow", "merge", "rough", "base", "third", "cluster", "verify", "pair")
+
+
+def set_octree_mode(mode):
+    """1: PCL's pointer octree (default), 0: Morton stable sort; returns the previous mode."""
+    return lib.orc_set_octree_mode(int(mode))
 
 
 def set_acos_mode(mode):

@@ -214,3 +214,21 @@ def test_lm_exact_problems_reach_scipy_optimum(oracle):
         q, tt = oracle.lm_refine(A)
         x = np.r_[Rotation.from_quat(q).as_rotvec(), tt]
         assert np.max(np.abs(_plane_pair_residuals(x, A.astype(np.float64)))) < 1e-4
+
+
+def test_pcl_pointer_octree_equals_morton_sort(oracle, fccf):
+    """The oracle's face_extrate / fine_verify octrees: PCL's pointer structure (branch
+    nodes, per-leaf index vectors, DFS leaf order; the CPU baseline's algorithm) and the
+    Morton stable sort give the same leaves, so every intermediate and T are equal."""
+    src, tar, _ = fccf.synth_pair(40_000, (12, 9, 3))
+    src[5] = np.nan  # a non-finite point belongs to no leaf in either structure
+    prev = oracle.set_octree_mode(1)
+    try:
+        a = oracle.Run(src, tar, 0.1, oracle.INTROSORT)
+        oracle.set_octree_mode(0)
+        b = oracle.Run(src, tar, 0.1, oracle.INTROSORT)
+    finally:
+        oracle.set_octree_mode(prev)
+    for name, dt in (("vox1", np.float32), ("vox2", np.float32), ("res1", np.float32), ("oct1", np.float64),
+                     ("fv0", np.float32), ("T", np.float32)):
+        np.testing.assert_array_equal(a.get(name, dt).view(np.uint8), b.get(name, dt).view(np.uint8), err_msg=name)
