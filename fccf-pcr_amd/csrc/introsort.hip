@@ -75,6 +75,31 @@ constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
 #define IS_STATS 1  // path counters in IsBufs::ctl[3..], when IsBufs::stats (debug sorts only)
 #endif
 
+#ifdef IS_PHASES
+// Development (variant builds, make VAR=ph EXTRA=-DIS_PHASES): per-phase shader cycles
+// of an instrumented kernel (thread 0 after each barrier), summed over workgroups, read
+// with fccf_debug_is_phases (tools/is_phases.py).
+__device__ unsigned long long g_is_ph[32];
+__device__ unsigned long long g_is_ph_last[4096];
+#define IS_PH(k)                                                                   \
+  do {                                                                             \
+    if (threadIdx.x == 0) {                                                        \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+      const unsigned slot_ = (blockIdx.x + blockIdx.y * gridDim.x) & 4095u;        \
+      atomicAdd(&g_is_ph[(k)], t_ - g_is_ph_last[slot_]);                         \
+      atomicAdd(&g_is_ph[16 + (k)], 1ull);                                         \
+      g_is_ph_last[slot_] = t_;                                                    \
+    }                                                                              \
+  } while (0)
+#define IS_PH_START()                                                              \
+  do {                                                                             \
+    if (threadIdx.x == 0)                                                          \
+      g_is_ph_last[(blockIdx.x + blockIdx.y * gridDim.x) & 4095u] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define IS_PH(k) do {} while (0)
+#define IS_PH_START() do {} while (0)
+#endif
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -980,10 +1005,11 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B2<const uint32_t*> K
 __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
                                                       B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
   KT();
+  IS_PH_START();
   extern __shared__ uint32_t dyn[];
   __shared__ uint64_t sh64[16];
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
-  __shared__ uint32_t scut;
+  __shared__ uint32_t scut, swin[4];
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
   const uint32_t t = blockIdx.x;
@@ -1033,6 +1059,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2,
     rl += sl;
   }
   const uint32_t le_tot = rl;
+  IS_PH(0);  // descriptor, tile loads issued, the segment's tile prefix
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const bool ok = a + c * IS_TT + threadIdx.x < b;
@@ -1043,6 +1070,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2,
     }
   }
   __syncthreads();
+  IS_PH(1);  // ballots, counts
   if (w == 0) {
     const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
     uint32_t xg = xg0, xl = xl0;
@@ -1055,8 +1083,40 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2,
       pg[lane] = xg - xg0 + preg[i];
       pl[lane] = xl - xl0 + prel[i];
     }
+    // Partner windows (as in k_is_scatter): a swapped >= element of rank gx takes the
+    // (le_tot-gx-1)-th <= element, a swapped <= element of rank lx the (le_tot-lx-1)-th
+    // >= element; this tile's ranks are contiguous, so their partners lie in a window of
+    // tiles found once here (four binary searches, one per lane) instead of per element.
+    const uint32_t cgt = (uint32_t)__shfl((int)xg, IS_TC * 4 - 1, 64), clt = (uint32_t)__shfl((int)xl, IS_TC * 4 - 1, 64);
+    const uint32_t ox = preg[i], oy = prel[i];
+    if (lane < 4) {
+      uint32_t x = 0;
+      if (lane == 0) x = le_tot > ox + cgt ? le_tot - ox - cgt : 0u;
+      if (lane == 1) x = le_tot > ox ? le_tot - ox - 1 : 0u;
+      if (lane == 2) x = le_tot > oy + clt ? le_tot - oy - clt : 0u;
+      if (lane == 3) x = le_tot > oy ? le_tot - oy - 1 : 0u;
+      swin[lane] = upper_index(lane < 2 ? prel : preg, nt, x);
+    }
   }
   __syncthreads();
+  IS_PH(2);  // chunk prefix, partner windows
+  const uint32_t wl_lo = swin[0], wl_hi = swin[1], wg_lo = swin[2], wg_hi = swin[3];
+  // largest u in [lo, hi] with pre[u] <= x (pre[lo] <= x and the answer <= hi by the
+  // window): a few steps forward when the window is short, else a binary search in it
+  auto in_window = [](const uint32_t* pre, uint32_t lo, uint32_t hi, uint32_t x) {
+    if (hi - lo <= 4) {
+      uint32_t u = lo;
+      while (u < hi && pre[u + 1] <= x) ++u;
+      return u;
+    }
+    uint32_t L = lo, H = hi + 1;
+    while (H - L > 1) {
+      const uint32_t mid = (L + H) >> 1;
+      if (pre[mid] <= x) L = mid;
+      else H = mid;
+    }
+    return L;
+  };
   // destinations: the swapped elements' partner positions come from the lists (all
   // list loads issued before any store)
   uint32_t cut = IS_NONE;
@@ -1075,12 +1135,12 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2,
     dst[c] = ok ? p : IS_NONE;
     if (sg) {  // R[gx+1]: the (le_tot-gx-1)-th <= P from the left
       const uint32_t x = le_tot - gx - 1;
-      const uint32_t u = upper_index(prel, nt, x);
+      const uint32_t u = in_window(prel, wl_lo, wl_hi, x);
       const uint32_t au = f + 1 + u * IS_TILE;
       dst[c] = au + W.lel[au + (x - prel[u])];
     } else if (sl) {  // L[kr]: the (kr-1)-th >= P from the left
       const uint32_t x = le_tot - lx - 1;
-      const uint32_t u = upper_index(preg, nt, x);
+      const uint32_t u = in_window(preg, wg_lo, wg_hi, x);
       const uint32_t au = f + 1 + u * IS_TILE;
       dst[c] = au + W.gel[au + (x - preg[u])];
     }
@@ -1096,9 +1156,11 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2,
     Ko[d] = kk[c];
     Vo[d] = vv[c];
   }
+  IS_PH(3);  // destinations (list loads), stores issued
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
   __syncthreads();
+  IS_PH(4);  // cut
   if (threadIdx.x == 0) {
     if (scut != IS_NONE) atomicMin(&W.cuts[(size_t)r * W.segmax + j], scut);
     if (i == 0) {
@@ -2457,3 +2519,14 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
 }
 
 }  // namespace fccf
+
+#ifdef IS_PHASES
+// Development export (variant builds only): the instrumented kernel's phase sums since
+// the last call (cycles [0..15], counts [16..31]), then reset.
+extern "C" int fccf_debug_is_phases(unsigned long long out[32]) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fccf::g_is_ph), 32 * sizeof(unsigned long long)) != hipSuccess) return -2;
+  unsigned long long z[32] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(fccf::g_is_ph), z, sizeof z) != hipSuccess) return -2;
+  return 0;
+}
+#endif

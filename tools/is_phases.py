@@ -1,4 +1,4 @@
-"""k_is_block phase profile (development): cycles per barrier phase from a variant build
+"""Phase profile of the IS_PH-instrumented kernel (k_is_scatter_s; development): cycles per phase from a variant build
 (make VAR=ph EXTRA=-DIS_PHASES; FCCF_LIB=fccf-pcr_amd/lib_ph/libfccf.so).
 Usage: FCCF_LIB=... python tools/is_phases.py [config]"""
 import ctypes
@@ -12,8 +12,7 @@ import fccf_amd as F  # noqa: E402
 
 cfg = F.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
 src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
-names = ["median+bar", "count+bar", "scan+bar", "swaprank+bar", "exchange+bar", "write+bar", "load+pop0",
-         "push+pop", "tasks"]
+names = ["desc+tile+prefix", "ballots+bar", "chunkscan+bar", "dest+stores", "cut+bar", "-", "-", "-", "-"]
 with F.Ctx(0) as c:
     fn = F._lib.fccf_debug_is_phases
     fn.argtypes = [ctypes.c_void_p]
