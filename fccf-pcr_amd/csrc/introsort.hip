@@ -160,6 +160,26 @@ __device__ __forceinline__ uint32_t median_pos(KP K, uint32_t f, uint32_t l) {
   return B;
 }
 
+// median_pos together with the four values a round's partition needs -- the pivot P =
+// K[m] and V[m], the first element K[f], V[f] -- from ONE round of global loads: the
+// median is one of the three probed positions, so their values are loaded with the keys
+// (the count kernels' thread 0 otherwise chains three dependent round trips: the
+// probes, then K[m], then the values; profiles/r03p)
+template <class KP, class VP>
+__device__ __forceinline__ void median_load(KP K, VP V, uint32_t f, uint32_t l, uint32_t& m, uint32_t& P,
+                                            uint32_t& vm, uint32_t& kf, uint32_t& vf) {
+  const uint32_t A = f + 1, B = f + (l - f) / 2, C = l - 1;
+  const uint32_t a = K[A], b = K[B], c = K[C], va = V[A], vb = V[B], vc = V[C];
+  kf = K[f];
+  vf = V[f];
+  int pick;  // 0: A, 1: B, 2: C (median_pos's comparisons)
+  if (a < b) pick = b < c ? 1 : (a < c ? 2 : 0);
+  else pick = a < c ? 0 : (b < c ? 2 : 1);
+  m = pick == 0 ? A : (pick == 1 ? B : C);
+  P = pick == 0 ? a : (pick == 1 ? b : c);
+  vm = pick == 0 ? va : (pick == 1 ? vb : vc);
+}
+
 // std::__adjust_heap / __make_heap / __sort_heap on (K, V) pairs by key (one thread)
 template <class KP, class VP>
 __device__ __forceinline__ void adjust_heap(KP K, VP V, int64_t hole, int64_t len, uint32_t vk, uint32_t vv) {
@@ -536,11 +556,12 @@ __device__ __forceinline__ void count_tile(const uint32_t* __restrict__ K, const
     kk[c] = p < b ? K[p] : 0u;
   }
   if (threadIdx.x == 0) {
-    const uint32_t m = median_pos(K, f, l);
+    uint32_t m, Pm, vm, kf0, vf0;
+    median_load(K, V, f, l, m, Pm, vm, kf0, vf0);
     bsh[0] = m;
-    bsh[1] = K[m];
-    bsh[2] = K[f];
-    const IsSeg rec{f, l, (int32_t)pt.z, tile0, m, bsh[1], bsh[2], V[f], V[m]};
+    bsh[1] = Pm;
+    bsh[2] = kf0;
+    const IsSeg rec{f, l, (int32_t)pt.z, tile0, m, Pm, kf0, vf0, vm};
     W.tdesc[t] = IsTile{j, rec};  // the scatter's one-load view of this tile's segment
     atomicExch(&W.tseg[t], j);
     if (t == tile0) {  // the segment's record, once
@@ -904,6 +925,7 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
       nown += s_ow;
     }
     __syncthreads();
+    IS_PH(5);  // count: the round's plan
     // (pad: elements partitioned this round, the scatter probe's unit count, summed by
     // the scatter's first tiles)
     if (t == 0 && threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
@@ -929,11 +951,12 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
       }
     }
     if (threadIdx.x == 0) {
-      m = median_pos(K, f, l);
+      uint32_t Pm, vm, kf0, vf0;
+      median_load(K, V, f, l, m, Pm, vm, kf0, vf0);
       bsh[0] = m;
-      bsh[1] = K[m];
-      bsh[2] = K[f];
-      const IsSeg rec{f, l, td[j], tile0, m, bsh[1], bsh[2], V[f], V[m]};
+      bsh[1] = Pm;
+      bsh[2] = kf0;
+      const IsSeg rec{f, l, td[j], tile0, m, Pm, kf0, vf0, vm};
       W.tseg[t] = j;
       W.tdesc[t] = IsTile{j, rec};  // the scatter's one-load view of this tile's segment
       if (t == tile0) {  // the segment's record, once
@@ -942,6 +965,7 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
       }
     }
     __syncthreads();
+    IS_PH(6);  // count: tile keys, median, descriptor
     m = bsh[0];
     P = bsh[1];
     kf = bsh[2];
@@ -962,6 +986,7 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
     }
   }
   __syncthreads();
+  IS_PH(7);  // count: ballots
   if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
     const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
     uint32_t xg = xg0, xl = xl0;
@@ -980,6 +1005,7 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
     }
   }
   __syncthreads();
+  IS_PH(8);  // count: chunk scan
 #pragma unroll
   for (int c = 0; c < IS_TC; ++c) {
     const uint32_t p = a + c * IS_TT + threadIdx.x;
@@ -989,12 +1015,14 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
     if (ge) W.gel[a + pg[c * 4 + w] + mbcnt(bg)] = (uint16_t)(p - a);
     if (le) W.lel[a + pl[c * 4 + w] + mbcnt(bl)] = (uint16_t)(p - a);
   }
+  IS_PH(9);  // count: lists written
 }
 
 // Dynamic LDS: 4 * segmax u32 (the round's segment table).
 __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
                                                          B2<IsBufs> W2, int r) {
   KT();
+  IS_PH_START();
   extern __shared__ uint32_t dyn[];
   const int e = blockIdx.y;
   is_count_body_s(K2[e], V2[e], W2[e], r, dyn);

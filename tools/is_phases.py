@@ -12,7 +12,7 @@ import fccf_amd as F  # noqa: E402
 
 cfg = F.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c3"]
 src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
-names = ["desc+tile+prefix", "ballots+bar", "chunkscan+bar", "dest+stores", "cut+bar", "-", "-", "-", "-"]
+names = ["sc:desc+tile+prefix", "sc:ballots+bar", "sc:chunkscan+bar", "sc:dest+stores", "sc:cut+bar", "ct:plan", "ct:tile+median+desc", "ct:ballots+bar", "ct:chunkscan+bar", "ct:lists"]
 with F.Ctx(0) as c:
     fn = F._lib.fccf_debug_is_phases
     fn.argtypes = [ctypes.c_void_p]
@@ -25,7 +25,7 @@ with F.Ctx(0) as c:
     fn(out.ctypes.data)
     cyc, cnt = out[:16].astype(float) / 5, out[16:].astype(float) / 5
     tot = cyc.sum()
-    for i in range(9):
+    for i in range(10):
         if cnt[i]:
             print(f"{names[i]:14s} count {cnt[i]:9.0f}  cycles/event {cyc[i] / cnt[i]:9.0f}  share {cyc[i] / tot:6.1%}")
     print(f"total cycles per registration (summed over workgroups) {tot:.3e}")
