@@ -2538,8 +2538,11 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
     step("scatter", r);
   }
   // algorithmic bytes: each element's key and value read once and written once
+  // k_is_block: IS_OWN_BLOCKS workgroups (one per CU) split over the clouds, so both
+  // clouds' items run at once and 8 CUs stay free for the small kernels of other
+  // streams (matching, fine verification); profiles/r03r
   FCCF_LAUNCH("k_is_block", (b[0].ctl + 20, 16.0, nbatch > 1 ? b[1].ctl + 20 : nullptr, 16.0, 0.0), k_is_block,
-              dim3(IS_OWN_BLOCKS, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+              dim3(IS_OWN_BLOCKS / nbatch, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
   FCCF_LAUNCH("k_is_wave", (b[0].ctl + 19, 16.0, nbatch > 1 ? b[1].ctl + 19 : nullptr, 16.0, 0.0), k_is_wave,
               dim3(IS_WAVE_BLOCKS, nbatch), IS_WT, 0, st, k0, v0, b);

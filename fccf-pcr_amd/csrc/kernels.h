@@ -35,7 +35,7 @@ constexpr int VG_KEY_BLOCKS = 512;
 
 // K1's sort in libstdc++ std::sort order (introsort.hip): workspace of one cloud.
 constexpr int IS_RMAX = 24;          // most partition rounds before the owner kernel
-constexpr int IS_OWN_BLOCKS = 256;   // block-kernel workgroups per cloud (one per CU)
+constexpr int IS_OWN_BLOCKS = 248;   // block-kernel workgroups of a launch, split over its clouds (one per CU)
 constexpr int IS_WAVE_BLOCKS = 512;  // wave-kernel workgroups per cloud (4 waves each)
 constexpr int IS_SHARD_MAX = 64;     // most ranks of a sharded sort (row D)
 struct IsRound {
