@@ -124,6 +124,14 @@ __device__ __forceinline__ void is_inject(const IsBufs& W, uint32_t bits) {
   if (b) is_fault(W.ctl, W.err, b);
 }
 
+// A final (key, value) write's point, when the sort writes sorted points (IsBufs::xyzs)
+__device__ __forceinline__ void put_xyz(const IsBufs& W, const float* __restrict__ src, uint32_t pos, uint32_t v) {
+  const float x = src[3 * (size_t)v], y = src[3 * (size_t)v + 1], z = src[3 * (size_t)v + 2];
+  W.xyzs[3 * (size_t)pos] = x;
+  W.xyzs[3 * (size_t)pos + 1] = y;
+  W.xyzs[3 * (size_t)pos + 2] = z;
+}
+
 // The fence before a workgroup barrier that hands global-memory data between the waves
 // of one workgroup (k_is_block's global phase).  Every sort kernel runs with TG_SPLIT = 0
 // (COMPUTE_PGM_RSRC3 bit 16; checked in tools/check_tgsplit.py), so all waves of a
@@ -1592,7 +1600,8 @@ __device__ __forceinline__ uint32_t level_rank(const WaveLds& S, int s, uint32_t
 // active (rare).  The leaves are then stably sorted by rank and written to K/V.
 template <int C>
 __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict__ K, uint32_t* __restrict__ V,
-                                                uint32_t f, uint32_t n, int d) {
+                                                uint32_t f, uint32_t n, int d, const IsBufs& W,
+                                                const float* __restrict__ src) {
   const uint32_t lane = lane_id();
   uint32_t ab[C];  // a | b << 16
 #pragma unroll
@@ -1769,6 +1778,7 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
     }
     K[f + a + rank] = key;
     V[f + a + rank] = S.v[p];
+    if (src) put_xyz(W, src, f + a + rank, S.v[p]);
   }
 }
 #endif
@@ -1984,6 +1994,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     else W.tasks[W.taskmax - 1u - (S.bc[2] + i - S.ntb)] = t;
   }
   // leaves: stable sort in place (the final insertion sort); task ranges as they are
+  const float* __restrict__ xsrc = W.xyzs ? W.vgp->src : nullptr;
   for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
     const uint32_t key = S.k[p];
     if ((S.intask[p >> 5] >> (p & 31)) & 1u) {
@@ -2016,6 +2027,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     }
     Ko[f + a + rank] = key;
     Vo[f + a + rank] = S.v[p];
+    if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);
   }
   __syncthreads();
 }
@@ -2282,6 +2294,8 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
             K0[gf + q] = K[gf + q];
             V0[gf + q] = V[gf + q];
           }
+        if (W.xyzs)
+          for (uint32_t q = threadIdx.x; q < len; q += IS_OT) put_xyz(W, W.vgp->src, gf + q, V[gf + q]);
         __syncthreads();
       } else {
         if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
@@ -2341,6 +2355,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
   // one per wave (a dynamic dequeue from one counter serialises on that counter:
   // ~18 ns per atomic, which at thousands of tasks was the kernel's whole time).
   const uint32_t nbig = W.ctl[16], ntasks = nbig + W.ctl[18];
+  const float* __restrict__ xsrc = W.xyzs ? W.vgp->src : nullptr;
   uint32_t* __restrict__ K = K02[e];
   uint32_t* __restrict__ V = V02[e];
   const uint32_t nw = gridDim.x * (IS_WT / 64);
@@ -2361,9 +2376,9 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
     const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
 #if IS_WLEVEL
     if (n > 64) {
-      if (n <= 128) wave_task_level<2>(S, K, V, f, n, d);
-      else if (n <= 256) wave_task_level<4>(S, K, V, f, n, d);
-      else wave_task_level<IS_WC>(S, K, V, f, n, d);
+      if (n <= 128) wave_task_level<2>(S, K, V, f, n, d, W, xsrc);
+      else if (n <= 256) wave_task_level<4>(S, K, V, f, n, d, W, xsrc);
+      else wave_task_level<IS_WC>(S, K, V, f, n, d, W, xsrc);
       if (S.son && lane == 0) atomicAdd(&S.lstat[2], 1u);
     } else
 #endif
@@ -2393,6 +2408,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02
       }
       K[f + a + rank] = key;
       V[f + a + rank] = S.v[p];
+      if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);
     }
     }
     wsync();
@@ -2489,6 +2505,8 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.stats = 0;
   b.err = nullptr;
   b.inject = nullptr;
+  b.vgp = nullptr;
+  b.xyzs = nullptr;
   return b;
 }
 

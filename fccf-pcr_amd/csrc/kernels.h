@@ -88,6 +88,11 @@ struct IsBufs {
   uint32_t* err;        // VGParams::sort_err of the pass's cloud (null: ctl[2] only)
   const uint32_t* inject;  // test hook (fccf_debug_inject_sort_fault): IS_FAULT_* bits raised once per
                            // sort by a designated thread at the matching site (null: off)
+  // Sorted points (VoxelGrid's first pass, unsharded): every final (key, value) write also
+  // writes the point vgp->src[value] to xyzs at the same position, so the centroid kernel
+  // reads each leaf's members contiguously instead of gathering them (null: off)
+  const struct VGParams* vgp;
+  float* xyzs;
 };
 // Invariant flags of the sort (IsBufs::ctl[2], VGParams::sort_err).  Each marks a
 // state the algorithm cannot reach; any of them makes fccf_register* fail with
@@ -115,6 +120,7 @@ struct VGBufs {
   uint32_t* nseg;
   SortScratch ss;
   IsBufs is;
+  float* xyzs;                  // 3 * cap: the first pass's points in sorted order (IsBufs::xyzs)
 };
 
 // xyz[0..*d_n) -> out[0..*d_m), PCL VoxelGrid<PointXYZ> semantics: the points of a

@@ -9,7 +9,7 @@ namespace fccf {
 
 inline size_t voxel_grid_bytes(uint32_t cap) {
   return 4 * sizeof(uint32_t) * (size_t)cap + sizeof(uint32_t) * ((size_t)cap + 1) + sizeof(float) * VG_BBOX_BLOCKS * 8 +
-         sizeof(VGParams) + 64 + sort_scratch_bytes(cap) + introsort_bytes(cap) + 8 * 256;
+         sizeof(VGParams) + 64 + sort_scratch_bytes(cap) + introsort_bytes(cap) + 12 * (size_t)cap + 9 * 256;
 }
 
 inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
@@ -25,6 +25,8 @@ inline VGBufs voxel_grid_carve(Arena& a, uint32_t cap) {
   b.ss = sort_scratch_carve(a.take(sort_scratch_bytes(cap)), cap);
   b.is = introsort_carve(a.take(introsort_bytes(cap)), cap);
   b.is.err = &b.params->sort_err;
+  b.is.vgp = b.params;
+  b.xyzs = a.take_n<float>(3 * (size_t)cap);
   return b;
 }
 

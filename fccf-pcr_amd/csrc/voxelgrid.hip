@@ -256,7 +256,8 @@ constexpr int CL = 4;
 __global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B2<VGParams*> P2, B2<const uint32_t*> vals2,
                                                      B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
                                                      B2<float*> out2, B2<uint32_t*> d_m2, int presorted,
-                                                     B2<float*> copy2, B2<const uint32_t*> inject2) {
+                                                     B2<float*> copy2, B2<const uint32_t*> inject2,
+                                                     B2<const float*> xyzs2) {
   KT();
   const int e = blockIdx.y;
   const VGParams q = *P2[e];
@@ -309,6 +310,7 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B
   }
   const uint32_t ns = q.nfinite ? *d_nseg : 0u;
   if (gid == 0) *d_m = ns;
+  const float* __restrict__ xs = xyzs2[e];
   __shared__ __attribute__((aligned(16))) float so[3 * 256];
   const bool al = (((uintptr_t)out) & 15u) == 0;
   for (uint32_t s0 = blockIdx.x * 256; s0 < ns; s0 += gsz) {
@@ -316,7 +318,22 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B
     if (s < ns) {
       const uint32_t b = starts[s], e1 = starts[s + 1];
       float sx = 0.f, sy = 0.f, sz = 0.f;
-      for (uint32_t k0 = b; k0 < e1; k0 += CL) {
+      if (xs) {  // members in sorted order, contiguous
+        for (uint32_t k0 = b; k0 < e1; k0 += CL) {
+          float px[CL], py[CL], pz[CL];
+#pragma unroll
+          for (int c = 0; c < CL; ++c) {
+            const size_t k = min(k0 + c, e1 - 1u);
+            px[c] = xs[3 * k];
+            py[c] = xs[3 * k + 1];
+            pz[c] = xs[3 * k + 2];
+          }
+#pragma unroll
+          for (int c = 0; c < CL; ++c)
+            if (k0 + c < e1) { sx += px[c]; sy += py[c]; sz += pz[c]; }
+        }
+      }
+      for (uint32_t k0 = b; !xs && k0 < e1; k0 += CL) {
         uint32_t j[CL];
         float px[CL], py[CL], pz[CL];
 #pragma unroll
@@ -402,7 +419,17 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
   // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
   const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
   FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
-  const B2<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
+  // the first pass's sort also writes the points in sorted order (IsBufs::xyzs), so the
+  // centroid reads each leaf's members contiguously; not for a sharded sort (each rank
+  // finishes only its range, and the gather moves keys and values only)
+  const bool sorted_pts = !presorted && b[0].is.shard_n <= 1;
+  B2<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
+  if (sorted_pts) {
+    isb.v[0].xyzs = b[0].xyzs;
+    if (nbatch > 1) isb.v[1].xyzs = b[1].xyzs;
+  }
+  const B2<const float*> xyzs = sorted_pts ? B2<const float*>(b[0].xyzs, nbatch > 1 ? b[1].xyzs : nullptr)
+                                           : B2<const float*>(nullptr);
   const B2<const VGParams*> Pc(P[0], P[1]);
   if (!presorted) {
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, false);
@@ -420,7 +447,7 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
                       nbatch, unsorted);
   }
   const B2<const uint32_t*> inj(b[0].is.inject, b[1].is.inject);
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj);
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
 }
 
 }  // namespace fccf
