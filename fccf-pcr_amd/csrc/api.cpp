@@ -171,6 +171,9 @@ int stage_downsample(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float
     uint32_t hm = 0, err = 0;
     HIP_CHECK(hipMemcpyAsync(&hm, d_sc + 1, 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(&err, &b.params->sort_err, 4, hipMemcpyDeviceToHost, st));
+    // the first pass's sort path counters, for fccf_debug_sort_stats (the presorted pass
+    // leaves them untouched unless it sorts)
+    HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     if (err) throw Error(FCCF_E_INTERNAL, "VoxelGrid: K1 sort invariant violated (flags " + std::to_string(err) + ")");
     HIP_CHECK(hipMemcpyAsync(out, d_out, 12 * (size_t)hm, hipMemcpyDeviceToHost, st));
@@ -252,9 +255,15 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     }
     const auto tsort = std::chrono::steady_clock::now();
     uint32_t sort_ns = 0;
-    hipEvent_t ev0, ev1;  // device time of the sort alone (sort_stats[31], ns)
-    HIP_CHECK(hipEventCreate(&ev0));
-    HIP_CHECK(hipEventCreate(&ev1));
+    struct Ev {  // device time of the sort alone (sort_stats[31], ns); destroyed on every path
+      hipEvent_t e = nullptr;
+      ~Ev() {
+        if (e) (void)hipEventDestroy(e);
+      }
+    } e0, e1;
+    HIP_CHECK(hipEventCreate(&e0.e));
+    HIP_CHECK(hipEventCreate(&e1.e));
+    hipEvent_t ev0 = e0.e, ev1 = e1.e;
     HIP_CHECK(hipEventRecord(ev0, st));
     introsort_u32(b.k0, b.v0, b.k1, b.v1, B2<const uint32_t*>(d_sc), B2<const VGParams*>(b.params), cap, b.is, st, 1,
                   exact_gate != 0);
@@ -303,8 +312,6 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
       float ms = 0.f;
       HIP_CHECK(hipEventSynchronize(ev1));
       HIP_CHECK(hipEventElapsedTime(&ms, ev0, ev1));
-      (void)hipEventDestroy(ev0);
-      (void)hipEventDestroy(ev1);
       sort_ns = (uint32_t)std::min(4.0e9, (double)ms * 1e6);
     }
     HIP_CHECK(hipStreamSynchronize(st));
@@ -315,7 +322,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
 }
 
 extern "C" int fccf_debug_inject_sort_fault(fccf_ctx* c, uint32_t bits) {
-  if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO))) return FCCF_E_ARG;
+  if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO | IS_POISON_XYZS))) return FCCF_E_ARG;
   return guarded(c, [&] {
     HIP_CHECK(hipDeviceSynchronize());  // no sort of this ctx in flight reads the word meanwhile
     HIP_CHECK(hipMemcpy(c->d_flags, &bits, 4, hipMemcpyHostToDevice));

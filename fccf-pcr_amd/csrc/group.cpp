@@ -254,6 +254,40 @@ int shard_sort_r0(int n_ranks) {
   return lg + 3;
 }
 
+void cloud_gate(Group* g) {
+  std::unique_lock<std::mutex> lk(g->om);
+  g->ocv.wait(lk, [&] { return g->order_abort || g->b1_issued >= g->cloud_need; });
+  if (g->order_abort) throw Error(FCCF_E_RCCL, "group: batch aborted before the sharded sort's gather");
+}
+
+void b1_done(Group* g) {
+  {
+    std::lock_guard<std::mutex> lk(g->om);
+    ++g->b1_issued;
+  }
+  g->ocv.notify_all();
+}
+
+void order_reset(Group* g) {
+  std::lock_guard<std::mutex> lk(g->om);
+  g->b1_issued = 0;
+  g->cloud_need = 0;
+  g->order_abort = false;
+}
+
+void order_need(Group* g, int64_t need) {
+  std::lock_guard<std::mutex> lk(g->om);
+  g->cloud_need = need;
+}
+
+void order_abort(Group* g) {
+  {
+    std::lock_guard<std::mutex> lk(g->om);
+    g->order_abort = true;
+  }
+  g->ocv.notify_all();
+}
+
 void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
                          int nbatch, hipStream_t st) {
   const int n = g->n;
@@ -261,6 +295,7 @@ void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2],
     HIP_CHECK(hipMemcpyAsync(g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1), bounds[e], 4 * (size_t)(n + 1),
                              hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  cloud_gate(g);  // (the batch's helper thread: after the previous pair's B1 collectives)
   std::vector<size_t> cnt((size_t)n), off((size_t)n);
   for (int e = 0; e < nbatch; ++e) {
     const uint32_t* b = g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1);

@@ -13,9 +13,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 
 #include "match.h"
 
@@ -58,7 +60,29 @@ struct Group {
   float* d_frecv[2] = {nullptr, nullptr};  // n x FE_BLK
   float* h_frecv[2] = {nullptr, nullptr};  // pinned copies
   uint32_t* h_bounds = nullptr;             // pinned: the sharded sort's rank bounds, per cloud (row D)
+  // One issue order of collectives per rank.  Communicators that are used concurrently
+  // must see their collectives issued in the same order on every rank, or their kernels
+  // can wait on each other across ranks.  The pipelined batch issues CH_MATCH and CH_FINE
+  // from phase B1 on the main thread and CH_CLOUD (row D) from the helper thread that
+  // enqueues the next pair's cloud stage, so the cloud gather of pair i + 1 waits here
+  // until the main thread has issued pair i's B1 collectives: order CLOUD(i), MATCH(i),
+  // FINE(i), CLOUD(i + 1), ... on every rank (cloud_gate, b1_done).
+  std::mutex om;
+  std::condition_variable ocv;
+  int64_t b1_issued = 0;   // pairs of the current batch whose phase-B1 collectives are issued
+  int64_t cloud_need = 0;  // the next CH_CLOUD gather waits for b1_issued >= cloud_need
+  bool order_abort = false;  // set on an error unwind: a waiting gather throws instead of hanging
 };
+// The collective-order gate (see Group::om): blocks until b1_issued >= cloud_need, or
+// throws FCCF_E_RCCL when the batch is unwinding after an error.
+void cloud_gate(Group* g);
+// Phase B1 of one more pair has issued its collectives (wakes a waiting cloud gather).
+void b1_done(Group* g);
+// Batch start / end: reset the gate; set the need of the next helper-issued cloud stage;
+// abort a waiting gather (error unwind).
+void order_reset(Group* g);
+void order_need(Group* g, int64_t need);
+void order_abort(Group* g);
 
 // Row D (K1's sort sharded after its first rounds, introsort.hip): whether the cloud
 // stage of clouds of cap points shards its sort over g, and the round it starts at.

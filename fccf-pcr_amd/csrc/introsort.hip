@@ -354,6 +354,11 @@ __global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*
     for (int i = 1; i < 32; ++i) W.ctl[i] = 0;
   }
   for (int i = threadIdx.x; i < 2 * IS_RMAX * IS_DONE_WORDS; i += 1024) W.done[i] = 0;
+  // Test hook (IS_POISON_XYZS): the sorted points are NaN before the sort, so a final
+  // position that no put_xyz writes shows up as a NaN centroid instead of reading the
+  // previous registration's point (the arena is reused)
+  if (W.xyzs && W.inject && (*W.inject & IS_POISON_XYZS))
+    for (uint32_t i = threadIdx.x; i < 3 * n; i += 1024) W.xyzs[i] = __uint_as_float(0x7FC00000u);
   if (ns > 0 && ns < n) {
     uint32_t* K = K2[e];
     uint32_t* V = V2[e];
@@ -2276,7 +2281,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       } else if (gd == 0 && distinct_keys(S, K + gf, (buf ? K0 : K1) + gf, (buf ? V0 : V1) + gf, len)) {
         // depth exhausted, distinct keys: the order is unique; go on with free pivots
         if (threadIdx.x == 0) {
-          W.ctl[2] |= 4u;
+          atomicOr(&W.ctl[2], 4u);  // (other workgroups atomicOr fault bits into the same word)
           if (S.son) atomicAdd(&W.ctl[9], 1u);
           S.gstk[S.gsp++] = make_uint4(gf, gl, 60u, 1u);
         }
@@ -2284,7 +2289,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
       } else if (gd == 0) {  // depth exhausted, a repeated key: heap sort in place (slow; adversarial only)
         if (threadIdx.x == 0) {
           heap_sort(K + gf, V + gf, (int64_t)len);
-          W.ctl[2] |= 2u;
+          atomicOr(&W.ctl[2], 2u);
           if (S.son) atomicAdd(&W.ctl[7], 1u);
         }
         hand_off_fence();
@@ -2301,7 +2306,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
         if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
         const uint32_t c = global_partition(S, K, V, buf ? K0 : K1, buf ? V0 : V1, gf, gl, gfree);
         if (threadIdx.x == 0) {
-          W.ctl[2] |= 1u;
+          atomicOr(&W.ctl[2], 1u);
           uint32_t s = S.gsp;
           const uint32_t cd = gfree ? 60u : (uint32_t)(gd - 1);  // (free: depth is irrelevant)
           // the larger child below the smaller (the segments are disjoint, so the order

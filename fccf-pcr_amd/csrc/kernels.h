@@ -162,6 +162,7 @@ const void* vg_entry_kernel();
 enum { VG_GENERAL = 0, VG_PRESORTED = 1, VG_OPTIMISTIC = 2 };
 constexpr uint32_t VG_REDO = 0x80000000u;       // CloudMail::fsc[k][1]: the optimistic pass must be redone
 constexpr uint32_t VG_FORCE_REDO = 0x10000u;    // test hook bit (fccf_debug_inject_sort_fault)
+constexpr uint32_t IS_POISON_XYZS = 0x20000u;   // test hook bit: sorted points filled with NaN before each sort
 void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
                 B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, int presorted = VG_GENERAL, int nbatch = 1,
                 B2<float*> out_copy = B2<float*>(nullptr), const uint32_t* n_in = nullptr,

@@ -268,6 +268,7 @@ struct PipeSet {
   const float *in_src = nullptr, *in_tar = nullptr;
   int64_t in_nsrc = 0, in_ntar = 0;
   float leaf = 0.f;
+  uint32_t sharded = 0;  // FCCF_SHARDED_* of the cloud stage (row D)
 };
 
 PipeSet& pset(fccf_ctx* c, int s) {
@@ -340,6 +341,7 @@ void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   // (introsort.hip, group.cpp); the stage then runs eagerly (a host step between the
   // sort and the gather of the sorted slices)
   Group* const DG = shard_sort_enabled(c->group, capmax, introsort_rounds(capmax)) ? c->group : nullptr;
+  ps.sharded = DG ? FCCF_SHARDED_SORT : 0u;
   for (int k = 0; k < 2; ++k) {
     w[k] = CloudWS();
     carve_cloud(cs.arena, w[k], capmax, false);
@@ -867,6 +869,9 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   pb.stats = stats;
   pb.t_all = t_all;
   pb.ht = ht;
+  pb.S.shard_ranks = c->group ? c->group->n : 1;
+  pb.S.sharded = ps.sharded | (G && G->n > 1 && K > 0 ? FCCF_SHARDED_SEARCH : 0u) | (FG && E > 0 ? FCCF_SHARDED_FINE : 0u);
+  if (c->group) b1_done(c->group);  // this pair's CH_MATCH / CH_FINE collectives are issued
 }
 
 // Phase B2: the fine scores of the pair on CloudSet s (launched by phase_b1), the
@@ -1161,6 +1166,7 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
                   float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
+  if (c->group) order_reset(c->group);
   if (!on_device) {
     const Staged in = stage_inputs(c, 0, src, n_src, tar, n_tar);
     src = in.src;
@@ -1185,6 +1191,9 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     bool armed = true;
     ~JoinOnUnwind() {
       if (!armed) return;
+      // a helper thread waiting at the group's collective-order gate for a B1 that will
+      // not come throws instead of hanging (Group::om)
+      if (c->group) order_abort(c->group);
       try {
         c->enq.wait();
       } catch (...) {
@@ -1192,6 +1201,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       (void)hipDeviceSynchronize();
     }
   } join_guard{c};
+  if (c->group) order_reset(c->group);
   // Host inputs: pair i+1's clouds are staged on the copy stream at the start of
   // pair i (from the helper thread: the pageable copy blocks its caller), so the host
   // link works while pair i's cloud stage runs.
@@ -1223,14 +1233,21 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
         HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
         clouds_enqueue(c, s ^ 1, dsrc(i + 1), n_src[i + 1], dtar(i + 1), n_tar[i + 1], !on_device, leaf, P);
       };
-      if (c->probe.on()) enq();
-      else c->enq.submit(enq);  // (after the staging task, which submit() joins first)
+      if (c->probe.on()) {
+        enq();
+      } else {
+        // with a group, the helper's sharded-sort gather (CH_CLOUD) waits until this
+        // pair's B1 has issued its CH_MATCH / CH_FINE collectives: one issue order per rank
+        if (c->group) order_need(c->group, i + 1);
+        c->enq.submit(enq);  // (after the staging task, which submit() joins first)
+      }
     });
     if (i > 0) phase_b2(c, s ^ 1);
   }
   c->enq.wait();
   phase_b2(c, (n - 1) & 1);
   join_guard.armed = false;
+  if (c->group) order_reset(c->group);
 }
 
 }  // namespace fccf

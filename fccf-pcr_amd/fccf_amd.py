@@ -48,7 +48,9 @@ class Stats(ctypes.Structure):
         ("overflow_passthrough", ctypes.c_int32), ("graph_captures", ctypes.c_int32),
         ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double),
         ("m1_src", ctypes.c_int64), ("m1_tar", ctypes.c_int64), ("leaves1", ctypes.c_int64), ("leaves2", ctypes.c_int64),
-        ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4), ("stage_redos", ctypes.c_int64)]
+        ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4), ("stage_redos", ctypes.c_int64),
+        ("shard_ranks", ctypes.c_int32), ("sharded", ctypes.c_uint32)]
+    SHARDED = {"search": 1, "fine": 2, "sort": 4, "faces": 8}  # fccf_stats.sharded bits (FCCF_SHARDED_*)
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "dev_ms")}
@@ -56,6 +58,7 @@ class Stats(ctypes.Structure):
         d["cand"] = list(self.cand)
         d["fine"] = list(self.fine)
         d["ms"] = dict(zip(T_NAMES, list(self.ms)))
+        d["sharded"] = sorted(k for k, b in self.SHARDED.items() if self.sharded & b)
         return d
 
 

@@ -94,7 +94,17 @@ typedef struct fccf_stats {
   /* appended in round 3 */
   int64_t stage_redos;           /* cloud stages redone because the driver's VoxelGrid
                                     input was not in leaf order */
+  /* appended in round 4 */
+  int32_t shard_ranks;           /* ranks of the attached group (1: no group)      */
+  uint32_t sharded;              /* FCCF_SHARDED_* stages this call split over them */
 } fccf_stats;
+/* fccf_stats.sharded bits */
+enum {
+  FCCF_SHARDED_SEARCH = 1u, /* K5 correspondence search, FCCF.cpp:1410-1428 */
+  FCCF_SHARDED_FINE = 2u,   /* F fine_verify evaluations, :785-839          */
+  FCCF_SHARDED_SORT = 4u,   /* D VoxelGrid's std::sort ranges, :1668-1678   */
+  FCCF_SHARDED_FACES = 8u   /* P 1 m face voxels by Morton range, :470-534  */
+};
 
 typedef struct fccf_ctx fccf_ctx;
 
@@ -284,7 +294,10 @@ int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
  * fccf_register* then fails with FCCF_E_INTERNAL, as it does for a real violation.
  * Bit 0x10000 instead makes the pipeline's optimistic driver VoxelGrid pass report its
  * input as out of leaf order, so the registration redoes its cloud stage with the
- * exact second pass (fccf_stats.stage_redos; the result is unchanged). */
+ * exact second pass (fccf_stats.stage_redos; the result is unchanged).  Bit 0x20000
+ * fills the first pass's sorted-point buffer with NaN before every sort, so a sorted
+ * position that the sort's finish kernels fail to write turns into a NaN centroid
+ * (a wrong result) instead of a stale point of an earlier call. */
 int fccf_debug_inject_sort_fault(fccf_ctx* ctx, uint32_t bits);
 /* Forces a graph capture on one stream concurrent with another thread's wait on
  * an event last recorded on that stream (the pipelined batch's hazard, guarded by

@@ -236,3 +236,46 @@ def test_fine_verify_sharded_host_mirror(fccf, pair):
             c.close()
     for g in got:
         np.testing.assert_array_equal(g.view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("n,cfg", [(4, "c4"), (8, "c5")])
+def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
+    """BASELINE configs[3]/[4] as named: c4 (5M/5M points) over 4 ranks and c5
+    (10M/10M) over 8, with the default FCCF_SHARD_D_MIN (2M points), so the K1 sort
+    (row D), the correspondence search (K5) and the fine evaluations (F) are all split
+    across the ranks and gathered in rank order.  Every virtual rank's single and
+    pipelined-batch registration equals the unsharded one and the oracle bit for bit
+    (FCCF.cpp:1410-1428, :785-839, :1668-1678), and the stats name the sharded stages."""
+    c = fccf.CONFIGS[cfg]
+    src, tar, _ = fccf.synth_pair(c["n"], c["room"])
+    leaf = c["leaf"]
+    run = oracle.Run(src, tar, leaf, oracle.INTROSORT)
+    T_orc = run.T.copy()
+    del run
+    with fccf.Ctx(0) as ctx:
+        T0, s0 = ctx.register(src, tar, leaf)
+    np.testing.assert_array_equal(bits(T0), bits(T_orc))
+    assert s0.shard_ranks == 1 and s0.sharded == 0
+    ctxs = [fccf.Ctx(0) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+
+        def work(r):
+            T, s = ctxs[r].register(src, tar, leaf)
+            Tb, sb = ctxs[r].register_batch([(src, tar)] * 2, leaf)
+            return T, s, Tb, sb
+
+        out = _on_threads(work, n)
+        for g in groups:
+            g.close()
+    finally:
+        for cx in ctxs:
+            cx.close()
+    for T, s, Tb, sb in out:
+        np.testing.assert_array_equal(bits(T), bits(T0))
+        for Tx in Tb:
+            np.testing.assert_array_equal(bits(Tx), bits(T0))
+        assert (s.K, s.K_pass, list(s.cand), s.vox1, s.vox2) == (s0.K, s0.K_pass, list(s0.cand), s0.vox1, s0.vox2)
+        for st in [s] + list(sb):
+            assert st.shard_ranks == n
+            assert sorted(st.as_dict()["sharded"]) == ["fine", "search", "sort"], st.as_dict()["sharded"]
