@@ -11,7 +11,12 @@ per registration, FCCF.cpp:1415-1427) processed by all ranks / wall time.
 Multi-GPU: registrations are independent objects, so each rank registers its own
 pair on its own GPU (weak scaling, no data-path collective); a gloo process group
 (CPU) provides only the barrier and the max-over-ranks of the timed span.  libfccf
-links the system ROCm HIP runtime, so torch never touches the GPU here.
+links the system ROCm HIP runtime, so torch never touches the GPU here.  After that
+leg, N > 1 also measures strong scaling as BASELINE configs[3]/[4] name it: ONE c4
+pair registered by min(N, 4) ranks and ONE c5 pair by N ranks of an RCCL group inside
+libfccf (fccf_group_create: search, fine verification and the VoxelGrid sort sharded),
+each rank in a child process with a time limit; reported under "sharded" beside the
+replica `value` (sharded_pass).
 """
 import argparse
 import json
@@ -247,27 +252,157 @@ def probe_pass(ctx, reg, kernel, steps):
     return ms, n, b
 
 
-def rccl_shard_pass(F, ctx, dist, ws, rank, src, tar, leaf, T_ref, steps):
-    """SURVEY.md §8(e) row K5, informational: every rank registers the SAME pair with
-    the correspondence search sharded over an RCCL group (source-pair blocks, rank-
-    ordered candidate gather over xGMI); the result must equal the unsharded T.  The
-    group's id travels over the gloo process group."""
-    ids = [F.group_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(ids, src=0)
-    g = F.Group(ctx, ids[0], ws, rank)
+SHARDED_PLAN = (("c4", 4), ("c5", 8))  # BASELINE configs[3]/[4]: the pair and its rank count (capped at N)
+
+
+def _wait_file(path, timeout_s):
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError(f"{path} did not appear within {timeout_s} s")
+        time.sleep(0.002)
+
+
+def sharded_child(args):
+    """One rank of the strong-scaling leg (a child process of bench rank `child_rank`,
+    so a collective that never completes cannot hang the bench: the parent kills it at
+    its time limit).  For each BASELINE multi-GPU config (c4 over min(N, 4) ranks, c5
+    over N): the pair is registered collectively by an RCCL group of the ranks
+    (fccf_group_create; rows K5, F and D of SURVEY.md §8(e) sharded, FCCF.cpp:1410-1428,
+    :785-839, :1668-1678), device-resident inputs, timed as one pipelined batch of
+    `steps` registrations and as single registrations; the group's T must equal this
+    GPU's unsharded T bit for bit.  Rank 0 first times the unsharded pipelined batch on
+    its own GPU (the one-GPU figure the speed-up is taken against).  Results go to
+    <dir>/res_<cfg>_<rank>.json; the group id travels through <dir>/id_<cfg>."""
+    d, rank, world = args.sharded_child, args.child_rank, args.child_world
+    steps = args.steps
+    for cfg_name, cap in SHARDED_PLAN:
+        ranks = min(world, cap)
+        if rank >= ranks:
+            continue
+        res = {"ranks": ranks}
+        outp = os.path.join(d, f"res_{cfg_name}_{rank}.json")
+        try:
+            if args.selftest:  # CPU stub (tests/test_dist.py): the merge logic only, no numbers
+                time.sleep(0.01)
+                res.update({"one_gpu_ms_per_registration": 2.0 if rank == 0 else None, "elapsed_s": 0.001 * steps,
+                            "e2e_s": [0.002] * min(steps, 10), "parity": "selftest-stub",
+                            "sharded": ["fine", "search", "sort"], "K": 100, "device_ms": {}})
+                raise StopIteration
+            import fccf_amd as F
+            cfg = F.CONFIGS[cfg_name]
+            src, tar, _ = F.synth_pair(cfg["n"], cfg["room"])
+            leaf = cfg["leaf"]
+            with F.Ctx(args.device) as ctx:
+                ds, dt = ctx.upload(src), ctx.upload(tar)
+                pair = ((ds, src.shape[0]), (dt, tar.shape[0]))
+                T0, _ = ctx.register_device(ds, src.shape[0], dt, tar.shape[0], leaf)  # unsharded reference
+                if rank == 0:
+                    ctx.register_batch([pair] * 2, leaf, on_device=True)  # warm
+                    a = time.perf_counter()
+                    ctx.register_batch([pair] * steps, leaf, on_device=True)
+                    res["one_gpu_ms_per_registration"] = (time.perf_counter() - a) / steps * 1e3
+                    uid = F.group_unique_id()
+                    with open(os.path.join(d, f"id_{cfg_name}.tmp"), "wb") as f:
+                        f.write(uid)
+                    os.replace(os.path.join(d, f"id_{cfg_name}.tmp"), os.path.join(d, f"id_{cfg_name}"))
+                else:
+                    _wait_file(os.path.join(d, f"id_{cfg_name}"), 120)
+                    uid = open(os.path.join(d, f"id_{cfg_name}"), "rb").read()
+                g = F.Group(ctx, uid, ranks, rank)
+                try:
+                    ctx.register_batch([pair] * 2, leaf, on_device=True)  # warm (graphs, communicator buffers)
+                    # file barrier, then one collective registration: the ranks start in step
+                    open(os.path.join(d, f"ready_{cfg_name}_{rank}"), "w").close()
+                    for r in range(ranks):
+                        _wait_file(os.path.join(d, f"ready_{cfg_name}_{r}"), 120)
+                    ctx.register_device(ds, src.shape[0], dt, tar.shape[0], leaf)
+                    a = time.perf_counter()
+                    Tb, sb = ctx.register_batch([pair] * steps, leaf, on_device=True)
+                    res["elapsed_s"] = time.perf_counter() - a
+                    per = []
+                    for _ in range(min(steps, 10)):
+                        a = time.perf_counter()
+                        T1, s1 = ctx.register_device(ds, src.shape[0], dt, tar.shape[0], leaf)
+                        per.append(time.perf_counter() - a)
+                    res["e2e_s"] = per
+                finally:
+                    g.close()
+                ctx.free(ds)
+                ctx.free(dt)
+            same = all(same_bits(T, T0) for T in list(Tb) + [T1])
+            res.update({"parity": "bit-exact vs this GPU's unsharded T" if same else "MISMATCH",
+                        "sharded": s1.as_dict()["sharded"], "K": int(s1.K),
+                        "device_ms": {k: round(v, 4) for k, v in s1.as_dict()["dev_ms"].items()}})
+        except StopIteration:
+            pass
+        except Exception as e:  # noqa: BLE001 (reported in the JSON line, never hidden)
+            res["error"] = f"{type(e).__name__}: {e}"
+        with open(outp + ".tmp", "w") as f:
+            json.dump(res, f)
+        os.replace(outp + ".tmp", outp)
+
+
+def sharded_pass(dist, ws, rank, local, args, timeout_s):
+    """Strong scaling of ONE registration (BASELINE configs[3]/[4]), run after the
+    replica leg: every rank starts a child process (sharded_child) on its GPU and waits
+    for it at most timeout_s; rank 0 merges the children's results.  Returns
+    {cfg: {...}} on rank 0 (None elsewhere)."""
+    import shutil
+    import subprocess
+    import tempfile
+    d = [tempfile.mkdtemp(prefix="fccf_shard_") if rank == 0 else None]
+    dist.broadcast_object_list(d, src=0)
+    d = d[0]
+    cmd = [sys.executable, os.path.abspath(__file__), "--sharded-child", d, "--child-rank", str(rank),
+           "--child-world", str(ws), "--device", str(local), "--steps", str(args.steps)] + \
+        (["--selftest"] if args.selftest else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                           "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    status = "ok"
     try:
-        ctx.register(src, tar, leaf)  # warm (graphs, communicator buffers)
-        barrier(dist)
-        a = time.perf_counter()
-        for _ in range(steps):
-            T, st = ctx.register(src, tar, leaf)
-        dt = allmax(dist, time.perf_counter() - a)
-    finally:
-        g.close()
-    assert np.array_equal(T.view(np.uint32), np.asarray(T_ref).view(np.uint32)), "sharded result differs"
-    return {"ranks": ws, "ms_per_registration": dt / steps * 1e3, "K": int(st.K), "K_pass": int(st.K_pass),
-            "note": "one pair registered collectively by all ranks (strong scaling of the search); "
-                    "host-array inputs; bit-identical to the unsharded T"}
+        rc = p.wait(timeout=timeout_s)
+        if rc != 0:
+            status = f"child exit {rc}"
+    except subprocess.TimeoutExpired:
+        status = f"child killed at its {timeout_s} s limit"
+        import signal
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.wait()
+    stats = [None] * ws
+    dist.all_gather_object(stats, status)
+    out = None
+    if rank == 0:
+        out = {}
+        for cfg_name, cap in SHARDED_PLAN:
+            ranks = min(ws, cap)
+            rs = []
+            for r in range(ranks):
+                f = os.path.join(d, f"res_{cfg_name}_{r}.json")
+                rs.append(json.load(open(f)) if os.path.exists(f) else {"error": f"rank {r}: {stats[r]}"})
+            errs = [x["error"] for x in rs if "error" in x]
+            if errs:
+                out[cfg_name] = {"ranks": ranks, "error": errs[0]}
+                continue
+            el = max(x["elapsed_s"] for x in rs)
+            e2e = [max(v) for v in zip(*[x["e2e_s"] for x in rs])]
+            one = rs[0].get("one_gpu_ms_per_registration")
+            ms = el / args.steps * 1e3
+            out[cfg_name] = {"ranks": ranks, "ms_per_registration": ms,
+                             "e2e_ms_median": statistics.median(e2e) * 1e3,
+                             "one_gpu_ms_per_registration": one,
+                             "speedup_vs_one_gpu": one / ms if one else None,
+                             "correspondences_per_s": rs[0]["K"] / (ms * 1e-3),
+                             "sharded_stages": rs[0]["sharded"],
+                             "parity": rs[0]["parity"] if all(x["parity"] == rs[0]["parity"] for x in rs)
+                             else "MISMATCH between ranks",
+                             "device_ms_rank0": rs[0]["device_ms"]}
+        shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 def ingest_pass(F, ctx, src, tar, leaf, T_ref, reps=3):
@@ -318,9 +453,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--selftest", action="store_true", help="CPU stub registration (tests only)")
     ap.add_argument("--probe-kernel", default="auto", help="kernel for the roofline object (auto = dominant)")
-    ap.add_argument("--rccl-shard", action="store_true",
-                    help="N>1, informational: also time registrations of ONE pair by all ranks with the "
-                         "correspondence search sharded over an RCCL group (fccf_group_create)")
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="N>1: skip the strong-scaling leg (one c4 / c5 registration by an RCCL group of ranks)")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0, help="time limit of a strong-scaling child")
+    ap.add_argument("--sharded-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-rank", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--child-world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--parity-configs", default=None,
                     help="comma-separated BASELINE configs checked bit for bit against the oracle after the "
                          "timed region (default c2,c4,c5 at N=1, none at N>1; the bench's own config is always "
@@ -328,12 +467,17 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="time K sequential fccf_register_device calls instead of one pipelined batch of K")
     args = ap.parse_args()
+    if args.sharded_child:
+        sharded_child(args)
+        return
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     rank, ws, local, dist = dist_setup(args.gpus)
+    if os.environ.get("FCCF_BENCH_ONE_DEVICE") == "1":
+        local = 0  # dev: every rank on device 0 (rehearsal of the N > 1 plumbing on a one-GPU box)
     if ws > 1 and "FCCF_HOST_THREADS" not in os.environ:
         # each rank's host stages get an equal share of this node's cores (<= 16 each),
         # so N ranks' worker pools do not oversubscribe the host
@@ -423,8 +567,8 @@ def main():
     if not args.selftest:
         assert np.array_equal(T2.view(np.uint32), np.asarray(T).view(np.uint32)), "host-input result differs"
     ingest = None if args.selftest or rank != 0 else ingest_pass(F, ctx, src, tar, leaf, T)
-    sharded = rccl_shard_pass(F, ctx, dist, ws, rank, src, tar, leaf, T, args.steps) \
-        if args.rccl_shard and ws > 1 and not args.selftest else None
+    sharded = sharded_pass(dist, ws, rank, local, args, args.sharded_timeout) \
+        if ws > 1 and not args.no_sharded else None
     roofline = None
     if probe:
         # Probe window right after the timed region, same inputs: every launch of
@@ -486,7 +630,8 @@ def main():
         if ingest is not None:
             out["ingest"] = ingest
         if sharded is not None:
-            out["rccl_sharded_search"] = sharded
+            # strong scaling: ONE registration of each multi-GPU BASELINE pair by all ranks
+            out["sharded"] = sharded
         if roofline is not None:
             roofline["stage"] = stage_rl
             out["roofline"] = roofline

@@ -22,6 +22,10 @@ def test_bench_two_ranks_gloo(tmp_path):
     # value = K summed over both ranks / the slowest rank's wall time
     assert abs(d["value"] - 2 * 5 * 100 / (d["ms_per_step"] * 5 / 1e3)) / d["value"] < 1e-6
     assert d["data"] == "selftest-stub" and "cpu_baseline" not in d
+    # the strong-scaling leg: one child process per rank, results merged by rank 0
+    sh = d["sharded"]
+    assert set(sh) == {"c4", "c5"} and sh["c4"]["ranks"] == 2 and sh["c5"]["ranks"] == 2, sh
+    assert sh["c5"]["ms_per_registration"] == 5 * 0.001 / 5 * 1e3 and sh["c5"]["speedup_vs_one_gpu"] == 2.0
 
 
 def test_bench_gpus2_self_launch(tmp_path):
