@@ -265,7 +265,7 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     HIP_CHECK(hipEventCreate(&e1.e));
     hipEvent_t ev0 = e0.e, ev1 = e1.e;
     HIP_CHECK(hipEventRecord(ev0, st));
-    introsort_u32(b.k0, b.v0, b.k1, b.v1, B2<const uint32_t*>(d_sc), B2<const VGParams*>(b.params), cap, b.is, st, 1,
+    introsort_u32(b.k0, b.v0, b.k1, b.v1, B4<const uint32_t*>(d_sc), B4<const VGParams*>(b.params), cap, b.is, st, 1,
                   exact_gate != 0);
     HIP_CHECK(hipEventRecord(ev1, st));
     if (tpath) {
@@ -308,6 +308,8 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     }
     if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
+    static_assert(sizeof c->sort_rounds == sizeof(IsRound) * IS_RMAX, "sort_rounds size");
+    HIP_CHECK(hipMemcpyAsync(c->sort_rounds, b.is.rounds, sizeof c->sort_rounds, hipMemcpyDeviceToHost, st));
     {
       float ms = 0.f;
       HIP_CHECK(hipEventSynchronize(ev1));
@@ -404,6 +406,12 @@ extern "C" int fccf_debug_sort_stats(fccf_ctx* c, uint32_t out[32]) {
   return FCCF_OK;
 }
 
+extern "C" int fccf_debug_sort_rounds(fccf_ctx* c, uint32_t out[96]) {
+  if (!c || !out) return FCCF_E_ARG;
+  std::memcpy(out, c->sort_rounds, sizeof c->sort_rounds);
+  return FCCF_OK;
+}
+
 extern "C" int fccf_stage_downsample_presorted(fccf_ctx* c, const float* xyz, int64_t n, float leaf, float* out,
                                                int64_t* m) {
   return stage_downsample(c, xyz, n, leaf, out, m, true);
@@ -480,11 +488,11 @@ extern "C" int fccf_stage_voxel_planes(fccf_ctx* c, const float* xyz, int64_t n,
     if (n) HIP_CHECK(hipMemcpyAsync(d_in, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(d_n, &hn, 4, hipMemcpyHostToDevice, st));
     exact_sum(d_in, 3, 3, nullptr, d_n, 1, d_cen, true, xs, st);  // compute3DCentroid (:473)
-    face_voxels_prepare(B2<const float*>(d_in), B2<const uint32_t*>(d_n), cap, (double)P.face_voxel_size,
-                        B2<FaceBufs>(fb), st, 1);
-    face_voxels_fit(B2<const uint32_t*>(d_n), cap, P.voxel_point_threshold, P.curvature_threshold, B2<float*>(d_res),
-                    B2<FaceBufs>(fb), st, 1);
-    face_voxels_orient(cap, B2<VoxRec*>(d_pl), B2<FaceBufs>(fb), st, 1);
+    face_voxels_prepare(B4<const float*>(d_in), B4<const uint32_t*>(d_n), cap, (double)P.face_voxel_size,
+                        B4<FaceBufs>(fb), st, 1);
+    face_voxels_fit(B4<const uint32_t*>(d_n), cap, P.voxel_point_threshold, P.curvature_threshold, B4<float*>(d_res),
+                    B4<FaceBufs>(fb), st, 1);
+    face_voxels_orient(cap, B4<VoxRec*>(d_pl), B4<FaceBufs>(fb), st, 1);
     HIP_CHECK(hipGetLastError());
     uint32_t sc[4] = {0, 0, 0, 0};
     float cen[3] = {0.f, 0.f, 0.f};

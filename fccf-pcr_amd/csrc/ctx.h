@@ -216,12 +216,15 @@ struct CachedGraph {
 
 struct fccf_ctx {
   int device = 0;
-  // The cloud device stage (both VoxelGrid passes, centroid, face voxels), double-
-  // buffered so a batch can run pair i+1's clouds while pair i's later stages run.
-  // Two sets never run their cloud stages at the same time, so they share streams:
-  // sa[0] the batched cloud stage, sa[2] the centroid sums, sa[1] fine
-  // verification, and sb for matching and everything else -- within the four
-  // hardware queues a process gets.
+  // Pair slots.  A cloud stage (both VoxelGrid passes, centroid, face voxels) runs the
+  // clouds of one or two pairs in the same launches (a pipelined batch pairs them up:
+  // the sort's dependent rounds are paid once for four clouds); stage group G uses
+  // slots 2G and 2G + 1, and the group's shared resources (arena of its clouds, stage
+  // graph, fork/join events) live in slot 2G.  Two groups double-buffer, so a batch can
+  // run the next group's clouds while this group's later stages run.  Two groups never
+  // run their cloud stages at the same time, so they share streams: sa[0] the batched
+  // cloud stage, sa[2] the centroid sums, sa[1] fine verification, and sb for matching
+  // and everything else -- within the four hardware queues a process gets.
   struct CloudSet {
     fccf::Arena arena;
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
@@ -232,12 +235,13 @@ struct fccf_ctx {
                                      // fork/join inside the one-graph cloud stage (capture-internal)
     hipEvent_t tev[6] = {};          // timing: [4] fine start, [5] fine done (fccf_stats::dev_ms[3]);
                                      // the cloud stage's spans are device stamps (CloudMail::stamp)
-    fccf::CachedGraph g_seg[1];      // the cloud stage of both clouds (VoxelGrid passes, centroids, faces)
+    fccf::CachedGraph g_seg[2];      // slot 2G: the group's cloud stage of one / two pairs (VoxelGrid passes,
+                                     // centroids, faces), one graph per pair count
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
-  } cs[2];
+  } cs[4];
   hipStream_t sa[3] = {};            // cloud stage streams (sa[1]: fine verification)
   hipStream_t sb = nullptr;          // matching, copies, stage exports
   fccf::Arena arena2;  // matching (and the stage exports)
@@ -254,6 +258,7 @@ struct fccf_ctx {
   bool cluster_device = false;  // transform_cluster's seeds, sort and averaging on the GPU (cluster.hip)
   fccf::Arena arena_v;       // device quick_verify batch (candidates in, refined T / scores out)
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
+  uint32_t sort_rounds[4 * 24] = {};  // IsBufs::rounds (IS_RMAX records) of the last fccf_debug_sort_keys
   uint32_t* d_flags = nullptr;   // device words (zeroed at creation): [0] injected K1 sort faults (test hook)
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;

@@ -33,22 +33,26 @@ size_t sort_scratch_bytes(uint32_t cap);
 SortScratch sort_scratch_carve(void* base, uint32_t cap);
 
 // Per-problem arguments of a batched launch: problem e = blockIdx.y uses v[e].
-// The primitives below run `nbatch` (1 or 2) independent problems -- the two
-// clouds of a registration -- in the same launches (a kernel boundary costs
-// ~1.7 us on gfx950 and two streams of dependent kernels interfere, so one
-// stream of batched launches is the fast shape).  A single value converts to a
-// batch of one.
+// The primitives below run `nbatch` (1 to 4) independent problems -- the clouds of
+// one registration, or of two registrations that a pipelined batch runs together --
+// in the same launches (a kernel boundary costs ~1.7 us on gfx950 and two streams of
+// dependent kernels interfere, so one stream of batched launches is the fast shape).
+// A single value converts to a batch of one.
+constexpr int BMAX = 4;
 template <class T>
-struct B2 {
-  T v[2];
-  B2() = default;
-  __host__ __device__ B2(T a) : v{a, a} {}
-  __host__ __device__ B2(T a, T b) : v{a, b} {}
+struct B4 {
+  T v[BMAX];
+  B4() = default;
+  __host__ __device__ B4(T a) : v{a, a, a, a} {}
+  __host__ __device__ B4(T a, T b) : v{a, b, b, b} {}
+  __host__ __device__ B4(T a, T b, T c, T d) : v{a, b, c, d} {}
   template <class U>
-  __host__ __device__ B2(const B2<U>& o) : v{o.v[0], o.v[1]} {}
+  __host__ __device__ B4(const B4<U>& o) : v{o.v[0], o.v[1], o.v[2], o.v[3]} {}
   // a select, not an index: a dynamically indexed by-value kernel argument is copied
   // to a per-thread private array (measured: 3x the runtime of a 12 MB pass)
-  __host__ __device__ T operator[](int i) const { return i ? v[1] : v[0]; }
+  __host__ __device__ __forceinline__ T operator[](int i) const {
+    return (i & 2) ? ((i & 1) ? v[3] : v[2]) : ((i & 1) ? v[1] : v[0]);
+  }
 };
 
 // Stable LSD radix sort of (key, val) by the low *d_nbits bits of key (8-bit
@@ -60,28 +64,28 @@ struct B2 {
 // once); the bits they leave run in one single-workgroup tail launch (k_rs_tail),
 // which also exits at once unless needed.  tail_need (optional): the tail runs only
 // where *tail_need != 0 (fast_bits == 0: a sort of keys usually already in order).
-void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr));
+void radix_sort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                    uint32_t cap, B4<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B4<SortScratch> s,
+                    hipStream_t st, int nbatch = 1, B4<const uint32_t*> tail_need = B4<const uint32_t*>(nullptr));
 // (k2, v2) optional: a third buffer, so a sort of three active passes ends in (k0, v0)
 // without a copy-back.
-void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch = 1, B2<const uint32_t*> tail_need = B2<const uint32_t*>(nullptr),
-                    B2<uint64_t*> k2 = B2<uint64_t*>(nullptr), B2<uint32_t*> v2 = B2<uint32_t*>(nullptr));
+void radix_sort_u64(B4<uint64_t*> k0, B4<uint32_t*> v0, B4<uint64_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                    uint32_t cap, B4<const uint32_t*> d_nbits, int fast_bits, bool vals_iota, B4<SortScratch> s,
+                    hipStream_t st, int nbatch = 1, B4<const uint32_t*> tail_need = B4<const uint32_t*>(nullptr),
+                    B4<uint64_t*> k2 = B4<uint64_t*>(nullptr), B4<uint32_t*> v2 = B4<uint32_t*>(nullptr));
 
 // Run-length segmentation of sorted keys[0..*d_n): starts[s] = first index of
 // segment s, starts[S] = *d_n, *d_nseg = S.  Keys equal to `invalid` (which sort
 // last) are excluded: the valid prefix ends at the first invalid key.
 // seg_of (optional): segment index of every valid element.
 // run (optional): skip problems whose *run == 0 (their outputs are left untouched).
-void segment_heads_u32(B2<const uint32_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
-                       B2<uint32_t*> starts, B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
-                       B2<uint32_t*> seg_of = B2<uint32_t*>(nullptr), int nbatch = 1,
-                       B2<const uint32_t*> run = B2<const uint32_t*>(nullptr));
-void segment_heads_u64(B2<const uint64_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, B2<uint32_t*> starts,
-                       B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
-                       B2<uint32_t*> seg_of = B2<uint32_t*>(nullptr), int nbatch = 1);
+void segment_heads_u32(B4<const uint32_t*> keys, B4<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
+                       B4<uint32_t*> starts, B4<uint32_t*> d_nseg, B4<SortScratch> s, hipStream_t st,
+                       B4<uint32_t*> seg_of = B4<uint32_t*>(nullptr), int nbatch = 1,
+                       B4<const uint32_t*> run = B4<const uint32_t*>(nullptr));
+void segment_heads_u64(B4<const uint64_t*> keys, B4<const uint32_t*> d_n, uint32_t cap, B4<uint32_t*> starts,
+                       B4<uint32_t*> d_nseg, B4<SortScratch> s, hipStream_t st,
+                       B4<uint32_t*> seg_of = B4<uint32_t*>(nullptr), int nbatch = 1);
 
 // Sequential float sums in the reference's left-to-right order, s = ((0 + v0) + v1) + ...
 // bit-exact, computed in parallel (exactsum.h).  Problem b sums elements
@@ -98,14 +102,17 @@ void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint3
 // out[0..K) and out[K..2K).  Scratch: rows = 2*K, cap = max of both counts.
 void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32_t* nb, int S, int K, float* out,
                 bool divide, XsBufs x, hipStream_t st);
+// The same for nprob (1 to 4) separate arrays data[b] with counts *cnt[b]; out = nprob * K values.
+void exact_sum_n(const float* const* data, const uint32_t* const* cnt, int nprob, int S, int K, float* out, bool divide,
+                 XsBufs x, hipStream_t st);
 
 // Exclusive scan of u32 values in[0..*d_n) -> out, *d_total = sum.
-void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
-                        B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch = 1);
+void exclusive_scan_u32(B4<const uint32_t*> in, B4<uint32_t*> out, B4<const uint32_t*> d_n, uint32_t cap,
+                        B4<uint32_t*> d_total, B4<SortScratch> s, hipStream_t st, int nbatch = 1);
 // Two such scans of the same length in the same two launches (the second's tile
 // totals use the scratch's radix histogram words, unused outside a sort).
-void exclusive_scan2_u32(B2<const uint32_t*> in_a, B2<uint32_t*> out_a, B2<uint32_t*> total_a,
-                         B2<const uint32_t*> in_b, B2<uint32_t*> out_b, B2<uint32_t*> total_b,
-                         B2<const uint32_t*> d_n, uint32_t cap, B2<SortScratch> s, hipStream_t st, int nbatch = 1);
+void exclusive_scan2_u32(B4<const uint32_t*> in_a, B4<uint32_t*> out_a, B4<uint32_t*> total_a,
+                         B4<const uint32_t*> in_b, B4<uint32_t*> out_b, B4<uint32_t*> total_b,
+                         B4<const uint32_t*> d_n, uint32_t cap, B4<SortScratch> s, hipStream_t st, int nbatch = 1);
 
 }  // namespace fccf

@@ -120,18 +120,23 @@ struct RsRing {
   K* k[3];
   uint32_t* v[3];
 };
-// buffer i of problem e, by selects only (no struct or array copy of the argument)
+// buffer i of problem e, by selects only (no struct or array copy of the argument:
+// no reference to a part of it either, which would make the compiler store it to scratch)
 template <class K>
-__device__ __forceinline__ K* ring_key(const B2<RsRing<K>>& R2, int e, int i) {
+__device__ __forceinline__ K* ring_key(const B4<RsRing<K>>& R2, int e, int i) {
   K* a = i == 0 ? R2.v[0].k[0] : (i == 1 ? R2.v[0].k[1] : R2.v[0].k[2]);
   K* b = i == 0 ? R2.v[1].k[0] : (i == 1 ? R2.v[1].k[1] : R2.v[1].k[2]);
-  return e ? b : a;
+  K* c = i == 0 ? R2.v[2].k[0] : (i == 1 ? R2.v[2].k[1] : R2.v[2].k[2]);
+  K* d = i == 0 ? R2.v[3].k[0] : (i == 1 ? R2.v[3].k[1] : R2.v[3].k[2]);
+  return (e & 2) ? ((e & 1) ? d : c) : ((e & 1) ? b : a);
 }
 template <class K>
-__device__ __forceinline__ uint32_t* ring_val(const B2<RsRing<K>>& R2, int e, int i) {
+__device__ __forceinline__ uint32_t* ring_val(const B4<RsRing<K>>& R2, int e, int i) {
   uint32_t* a = i == 0 ? R2.v[0].v[0] : (i == 1 ? R2.v[0].v[1] : R2.v[0].v[2]);
   uint32_t* b = i == 0 ? R2.v[1].v[0] : (i == 1 ? R2.v[1].v[1] : R2.v[1].v[2]);
-  return e ? b : a;
+  uint32_t* c = i == 0 ? R2.v[2].v[0] : (i == 1 ? R2.v[2].v[1] : R2.v[2].v[2]);
+  uint32_t* d = i == 0 ? R2.v[3].v[0] : (i == 1 ? R2.v[3].v[1] : R2.v[3].v[2]);
+  return (e & 2) ? ((e & 1) ? d : c) : ((e & 1) ? b : a);
 }
 __device__ __forceinline__ uint32_t rs_active(uint32_t nbits, int fast_passes) {
   return min(rs_plan(nbits).passes, (uint32_t)fast_passes);
@@ -144,8 +149,8 @@ __device__ __forceinline__ int rs_dst(int p, uint32_t P, bool three) {
 }
 
 template <class K>
-__global__ void __launch_bounds__(ST) k_rs_hist(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2,
-                                                B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
+__global__ void __launch_bounds__(ST) k_rs_hist(B4<RsRing<K>> R2, B4<const uint32_t*> d_n2,
+                                                B4<const uint32_t*> d_nbits2, int pass, B4<SortScratch> ss,
                                                 uint32_t nblocks, int fast_passes) {
   KT();
   const int e = blockIdx.y;
@@ -185,7 +190,7 @@ __global__ void __launch_bounds__(ST) k_rs_hist(B2<RsRing<K>> R2, B2<const uint3
 }
 
 // One block per digit: exclusive scan of that digit's per-block counts in place.
-__global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t nblocks, B2<const uint32_t*> d_nbits2,
+__global__ void __launch_bounds__(T) k_rs_rowscan(B4<SortScratch> ss, uint32_t nblocks, B4<const uint32_t*> d_nbits2,
                                                   int pass) {
   KT();
   const int e = blockIdx.y;
@@ -211,8 +216,8 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(B2<SortScratch> ss, uint32_t n
 // writes each digit run to its global slot with consecutive lanes on consecutive
 // addresses.  *active (probe, may be null) is cleared when the pass is skipped.
 template <class K>
-__global__ void __launch_bounds__(ST) k_rs_scatter(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2,
-                                                   B2<const uint32_t*> d_nbits2, int pass, B2<SortScratch> ss,
+__global__ void __launch_bounds__(ST) k_rs_scatter(B4<RsRing<K>> R2, B4<const uint32_t*> d_n2,
+                                                   B4<const uint32_t*> d_nbits2, int pass, B4<SortScratch> ss,
                                                    uint32_t nblocks, int iota, uint32_t* __restrict__ active,
                                                    int fast_passes) {
   KT();
@@ -228,8 +233,13 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<RsRing<K>> R2, B2<const ui
   const uint32_t* __restrict__ tot = ss[e].tot;
   const RsPlan pl = rs_plan(*d_nbits2[e]);
   const bool run = (uint32_t)pass < pl.passes;
-  if (active && e == 0 && blockIdx.x == 0 && threadIdx.x == 0)  // probe: any problem of the batch active
-    *active = (run || (gridDim.y > 1 && (uint32_t)pass < rs_plan(*d_nbits2[1]).passes)) ? 1u : 0u;
+  if (active && e == 0 && blockIdx.x == 0 && threadIdx.x == 0) {  // probe: any problem of the batch active
+    bool any = run;
+#pragma unroll
+    for (int q = 1; q < BMAX; ++q)  // (constant indices: a dynamic one would copy the argument to scratch)
+      if (q < (int)gridDim.y) any = any || (uint32_t)pass < rs_plan(*d_nbits2.v[q]).passes;
+    *active = any ? 1u : 0u;
+  }
   const uint32_t n = *d_n2[e];
   const uint32_t tile0 = blockIdx.x * SORT_TILE;
   if (!run || tile0 >= n) return;  // grids are sized for the capacity; tiles past n are empty
@@ -319,9 +329,9 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B2<RsRing<K>> R2, B2<const ui
 // Slow (one CU) but a single launch that exits at once in the common case, where
 // the launches of never-needed fast passes would each cost a kernel boundary.
 template <class K>
-__global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B2<K*> k12, B2<uint32_t*> v12,
-                                                B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2,
-                                                int fast_passes, B2<const uint32_t*> need2) {
+__global__ void __launch_bounds__(ST) k_rs_tail(B4<K*> k02, B4<uint32_t*> v02, B4<K*> k12, B4<uint32_t*> v12,
+                                                B4<const uint32_t*> d_n2, B4<const uint32_t*> d_nbits2,
+                                                int fast_passes, B4<const uint32_t*> need2) {
   KT();
   const int e = blockIdx.y;
   const uint32_t nbits = *d_nbits2[e], n = *d_n2[e];
@@ -441,7 +451,7 @@ __global__ void __launch_bounds__(ST) k_rs_tail(B2<K*> k02, B2<uint32_t*> v02, B
 }
 
 template <class K>
-__global__ void k_rs_copyback(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2, B2<const uint32_t*> d_nbits2,
+__global__ void k_rs_copyback(B4<RsRing<K>> R2, B4<const uint32_t*> d_n2, B4<const uint32_t*> d_nbits2,
                               int max_passes) {
   KT();
   const int e = blockIdx.y;
@@ -459,18 +469,18 @@ __global__ void k_rs_copyback(B2<RsRing<K>> R2, B2<const uint32_t*> d_n2, B2<con
 }
 
 template <class K>
-void radix_sort(B2<K*> k0, B2<uint32_t*> v0, B2<K*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n, uint32_t cap,
-                B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s, hipStream_t st,
-                int nbatch, B2<const uint32_t*> tail_need, B2<K*> k2, B2<uint32_t*> v2) {
+void radix_sort(B4<K*> k0, B4<uint32_t*> v0, B4<K*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n, uint32_t cap,
+                B4<const uint32_t*> d_nbits, int fast_bits, bool iota, B4<SortScratch> s, hipStream_t st,
+                int nbatch, B4<const uint32_t*> tail_need, B4<K*> k2, B4<uint32_t*> v2) {
   const uint32_t nb = sort_blocks(cap);
   if (nb == 0) return;
   if (fast_bits == 0 && iota) throw Error(FCCF_E_INTERNAL, "radix_sort: a tail-only sort takes its values as input");
   if ((v0[0] == nullptr) != (v1[0] == nullptr)) throw Error(FCCF_E_INTERNAL, "radix_sort: both or no value buffers");
-  if ((k2[0] == nullptr) != (k2[nbatch > 1 ? 1 : 0] == nullptr) || (k2[0] && (v2[0] == nullptr) != (v0[0] == nullptr)))
+  if ((k2[0] == nullptr) != (k2[nbatch - 1] == nullptr) || (k2[0] && (v2[0] == nullptr) != (v0[0] == nullptr)))
     throw Error(FCCF_E_INTERNAL, "radix_sort: third buffer on every problem, values with values");
   const int fast_passes = fast_bits / 8;
-  B2<RsRing<K>> R;
-  for (int e = 0; e < 2; ++e) R.v[e] = RsRing<K>{{k0[e], k1[e], k2[e]}, {v0[e], v1[e], v2[e]}};  // host side
+  B4<RsRing<K>> R;
+  for (int e = 0; e < BMAX; ++e) R.v[e] = RsRing<K>{{k0[e], k1[e], k2[e]}, {v0[e], v1[e], v2[e]}};  // host side
   for (int p = 0; p < fast_passes; ++p) {  // pass p: digit p of the device-side plan (rs_plan)
     k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(R, d_n, d_nbits, p, s, nb, fast_passes);
     k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
@@ -524,8 +534,8 @@ __device__ __forceinline__ uint32_t tiles_before(const uint32_t* __restrict__ bl
 __device__ __forceinline__ bool owns_last(uint32_t n) { return blockIdx.x == (n ? (n - 1u) / RS_TILE : 0u); }
 
 template <class K, bool HasInvalid>
-__global__ void __launch_bounds__(T) k_seg_count(B2<const K*> keys2, B2<const uint32_t*> d_n2, K invalid,
-                                                 B2<SortScratch> ss, B2<const uint32_t*> run2) {
+__global__ void __launch_bounds__(T) k_seg_count(B4<const K*> keys2, B4<const uint32_t*> d_n2, K invalid,
+                                                 B4<SortScratch> ss, B4<const uint32_t*> run2) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
@@ -544,9 +554,9 @@ __global__ void __launch_bounds__(T) k_seg_count(B2<const K*> keys2, B2<const ui
 }
 
 template <class K, bool HasInvalid>
-__global__ void __launch_bounds__(T) k_seg_write(B2<const K*> keys2, B2<const uint32_t*> d_n2, K invalid,
-                                                 B2<SortScratch> ss, B2<uint32_t*> starts2, B2<uint32_t*> d_nseg2,
-                                                 B2<uint32_t*> seg_of2, B2<const uint32_t*> run2) {
+__global__ void __launch_bounds__(T) k_seg_write(B4<const K*> keys2, B4<const uint32_t*> d_n2, K invalid,
+                                                 B4<SortScratch> ss, B4<uint32_t*> starts2, B4<uint32_t*> d_nseg2,
+                                                 B4<uint32_t*> seg_of2, B4<const uint32_t*> run2) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
@@ -584,9 +594,9 @@ __global__ void __launch_bounds__(T) k_seg_write(B2<const K*> keys2, B2<const ui
 }
 
 template <class K, bool HasInvalid>
-void segment_heads(B2<const K*> keys, B2<const uint32_t*> d_n, uint32_t cap, K invalid, B2<uint32_t*> starts,
-                   B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st, B2<uint32_t*> seg_of, int nbatch,
-                   B2<const uint32_t*> run) {
+void segment_heads(B4<const K*> keys, B4<const uint32_t*> d_n, uint32_t cap, K invalid, B4<uint32_t*> starts,
+                   B4<uint32_t*> d_nseg, B4<SortScratch> s, hipStream_t st, B4<uint32_t*> seg_of, int nbatch,
+                   B4<const uint32_t*> run) {
   const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
   k_seg_count<K, HasInvalid><<<dim3(nb, nbatch), T, 0, st>>>(keys, d_n, invalid, s, run);
   k_seg_write<K, HasInvalid><<<dim3(nb, nbatch), T, 0, st>>>(keys, d_n, invalid, s, starts, d_nseg, seg_of, run);
@@ -596,8 +606,8 @@ void segment_heads(B2<const K*> keys, B2<const uint32_t*> d_n, uint32_t cap, K i
 // out2b with its tile totals in the scratch's hist words (free outside a radix sort).
 __device__ __forceinline__ uint32_t* scan_blk(const SortScratch& s) { return blockIdx.z ? s.hist : s.blk; }
 
-__global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<const uint32_t*> in2b,
-                                                 B2<const uint32_t*> d_n2, B2<SortScratch> ss) {
+__global__ void __launch_bounds__(T) k_sum_tiles(B4<const uint32_t*> in2, B4<const uint32_t*> in2b,
+                                                 B4<const uint32_t*> d_n2, B4<SortScratch> ss) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
@@ -615,10 +625,10 @@ __global__ void __launch_bounds__(T) k_sum_tiles(B2<const uint32_t*> in2, B2<con
   if (threadIdx.x == 0) scan_blk(ss[e])[blockIdx.x] = t;
 }
 
-__global__ void __launch_bounds__(T) k_scan_tiles(B2<const uint32_t*> in2, B2<uint32_t*> out2, B2<uint32_t*> d_total2,
-                                                  B2<const uint32_t*> in2b, B2<uint32_t*> out2b,
-                                                  B2<uint32_t*> d_total2b, B2<const uint32_t*> d_n2,
-                                                  B2<SortScratch> ss) {
+__global__ void __launch_bounds__(T) k_scan_tiles(B4<const uint32_t*> in2, B4<uint32_t*> out2, B4<uint32_t*> d_total2,
+                                                  B4<const uint32_t*> in2b, B4<uint32_t*> out2b,
+                                                  B4<uint32_t*> d_total2b, B4<const uint32_t*> d_n2,
+                                                  B4<SortScratch> ss) {
   KT();
   __shared__ uint32_t sh[4];
   const int e = blockIdx.y;
@@ -667,37 +677,37 @@ SortScratch sort_scratch_carve(void* base, uint32_t cap) {
   return s;
 }
 
-void radix_sort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need) {
+void radix_sort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                    uint32_t cap, B4<const uint32_t*> d_nbits, int fast_bits, bool iota, B4<SortScratch> s,
+                    hipStream_t st, int nbatch, B4<const uint32_t*> tail_need) {
   radix_sort<uint32_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need,
-                       B2<uint32_t*>(nullptr), B2<uint32_t*>(nullptr));
+                       B4<uint32_t*>(nullptr), B4<uint32_t*>(nullptr));
 }
-void radix_sort_u64(B2<uint64_t*> k0, B2<uint32_t*> v0, B2<uint64_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                    uint32_t cap, B2<const uint32_t*> d_nbits, int fast_bits, bool iota, B2<SortScratch> s,
-                    hipStream_t st, int nbatch, B2<const uint32_t*> tail_need, B2<uint64_t*> k2, B2<uint32_t*> v2) {
+void radix_sort_u64(B4<uint64_t*> k0, B4<uint32_t*> v0, B4<uint64_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                    uint32_t cap, B4<const uint32_t*> d_nbits, int fast_bits, bool iota, B4<SortScratch> s,
+                    hipStream_t st, int nbatch, B4<const uint32_t*> tail_need, B4<uint64_t*> k2, B4<uint32_t*> v2) {
   radix_sort<uint64_t>(k0, v0, k1, v1, d_n, cap, d_nbits, fast_bits, iota, s, st, nbatch, tail_need, k2, v2);
 }
-void segment_heads_u32(B2<const uint32_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
-                       B2<uint32_t*> starts, B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st,
-                       B2<uint32_t*> seg_of, int nbatch, B2<const uint32_t*> run) {
+void segment_heads_u32(B4<const uint32_t*> keys, B4<const uint32_t*> d_n, uint32_t cap, uint32_t invalid,
+                       B4<uint32_t*> starts, B4<uint32_t*> d_nseg, B4<SortScratch> s, hipStream_t st,
+                       B4<uint32_t*> seg_of, int nbatch, B4<const uint32_t*> run) {
   segment_heads<uint32_t, true>(keys, d_n, cap, invalid, starts, d_nseg, s, st, seg_of, nbatch, run);
 }
-void segment_heads_u64(B2<const uint64_t*> keys, B2<const uint32_t*> d_n, uint32_t cap, B2<uint32_t*> starts,
-                       B2<uint32_t*> d_nseg, B2<SortScratch> s, hipStream_t st, B2<uint32_t*> seg_of, int nbatch) {
+void segment_heads_u64(B4<const uint64_t*> keys, B4<const uint32_t*> d_n, uint32_t cap, B4<uint32_t*> starts,
+                       B4<uint32_t*> d_nseg, B4<SortScratch> s, hipStream_t st, B4<uint32_t*> seg_of, int nbatch) {
   segment_heads<uint64_t, true>(keys, d_n, cap, ~(uint64_t)0, starts, d_nseg, s, st, seg_of, nbatch,
-                                B2<const uint32_t*>(nullptr));
+                                B4<const uint32_t*>(nullptr));
 }
-void exclusive_scan_u32(B2<const uint32_t*> in, B2<uint32_t*> out, B2<const uint32_t*> d_n, uint32_t cap,
-                        B2<uint32_t*> d_total, B2<SortScratch> s, hipStream_t st, int nbatch) {
+void exclusive_scan_u32(B4<const uint32_t*> in, B4<uint32_t*> out, B4<const uint32_t*> d_n, uint32_t cap,
+                        B4<uint32_t*> d_total, B4<SortScratch> s, hipStream_t st, int nbatch) {
   const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
   k_sum_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, in, d_n, s);
   k_scan_tiles<<<dim3(nb, nbatch), T, 0, st>>>(in, out, d_total, in, out, d_total, d_n, s);
 }
 
-void exclusive_scan2_u32(B2<const uint32_t*> in_a, B2<uint32_t*> out_a, B2<uint32_t*> total_a,
-                         B2<const uint32_t*> in_b, B2<uint32_t*> out_b, B2<uint32_t*> total_b,
-                         B2<const uint32_t*> d_n, uint32_t cap, B2<SortScratch> s, hipStream_t st, int nbatch) {
+void exclusive_scan2_u32(B4<const uint32_t*> in_a, B4<uint32_t*> out_a, B4<uint32_t*> total_a,
+                         B4<const uint32_t*> in_b, B4<uint32_t*> out_b, B4<uint32_t*> total_b,
+                         B4<const uint32_t*> d_n, uint32_t cap, B4<SortScratch> s, hipStream_t st, int nbatch) {
   const uint32_t nb = rs_blocks(cap) ? rs_blocks(cap) : 1u;
   if ((size_t)nb > hist_words(cap)) throw Error(FCCF_E_INTERNAL, "exclusive_scan2_u32: scratch");
   k_sum_tiles<<<dim3(nb, nbatch, 2), T, 0, st>>>(in_a, in_b, d_n, s);

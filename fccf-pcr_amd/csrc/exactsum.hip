@@ -127,24 +127,30 @@ struct Prob {
 };
 
 // Where the problems live: either one array with per-problem offsets/counts
-// (off may be null), or (data2 != null) two separate arrays, problem 0 = data with
-// count *cnt and problem 1 = data2 with count *cnt2 (both clouds' centroids).
+// (off may be null), or (multi != 0) up to four separate arrays, problem b = dp[b]
+// with count *cp[b] (the clouds' centroids of a cloud stage).
 struct XsIn {
   const float* data;
   const uint32_t* off;
   const uint32_t* cnt;
-  const float* data2;
-  const uint32_t* cnt2;
+  int multi;
+  const float* dp[4];
+  const uint32_t* cp[4];
 };
 
+template <class T>
+__device__ __forceinline__ T sel4(const T (&a)[4], int b) {  // a select, not an index (see B4)
+  return b == 0 ? a[0] : (b == 1 ? a[1] : (b == 2 ? a[2] : a[3]));
+}
+
 __device__ __forceinline__ uint32_t prob_n(const XsIn& in, int b) {
-  return (in.data2 && b == 1) ? *in.cnt2 : in.cnt[b];
+  return in.multi ? *sel4(in.cp, b) : in.cnt[b];
 }
 
 __device__ __forceinline__ Prob prob_of(const XsIn& in, int S, int b) {
   Prob p;
   p.n = prob_n(in, b);
-  p.base = (in.data2 && b == 1) ? in.data2 : in.data + (size_t)(in.off ? in.off[b] : 0u) * S;
+  p.base = in.multi ? sel4(in.dp, b) : in.data + (size_t)(in.off ? in.off[b] : 0u) * S;
   p.nch = (p.n + XS_L - 1) / XS_L;
   return p;
 }
@@ -488,10 +494,12 @@ void exact_sum_in(const XsIn& in, int S, int K, int nprob, float* out, bool divi
   if (S == 3) {
     k_xs_csum<3><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
-    // probe bytes: 12 B per element of every problem (two-array form: both counts)
-    const uint32_t* c2 = in.data2 ? in.cnt2 : nullptr;
-    FCCF_LAUNCH("k_xs_chunk", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
-    FCCF_LAUNCH("k_xs_chain", (in.cnt, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
+    // probe bytes: 12 B per element of every problem (separate arrays: the first two
+    // problems' counts; probed calls batch one pair)
+    const uint32_t* c1 = in.multi ? in.cp[0] : in.cnt;
+    const uint32_t* c2 = in.multi && nprob > 1 ? in.cp[1] : nullptr;
+    FCCF_LAUNCH("k_xs_chunk", (c1, 12.0, c2, 12.0, 0.0), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
+    FCCF_LAUNCH("k_xs_chain", (c1, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
   } else {
     k_xs_csum<1><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
@@ -503,12 +511,30 @@ void exact_sum_in(const XsIn& in, int S, int K, int nprob, float* out, bool divi
 
 void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint32_t* cnt, int nprob, float* out,
                bool divide, XsBufs x, hipStream_t st) {
-  exact_sum_in(XsIn{data, off, cnt, nullptr, nullptr}, S, K, nprob, out, divide, x, st);
+  XsIn in{};
+  in.data = data;
+  in.off = off;
+  in.cnt = cnt;
+  exact_sum_in(in, S, K, nprob, out, divide, x, st);
+}
+
+void exact_sum_n(const float* const* data, const uint32_t* const* cnt, int nprob, int S, int K, float* out, bool divide,
+                 XsBufs x, hipStream_t st) {
+  if (nprob < 1 || nprob > 4) throw Error(FCCF_E_INTERNAL, "exact_sum_n: 1 to 4 arrays");
+  XsIn in{};
+  in.multi = 1;
+  for (int b = 0; b < 4; ++b) {
+    in.dp[b] = data[b < nprob ? b : nprob - 1];
+    in.cp[b] = cnt[b < nprob ? b : nprob - 1];
+  }
+  exact_sum_in(in, S, K, nprob, out, divide, x, st);
 }
 
 void exact_sum2(const float* a, const uint32_t* na, const float* b, const uint32_t* nb, int S, int K, float* out,
                 bool divide, XsBufs x, hipStream_t st) {
-  exact_sum_in(XsIn{a, nullptr, na, b, nb}, S, K, 2, out, divide, x, st);
+  const float* d[2] = {a, b};
+  const uint32_t* c[2] = {na, nb};
+  exact_sum_n(d, c, 2, S, K, out, divide, x, st);
 }
 
 }  // namespace fccf

@@ -16,6 +16,7 @@
 #include "probe.h"
 #include "kernels.h"
 #include "mail.h"
+#include "ctx.h"
 
 namespace fccf {
 namespace {
@@ -168,9 +169,9 @@ __global__ void __launch_bounds__(64) k_oct_sim(const float* __restrict__ xyz0, 
   if (lane == 0) *state = S;
 }
 
-__global__ void __launch_bounds__(256) k_oct_codes(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
-                                                   B2<const OctState*> state2, double res, B2<uint64_t*> codes2,
-                                                   B2<uint32_t*> d_nbits2) {
+__global__ void __launch_bounds__(256) k_oct_codes(B4<const float*> xyz2, B4<const uint32_t*> d_n2,
+                                                   B4<const OctState*> state2, double res, B4<uint64_t*> codes2,
+                                                   B4<uint32_t*> d_nbits2) {
   KT();
   const int e = blockIdx.y;
   const OctState S = *state2[e];
@@ -274,8 +275,8 @@ __device__ void eig_min(const float A[3][3], float& ev, f3& v) {
 
 // Points in leaf order (Morton, then index): the per-leaf loops below then read
 // contiguous memory instead of gathering through the sort permutation.
-__global__ void __launch_bounds__(256) k_gather(B2<const float*> xyz2, B2<const uint32_t*> vals2,
-                                                B2<const uint32_t*> d_n2, B2<float*> sp2) {
+__global__ void __launch_bounds__(256) k_gather(B4<const float*> xyz2, B4<const uint32_t*> vals2,
+                                                B4<const uint32_t*> d_n2, B4<float*> sp2) {
   KT();
   const int e = blockIdx.y;
   const uint32_t n = *d_n2[e];
@@ -296,7 +297,7 @@ constexpr uint32_t VFIT_BLOCKS = 512;  // 2048 waves per cloud; leaves are a few
 // LDS as (x, y, z, 1) so every lane computes term = p[i1] * p[i2] (the linear sums
 // use i2 = w = 1, and x * 1 == x exactly).  compute3DCentroid (:490) is the same
 // sequential x/y/z sum divided by n, i.e. accumulators 6..8 / n bit-for-bit.
-__global__ void __launch_bounds__(256) k_voxel_fit(B2<FaceBufs> fb, float vpt, float cthr) {
+__global__ void __launch_bounds__(256) k_voxel_fit(B4<FaceBufs> fb, float vpt, float cthr) {
   KT();
   constexpr uint32_t VB = 256;  // points per LDS burst of a wave (four per lane)
   __shared__ __attribute__((aligned(16))) float pts[4][VB * 4];
@@ -407,7 +408,7 @@ __global__ void __launch_bounds__(256) k_voxel_fit(B2<FaceBufs> fb, float vpt, f
 }
 
 // cloud_sub (:527-530): every point of a non-planar leaf, leaf order then index order.
-__global__ void __launch_bounds__(256) k_compact_resid(B2<FaceBufs> fb, B2<const uint32_t*> d_n2, B2<float*> rout2) {
+__global__ void __launch_bounds__(256) k_compact_resid(B4<FaceBufs> fb, B4<const uint32_t*> d_n2, B4<float*> rout2) {
   KT();
   const int e = blockIdx.y;
   const FaceBufs& B = fb.v[e];
@@ -429,8 +430,8 @@ __global__ void __launch_bounds__(256) k_compact_resid(B2<FaceBufs> fb, B2<const
 // Planar leaves with the normal oriented towards the cloud centroid (:504-516).
 // With a mailbox, the records (up to its capacity) and both clouds' counts are
 // also written to pinned host memory: phase B reads them after one event sync.
-__global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxRec*> pout2, CloudMail* __restrict__ mail,
-                                                        B2<const uint32_t*> sc2) {
+__global__ void __launch_bounds__(256) k_compact_planar(B4<FaceBufs> fb, B4<VoxRec*> pout2, CloudMail* __restrict__ mail,
+                                                        B4<const uint32_t*> sc2) {
   KT();
   const int e = blockIdx.y;
   const FaceBufs& B = fb.v[e];
@@ -440,21 +441,24 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
   const float* __restrict__ cc = B.centroid;
   VoxRec* __restrict__ pout = pout2[e];
   const uint32_t nl = *B.nleaf;
-  if (mail && blockIdx.x == 0 && threadIdx.x < 8) {
+  // clouds 2j and 2j + 1 are pair j of the batch: their mailbox is mail[j]
+  CloudMail* __restrict__ pm = mail ? mail + (e >> 1) : nullptr;
+  const int ce = e & 1;
+  if (pm && blockIdx.x == 0 && threadIdx.x < 8) {
     const uint32_t i = threadIdx.x & 3u;
-    if (threadIdx.x < 4) mail->sc[e][i] = sc2[e][i];
-    else if (i == 1) mail->fsc[e][1] = B.vgp ? B.vgp->sort_err | (B.vgp->redo ? VG_REDO : 0u) : 0u;  // both passes' sort flags, redo
-    else mail->fsc[e][i] = B.nleaf[i];
+    if (threadIdx.x < 4) pm->sc[ce][i] = sc2[e][i];
+    else if (i == 1) pm->fsc[ce][1] = B.vgp ? B.vgp->sort_err | (B.vgp->redo ? VG_REDO : 0u) : 0u;  // both passes' sort flags, redo
+    else pm->fsc[ce][i] = B.nleaf[i];
   }
   // the cloud stage's device spans: the stamps of main's pass, the driver's pass and the
   // face stage, and now (this last kernel of the stage, ~5 us, starts) into the mailbox.
   // (A finished-block count to stamp the true end cost 8192 same-address atomics:
   // ~70 us.)
-  if (mail && e == 0 && blockIdx.x == 0 && threadIdx.x == 0 && B.vgp) {
-    mail->stamp[3] = __builtin_amdgcn_s_memrealtime();
-    mail->stamp[0] = B.vgp->t_main;
-    mail->stamp[1] = B.vgp->t_driver;
-    mail->stamp[2] = *B.t_faces;
+  if (pm && ce == 0 && blockIdx.x == 0 && threadIdx.x == 0 && B.vgp) {
+    pm->stamp[3] = __builtin_amdgcn_s_memrealtime();
+    pm->stamp[0] = B.vgp->t_main;
+    pm->stamp[1] = B.vgp->t_driver;
+    pm->stamp[2] = *B.t_faces;
   }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
     if (!planar[s]) continue;
@@ -464,7 +468,7 @@ __global__ void __launch_bounds__(256) k_compact_planar(B2<FaceBufs> fb, B2<VoxR
     if (!(dot3(to, nv) < 0.f)) { r.n[0] = -nv.x; r.n[1] = -nv.y; r.n[2] = -nv.z; }
     const uint32_t o = poff[s];
     pout[o] = r;
-    if (mail && o < CloudMail::REC_CAP) mail->rec[e][o] = r;
+    if (pm && o < CloudMail::REC_CAP) pm->rec[ce][o] = r;
   }
 }
 
@@ -489,20 +493,141 @@ void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res,
 }
 
 namespace {
+// the batched octree launches address sequence e at a fixed byte stride from sequence 0:
+// every cloud of a batch is carved alike (pipeline.cpp carve_cloud)
 template <class T>
-size_t byte_stride(const B2<T*>& p, int nbatch) {
-  return nbatch > 1 ? (size_t)((const char*)p[1] - (const char*)p[0]) : 0;
+size_t byte_stride(const B4<T*>& p, int nbatch) {
+  if (nbatch < 2) return 0;
+  const ptrdiff_t d = (const char*)p[1] - (const char*)p[0];
+  for (int e = 2; e < nbatch; ++e)
+    if ((const char*)p[e] - (const char*)p[0] != e * d) throw Error(FCCF_E_INTERNAL, "face stage: clouds not carved alike");
+  return (size_t)d;
 }
 template <class F>
-auto pick(const B2<FaceBufs>& b, F get) -> B2<decltype(get(b[0]))> {
-  return B2<decltype(get(b[0]))>(get(b[0]), get(b[1]));
+auto pick(const B4<FaceBufs>& b, F get) -> B4<decltype(get(b[0]))> {
+  return B4<decltype(get(b[0]))>(get(b[0]), get(b[1]), get(b[2]), get(b[3]));
 }
 }  // namespace
 
-void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, double res, B2<FaceBufs> b,
-                         hipStream_t st, int nbatch) {
-  const B2<OctState*> oct = pick(b, [](const FaceBufs& f) { return f.oct; });
-  const B2<float*> aggr = pick(b, [](const FaceBufs& f) { return f.aggr; });
+namespace {
+// ---------------------------------------------------------------- row P (sharded face stage)
+// Rank r of N fits only the 1 m leaves of its range of codes: the points are binned by
+// the top FACE_BINS_LG bits of their leaf code (a leaf's points share their code, so a bin
+// boundary never splits a leaf), the bins are split into N ranges of about equal point
+// counts, and the rank's points are compacted in input order (so its sort keeps PCL's
+// insertion order within a leaf).  group.cpp face_voxels_sharded runs the exchange.
+constexpr int FACE_BINS_LG = 12;
+constexpr uint32_t FACE_BINS = 1u << FACE_BINS_LG;
+constexpr uint32_t FACE_HIST_BLOCKS = 256;
+
+__device__ __forceinline__ uint32_t face_shift(uint32_t nbits) {
+  return nbits > (uint32_t)FACE_BINS_LG ? nbits - (uint32_t)FACE_BINS_LG : 0u;
+}
+
+// hist (FACE_BINS u32, zeroed by the caller): points per bin
+__global__ void __launch_bounds__(256) k_face_hist(B4<const uint64_t*> codes2, B4<const uint32_t*> d_n2,
+                                                   B4<const uint32_t*> nbits2, B4<uint32_t*> hist2) {
+  KT();
+  __shared__ uint32_t h[FACE_BINS];
+  const int e = blockIdx.y;
+  for (uint32_t i = threadIdx.x; i < FACE_BINS; i += 256) h[i] = 0u;
+  __syncthreads();
+  const uint64_t* __restrict__ codes = codes2[e];
+  const uint32_t n = *d_n2[e], sh = face_shift(*nbits2[e]);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    atomicAdd(&h[(uint32_t)(codes[i] >> sh) & (FACE_BINS - 1u)], 1u);
+  __syncthreads();
+  uint32_t* __restrict__ hist = hist2[e];
+  for (uint32_t i = threadIdx.x; i < FACE_BINS; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// One block per cloud: bound j = the first bin b with (points before b) * N >= j * n;
+// rank r takes bins [bound_r, bound_{r+1}).  rng = {lo, hi, shift}.
+__global__ void __launch_bounds__(1024) k_face_range(B4<const uint32_t*> hist2, B4<const uint32_t*> d_n2,
+                                                     B4<const uint32_t*> nbits2, B4<uint32_t*> rng2, int rank,
+                                                     int nranks) {
+  KT();
+  __shared__ uint32_t sb[IS_SHARD_MAX + 1];
+  __shared__ uint32_t sh[16];
+  const int e = blockIdx.y;
+  const uint32_t* __restrict__ hist = hist2[e];
+  const uint64_t n = *d_n2[e];
+  constexpr int PER = FACE_BINS / 1024;
+  for (int j = threadIdx.x; j <= nranks; j += 1024) sb[j] = j == 0 ? 0u : FACE_BINS;
+  uint32_t h[PER], tot = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    h[k] = hist[threadIdx.x * PER + k];
+    tot += h[k];
+  }
+  // exclusive scan of the per-thread totals (points before this thread's first bin)
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint32_t before = x - tot;
+  for (uint32_t w = 0; w < wave; ++w) before += sh[w];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t b = threadIdx.x * PER + k;
+    for (int j = 1; j < nranks; ++j)
+      if ((uint64_t)before * (uint64_t)nranks >= (uint64_t)j * n) atomicMin(&sb[j], b);
+    before += h[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* rng = rng2[e];
+    rng[0] = sb[rank];
+    rng[1] = sb[rank + 1];
+    rng[2] = face_shift(*nbits2[e]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_face_flag(B4<const uint64_t*> codes2, B4<const uint32_t*> d_n2,
+                                                   B4<const uint32_t*> rng2, B4<uint32_t*> flag2) {
+  KT();
+  const int e = blockIdx.y;
+  const uint64_t* __restrict__ codes = codes2[e];
+  const uint32_t* rng = rng2[e];
+  const uint32_t n = *d_n2[e], lo = rng[0], hi = rng[1], sh = rng[2];
+  uint32_t* __restrict__ flag = flag2[e];
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t b = (uint32_t)(codes[i] >> sh) & (FACE_BINS - 1u);
+    flag[i] = (b >= lo && b < hi) ? 1u : 0u;
+  }
+}
+
+// this rank's points, in input order: codes to cout, input positions to iout
+__global__ void __launch_bounds__(256) k_face_pick(B4<const uint64_t*> codes2, B4<const uint32_t*> d_n2,
+                                                   B4<const uint32_t*> flag2, B4<const uint32_t*> off2,
+                                                   B4<uint64_t*> cout2, B4<uint32_t*> iout2) {
+  KT();
+  const int e = blockIdx.y;
+  const uint64_t* __restrict__ codes = codes2[e];
+  const uint32_t* __restrict__ flag = flag2[e];
+  const uint32_t* __restrict__ off = off2[e];
+  uint64_t* __restrict__ cout = cout2[e];
+  uint32_t* __restrict__ iout = iout2[e];
+  const uint32_t n = *d_n2[e];
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    if (flag[i]) {
+      cout[off[i]] = codes[i];
+      iout[off[i]] = i;
+    }
+}
+
+}  // namespace
+
+// block_aggr + octree_sim + codes of every point (replicated in the sharded form)
+void face_codes(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b, hipStream_t st,
+                int nbatch) {
+  const B4<OctState*> oct = pick(b, [](const FaceBufs& f) { return f.oct; });
+  const B4<float*> aggr = pick(b, [](const FaceBufs& f) { return f.aggr; });
   SeqStrides sd;
   sd.xyz = byte_stride(xyz, nbatch);
   sd.aggr = byte_stride(aggr, nbatch);
@@ -510,10 +635,84 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   sd.n = byte_stride(d_n, nbatch);
   block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd, oct[0], b[0].t_faces);  // also resets the octree states
   octree_sim(xyz[0], d_n[0], cap, res, aggr[0], oct[0], st, nbatch, sd);
-  const B2<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
-  const B2<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
-  const B2<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
-  k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B2<const OctState*>(oct), res, c0, nbits);
+  k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B4<const OctState*>(oct), res,
+                                                          pick(b, [](const FaceBufs& f) { return f.c0; }),
+                                                          pick(b, [](const FaceBufs& f) { return f.nbits; }));
+}
+
+void face_shard_select(B4<const uint32_t*> d_n, uint32_t cap, B4<FaceBufs> b, int rank, int nranks, hipStream_t st,
+                       int nbatch) {
+  if (cap < 2 * FACE_BINS) throw Error(FCCF_E_INTERNAL, "sharded face stage: cloud capacity below the bin table");
+  if (nranks < 1 || nranks > IS_SHARD_MAX) throw Error(FCCF_E_INTERNAL, "sharded face stage: rank count");
+  // scratch: the histogram in c2 (free until the sort), the flags in v0, their offsets in v2
+  const B4<uint32_t*> hist = pick(b, [](const FaceBufs& f) { return (uint32_t*)f.c2; });
+  for (int e = 0; e < nbatch; ++e) HIP_CHECK(hipMemsetAsync(hist[e], 0, 4 * FACE_BINS, st));
+  const B4<const uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return (const uint64_t*)f.c0; });
+  const B4<const uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nbits; });
+  const B4<uint32_t*> rng = pick(b, [](const FaceBufs& f) { return f.nleaf + 8; });  // FaceBufs scalars [8..10]
+  const B4<uint32_t*> nr = pick(b, [](const FaceBufs& f) { return f.nleaf + 11; });  // [11]: this rank's points
+  k_face_hist<<<dim3(FACE_HIST_BLOCKS, nbatch), 256, 0, st>>>(c0, d_n, nbits, hist);
+  k_face_range<<<dim3(1, nbatch), 1024, 0, st>>>(B4<const uint32_t*>(hist), d_n, nbits, rng, rank, nranks);
+  const B4<uint32_t*> flag = pick(b, [](const FaceBufs& f) { return f.v0; });
+  const B4<uint32_t*> off = pick(b, [](const FaceBufs& f) { return f.v2; });
+  k_face_flag<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(c0, d_n, B4<const uint32_t*>(rng), flag);
+  exclusive_scan_u32(B4<const uint32_t*>(flag), off, d_n, cap, nr, pick(b, [](const FaceBufs& f) { return f.ss; }), st,
+                     nbatch);
+  k_face_pick<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(c0, d_n, B4<const uint32_t*>(flag), B4<const uint32_t*>(off),
+                                                          pick(b, [](const FaceBufs& f) { return f.c1; }),
+                                                          pick(b, [](const FaceBufs& f) { return f.v1; }));
+}
+
+// The rank's points (codes c1, positions v1, count FaceBufs scalar [11]) sorted into leaf
+// order, their leaves (local: starts, nleaf, seg_of) and the points in that order (sp).
+void face_shard_sort(B4<const float*> xyz, uint32_t cap, B4<FaceBufs> b, hipStream_t st, int nbatch) {
+  const B4<const uint32_t*> nr = pick(b, [](const FaceBufs& f) { return (const uint32_t*)(f.nleaf + 11); });
+  const B4<uint64_t*> c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
+  const B4<uint32_t*> v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
+  radix_sort_u64(c1, v1, pick(b, [](const FaceBufs& f) { return f.c0; }), pick(b, [](const FaceBufs& f) { return f.v0; }),
+                 nr, cap, pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nbits; }), 32, false,
+                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B4<const uint32_t*>(nullptr),
+                 pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
+  segment_heads_u64(B4<const uint64_t*>(c1), nr, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
+                    pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
+                    st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
+  k_gather<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, B4<const uint32_t*>(v1), nr,
+                                                       pick(b, [](const FaceBufs& f) { return f.sp; }));
+}
+
+// The rank's leaves fitted into views of the full arrays (bv: recs, flag_planar,
+// resid_cnt, resid_off shifted to the rank's first leaf); its residual offsets (local
+// total in scalar [3]).
+void face_shard_fit(uint32_t cap, float vpt, float cthr, B4<FaceBufs> bv, hipStream_t st, int nbatch) {
+  k_voxel_fit<<<dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st>>>(bv, vpt, cthr);
+  exclusive_scan_u32(pick(bv, [](const FaceBufs& f) { return (const uint32_t*)f.resid_cnt; }),
+                     pick(bv, [](const FaceBufs& f) { return f.resid_off; }),
+                     pick(bv, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; }), cap,
+                     pick(bv, [](const FaceBufs& f) { return f.nresid; }), pick(bv, [](const FaceBufs& f) { return f.ss; }),
+                     st, nbatch);
+}
+
+// The rank's residual points into rout (already shifted to the rank's first residual point)
+void face_shard_resid(uint32_t cap, B4<FaceBufs> bv, B4<float*> rout, hipStream_t st, int nbatch) {
+  k_compact_resid<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(
+      bv, pick(bv, [](const FaceBufs& f) { return (const uint32_t*)(f.nleaf + 11); }), rout);
+}
+
+// After the exchange: the planar offsets over every leaf (scalar [0] = all leaves)
+void face_planar_scan(uint32_t cap, B4<FaceBufs> b, hipStream_t st, int nbatch) {
+  exclusive_scan_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
+                     pick(b, [](const FaceBufs& f) { return f.planar_off; }),
+                     pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; }), cap,
+                     pick(b, [](const FaceBufs& f) { return f.nplanar; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
+                     st, nbatch);
+}
+
+void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b,
+                         hipStream_t st, int nbatch) {
+  face_codes(xyz, d_n, cap, res, b, st, nbatch);
+  const B4<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
+  const B4<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
+  const B4<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
   // codes are 3 bits per octree level (+1): the device plan takes 3 passes of <= 9-bit
   // digits up to depth 8 (extents up to ~256 x face_voxel_size; c3: depth 6, 19 bits)
   // and 4 passes of 8 bits at depth 9-10 (~1 km at 1 m voxels, outdoor scans), so four
@@ -521,23 +720,23 @@ void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t
   // launches per registration), and only trees deeper than 10 levels reach the
   // single-workgroup tail launch.  With the third buffer a three-pass sort ends in
   // (c0, v0) without a copy-back; a four-pass sort ends there by ping-pong.
-  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B2<const uint32_t*>(nbits), 32, true,
-                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B2<const uint32_t*>(nullptr),
+  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B4<const uint32_t*>(nbits), 32, true,
+                 pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B4<const uint32_t*>(nullptr),
                  pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
-  segment_heads_u64(B2<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
+  segment_heads_u64(B4<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
                     pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
                     st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
   const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
-  FCCF_LAUNCH("k_gather", (d_n[0], 28.0, n2, 28.0), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B2<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
+  FCCF_LAUNCH("k_gather", (d_n[0], 28.0, n2, 28.0), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B4<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
 }
 
-void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float vpt, float cthr, B2<float*> resid_out,
-                     B2<FaceBufs> b, hipStream_t st, int nbatch) {
+void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float vpt, float cthr, B4<float*> resid_out,
+                     B4<FaceBufs> b, hipStream_t st, int nbatch) {
   const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
   const uint32_t* l2 = nbatch > 1 ? b[1].nleaf : nullptr;
   FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st, b, vpt, cthr);
-  const B2<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
-  const B2<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
+  const B4<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
+  const B4<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
   exclusive_scan2_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),
                       pick(b, [](const FaceBufs& f) { return f.planar_off; }),
                       pick(b, [](const FaceBufs& f) { return f.nplanar; }),
@@ -553,8 +752,8 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
   octree_sim(xyz, d_n, cap, res, aggr, state, st);
 }
 
-void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch,
-                        CloudMail* mail, B2<const uint32_t*> sc) {
+void face_voxels_orient(uint32_t cap, B4<VoxRec*> planar_out, B4<FaceBufs> b, hipStream_t st, int nbatch,
+                        CloudMail* mail, B4<const uint32_t*> sc) {
   k_compact_planar<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, planar_out, mail, sc);
 }
 

@@ -177,7 +177,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   k_fv_keys<<<dim3(grid_for(n1 + n2, 256, 1024), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0);
   // (e | morton | is_target): 4 fast passes cover depth <= 9 with <= 15 evaluations.
   // Keys only: the counts below read the sorted keys, never a permutation.
-  radix_sort_u64(b.k0, B2<uint32_t*>(nullptr), b.k1, B2<uint32_t*>(nullptr), b.scal, n, b.scal + 1, 32, false, b.ss,
+  radix_sort_u64(b.k0, B4<uint32_t*>(nullptr), b.k1, B4<uint32_t*>(nullptr), b.scal, n, b.scal + 1, 32, false, b.ss,
                  st);
   k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
   segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);

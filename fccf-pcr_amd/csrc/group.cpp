@@ -310,6 +310,78 @@ void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2],
   }
 }
 
+void face_voxels_sharded(Group* g, B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, float vpt,
+                         float cthr, B4<float*> resid_out, B4<FaceBufs> b, hipStream_t st, int nbatch) {
+  const int n = g->n;
+  if (nbatch > 2) throw Error(FCCF_E_INTERNAL, "sharded face stage: one pair per cloud stage");
+  face_codes(xyz, d_n, cap, res, b, st, nbatch);  // replicated: the octree bounds depend on every point in order
+  face_shard_select(d_n, cap, b, g->rank, n, st, nbatch);
+  face_shard_sort(xyz, cap, b, st, nbatch);
+  cloud_gate(g);  // (the batch's helper thread: after the previous pair's B1 collectives)
+  // the ranks' counts (cnt(e) = scalar k of cloud e), all-gathered: every rank's base
+  auto gather_counts = [&](int k, std::vector<uint32_t>& base, uint32_t tot[2]) {
+    for (int e = 0; e < 2; ++e)
+      HIP_CHECK(hipMemcpyAsync(g->d_fcnt + e, b[e < nbatch ? e : 0].nleaf + k, 4, hipMemcpyDeviceToDevice, st));
+    g->tr->allgather(CH_CLOUD, g->d_fcnt, g->d_fcnt + 4, 16, st);
+    HIP_CHECK(hipMemcpyAsync(g->h_fcnt, g->d_fcnt + 4, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    base.assign(2 * (size_t)(n + 1), 0u);
+    for (int e = 0; e < 2; ++e) {
+      uint32_t run = 0;
+      for (int r = 0; r < n; ++r) {
+        base[(size_t)e * (n + 1) + r] = run;
+        run += g->h_fcnt[4 * r + e];
+      }
+      base[(size_t)e * (n + 1) + n] = run;
+      tot[e] = run;
+    }
+  };
+  std::vector<uint32_t> lb, rb;
+  uint32_t ltot[2], rtot[2];
+  gather_counts(0, lb, ltot);  // leaves per rank
+  // views of the full leaf arrays at this rank's first leaf
+  B4<FaceBufs> bv = b;
+  for (int e = 0; e < BMAX; ++e) {
+    const uint32_t o = lb[(size_t)(e < nbatch ? e : 0) * (n + 1) + g->rank];
+    bv.v[e].recs += o;
+    bv.v[e].flag_planar += o;
+    bv.v[e].resid_cnt += o;
+    bv.v[e].resid_off += o;
+  }
+  face_shard_fit(cap, vpt, cthr, bv, st, nbatch);
+  gather_counts(3, rb, rtot);  // residual points per rank
+  B4<float*> rv = resid_out;
+  for (int e = 0; e < BMAX; ++e) rv.v[e] += 3 * (size_t)rb[(size_t)(e < nbatch ? e : 0) * (n + 1) + g->rank];
+  face_shard_resid(cap, bv, rv, st, nbatch);
+  // rank-ordered all-gathers into the full arrays (in place: each rank's part is already there)
+  std::vector<size_t> cnt((size_t)n), off((size_t)n);
+  auto allgv = [&](void* base, const std::vector<uint32_t>& bs, int e, size_t unit) {
+    for (int r = 0; r < n; ++r) {
+      const size_t i = (size_t)e * (n + 1) + r;
+      cnt[(size_t)r] = unit * (bs[i + 1] - bs[i]);
+      off[(size_t)r] = unit * bs[i];
+    }
+    g->tr->allgatherv(CH_CLOUD, (const char*)base + off[(size_t)g->rank], base, cnt.data(), off.data(), st);
+  };
+  for (int e = 0; e < nbatch; ++e) {
+    allgv(b[e].recs, lb, e, sizeof(VoxRec));
+    allgv(b[e].flag_planar, lb, e, 4);
+    allgv(b[e].resid_cnt, lb, e, 4);  // (read only by the debug dumps: a leaf's residual flag)
+    allgv(resid_out[e], rb, e, 12);
+  }
+  // the full counts where the unsharded stage leaves them: leaves (scalar 0), residual
+  // points (3); then the planar offsets over every leaf (nplanar, scalar 2)
+  uint32_t* h = g->h_fcnt + 4 * (size_t)n;
+  for (int e = 0; e < nbatch; ++e) {
+    h[4 * e] = ltot[e];
+    h[4 * e + 1] = rtot[e];
+    HIP_CHECK(hipMemcpyAsync(b[e].nleaf, h + 4 * e, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(b[e].nresid, h + 4 * e + 1, 4, hipMemcpyHostToDevice, st));
+  }
+  face_planar_scan(cap, b, st, nbatch);
+  HIP_CHECK(hipStreamSynchronize(st));  // (h is reused by the next call)
+}
+
 }  // namespace fccf
 
 using namespace fccf;
@@ -330,7 +402,10 @@ void group_alloc(Group& g) {
     throw Error(FCCF_E_OOM, "hipHostMalloc");
   if (hipHostMalloc((void**)&g.h_bounds, 4 * 2 * (IS_SHARD_MAX + 1), hipHostMallocDefault) != hipSuccess)
     throw Error(FCCF_E_OOM, "hipHostMalloc");
-  for (int s = 0; s < 2; ++s) {
+  if (hipMalloc((void**)&g.d_fcnt, 16 * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
+  if (hipHostMalloc((void**)&g.h_fcnt, 16 * (n + 1) + 64, hipHostMallocDefault) != hipSuccess)
+    throw Error(FCCF_E_OOM, "hipHostMalloc");
+  for (int s = 0; s < Group::SLOTS; ++s) {
     if (hipMalloc((void**)&g.d_fsend[s], sizeof(float) * Group::FE_BLK) != hipSuccess ||
         hipMalloc((void**)&g.d_frecv[s], sizeof(float) * Group::FE_BLK * n) != hipSuccess)
       throw Error(FCCF_E_OOM, "hipMalloc");
@@ -347,7 +422,7 @@ void group_free(Group& g) {
     }
   if (g.d_cnt) (void)hipFree(g.d_cnt);
   if (g.h_cnt) (void)hipHostFree(g.h_cnt);
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < Group::SLOTS; ++s) {
     if (g.d_fsend[s]) (void)hipFree(g.d_fsend[s]);
     if (g.d_frecv[s]) (void)hipFree(g.d_frecv[s]);
     if (g.h_frecv[s]) (void)hipHostFree(g.h_frecv[s]);
@@ -355,6 +430,9 @@ void group_free(Group& g) {
   }
   if (g.h_bounds) (void)hipHostFree(g.h_bounds);
   g.h_bounds = nullptr;
+  if (g.d_fcnt) (void)hipFree(g.d_fcnt);
+  if (g.h_fcnt) (void)hipHostFree(g.h_fcnt);
+  g.d_fcnt = g.h_fcnt = nullptr;
   g.d_cnt = nullptr;
   g.h_cnt = nullptr;
   g.tr.reset();

@@ -19,6 +19,7 @@
 #include <memory>
 #include <mutex>
 
+#include "kernels.h"
 #include "match.h"
 
 struct fccf_ctx;
@@ -53,13 +54,16 @@ struct Group {
   std::unique_ptr<Transport> tr;
   uint32_t* d_cnt = nullptr;  // device: this rank's 4 counts, then all ranks' (n x 4)
   uint32_t* h_cnt = nullptr;  // pinned copy of all ranks' counts
-  // sharded fine verification, per cloud set s (the pipelined batch overlaps two pairs):
+  // sharded fine verification, per pair slot s (the pipelined batch overlaps pairs):
   // this rank's block of scores + its error word (FE_BLK floats), all ranks' blocks
   static constexpr int FE_BLK = MAX_EVAL + 1;
-  float* d_fsend[2] = {nullptr, nullptr};
-  float* d_frecv[2] = {nullptr, nullptr};  // n x FE_BLK
-  float* h_frecv[2] = {nullptr, nullptr};  // pinned copies
+  static constexpr int SLOTS = 4;
+  float* d_fsend[SLOTS] = {};
+  float* d_frecv[SLOTS] = {};  // n x FE_BLK
+  float* h_frecv[SLOTS] = {};  // pinned copies
   uint32_t* h_bounds = nullptr;             // pinned: the sharded sort's rank bounds, per cloud (row D)
+  uint32_t* d_fcnt = nullptr;               // row P: this rank's 4 counts, then all ranks' (n x 4), device
+  uint32_t* h_fcnt = nullptr;               // ... their pinned copy, then 8 words of totals for the device
   // One issue order of collectives per rank.  Communicators that are used concurrently
   // must see their collectives issued in the same order on every rank, or their kernels
   // can wait on each other across ranks.  The pipelined batch issues CH_MATCH and CH_FINE
@@ -93,6 +97,14 @@ int shard_sort_r0(int n_ranks);
 // device copy of cloud e's bounds (IsBufs::bounds).  Synchronises st (the bounds).
 void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
                          int nbatch, hipStream_t st);
+
+// Row P (FCCF.cpp:470-534): the face stage of the batch's clouds (the
+// driver's downsampled clouds xyz, counts d_n) with each rank fitting only its Morton
+// range of 1 m leaves; leaf records, planar flags and residual points are all-gathered
+// in rank order into the same arrays (and counts) the unsharded stage fills.  Runs on
+// st on the CH_CLOUD channel, synchronising st twice (the ranks' leaf and residual counts).
+void face_voxels_sharded(Group* g, B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, float vpt,
+                         float cthr, B4<float*> resid_out, B4<FaceBufs> b, hipStream_t st, int nbatch);
 
 // the Group inside a C-ABI handle (null for null)
 Group* group_of(fccf_group* g);

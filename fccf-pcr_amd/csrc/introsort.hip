@@ -124,12 +124,27 @@ __device__ __forceinline__ void is_inject(const IsBufs& W, uint32_t bits) {
   if (b) is_fault(W.ctl, W.err, b);
 }
 
-// A final (key, value) write's point, when the sort writes sorted points (IsBufs::xyzs)
+// A final (key, value) write's point, when the sort writes sorted points (IsBufs::xyzs).
+// The points are read and written as one 12-byte global access each (the source pointer
+// comes from memory, so without the address-space cast the compiler emits flat loads,
+// which also wait on LDS traffic); callers with several points issue every load before
+// the first store (load_xyz / store_xyz), so the random gathers overlap instead of each
+// waiting out its own memory latency.
+struct Pt3 {
+  float x, y, z;
+};
+// (the global address space exists only in the device compilation of this file)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) const Pt3* GPt3c;
+typedef __attribute__((address_space(1))) Pt3* GPt3;
+#else
+typedef const Pt3* GPt3c;
+typedef Pt3* GPt3;
+#endif
+__device__ __forceinline__ Pt3 load_xyz(const float* src, uint32_t v) { return ((GPt3c)(const Pt3*)src)[v]; }
+__device__ __forceinline__ void store_xyz(const IsBufs& W, uint32_t pos, const Pt3& q) { ((GPt3)(Pt3*)W.xyzs)[pos] = q; }
 __device__ __forceinline__ void put_xyz(const IsBufs& W, const float* __restrict__ src, uint32_t pos, uint32_t v) {
-  const float x = src[3 * (size_t)v], y = src[3 * (size_t)v + 1], z = src[3 * (size_t)v + 2];
-  W.xyzs[3 * (size_t)pos] = x;
-  W.xyzs[3 * (size_t)pos + 1] = y;
-  W.xyzs[3 * (size_t)pos + 2] = z;
+  store_xyz(W, pos, load_xyz(src, v));
 }
 
 // The fence before a workgroup barrier that hands global-memory data between the waves
@@ -340,8 +355,8 @@ __device__ void plan_round(const IsBufs& W, int r, uint32_t nsort, uint64_t* sh6
 // mark the tail invalid.  ctl[0] = sort length, ctl[1] = k_is_block's dequeue head;
 // the rounds' completion counters zeroed and round 0 planned (plan_round).
 // exact_gate (the driver's presorted second pass): sort only when the order check failed.
-__global__ void __launch_bounds__(1024) k_is_prep(B2<uint32_t*> K2, B2<uint32_t*> V2, B2<const uint32_t*> d_n2,
-                                                   B2<const VGParams*> P2, B2<IsBufs> W2, int exact_gate) {
+__global__ void __launch_bounds__(1024) k_is_prep(B4<uint32_t*> K2, B4<uint32_t*> V2, B4<const uint32_t*> d_n2,
+                                                   B4<const VGParams*> P2, B4<IsBufs> W2, int exact_gate) {
   KT();
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
@@ -697,8 +712,8 @@ __device__ void tile_prefix(const IsBufs& W, int r, uint32_t* base, uint64_t* sh
 }
 
 // Dynamic LDS: 2 * segmax u32 (tile_prefix).
-__global__ void __launch_bounds__(IS_TT) k_is_count_plan(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
-                                                         B2<IsBufs> W2, int r) {
+__global__ void __launch_bounds__(IS_TT) k_is_count_plan(B4<const uint32_t*> K2, B4<const uint32_t*> V2,
+                                                         B4<IsBufs> W2, int r) {
   KT();
   extern __shared__ uint32_t dyn[];
   __shared__ uint64_t sh64[16];
@@ -729,8 +744,8 @@ constexpr uint32_t IS_WIN = 256;  // prefix window in LDS (larger windows: binar
 #ifndef IS_SCATTER_MINB
 #define IS_SCATTER_MINB 1
 #endif
-__global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
-                                                      B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r,
+__global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
+                                                      B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r,
                                                       int R) {
   KT();
   __shared__ uint64_t sh64[16];
@@ -1032,8 +1047,8 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
 }
 
 // Dynamic LDS: 4 * segmax u32 (the round's segment table).
-__global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B2<const uint32_t*> K2, B2<const uint32_t*> V2,
-                                                         B2<IsBufs> W2, int r) {
+__global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B4<const uint32_t*> K2, B4<const uint32_t*> V2,
+                                                         B4<IsBufs> W2, int r) {
   KT();
   IS_PH_START();
   extern __shared__ uint32_t dyn[];
@@ -1043,8 +1058,8 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B2<const uint32_t*> K
 
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
-__global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B2<const uint32_t*> Ki2, B2<const uint32_t*> Vi2,
-                                                      B2<uint32_t*> Ko2, B2<uint32_t*> Vo2, B2<IsBufs> W2, int r) {
+__global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
+                                                      B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r) {
   KT();
   IS_PH_START();
   extern __shared__ uint32_t dyn[];
@@ -1770,9 +1785,12 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
     wsync();  // (the cut reads precede the next level's resets)
   }
   // stable sort of every leaf (<= 16 positions) by rank, straight to K/V
+  uint32_t dpos[C], dval[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const uint32_t p = c * 64 + lane;
+    dpos[c] = IS_NONE;
+    dval[c] = 0u;
     if (p >= n) continue;
     const uint32_t a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
     const uint32_t key = S.k[p];
@@ -1781,9 +1799,18 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       const uint32_t kq = S.k[q];
       rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
     }
-    K[f + a + rank] = key;
-    V[f + a + rank] = S.v[p];
-    if (src) put_xyz(W, src, f + a + rank, S.v[p]);
+    dpos[c] = f + a + rank;
+    dval[c] = S.v[p];
+    K[dpos[c]] = key;
+    V[dpos[c]] = dval[c];
+  }
+  if (src) {  // every gather issued before the first point store
+    Pt3 pt[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) pt[c] = load_xyz(src, dval[c]);  // (dval = 0 past n: a valid point, not stored)
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (dpos[c] != IS_NONE) store_xyz(W, dpos[c], pt[c]);
   }
 }
 #endif
@@ -2032,7 +2059,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     }
     Ko[f + a + rank] = key;
     Vo[f + a + rank] = S.v[p];
-    if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);
+    if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);  // (the block's leaf elements are few: most go to wave tasks)
   }
   __syncthreads();
 }
@@ -2192,8 +2219,8 @@ __device__ bool distinct_keys(BlockLds& S, const uint32_t* K, uint32_t* T0, uint
 
 // One workgroup per remaining segment: the final children of the last round first
 // (they may exceed IS_LCAP), then the owned list, dequeued from ctl[1].
-__global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<uint32_t*> K12,
-                                                    B2<uint32_t*> V12, B2<IsBufs> W2, int R) {
+__global__ void __launch_bounds__(IS_OT) k_is_block(B4<uint32_t*> K02, B4<uint32_t*> V02, B4<uint32_t*> K12,
+                                                    B4<uint32_t*> V12, B4<IsBufs> W2, int R) {
   KT();
   __shared__ BlockLds S;
   __shared__ uint32_t s_idx;
@@ -2340,7 +2367,7 @@ __global__ void __launch_bounds__(IS_OT) k_is_block(B2<uint32_t*> K02, B2<uint32
 #ifndef IS_WAVE_LB
 #define IS_WAVE_LB 4  // 4 waves per SIMD: 128 VGPRs, no spill (1.19 vs 1.21 ms pipelined, profiles/r02j)
 #endif
-__global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B2<uint32_t*> K02, B2<uint32_t*> V02, B2<IsBufs> W2) {
+__global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02, B4<uint32_t*> V02, B4<IsBufs> W2) {
   KT();
   __shared__ WaveLds WL[IS_WT / 64];
   const int e = blockIdx.y;
@@ -2515,8 +2542,8 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   return b;
 }
 
-void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                   B2<const VGParams*> P, uint32_t cap, B2<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate) {
+void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                   B4<const VGParams*> P, uint32_t cap, B4<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate) {
   const int R = exact_gate ? 0 : introsort_rounds(cap);
   static const bool trace = std::getenv("FCCF_IS_TRACE") != nullptr;  // dev: sync + log after each launch
   auto step = [&](const char* what, int r) {
@@ -2533,30 +2560,30 @@ void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint
   const char* pm = std::getenv("FCCF_IS_PLAN");
   const bool large = b[0].shard_n > 1 || (pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN));
   for (int r = 0; r < R; ++r) {
-    const B2<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
-    const B2<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
+    const B4<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
+    const B4<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
     if (large) {
       // algorithmic bytes: the key read, a 2-byte list entry written (x2: >= and <= lists share a unit)
       FCCF_LAUNCH("k_is_count_plan",
                   (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
-                  k_is_count_plan, dim3(maxtiles_l, nbatch), IS_TT, 8 * (size_t)segmax, st, B2<const uint32_t*>(ki),
-                  B2<const uint32_t*>(vi), b, r);
+                  k_is_count_plan, dim3(maxtiles_l, nbatch), IS_TT, 8 * (size_t)segmax, st, B4<const uint32_t*>(ki),
+                  B4<const uint32_t*>(vi), b, r);
       step("count", r);
       // algorithmic bytes: key + value read and written, plus a 2-byte list entry
       FCCF_LAUNCH("k_is_scatter",
                   (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
-                  k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st, B2<const uint32_t*>(ki),
-                  B2<const uint32_t*>(vi), ko, vo, b, r, R);
+                  k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st, B4<const uint32_t*>(ki),
+                  B4<const uint32_t*>(vi), ko, vo, b, r, R);
     } else {
       FCCF_LAUNCH("k_is_count_plan",
                   (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
-                  k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B2<const uint32_t*>(ki),
-                  B2<const uint32_t*>(vi), b, r);
+                  k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B4<const uint32_t*>(ki),
+                  B4<const uint32_t*>(vi), b, r);
       step("count", r);
       FCCF_LAUNCH("k_is_scatter",
                   (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
-                  k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)maxtiles, st, B2<const uint32_t*>(ki),
-                  B2<const uint32_t*>(vi), ko, vo, b, r);
+                  k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki),
+                  B4<const uint32_t*>(vi), ko, vo, b, r);
     }
     step("scatter", r);
   }

@@ -109,8 +109,8 @@ int introsort_rounds(uint32_t cap);
 // positions -- exactly as std::sort orders PCL's index vector of the finite points;
 // the result is left in (k0, v0) with the invalid keys after it.  (k1, v1) are the
 // other buffer.  exact_gate: sort only if P->unsorted (the presorted second pass).
-void introsort_u32(B2<uint32_t*> k0, B2<uint32_t*> v0, B2<uint32_t*> k1, B2<uint32_t*> v1, B2<const uint32_t*> d_n,
-                   B2<const VGParams*> P, uint32_t cap, B2<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate);
+void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
+                   B4<const VGParams*> P, uint32_t cap, B4<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate);
 
 struct VGBufs {
   uint32_t *k0, *v0, *k1, *v1;  // cap each
@@ -140,12 +140,12 @@ struct VGBufs {
 // inputs are read in place, never staged.  set_n: the count is n (by value) and the
 // kernel stores it to d_n for the later kernels; otherwise it is read from d_n.
 struct VGEntry {
-  B2<const float*> xyz;
-  B2<uint32_t*> d_n;
-  B2<uint32_t> n;
+  B4<const float*> xyz;
+  B4<uint32_t*> d_n;
+  B4<uint32_t> n;
   int set_n = 0;
-  B2<float*> part;
-  B2<VGParams*> P;
+  B4<float*> part;
+  B4<VGParams*> P;
   void* args[6];
   void bind() {
     args[0] = &xyz; args[1] = &d_n; args[2] = &n; args[3] = &set_n; args[4] = &part; args[5] = &P;
@@ -163,9 +163,9 @@ enum { VG_GENERAL = 0, VG_PRESORTED = 1, VG_OPTIMISTIC = 2 };
 constexpr uint32_t VG_REDO = 0x80000000u;       // CloudMail::fsc[k][1]: the optimistic pass must be redone
 constexpr uint32_t VG_FORCE_REDO = 0x10000u;    // test hook bit (fccf_debug_inject_sort_fault)
 constexpr uint32_t IS_POISON_XYZS = 0x20000u;   // test hook bit: sorted points filled with NaN before each sort
-void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_n, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, int presorted = VG_GENERAL, int nbatch = 1,
-                B2<float*> out_copy = B2<float*>(nullptr), const uint32_t* n_in = nullptr,
+void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_n, uint32_t cap, float leaf, B4<float*> out,
+                B4<uint32_t*> d_m, B4<VGBufs> b, hipStream_t st, int presorted = VG_GENERAL, int nbatch = 1,
+                B4<float*> out_copy = B4<float*>(nullptr), const uint32_t* n_in = nullptr,
                 VGEntry* entry = nullptr);
 
 // ------------------------------------------------ K2/K3: 1 m face voxels (FCCF.cpp:470-534)
@@ -223,16 +223,28 @@ struct FaceBufs {
 
 // Octree leaves (Morton order) of each cloud of the batch.  Batched clouds must be
 // carved identically: every pointer of cloud 1 sits `stride` bytes after cloud 0's.
-void face_voxels_prepare(B2<const float*> xyz, B2<const uint32_t*> d_n, uint32_t cap, double res, B2<FaceBufs> b,
+void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b,
                          hipStream_t st, int nbatch = 1);
+// Row P (the face stage sharded by Morton range of 1 m leaves, group.cpp
+// face_voxels_sharded): the codes of every point; this rank's points (in input order)
+// and their sort into leaf order; the fit of its leaves into views of the full arrays;
+// its residual points; the planar offsets over all leaves after the exchange.
+void face_codes(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b, hipStream_t st,
+                int nbatch);
+void face_shard_select(B4<const uint32_t*> d_n, uint32_t cap, B4<FaceBufs> b, int rank, int nranks, hipStream_t st,
+                       int nbatch);
+void face_shard_sort(B4<const float*> xyz, uint32_t cap, B4<FaceBufs> b, hipStream_t st, int nbatch);
+void face_shard_fit(uint32_t cap, float vpt, float cthr, B4<FaceBufs> bv, hipStream_t st, int nbatch);
+void face_shard_resid(uint32_t cap, B4<FaceBufs> bv, B4<float*> rout, hipStream_t st, int nbatch);
+void face_planar_scan(uint32_t cap, B4<FaceBufs> b, hipStream_t st, int nbatch);
 // Per-leaf fit, planar/residual flags and the residual cloud.
-void face_voxels_fit(B2<const uint32_t*> d_n, uint32_t cap, float voxel_point_threshold, float curvature_threshold, B2<float*> resid_out,
-                     B2<FaceBufs> b, hipStream_t st, int nbatch = 1);
+void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float voxel_point_threshold, float curvature_threshold, B4<float*> resid_out,
+                     B4<FaceBufs> b, hipStream_t st, int nbatch = 1);
 // Planar records, oriented towards b.centroid (must be ready: the caller orders streams).
 struct CloudMail;
 // mail (may be null): pinned mailbox receiving the records and both clouds' counts (sc = scalars of each cloud)
-void face_voxels_orient(uint32_t cap, B2<VoxRec*> planar_out, B2<FaceBufs> b, hipStream_t st, int nbatch = 1,
-                        CloudMail* mail = nullptr, B2<const uint32_t*> sc = B2<const uint32_t*>(nullptr));
+void face_voxels_orient(uint32_t cap, B4<VoxRec*> planar_out, B4<FaceBufs> b, hipStream_t st, int nbatch = 1,
+                        CloudMail* mail = nullptr, B4<const uint32_t*> sc = B4<const uint32_t*>(nullptr));
 
 // Byte strides between the sequences of a batched octree launch: sequence e uses
 // xyz + e*xyz, aggr + e*aggr, state + e*state, d_n + e*n (bytes; 0 = shared).

@@ -13,7 +13,7 @@
 
 namespace fccf {
 
-struct CloudMail {                     // one per cloud set (double-buffered pairs)
+struct CloudMail {                     // one per pair slot (fccf_ctx::cs)
   static constexpr uint32_t REC_CAP = 16384;   // planar 1 m voxels per cloud
   uint32_t sc[2][4];                   // per cloud: n_in, M1, M1 finite, M2
   uint32_t fsc[2][4];                  // per cloud: leaves, K1 sort fault flags (VGParams::sort_err),
@@ -49,9 +49,9 @@ struct FineMail {
 };
 
 struct HostMail {
-  CloudMail clouds[2];
+  CloudMail clouds[4];  // per pair slot; a stage group's two slots are adjacent (k_compact_planar)
   MatchMail match;
-  FineMail fine[2];  // per cloud set: a pair's fine verification overlaps the next pair's phase B
+  FineMail fine[4];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
 };
 
 }  // namespace fccf

@@ -44,8 +44,8 @@ double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::
 // overflow) holds the input as is, so the flag is almost never set: then ds1f is
 // already the NaN-free cloud and only its count is written.  Otherwise this single
 // workgroup compacts ds1 into ds1f in order, 1024 points per step (slow, rare).
-__global__ void __launch_bounds__(1024) k_finite_fix(B2<const float*> xyz2, B2<const uint32_t*> d_n2,
-                                                     B2<const VGParams*> P2, B2<float*> out2, B2<uint32_t*> d_m2) {
+__global__ void __launch_bounds__(1024) k_finite_fix(B4<const float*> xyz2, B4<const uint32_t*> d_n2,
+                                                     B4<const VGParams*> P2, B4<float*> out2, B4<uint32_t*> d_m2) {
   KT();
   const int e = blockIdx.y;
   if (threadIdx.x == 0) const_cast<VGParams*>(P2[e])->t_driver = __builtin_amdgcn_s_memrealtime();
@@ -135,49 +135,64 @@ void carve_cloud(Arena& a, CloudWS& w, uint32_t cap, bool) {
   w.fstate = a.take_n<OctState>(1);
 }
 
-// Device part of both clouds of a pair, batched (blockIdx.y = cloud, both clouds
-// carved identically) in two graph segments on one stream:
+// Device part of the clouds of one or two pairs, batched (blockIdx.y = cloud, every
+// cloud carved alike), nc = 2 * pairs clouds: pair j's clouds are 2j (the driver's
+// source) and 2j + 1.  One graph on one stream:
 //   A  both VoxelGrid passes with remove-NaN between them
 //   F  octree leaves, per-leaf fit, residual cloud, after A
-// plus, on the side stream after A, one graph summing both cloud centroids (the
-// sequential compute3DCentroid sums, six rows in one launch set), and the planar
-// compaction, which orients normals towards the centroid, after F and the sums.
+// plus, on the side stream after A, the sequential compute3DCentroid sums of every
+// cloud (three rows each, one launch set), and the planar compaction, which orients
+// normals towards the centroid, after F and the sums.
 template <class T, class F>
-B2<T> both(const CloudWS* w, F get) { return B2<T>(get(w[0]), get(w[1])); }
+B4<T> all_of(const CloudWS* w, int nc, F get) {
+  T v[BMAX];
+  for (int e = 0; e < BMAX; ++e) v[e] = get(w[e < nc ? e : nc - 1]);
+  return B4<T>(v[0], v[1], v[2], v[3]);
+}
 
 // main's VoxelGrid pass (:1668-1678) over the inputs xin (n points each), its
 // output also into ds1f; entry receives its entry kernel's arguments (graph patch)
-void seg_pass1(CloudWS* w, const float* const xin[2], const uint32_t n[2], float leaf, hipStream_t st,
+void seg_pass1(CloudWS* w, int nc, const float* const* xin, const uint32_t* n, float leaf, hipStream_t st,
                VGEntry* entry) {
   const uint32_t cap = w[0].cap;
-  auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
-  const B2<VGBufs> vg(w[0].vg, w[1].vg);
-  voxel_grid(B2<const float*>(xin[0], xin[1]), sc(0), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds1; }),
-             sc(1), vg, st, false, 2, both<float*>(w, [](const CloudWS& c) { return c.ds1f; }), n, entry);
+  auto sc = [&](int i) { return all_of<uint32_t*>(w, nc, [i](const CloudWS& c) { return c.sc + i; }); };
+  const B4<VGBufs> vg = all_of<VGBufs>(w, nc, [](const CloudWS& c) { return c.vg; });
+  const float* x[BMAX];
+  for (int e = 0; e < BMAX; ++e) x[e] = xin[e < nc ? e : nc - 1];
+  voxel_grid(B4<const float*>(x[0], x[1], x[2], x[3]), sc(0), cap, leaf,
+             all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1; }), sc(1), vg, st, false, nc,
+             all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1f; }), n, entry);
 }
 // the driver's remove-NaN and second VoxelGrid pass (:1374-1387); mode VG_OPTIMISTIC
 // (the pipeline's default: no fallback sort launches, the host redoes a pass that was
 // not in leaf order) or VG_PRESORTED (the redo)
-void seg_downsample(CloudWS* w, float leaf, hipStream_t st, int mode) {
+void seg_downsample(CloudWS* w, int nc, float leaf, hipStream_t st, int mode) {
   const uint32_t cap = w[0].cap;
-  auto sc = [&](int i) { return B2<uint32_t*>(w[0].sc + i, w[1].sc + i); };
-  const B2<VGBufs> vg(w[0].vg, w[1].vg);
-  const B2<float*> ds1 = both<float*>(w, [](const CloudWS& c) { return c.ds1; });
-  const B2<float*> ds1f = both<float*>(w, [](const CloudWS& c) { return c.ds1f; });
-  k_finite_fix<<<dim3(1, 2), 1024, 0, st>>>(B2<const float*>(ds1), sc(1),
-                                            B2<const VGParams*>(w[0].vg.params, w[1].vg.params), ds1f,
-                                            sc(2));  // driver :1374-1375
-  voxel_grid(B2<const float*>(ds1f), sc(2), cap, leaf, both<float*>(w, [](const CloudWS& c) { return c.ds2; }), sc(3),
-             vg, st, mode, 2);  // driver :1377-1387
+  auto sc = [&](int i) { return all_of<uint32_t*>(w, nc, [i](const CloudWS& c) { return c.sc + i; }); };
+  const B4<VGBufs> vg = all_of<VGBufs>(w, nc, [](const CloudWS& c) { return c.vg; });
+  const B4<float*> ds1 = all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1; });
+  const B4<float*> ds1f = all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1f; });
+  k_finite_fix<<<dim3(1, nc), 1024, 0, st>>>(B4<const float*>(ds1), sc(1),
+                                             all_of<const VGParams*>(w, nc, [](const CloudWS& c) { return (const VGParams*)c.vg.params; }),
+                                             ds1f, sc(2));  // driver :1374-1375
+  voxel_grid(B4<const float*>(ds1f), sc(2), cap, leaf, all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds2; }),
+             sc(3), vg, st, mode, nc);  // driver :1377-1387
 }
-void seg_faces(CloudWS* w, const fccf_params& P, hipStream_t st) {
+// PG: row P, the face stage sharded over a group's ranks by Morton range (group.cpp)
+void seg_faces(CloudWS* w, int nc, const fccf_params& P, hipStream_t st, Group* PG = nullptr) {
   const uint32_t cap = w[0].cap;
-  const B2<FaceBufs> fb(w[0].fb, w[1].fb);
-  const B2<const uint32_t*> m2(w[0].sc + 3, w[1].sc + 3);
-  face_voxels_prepare(both<const float*>(w, [](const CloudWS& c) { return (const float*)c.ds2; }), m2, cap,
-                      (double)P.face_voxel_size, fb, st, 2);
+  const B4<FaceBufs> fb = all_of<FaceBufs>(w, nc, [](const CloudWS& c) { return c.fb; });
+  const B4<const uint32_t*> m2 = all_of<const uint32_t*>(w, nc, [](const CloudWS& c) { return (const uint32_t*)c.sc + 3; });
+  if (PG) {
+    face_voxels_sharded(PG, all_of<const float*>(w, nc, [](const CloudWS& c) { return (const float*)c.ds2; }), m2, cap,
+                        (double)P.face_voxel_size, P.voxel_point_threshold, P.curvature_threshold,
+                        all_of<float*>(w, nc, [](const CloudWS& c) { return c.resid; }), fb, st, nc);
+    return;
+  }
+  face_voxels_prepare(all_of<const float*>(w, nc, [](const CloudWS& c) { return (const float*)c.ds2; }), m2, cap,
+                      (double)P.face_voxel_size, fb, st, nc);
   face_voxels_fit(m2, cap, P.voxel_point_threshold, P.curvature_threshold,
-                  both<float*>(w, [](const CloudWS& c) { return c.resid; }), fb, st, 2);
+                  all_of<float*>(w, nc, [](const CloudWS& c) { return c.resid; }), fb, st, nc);
 }
 // The residual cloud of the driver source is fine_verify's S1 (:788-805): its
 // octree bounds do not depend on any candidate, so they are replayed after the
@@ -256,12 +271,10 @@ struct PhaseB {
 // State of the registration whose clouds occupy CloudSet s.
 struct PipeSet {
   PhaseB pb;
-  CloudWS w[2];
+  CloudWS w[2];          // this pair's two clouds (inside its stage group's arena)
   int64_t nin[2] = {0, 0};
   uint32_t cap[2] = {1, 1};
   float* cen = nullptr;  // both cloud centroids: cloud k at cen[3k .. 3k+2]
-  XsBufs xs;             // their exact-sum scratch (6 rows)
-  VGEntry entry;         // arguments of pass 1's entry kernel, patched into g_seg[0] per call
   bool staged = false;   // host inputs copied by stage_inputs (ev_in0 .. ev_in time the H2D)
   clk::time_point t_enq;
   // the pair's device inputs and leaf, for a redo of the stage (VG_REDO)
@@ -269,6 +282,11 @@ struct PipeSet {
   int64_t in_nsrc = 0, in_ntar = 0;
   float leaf = 0.f;
   uint32_t sharded = 0;  // FCCF_SHARDED_* of the cloud stage (row D)
+  // (slot 2G only) the stage group's last stage: how many pairs, the entry kernel's
+  // arguments (patched into g_seg per call) and the centroid sums' scratch
+  int group_pairs = 0;
+  VGEntry entry;
+  XsBufs xs;
 };
 
 PipeSet& pset(fccf_ctx* c, int s) {
@@ -301,99 +319,166 @@ Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   return {ds, dt};
 }
 
-// Phase A: enqueue the cloud device stage of one pair on CloudSet s (returns at
-// once).  src/tar are device clouds (staged ones wait for ev_in).  cloud 0 = driver
-// source = TAR file; cloud 1 = driver target = SRC file (:1683).
+// Phase A: enqueue the cloud device stage of the pairs in[0 .. P) (P = 1 or 2) of
+// stage group G, pair j on slot 2G + j (returns at once).  src/tar are device clouds
+// (staged ones wait for their slot's ev_in).  Per pair: cloud 0 = driver source = TAR
+// file; cloud 1 = driver target = SRC file (:1683).
 // exact2: the driver's pass as VG_PRESORTED, eagerly (the redo of a stage whose
 // optimistic second pass found its input out of leaf order; rare).
-void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
-                    bool staged, float leaf, const fccf_params& P, bool exact2 = false) {
-  auto& cs = c->cs[s];
-  PipeSet& ps = pset(c, s);
-  ps.t_enq = clk::now();
-  ps.in_src = src;
-  ps.in_tar = tar;
-  ps.in_nsrc = n_src;
-  ps.in_ntar = n_tar;
-  ps.leaf = leaf;
-  CloudWS* w = ps.w;
-  ps.nin[0] = n_tar;
-  ps.nin[1] = n_src;
-  const float* hin[2] = {tar, src};
-  // both clouds get the larger capacity, so their workspaces are laid out alike
-  // (batched launches address cloud 1 at a fixed offset from cloud 0)
-  const uint32_t capmax = (uint32_t)std::max<int64_t>(std::max(ps.nin[0], ps.nin[1]), 1);
-  ps.cap[0] = ps.cap[1] = capmax;
+struct PairIn {
+  const float *src, *tar;
+  int64_t n_src, n_tar;
+  bool staged;
+};
+void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float leaf, const fccf_params& Pa,
+                          bool exact2 = false) {
+  if (P < 1 || P > 2 || (P > 1 && c->group)) throw Error(FCCF_E_INTERNAL, "cloud stage: 1 pair, or 2 without a group");
+  auto& cg = c->cs[2 * G];  // the group's arena, stage graphs and fork/join events
+  PipeSet& gs = pset(c, 2 * G);
+  const int nc = 2 * P;
   hipStream_t st0 = c->sa[0], ss = c->sa[2];
-  // the previous pair on this set may still be in fine verification, which reads
-  // this workspace (residual clouds, S1 octree state): the stage waits for it
-  guarded_stream_wait(st0, cs.ev[3]);  // ev[3] is recorded on the fine stream (captured by phase B)
-  cs.arena.ensure(2 * cloud_bytes(capmax, false) + exact_sum_bytes(6, capmax) + (1 << 20));
-  cs.arena.reset();
-  // The inputs (caller-owned device clouds, or the staged copies of host arrays) are
-  // read in place: their pointers and counts are patched into pass 1's entry kernel
-  // node.
-  const float* xin[2] = {nullptr, nullptr};
-  uint32_t nv[2] = {0, 0};
-  ps.cen = cs.arena.take_n<float>(8);
-  ps.xs = exact_sum_carve(cs.arena.take(exact_sum_bytes(6, capmax)), 6, capmax);
+  // both clouds get the larger capacity (all clouds of a stage, in fact), so their
+  // workspaces are laid out alike (batched launches address cloud e at a fixed offset)
+  uint32_t capmax = 1;
+  for (int j = 0; j < P; ++j)
+    capmax = (uint32_t)std::max<int64_t>(capmax, std::max(in[j].n_src, in[j].n_tar));
+  // the previous pairs on these slots may still be in fine verification, which reads
+  // this workspace (residual clouds, S1 octree state): the stage waits for them
+  for (int j = 0; j < 2; ++j) guarded_stream_wait(st0, c->cs[2 * G + j].ev[3]);  // (recorded on the fine stream)
+  cg.arena.ensure(nc * cloud_bytes(capmax, false) + exact_sum_bytes(3 * nc, capmax) + (1 << 20));
+  cg.arena.reset();
+  float* cen = cg.arena.take_n<float>(3 * BMAX + 4);
+  gs.xs = exact_sum_carve(cg.arena.take(exact_sum_bytes(3 * nc, capmax)), 3 * nc, capmax);
   // Row D: with a group, large clouds shard their K1 sort after its first rounds
   // (introsort.hip, group.cpp); the stage then runs eagerly (a host step between the
   // sort and the gather of the sorted slices)
   Group* const DG = shard_sort_enabled(c->group, capmax, introsort_rounds(capmax)) ? c->group : nullptr;
-  ps.sharded = DG ? FCCF_SHARDED_SORT : 0u;
-  for (int k = 0; k < 2; ++k) {
-    w[k] = CloudWS();
-    carve_cloud(cs.arena, w[k], capmax, false);
-    w[k].vg.is.inject = c->d_flags;     // (test hook; a constant pointer per ctx)
-    if (DG) {
-      w[k].vg.is.shard_n = (uint32_t)DG->n;
-      w[k].vg.is.shard_rank = (uint32_t)DG->rank;
-      w[k].vg.is.shard_r0 = (uint32_t)shard_sort_r0(DG->n);
-      w[k].vg.is.shard_group = DG;
+  // Row P shards with row D (FCCF_SHARD_P=0 keeps the face stage whole)
+  const char* pe = std::getenv("FCCF_SHARD_P");
+  Group* const PG = (DG && capmax >= 8192 && !(pe && pe[0] == '0')) ? DG : nullptr;
+  CloudWS w[BMAX];
+  const float* xin[BMAX] = {};
+  uint32_t nv[BMAX] = {};
+  for (int j = 0; j < P; ++j) {
+    PipeSet& ps = pset(c, 2 * G + j);
+    ps.t_enq = clk::now();
+    ps.in_src = in[j].src;
+    ps.in_tar = in[j].tar;
+    ps.in_nsrc = in[j].n_src;
+    ps.in_ntar = in[j].n_tar;
+    ps.leaf = leaf;
+    ps.staged = in[j].staged;
+    ps.nin[0] = in[j].n_tar;
+    ps.nin[1] = in[j].n_src;
+    ps.cap[0] = ps.cap[1] = capmax;
+    ps.cen = cen + 6 * j;
+    ps.sharded = (DG ? FCCF_SHARDED_SORT : 0u) | (PG ? FCCF_SHARDED_FACES : 0u);
+    const float* hin[2] = {in[j].tar, in[j].src};
+    for (int k = 0; k < 2; ++k) {
+      CloudWS& x = w[2 * j + k];
+      x = CloudWS();
+      carve_cloud(cg.arena, x, capmax, false);
+      x.vg.is.inject = c->d_flags;  // (test hook; a constant pointer per ctx)
+      if (DG) {
+        x.vg.is.shard_n = (uint32_t)DG->n;
+        x.vg.is.shard_rank = (uint32_t)DG->rank;
+        x.vg.is.shard_r0 = (uint32_t)shard_sort_r0(DG->n);
+        x.vg.is.shard_group = DG;
+      }
+      x.fb.centroid = cen + 3 * (2 * j + k);  // exact_sum_n writes cloud e's centroid to out[3e .. 3e+2]
+      nv[2 * j + k] = (uint32_t)ps.nin[k];
+      xin[2 * j + k] = hin[k];
+      ps.w[k] = x;
     }
-    w[k].fb.centroid = ps.cen + 3 * k;  // exact_sum2 writes out[3k .. 3k+2]
-    nv[k] = (uint32_t)ps.nin[k];
-    xin[k] = hin[k];
+    // host inputs: staged by stage_inputs() into the slot's inarena on the copy stream
+    if (in[j].staged) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[2 * G + j].ev_in, 0));
   }
-  // host inputs: staged by stage_inputs() into cs.inarena on the copy stream
-  ps.staged = staged;
-  if (staged) HIP_CHECK(hipStreamWaitEvent(st0, cs.ev_in, 0));
+  gs.group_pairs = P;
   struct {
     const void* base;
     size_t acap;
     uint32_t cap;
+    int32_t pairs;
     float leaf, fvs, vpt, ct, fine_res;
-  } key = {cs.arena.base, cs.arena.cap, capmax, leaf, P.face_voxel_size, P.voxel_point_threshold,
-           P.curvature_threshold, P.fine_verify_voxel_size};
-  ps.entry.xyz = B2<const float*>(xin[0], xin[1]);
-  ps.entry.n = B2<uint32_t>(nv[0], nv[1]);
-  ps.entry.bind();
+  } key = {cg.arena.base, cg.arena.cap, capmax, P, leaf, Pa.face_voxel_size, Pa.voxel_point_threshold,
+           Pa.curvature_threshold, Pa.fine_verify_voxel_size};
+  // The inputs (caller-owned device clouds, or the staged copies of host arrays) are
+  // read in place: their pointers and counts are patched into pass 1's entry kernel
+  // node.
+  {
+    const float* x[BMAX];
+    uint32_t n[BMAX];
+    for (int e = 0; e < BMAX; ++e) {
+      x[e] = xin[e < nc ? e : nc - 1];
+      n[e] = e < nc ? nv[e] : 0u;
+    }
+    gs.entry.xyz = B4<const float*>(x[0], x[1], x[2], x[3]);
+    gs.entry.n = B4<uint32_t>(n[0], n[1], n[2], n[3]);
+  }
+  gs.entry.bind();
   // The whole cloud stage is ONE graph: both VoxelGrid passes, then the centroid sums
   // forked onto ss beside the face voxels, joined before the orientation.  ROCm 7.2
   // runs the two branches of a replay concurrently (tools/graph_fork_probe.hip).  The
   // device spans come from s_memrealtime stamps the stage's kernels write (no timing
   // events, which would split the graph: four graphs with events between them were
   // 0.04 ms per registration slower).
-  CloudMail* cmail = &host_mail(c)->clouds[s];  // allocated on first use: never inside the capture
-  cs.g_seg[0].run(&key, sizeof key, st0, [&] {
-    seg_pass1(w, xin, nv, leaf, st0, &ps.entry);
-    seg_downsample(w, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
-    HIP_CHECK(hipEventRecord(cs.ev[6], st0));
-    HIP_CHECK(hipStreamWaitEvent(ss, cs.ev[6], 0));
-    exact_sum2(w[0].ds2, w[0].sc + 3, w[1].ds2, w[1].sc + 3, 3, 3, ps.cen, true, ps.xs, ss);  // compute3DCentroid (:473)
-    HIP_CHECK(hipEventRecord(cs.ev[7], ss));
-    seg_faces(w, P, st0);
-    HIP_CHECK(hipStreamWaitEvent(st0, cs.ev[7], 0));
-    face_voxels_orient(capmax, B2<VoxRec*>(w[0].planar, w[1].planar), B2<FaceBufs>(w[0].fb, w[1].fb), st0, 2,
-                       cmail, B2<const uint32_t*>(w[0].sc, w[1].sc));
-  }, vg_entry_kernel(), ps.entry.args, DG != nullptr || exact2);
-  // external signal for stage_inputs (this set's inputs have been read): after the graph
-  HIP_CHECK(hipEventRecord(cs.ev[0], st0));
-  HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
-  cs.g_rep.run(&key, sizeof key, st0, [&] { seg_s1_replay(w, P, st0); });
-  HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
+  CloudMail* cmail = &host_mail(c)->clouds[2 * G];  // (slots 2G, 2G + 1 adjacent); never allocated inside the capture
+  const XsBufs xs = gs.xs;
+  cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
+    seg_pass1(w, nc, xin, nv, leaf, st0, &gs.entry);
+    seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
+    HIP_CHECK(hipEventRecord(cg.ev[6], st0));
+    HIP_CHECK(hipStreamWaitEvent(ss, cg.ev[6], 0));
+    const float* d2[BMAX];
+    const uint32_t* n2[BMAX];
+    for (int e = 0; e < nc; ++e) {
+      d2[e] = w[e].ds2;
+      n2[e] = w[e].sc + 3;
+    }
+    exact_sum_n(d2, n2, nc, 3, 3, cen, true, xs, ss);  // compute3DCentroid (:473)
+    HIP_CHECK(hipEventRecord(cg.ev[7], ss));
+    seg_faces(w, nc, Pa, st0, PG);
+    HIP_CHECK(hipStreamWaitEvent(st0, cg.ev[7], 0));
+    face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
+                       all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), st0, nc, cmail,
+                       all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
+  }, vg_entry_kernel(), gs.entry.args, DG != nullptr || exact2);
+  for (int j = 0; j < P; ++j) {
+    auto& cs = c->cs[2 * G + j];
+    PipeSet& ps = pset(c, 2 * G + j);
+    // external signal for stage_inputs (this slot's inputs have been read): after the graph
+    HIP_CHECK(hipEventRecord(cs.ev[0], st0));
+    HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
+    // (keyed by the pointers the replay reads: the layout of a one-pair and a two-pair
+    // stage differ, and a replay with another layout's pointers reads a stale count)
+    struct {
+      const void *resid, *nresid, *aggr, *state;
+      uint32_t cap;
+      float res;
+    } rkey = {ps.w[0].resid, ps.w[0].fb.nresid, ps.w[0].faggr, ps.w[0].fstate, capmax, Pa.fine_verify_voxel_size};
+    cs.g_rep.run(&rkey, sizeof rkey, st0, [&] { seg_s1_replay(ps.w, Pa, st0); });
+    HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
+  }
   HIP_CHECK(hipGetLastError());
+}
+
+// One pair on slot s (s even: its group's first slot)
+void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
+                    bool staged, float leaf, const fccf_params& P, bool exact2 = false) {
+  const PairIn in{src, tar, n_src, n_tar, staged};
+  clouds_enqueue_group(c, s / 2, 1, &in, leaf, P, exact2);
+}
+
+// The redo of slot s's stage group (VG_REDO): the same pairs, exact second pass
+void clouds_redo(fccf_ctx* c, int s, const fccf_params& P) {
+  const int G = s / 2;
+  const int np = pset(c, 2 * G).group_pairs;
+  PairIn in[2];
+  for (int j = 0; j < np; ++j) {
+    const PipeSet& ps = pset(c, 2 * G + j);
+    in[j] = PairIn{ps.in_src, ps.in_tar, ps.in_nsrc, ps.in_ntar, ps.staged};
+  }
+  clouds_enqueue_group(c, G, np, in, pset(c, s).leaf, P, true);
 }
 
 // Phase B1: everything after the cloud stage of the pair on CloudSet s up to the
@@ -419,14 +504,20 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
   c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
-  HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+  {
+    // (under the capture lock: with two pairs per stage, the second pair's B1 runs while
+    // the helper thread may be capturing the next stage on the stream ev[4] was recorded
+    // on, and HIP refuses to synchronize such an event; ev[4] is complete by then)
+    std::lock_guard<std::mutex> lk(capture_mutex());
+    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+  }
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
   std::memcpy(fsc, cm.fsc, sizeof fsc);
   if ((fsc[0][1] | fsc[1][1]) & VG_REDO) {
     // the driver's pass found main's output out of leaf order (optimistic mode ran no
     // sort): the stage again with the exact second pass, before the next pair is enqueued
-    clouds_enqueue(c, s, ps.in_src, ps.in_nsrc, ps.in_tar, ps.in_ntar, ps.staged, ps.leaf, P, true);
+    clouds_redo(c, s, P);
     HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
     std::memcpy(sc, cm.sc, sizeof sc);
     std::memcpy(fsc, cm.fsc, sizeof fsc);
@@ -1202,50 +1293,70 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
   } join_guard{c};
   if (c->group) order_reset(c->group);
-  // Host inputs: pair i+1's clouds are staged on the copy stream at the start of
-  // pair i (from the helper thread: the pageable copy blocks its caller), so the host
-  // link works while pair i's cloud stage runs.
+  // Pairs per cloud stage: two -- both pairs' four clouds in the same launches, so the
+  // sort's dependent rounds and the face stage's small launches are paid once for both
+  //  -- unless a group is attached (its sharded sort gathers one pair's
+  // slices), a probe runs (its launch records count one pair), or FCCF_PAIR_BATCH=1.
+  const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
+  const bool one_pair = pb_env && pb_env[0] == '1';
+  const int PP = (c->group || c->probe.on() || one_pair) ? 1 : 2;
+  const int ng = (n + PP - 1) / PP;  // stage groups; group g uses slots 2 (g & 1) + j
+  auto cnt = [&](int g) { return std::min(PP, n - g * PP); };
+  auto slot = [&](int i) { return 2 * ((i / PP) & 1) + i % PP; };
+  // Host inputs: group g+1's clouds are staged on the copy stream at the start of
+  // group g (from the helper thread: the pageable copy blocks its caller), so the host
+  // link works while group g's cloud stage runs.
   std::vector<Staged> in(on_device ? 0 : n);
   auto dsrc = [&](int i) { return on_device ? src[i] : in[(size_t)i].src; };
   auto dtar = [&](int i) { return on_device ? tar[i] : in[(size_t)i].tar; };
-  if (!on_device) in[0] = stage_inputs(c, 0, src[0], n_src[0], tar[0], n_tar[0]);
-  clouds_enqueue(c, 0, dsrc(0), n_src[0], dtar(0), n_tar[0], !on_device, leaf, P);
-  // pair i: B1 (its clouds done -> enqueue pair i+1's clouds -> host stages ->
-  // launch fine verification), then B2 of pair i-1, whose fine verification ran
-  // on the GPU during pair i's host stages
-  for (int i = 0; i < n; ++i) {
-    const int s = i & 1;
-    c->enq.wait();  // this pair's cloud stage is fully enqueued (its events recorded)
-    if (!on_device && i + 1 < n) {
-      auto stage = [c, s, i, src, n_src, tar, n_tar, &in] {
-        HIP_CHECK(hipSetDevice(c->device));
-        in[(size_t)i + 1] = stage_inputs(c, s ^ 1, src[i + 1], n_src[i + 1], tar[i + 1], n_tar[i + 1]);
-      };
-      if (c->probe.on()) stage();
-      else c->enq.submit(stage);
+  auto stage_group = [c, &in, src, n_src, tar, n_tar, cnt, slot, PP](int g) {
+    HIP_CHECK(hipSetDevice(c->device));
+    for (int j = 0; j < cnt(g); ++j) {
+      const int i = g * PP + j;
+      in[(size_t)i] = stage_inputs(c, slot(i), src[i], n_src[i], tar[i], n_tar[i]);
     }
-    phase_b1(c, s, P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
-      if (i + 1 >= n) return;
-      // the next pair's cloud stage is enqueued from a helper thread while this
-      // thread runs the host stages (launches are ~60 us of host time); probed
-      // runs stay on this thread (the probe's launch records are not shared)
-      auto enq = [c, s, i, n_src, n_tar, on_device, leaf, &P, dsrc, dtar] {
-        HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
-        clouds_enqueue(c, s ^ 1, dsrc(i + 1), n_src[i + 1], dtar(i + 1), n_tar[i + 1], !on_device, leaf, P);
-      };
-      if (c->probe.on()) {
-        enq();
-      } else {
-        // with a group, the helper's sharded-sort gather (CH_CLOUD) waits until this
-        // pair's B1 has issued its CH_MATCH / CH_FINE collectives: one issue order per rank
-        if (c->group) order_need(c->group, i + 1);
-        c->enq.submit(enq);  // (after the staging task, which submit() joins first)
-      }
-    });
-    if (i > 0) phase_b2(c, s ^ 1);
+  };
+  auto enq_group = [c, n_src, n_tar, on_device, leaf, &P, dsrc, dtar, cnt, PP](int g) {
+    HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
+    PairIn pin[2];
+    for (int j = 0; j < cnt(g); ++j) {
+      const int i = g * PP + j;
+      pin[j] = PairIn{dsrc(i), dtar(i), n_src[i], n_tar[i], !on_device};
+    }
+    clouds_enqueue_group(c, g & 1, cnt(g), pin, leaf, P);
+  };
+  if (!on_device) stage_group(0);
+  enq_group(0);
+  // pair i: B1 (its clouds done -> the first pair of a group enqueues the next group's
+  // clouds -> host stages -> launch fine verification), then B2 of pair i-1, whose fine
+  // verification ran on the GPU during pair i's host stages
+  for (int g = 0; g < ng; ++g) {
+    c->enq.wait();  // this group's cloud stage is fully enqueued (its events recorded)
+    if (!on_device && g + 1 < ng) {
+      if (c->probe.on()) stage_group(g + 1);
+      else c->enq.submit([stage_group, g] { stage_group(g + 1); });
+    }
+    for (int j = 0; j < cnt(g); ++j) {
+      const int i = g * PP + j;
+      phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
+        if (j != 0 || g + 1 >= ng) return;
+        // the next group's cloud stage is enqueued from a helper thread while this
+        // thread runs the host stages (launches are ~60 us of host time); probed
+        // runs stay on this thread (the probe's launch records are not shared)
+        if (c->probe.on()) {
+          enq_group(g + 1);
+        } else {
+          // with a group, the helper's sharded-sort gather (CH_CLOUD) waits until this
+          // pair's B1 has issued its CH_MATCH / CH_FINE collectives: one issue order per rank
+          if (c->group) order_need(c->group, i + 1);
+          c->enq.submit([enq_group, g] { enq_group(g + 1); });  // (after the staging task, which submit() joins first)
+        }
+      });
+      if (i > 0) phase_b2(c, slot(i - 1));
+    }
   }
   c->enq.wait();
-  phase_b2(c, (n - 1) & 1);
+  phase_b2(c, slot(n - 1));
   join_guard.armed = false;
   if (c->group) order_reset(c->group);
 }

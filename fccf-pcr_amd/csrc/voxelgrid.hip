@@ -14,6 +14,7 @@
 #include "probe.h"
 #include "kernels.h"
 #include "group.h"
+#include "ctx.h"
 
 namespace fccf {
 namespace {
@@ -34,8 +35,8 @@ __device__ __forceinline__ float wave_max(float v) {
 // Tag: 0 = a first pass (the patched entry node), 1 = a presorted second pass, so the
 // two passes are distinct kernels when one graph holds both.
 template <int Tag>
-__global__ void __launch_bounds__(256) k_vg_bbox(B2<const float*> xyz2, B2<uint32_t*> d_n2, B2<uint32_t> n2,
-                                                 int set_n, B2<float*> part2, B2<VGParams*> P2) {
+__global__ void __launch_bounds__(256) k_vg_bbox(B4<const float*> xyz2, B4<uint32_t*> d_n2, B4<uint32_t> n2,
+                                                 int set_n, B4<float*> part2, B4<VGParams*> P2) {
   KT();
   __shared__ float sh[4][7];
   const int e = blockIdx.y;
@@ -195,9 +196,9 @@ __device__ __forceinline__ uint32_t vg_key(const VGParams& q, float x, float y, 
 // strictly above its predecessor -- or any non-finite point -- sets P->unsorted;
 // otherwise every leaf holds exactly one point and the pass is the identity (the
 // sort tail, segmentation and centroid kernels take their shortcut).
-__global__ void __launch_bounds__(256) k_vg_keys(B2<const uint32_t*> d_n2, B2<VGParams*> P2,
-                                                 B2<uint32_t*> keys2, B2<uint32_t*> vals2, int presorted,
-                                                 B2<const float*> part2, int nparts, float leaf) {
+__global__ void __launch_bounds__(256) k_vg_keys(B4<const uint32_t*> d_n2, B4<VGParams*> P2,
+                                                 B4<uint32_t*> keys2, B4<uint32_t*> vals2, int presorted,
+                                                 B4<const float*> part2, int nparts, float leaf) {
   KT();
   const int e = blockIdx.y;
   VGParams* P = P2[e];
@@ -253,11 +254,11 @@ __global__ void __launch_bounds__(256) k_vg_keys(B2<const uint32_t*> d_n2, B2<VG
 // dependent chain); each block's 256 centroids are staged in LDS and written as
 // coalesced 16-byte words.  The pass-through cases are flat 16-byte copies.
 constexpr int CL = 4;
-__global__ void __launch_bounds__(256) k_vg_centroid(B2<const uint32_t*> d_n2, B2<VGParams*> P2, B2<const uint32_t*> vals2,
-                                                     B2<const uint32_t*> starts2, B2<const uint32_t*> d_nseg2,
-                                                     B2<float*> out2, B2<uint32_t*> d_m2, int presorted,
-                                                     B2<float*> copy2, B2<const uint32_t*> inject2,
-                                                     B2<const float*> xyzs2) {
+__global__ void __launch_bounds__(256) k_vg_centroid(B4<const uint32_t*> d_n2, B4<VGParams*> P2, B4<const uint32_t*> vals2,
+                                                     B4<const uint32_t*> starts2, B4<const uint32_t*> d_nseg2,
+                                                     B4<float*> out2, B4<uint32_t*> d_m2, int presorted,
+                                                     B4<float*> copy2, B4<const uint32_t*> inject2,
+                                                     B4<const float*> xyzs2) {
   KT();
   const int e = blockIdx.y;
   const VGParams q = *P2[e];
@@ -384,22 +385,23 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 const void* vg_entry_kernel() { return (const void*)k_vg_bbox<0>; }
 
-void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float leaf, B2<float*> out,
-                B2<uint32_t*> d_m, B2<VGBufs> b, hipStream_t st, int presorted, int nbatch, B2<float*> out_copy,
+void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float leaf, B4<float*> out,
+                B4<uint32_t*> d_m, B4<VGBufs> b, hipStream_t st, int presorted, int nbatch, B4<float*> out_copy,
                 const uint32_t* n_in, VGEntry* entry) {
-  const B2<const uint32_t*> d_n(d_nw[0], d_nw[1]);
-  auto F = [&](auto get) { return B2<decltype(get(b[0]))>(get(b[0]), get(b[1])); };
-  const B2<VGParams*> P = F([](const VGBufs& v) { return v.params; });
-  const B2<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
-  const B2<uint32_t*> k1 = F([](const VGBufs& v) { return v.k1; }), v1 = F([](const VGBufs& v) { return v.v1; });
-  const B2<uint32_t*> starts = F([](const VGBufs& v) { return v.starts; }), nseg = F([](const VGBufs& v) { return v.nseg; });
-  const B2<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
-  const B2<const uint32_t*> nbits(&b[0].params->nbits, &b[1].params->nbits);
+  const B4<const uint32_t*> d_n(d_nw);
+  // one field of every problem's buffers (entries past nbatch repeat the caller's last)
+  auto F = [&](auto get) { return B4<decltype(get(b[0]))>(get(b[0]), get(b[1]), get(b[2]), get(b[3])); };
+  const B4<VGParams*> P = F([](const VGBufs& v) { return v.params; });
+  const B4<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
+  const B4<uint32_t*> k1 = F([](const VGBufs& v) { return v.k1; }), v1 = F([](const VGBufs& v) { return v.v1; });
+  const B4<uint32_t*> starts = F([](const VGBufs& v) { return v.starts; }), nseg = F([](const VGBufs& v) { return v.nseg; });
+  const B4<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
   const dim3 g(grid_for(cap), nbatch);
   VGEntry en;
   en.xyz = xyz;
   en.d_n = d_nw;
-  en.n = n_in ? B2<uint32_t>(n_in[0], nbatch > 1 ? n_in[1] : 0u) : B2<uint32_t>(0u);
+  en.n = B4<uint32_t>(0u);
+  for (int e = 0; n_in && e < nbatch; ++e) en.n.v[e] = n_in[e];
   en.set_n = n_in ? 1 : 0;
   en.part = F([](const VGBufs& v) { return v.part; });
   en.P = P;
@@ -412,9 +414,9 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
     *entry = en;
     entry->bind();
   }
-  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts
+  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts (probed calls batch <= 2)
   const uint32_t* m2 = nbatch > 1 ? d_m[1] : nullptr;
-  const B2<const uint32_t*> unsorted(&b[0].params->unsorted, &b[1].params->unsorted);
+  const B4<const uint32_t*> unsorted = F([](const VGBufs& v) { return (const uint32_t*)&v.params->unsorted; });
   // the keys kernel also derives the parameters (k_vg_params folded in): each of its
   // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
   const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
@@ -423,31 +425,31 @@ void voxel_grid(B2<const float*> xyz, B2<uint32_t*> d_nw, uint32_t cap, float le
   // centroid reads each leaf's members contiguously; not for a sharded sort (each rank
   // finishes only its range, and the gather moves keys and values only)
   const bool sorted_pts = !presorted && b[0].is.shard_n <= 1;
-  B2<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
+  B4<IsBufs> isb = F([](const VGBufs& v) { return v.is; });
   if (sorted_pts) {
-    isb.v[0].xyzs = b[0].xyzs;
-    if (nbatch > 1) isb.v[1].xyzs = b[1].xyzs;
+    for (int e = 0; e < BMAX; ++e) isb.v[e].xyzs = b[e].xyzs;
   }
-  const B2<const float*> xyzs = sorted_pts ? B2<const float*>(b[0].xyzs, nbatch > 1 ? b[1].xyzs : nullptr)
-                                           : B2<const float*>(nullptr);
-  const B2<const VGParams*> Pc(P[0], P[1]);
+  const B4<const float*> xyzs = sorted_pts ? F([](const VGBufs& v) { return (const float*)v.xyzs; })
+                                           : B4<const float*>(nullptr);
+  const B4<const VGParams*> Pc(P);
   if (!presorted) {
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, false);
-    if (b[0].is.shard_n > 1) {  // row D: every rank's sorted slice, gathered in rank order
+    if (b[0].is.shard_n > 1) {  // row D: every rank's sorted slice, gathered in rank order (one pair)
+      if (nbatch > 2) throw Error(FCCF_E_INTERNAL, "sharded sort: one pair per cloud stage");
       uint32_t* const kk[2] = {k0[0], k0[1]};
       uint32_t* const vv[2] = {v0[0], v0[1]};
       const uint32_t* const bb[2] = {b[0].is.bounds, b[1].is.bounds};
       shard_gather_sorted((Group*)b[0].is.shard_group, kk, vv, bb, nbatch, st);
     }
-    segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
+    segment_heads_u32(B4<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B4<uint32_t*>(nullptr),
                       nbatch);
   } else if (presorted == VG_PRESORTED) {  // usually already in leaf order: a sort and segmentation that run only if not
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, true);
-    segment_heads_u32(B2<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B2<uint32_t*>(nullptr),
+    segment_heads_u32(B4<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B4<uint32_t*>(nullptr),
                       nbatch, unsorted);
   }
-  const B2<const uint32_t*> inj(b[0].is.inject, b[1].is.inject);
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B2<const uint32_t*>(v0), B2<const uint32_t*>(starts), B2<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
+  const B4<const uint32_t*> inj = F([](const VGBufs& v) { return v.is.inject; });
+  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B4<const uint32_t*>(v0), B4<const uint32_t*>(starts), B4<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
 }
 
 }  // namespace fccf

@@ -108,6 +108,8 @@ _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctype
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
 _sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
+if hasattr(_lib, "fccf_debug_sort_rounds"):  # (dev A/B runs load older builds through FCCF_LIB)
+    _sig("fccf_debug_sort_rounds", ctypes.c_int, _P, _P)
 _sig("fccf_debug_inject_sort_fault", ctypes.c_int, _P, ctypes.c_uint32)
 _sig("fccf_debug_capture_race", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, _P)
 _sig("fccf_ply_read", ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_float)),
@@ -330,6 +332,12 @@ class Ctx:
         return dict(n=int(a[0]), flags=int(a[2]), global_parts=int(a[3]), lds_segments=int(a[4]),
                     block_parts=int(a[5]), wave_parts=int(a[6]), heaps=int(a[7]), depth0_distinct=int(a[9]),
                     wave_tasks=int(a[16]) + int(a[18]), raw=a)
+
+    def sort_rounds(self) -> np.ndarray:
+        """Round records of the last sort_keys: rows {segments, tiles, owned so far, elements}."""
+        a = np.zeros(96, np.uint32)
+        _check(_lib.fccf_debug_sort_rounds(self._h, a.ctypes.data), "fccf_debug_sort_rounds", self._h)
+        return a.reshape(24, 4)
 
     def capture_race(self, hold_ms: int = 200, guard: bool = True) -> dict:
         """Test hook: a graph capture held for hold_ms concurrent with another thread's

@@ -154,3 +154,37 @@ def downsample_sharded(ctx, xyz_slice, leaf: float, rank: int, world: int, gathe
     if whole.shape[0] == 0:
         return np.zeros((0, 3), np.float32)
     return ctx.downsample(whole, leaf)
+
+
+# ---------------------------------------------------------------- row P (face stage)
+FACE_BINS_LG = 12  # facefit.hip FACE_BINS_LG
+
+
+def face_bin_bounds(codes, nbits: int, world: int) -> np.ndarray:
+    """Row P's split (group.cpp face_voxels_sharded, facefit.hip k_face_range): the
+    points' leaf codes binned by their top FACE_BINS_LG bits (a leaf's points share one
+    code, so a bin never splits a leaf); bound j = the first bin b whose preceding
+    points * world >= j * n; rank r takes bins [bounds[r], bounds[r + 1])."""
+    shift = max(0, int(nbits) - FACE_BINS_LG)
+    c = np.asarray(codes, np.uint64)
+    hist = np.bincount((c >> np.uint64(shift)).astype(np.int64) & ((1 << FACE_BINS_LG) - 1),
+                       minlength=1 << FACE_BINS_LG)
+    before = np.concatenate([[0], np.cumsum(hist)[:-1]]).astype(np.int64)
+    n = int(c.size)
+    b = np.full(world + 1, 1 << FACE_BINS_LG, np.int64)
+    b[0] = 0
+    for j in range(1, world):
+        hit = np.flatnonzero(before * world >= j * n)
+        b[j] = hit[0] if hit.size else 1 << FACE_BINS_LG
+    return b
+
+
+def face_rank_points(codes, nbits: int, rank: int, world: int) -> np.ndarray:
+    """The input positions of rank `rank`'s points in leaf order: its bins' points in
+    input order, stably sorted by code (PCL's insertion order within a leaf)."""
+    c = np.asarray(codes, np.uint64)
+    shift = max(0, int(nbits) - FACE_BINS_LG)
+    b = face_bin_bounds(c, nbits, world)
+    bins = (c >> np.uint64(shift)).astype(np.int64) & ((1 << FACE_BINS_LG) - 1)
+    mine = np.flatnonzero((bins >= b[rank]) & (bins < b[rank + 1]))
+    return mine[np.argsort(c[mine], kind="stable")]

@@ -288,6 +288,9 @@ int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exa
  * where |x| is beyond its argument reduction. */
 int fccf_debug_sincos(fccf_ctx* ctx, const double* x, int64_t n, double* s, double* c, uint32_t* ok);
 int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
+/* Test hook: the round records of the last fccf_debug_sort_keys, 24 x {segments
+ * partitioned, their tiles, owned segments so far, elements partitioned}. */
+int fccf_debug_sort_rounds(fccf_ctx* ctx, uint32_t out[96]);
 /* Test hook: every later sort of K1 on ctx raises the invariant flags in bits (0x100
  * round scatter outside its segment, 0x200 block item guard, 0x400 wave task stack,
  * 0x1000 block partition stack) as if the check had fired, until called with 0.

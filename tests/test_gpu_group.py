@@ -278,4 +278,35 @@ def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
         assert (s.K, s.K_pass, list(s.cand), s.vox1, s.vox2) == (s0.K, s0.K_pass, list(s0.cand), s0.vox1, s0.vox2)
         for st in [s] + list(sb):
             assert st.shard_ranks == n
-            assert sorted(st.as_dict()["sharded"]) == ["fine", "search", "sort"], st.as_dict()["sharded"]
+            assert sorted(st.as_dict()["sharded"]) == ["faces", "fine", "search", "sort"], st.as_dict()["sharded"]
+
+
+@pytest.mark.parametrize("n,cfg", [(2, "c2"), (3, "c3")])
+def test_virtual_ranks_shard_the_face_stage_debug_exact(fccf, oracle, n, cfg, monkeypatch):
+    """Row P (the 1 m face stage split by Morton range of leaves, FCCF.cpp:470-534) with
+    row D (FCCF_SHARD_D_MIN=0): every virtual rank's intermediates -- downsampled clouds,
+    octree bounds, per-leaf counts / flags / curvatures, planar records, residual clouds
+    -- and T equal the oracle bit for bit, on debug contexts."""
+    from test_gpu_register import STAGES, as_bits
+    c = fccf.CONFIGS[cfg]
+    src, tar, _ = fccf.synth_pair(c["n"], c["room"])
+    leaf = c["leaf"]
+    run = oracle.Run(src, tar, leaf, oracle.INTROSORT)
+    monkeypatch.setenv("FCCF_SHARD_D_MIN", "0")
+    ctxs = [fccf.Ctx(0, debug=True) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+        out = _on_threads(lambda r: ctxs[r].register(src, tar, leaf), n)
+        dumps = [{name: ctxs[r].debug(name, dt) for name, dt in STAGES} for r in range(n)]
+        for g in groups:
+            g.close()
+    finally:
+        for cx in ctxs:
+            cx.close()
+    for r, (T, s) in enumerate(out):
+        assert sorted(s.as_dict()["sharded"]) == ["faces", "fine", "search", "sort"]
+        for name, dt in STAGES:
+            ref, got = run.get(name, dt), dumps[r][name]
+            assert got is not None and got.shape == ref.shape, (r, name)
+            assert np.array_equal(as_bits(got), as_bits(ref)), (r, name)
+        np.testing.assert_array_equal(bits(T), bits(run.T))

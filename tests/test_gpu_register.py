@@ -321,3 +321,33 @@ def test_optimistic_driver_pass_redo(ctx, oracle, fccf):
     T2, st2 = ctx.register(src, tar, 0.1)  # the cached graphs are intact afterwards
     assert st2.stage_redos == 0
     np.testing.assert_array_equal(T2.view(np.uint32), ref.view(np.uint32))
+
+
+def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monkeypatch):
+    """fccf_register_batch runs the clouds of two pairs in the same launches (stage
+    groups of two pairs, the last one single for an odd count; pipeline.cpp
+    clouds_enqueue_group).  Pairs of different sizes within a group, single
+    registrations between batches (the one-pair and two-pair stages lay the workspace
+    out differently, so their cached graphs must never be mixed), and the one-pair
+    form (FCCF_PAIR_BATCH=1) must all give the oracle's T bit for bit."""
+    base_src, base_tar, _ = fccf.synth_pair(90_000)
+    rng = np.random.default_rng(21)
+    pairs = []
+    for k in range(5):
+        jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
+        pairs.append(((base_src + jit).astype(np.float32)[: 90_000 - 7000 * k], base_tar[: 60_000 + 6000 * k]))
+    refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
+    for rep in range(2):
+        Tb, _ = ctx.register_batch(pairs, 0.1)
+        for T, ref in zip(Tb, refs):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+        for (s, t), ref in list(zip(pairs, refs))[:2]:  # one-pair stages between the batches
+            T, _ = ctx.register(s, t, 0.1)
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    Tb, _ = ctx.register_batch(pairs[:2], 0.1)  # one group of two
+    for T, ref in zip(Tb, refs[:2]):
+        np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    monkeypatch.setenv("FCCF_PAIR_BATCH", "1")
+    Tb1, _ = ctx.register_batch(pairs, 0.1)
+    for T, ref in zip(Tb1, refs):
+        np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))

@@ -102,6 +102,10 @@ lo, hi = shard.shard_range(len(xyz), r, w)
 vctx = test_shard.StubVoxelCtx()
 got = shard.downsample_sharded(vctx, xyz[lo:hi], 0.25, r, w, shard.torch_gather())
 assert np.array_equal(got.view(np.uint32), vctx.downsample(xyz, 0.25).view(np.uint32))
+codes, nbits = test_shard.face_codes(40000, 9)
+part = shard.face_rank_points(codes, nbits, r, w)
+whole = np.concatenate(shard.torch_gather()(part.astype(np.float64))).astype(np.int64)
+assert np.array_equal(whole, np.argsort(codes, kind="stable")), "row P split differs"
 dist.barrier(); dist.destroy_process_group()
 print("ok", r)
 '''
@@ -270,3 +274,29 @@ def test_gloo_two_ranks(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.count("ok") == 2
+
+
+def face_codes(n, seed):
+    """Leaf codes of a synthetic cloud: ~n/20 occupied leaves of a depth-7 octree (22-bit
+    codes), clustered like a room's surfaces, points of a leaf scattered in input order."""
+    rng = np.random.default_rng(seed)
+    leaves = np.unique(rng.integers(0, 1 << 21, n // 20) * 2 + (rng.random(n // 20) < 0.1))
+    leaves = np.sort(leaves)[: max(1, n // 20)]
+    return leaves[np.minimum(rng.zipf(1.3, n), leaves.size) - 1].astype(np.uint64), 22
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 64])
+def test_face_split_concatenates_to_leaf_order(world):
+    """Row P: the ranks' bin ranges tile the code space, no leaf is
+    split across ranks, the ranks' sizes are balanced, and their leaf-ordered points
+    concatenated in rank order are the unsharded leaf order (code, then input position)."""
+    codes, nbits = face_codes(50_000, 4)
+    parts = [shard.face_rank_points(codes, nbits, r, world) for r in range(world)]
+    whole = np.concatenate(parts)
+    assert np.array_equal(whole, np.argsort(codes, kind="stable"))
+    leaf_rank = {}
+    for r, p in enumerate(parts):
+        for c in np.unique(codes[p]):
+            assert leaf_rank.setdefault(int(c), r) == r
+    sizes = [len(p) for p in parts]
+    assert sum(sizes) == len(codes)
