@@ -48,11 +48,11 @@ struct B4 {
   __host__ __device__ B4(T a, T b, T c, T d) : v{a, b, c, d} {}
   template <class U>
   __host__ __device__ B4(const B4<U>& o) : v{o.v[0], o.v[1], o.v[2], o.v[3]} {}
-  // a select, not an index: a dynamically indexed by-value kernel argument is copied
-  // to a per-thread private array (measured: 3x the runtime of a 12 MB pass)
-  __host__ __device__ __forceinline__ T operator[](int i) const {
-    return (i & 2) ? ((i & 1) ? v[3] : v[2]) : ((i & 1) ? v[1] : v[0]);
-  }
+  // (an index into the kernel argument: ROCm 7.2 reads the selected entry from the
+  // kernarg segment with scalar loads -- no scratch copy, fewer SGPRs than a select
+  // chain, which on structs of four entries made the compiler spill to scratch; an
+  // older toolchain copied such arguments to a private array, round 1)
+  __host__ __device__ __forceinline__ T operator[](int i) const { return v[i]; }
 };
 
 // Stable LSD radix sort of (key, val) by the low *d_nbits bits of key (8-bit
