@@ -283,9 +283,11 @@ struct PipeSet {
   float leaf = 0.f;
   uint32_t sharded = 0;  // FCCF_SHARDED_* of the cloud stage (row D)
   // (slot 2G only) the stage group's last stage: how many pairs, the entry kernel's
-  // arguments (patched into g_seg per call) and the centroid sums' scratch
+  // arguments (patched into g_seg[P - 1] per call; one per graph, because the fields
+  // other than the inputs are set only when that graph is captured) and the centroid
+  // sums' scratch
   int group_pairs = 0;
-  VGEntry entry;
+  VGEntry entry[2];
   XsBufs xs;
 };
 
@@ -412,10 +414,11 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
       x[e] = xin[e < nc ? e : nc - 1];
       n[e] = e < nc ? nv[e] : 0u;
     }
-    gs.entry.xyz = B4<const float*>(x[0], x[1], x[2], x[3]);
-    gs.entry.n = B4<uint32_t>(n[0], n[1], n[2], n[3]);
+    gs.entry[P - 1].xyz = B4<const float*>(x[0], x[1], x[2], x[3]);
+    gs.entry[P - 1].n = B4<uint32_t>(n[0], n[1], n[2], n[3]);
   }
-  gs.entry.bind();
+  VGEntry& entry = gs.entry[P - 1];
+  entry.bind();
   // The whole cloud stage is ONE graph: both VoxelGrid passes, then the centroid sums
   // forked onto ss beside the face voxels, joined before the orientation.  ROCm 7.2
   // runs the two branches of a replay concurrently (tools/graph_fork_probe.hip).  The
@@ -425,7 +428,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   CloudMail* cmail = &host_mail(c)->clouds[2 * G];  // (slots 2G, 2G + 1 adjacent); never allocated inside the capture
   const XsBufs xs = gs.xs;
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
-    seg_pass1(w, nc, xin, nv, leaf, st0, &gs.entry);
+    seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
     seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
     HIP_CHECK(hipEventRecord(cg.ev[6], st0));
     HIP_CHECK(hipStreamWaitEvent(ss, cg.ev[6], 0));
@@ -442,7 +445,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
                        all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), st0, nc, cmail,
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
-  }, vg_entry_kernel(), gs.entry.args, DG != nullptr || exact2);
+  }, vg_entry_kernel(), entry.args, DG != nullptr || exact2);
   for (int j = 0; j < P; ++j) {
     auto& cs = c->cs[2 * G + j];
     PipeSet& ps = pset(c, 2 * G + j);

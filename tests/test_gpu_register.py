@@ -331,13 +331,20 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
     out differently, so their cached graphs must never be mixed), and the one-pair
     form (FCCF_PAIR_BATCH=1) must all give the oracle's T bit for bit."""
     base_src, base_tar, _ = fccf.synth_pair(90_000)
-    rng = np.random.default_rng(21)
-    pairs = []
-    for k in range(5):
-        jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
-        pairs.append(((base_src + jit).astype(np.float32)[: 90_000 - 7000 * k], base_tar[: 60_000 + 6000 * k]))
-    refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
+
+    def make_pairs(seed):  # the same sizes (so the same cached stage graphs), new points
+        rng = np.random.default_rng(seed)
+        out = []
+        for k in range(5):
+            jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
+            out.append(((base_src + jit).astype(np.float32)[: 90_000 - 7000 * k], base_tar[: 60_000 + 6000 * k]))
+        return out
+
     for rep in range(2):
+        # a replayed two-pair graph after one-pair captures (rep 1) must patch its own
+        # entry arguments: new points of the same sizes show stale ones as a wrong T
+        pairs = make_pairs(21 + rep)
+        refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
         Tb, _ = ctx.register_batch(pairs, 0.1)
         for T, ref in zip(Tb, refs):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
