@@ -282,6 +282,7 @@ struct PipeSet {
   int64_t in_nsrc = 0, in_ntar = 0;
   float leaf = 0.f;
   uint32_t sharded = 0;  // FCCF_SHARDED_* of the cloud stage (row D)
+  bool redone = false;   // the stage (this pair's stage group) was redone (VG_REDO)
   // (slot 2G only) the stage group's last stage: how many pairs, the entry kernel's
   // arguments (patched into g_seg[P - 1] per call; one per graph, because the fields
   // other than the inputs are set only when that graph is captured) and the centroid
@@ -375,6 +376,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     ps.cap[0] = ps.cap[1] = capmax;
     ps.cen = cen + 6 * j;
     ps.sharded = (DG ? FCCF_SHARDED_SORT : 0u) | (PG ? FCCF_SHARDED_FACES : 0u);
+    ps.redone = exact2;
     const float* hin[2] = {in[j].tar, in[j].src};
     for (int k = 0; k < 2; ++k) {
       CloudWS& x = w[2 * j + k];
@@ -524,8 +526,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
     std::memcpy(sc, cm.sc, sizeof sc);
     std::memcpy(fsc, cm.fsc, sizeof fsc);
-    ++S.stage_redos;
   }
+  if (ps.redone) ++S.stage_redos;  // (also the group's other pair, whose stage was redone with this one)
   guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
   std::vector<VoxRec> vox[2];
   for (int k = 0; k < 2; ++k) {

@@ -93,7 +93,8 @@ typedef struct fccf_stats {
                                     stamps of the cloud stage's kernels), fine verify */
   /* appended in round 3 */
   int64_t stage_redos;           /* cloud stages redone because the driver's VoxelGrid
-                                    input was not in leaf order */
+                                    input was not in leaf order; in a
+                                    batch, counted for every pair of the redone stage */
   /* appended in round 4 */
   int32_t shard_ranks;           /* ranks of the attached group (1: no group)      */
   uint32_t sharded;              /* FCCF_SHARDED_* stages this call split over them */
