@@ -398,14 +398,18 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     if (in[j].staged) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[2 * G + j].ev_in, 0));
   }
   gs.group_pairs = P;
+  // (graph keys are compared bytewise: no padding bytes, or their stack garbage forces
+  // a re-capture -- about 10 ms -- on most calls)
   struct {
     const void* base;
     size_t acap;
     uint32_t cap;
     int32_t pairs;
     float leaf, fvs, vpt, ct, fine_res;
+    uint32_t zero;
   } key = {cg.arena.base, cg.arena.cap, capmax, P, leaf, Pa.face_voxel_size, Pa.voxel_point_threshold,
-           Pa.curvature_threshold, Pa.fine_verify_voxel_size};
+           Pa.curvature_threshold, Pa.fine_verify_voxel_size, 0u};
+  static_assert(sizeof key == 8 + 8 + 4 + 4 + 5 * 4 + 4, "graph key without padding");
   // The inputs (caller-owned device clouds, or the staged copies of host arrays) are
   // read in place: their pointers and counts are patched into pass 1's entry kernel
   // node.
@@ -461,6 +465,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
       uint32_t cap;
       float res;
     } rkey = {ps.w[0].resid, ps.w[0].fb.nresid, ps.w[0].faggr, ps.w[0].fstate, capmax, Pa.fine_verify_voxel_size};
+    static_assert(sizeof rkey == 4 * 8 + 4 + 4, "graph key without padding");
     cs.g_rep.run(&rkey, sizeof rkey, st0, [&] { seg_s1_replay(ps.w, Pa, st0); });
     HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
   }
@@ -938,6 +943,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       int32_t E;
       float res;
     } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size};
+    static_assert(sizeof fkey == 5 * 8 + 4 * 4, "graph key without padding");
     ht.mark("fine_setup");
     // S1 octree bounds replayed (after the clouds); ev[5]'s stream may be capturing the next pair's clouds
     guarded_stream_wait(sf, c->cs[s].ev[5]);
