@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(256) k_compact_planar(B4<FaceBufs> fb, B4<VoxR
     pm->stamp[3] = __builtin_amdgcn_s_memrealtime();
     pm->stamp[0] = B.vgp->t_main;
     pm->stamp[1] = B.vgp->t_driver;
-    pm->stamp[2] = *B.t_faces;
+    pm->stamp[2] = *fb.v[0].t_faces;  // (the batch's face stage starts once, stamped in cloud 0's buffers)
   }
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < nl; s += gridDim.x * 256) {
     if (!planar[s]) continue;

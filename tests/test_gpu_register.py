@@ -345,9 +345,12 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
         # entry arguments: new points of the same sizes show stale ones as a wrong T
         pairs = make_pairs(21 + rep)
         refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
-        Tb, _ = ctx.register_batch(pairs, 0.1)
+        Tb, sb = ctx.register_batch(pairs, 0.1)
         for T, ref in zip(Tb, refs):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+        for x in sb:  # every pair's device spans come from its own stage's stamps
+            ms = x.as_dict()["ms"]
+            assert 0.0 < ms["downsample"] < 1000.0 and 0.0 < ms["voxelfit"] < 1000.0, ms
         for (s, t), ref in list(zip(pairs, refs))[:2]:  # one-pair stages between the batches
             T, _ = ctx.register(s, t, 0.1)
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))

@@ -1,19 +1,34 @@
-"""Summarise rocprofv3 PMC passes into per-launch HBM traffic for bench.py.
+"""Summarise rocprofv3 PMC passes over the bench command into per-launch traffic for
+bench.py's roofline.traffic (tools/gpu_pmc_calib.sh writes the passes).
 
 Usage:
-  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [MIN_FRAC]
+  python tools/pmc_traffic.py PMC_DIR CONFIG OUT.json [MIN_FRAC]
 
-FETCH_DIR / WRITE_DIR hold the `*counter_collection.csv` of two separate passes
-(`rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv ...` and the same with
-WRITE_SIZE; they cannot share a pass on gfx950). Following MI355X_MICROARCH.md
-("HBM"): FETCH_SIZE and WRITE_SIZE are kilobytes from the L2 memory-side request
-counters, and on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read,
-so traffic = 2 * FETCH_SIZE + WRITE_SIZE. The doubling is exact only for
-16-B-per-lane streaming loads; narrower patterns are uncalibrated, as the guide warns,
-so the raw counters are kept beside the corrected figure.  Dispatches whose
-counter stays below MIN_FRAC (default 0.05) of the kernel's largest dispatch are
-launches that skipped their work (radix passes past the key width exit at once) and
-are left out, matching bench.py's probe, which times active launches only.
+PMC_DIR holds bench_p1 .. bench_p4, one counter pass per process (rocprofv3 does not
+split counters over passes, and a pass holds at most 4 TCC counters):
+  p1  TCC_EA0_RDREQ_sum, TCC_EA0_RDREQ_32B_sum, _64B_sum, _128B_sum
+  p2  TCC_EA0_WRREQ_sum, TCC_EA0_WRREQ_64B_sum
+  p3  FETCH_SIZE            p4  WRITE_SIZE
+and bench_p1.json, the bench line of pass 1, whose kernel_table carries each kernel's
+algorithmic bytes per launch (SURVEY.md §8(d) figures, bench.py's probe).
+
+Three figures per kernel and launch:
+  raw        FETCH_SIZE + WRITE_SIZE (kilobytes x 1024);
+  guide      2 x FETCH_SIZE + WRITE_SIZE: MI355X_MICROARCH.md's gfx950 correction, exact
+             for wide coalesced reads only (128-B requests tallied at 64 B);
+  exact      32 x RDREQ_32B + 64 x RDREQ_64B + 128 x RDREQ_128B read bytes plus
+             32 x (WRREQ - WRREQ_64B) + 64 x WRREQ_64B write bytes.  Calibrated on known
+             byte counts for every access width the sort uses (tools/pmc_calib.hip,
+             profiles/r04*/pmc_calib.json): 1.000 of the algorithmic bytes for 2-, 4- and
+             16-B coalesced loads and for 4- and 16-B coalesced stores, and exactly one
+             128-B line per random 2-, 4- or 12-B load.  hbm_bytes_per_launch is this one.
+All three count the L2's memory-side requests, Infinity-Cache hits included (the guide:
+"appear to be counted, not excluded"; TCC_EA0_RDREQ_DRAM reads the same as RDREQ in the
+calibration), so they are L2-miss traffic, an upper bound on HBM bytes.
+
+Dispatches whose counter stays below MIN_FRAC (default 0.05) of the kernel's largest
+dispatch are left out (launches that skip their work), as bench.py's probe times active
+launches only.
 """
 import csv
 import glob
@@ -29,38 +44,70 @@ def short(name):
     return m.group(1) if m else name
 
 
-def per_kernel(d, counter, min_frac):
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+def per_kernel(d):
+    """{kernel: {counter: [value per dispatch, in dispatch order]}}"""
     acc = {}
-    for f in files:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter:
-                    continue
-                k = short(row["Kernel_Name"])
-                v = float(row["Counter_Value"])
-                acc.setdefault(k, []).append(v)
-    return {k: [x for x in v if x >= min_frac * max(v)] for k, v in acc.items()}
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Dispatch_Id"]))
+        for row in rows:
+            acc.setdefault(short(row["Kernel_Name"]), {}).setdefault(row["Counter_Name"], []).append(
+                float(row["Counter_Value"]))
+    return acc
+
+
+def active_mean(vals, min_frac):
+    if not vals:
+        return None, 0
+    mx = max(vals)
+    keep = [v for v in vals if v >= min_frac * mx] if mx > 0 else vals
+    return statistics.mean(keep), len(keep)
 
 
 def main():
-    fetch_dir, write_dir, out = sys.argv[1:4]
+    pmc_dir, config, out = sys.argv[1:4]
     min_frac = float(sys.argv[4]) if len(sys.argv) > 4 else 0.05
-    fetch = per_kernel(fetch_dir, "FETCH_SIZE", min_frac)
-    write = per_kernel(write_dir, "WRITE_SIZE", min_frac)
-    res = {"units": "bytes per launch", "correction": "2*FETCH_SIZE (gfx950 wide-read half count) + WRITE_SIZE",
+    passes = {}
+    for i in range(1, 5):
+        for k, cs in per_kernel(os.path.join(pmc_dir, f"bench_p{i}")).items():
+            passes.setdefault(k, {}).update(cs)
+    alg = {}
+    bj = os.path.join(pmc_dir, "bench_p1.json")
+    if os.path.exists(bj):
+        for k, v in json.load(open(bj)).get("kernel_table", {}).items():
+            alg[k] = v.get("algorithmic_bytes_per_launch")
+    res = {"config": config, "units": "bytes per launch (active launches)",
+           "hbm_bytes_per_launch": "exact: calibrated request-size buckets (see tools/pmc_traffic.py)",
            "kernels": {}}
-    for k in sorted(set(fetch) & set(write)):
-        if not fetch[k] or not write[k]:
+    for k, cs in sorted(passes.items()):
+        m = {}
+        n = {}
+        for c, v in cs.items():
+            m[c], n[c] = active_mean(v, min_frac)
+        need = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_WRREQ_sum",
+                "TCC_EA0_WRREQ_64B_sum", "FETCH_SIZE", "WRITE_SIZE")
+        if any(m.get(c) is None for c in need):
             continue
-        f_kb = statistics.mean(fetch[k])
-        w_kb = statistics.mean(write[k])
-        res["kernels"][k] = {"launches_fetch_pass": len(fetch[k]), "launches_write_pass": len(write[k]),
-                             "FETCH_SIZE_KB_mean": f_kb, "WRITE_SIZE_KB_mean": w_kb,
-                             "hbm_bytes_per_launch": (2.0 * f_kb + w_kb) * 1024.0, "active_min_frac": min_frac}
+        rd = 32 * m["TCC_EA0_RDREQ_32B_sum"] + 64 * m["TCC_EA0_RDREQ_64B_sum"] + 128 * m["TCC_EA0_RDREQ_128B_sum"]
+        wr = 32 * (m["TCC_EA0_WRREQ_sum"] - m["TCC_EA0_WRREQ_64B_sum"]) + 64 * m["TCC_EA0_WRREQ_64B_sum"]
+        f_b, w_b = m["FETCH_SIZE"] * 1024.0, m["WRITE_SIZE"] * 1024.0
+        a = alg.get(k) or alg.get(k[:-2] if k.endswith("_s") else k)
+        e = {"launches": n["FETCH_SIZE"], "raw_bytes": f_b + w_b, "guide_bytes": 2 * f_b + w_b,
+             "exact_read_bytes": rd, "exact_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+             "algorithmic_bytes_per_launch": a,
+             "exact_over_algorithmic": (rd + wr) / a if a else None,
+             "raw_over_algorithmic": (f_b + w_b) / a if a else None,
+             "active_min_frac": min_frac}
+        res["kernels"][k] = e
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
-    print(json.dumps(res, indent=1))
+    for k, e in sorted(res["kernels"].items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
+        if e["hbm_bytes_per_launch"] < 1e6:
+            continue
+        r = e["exact_over_algorithmic"]
+        print(f"{k:22s} exact {e['hbm_bytes_per_launch'] / 1e6:9.2f} MB  raw {e['raw_bytes'] / 1e6:9.2f}  "
+              f"guide {e['guide_bytes'] / 1e6:9.2f}  alg {(e['algorithmic_bytes_per_launch'] or 0) / 1e6:8.2f}  "
+              f"exact/alg {r if r is not None else float('nan'):.2f}")
 
 
 if __name__ == "__main__":
