@@ -2,7 +2,7 @@
 # PMC calibration: the request-size-bucketed L2->fabric counters
 # (TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B) beside FETCH_SIZE / WRITE_SIZE, over
 # tools/pmc_calib (known bytes per access pattern) and over the bench command, one
-# counter pass per process.  Usage (via gpurun): [CFG=c3] [STEPS=5] bash tools/gpu_pmc_calib.sh <tag>
+# counter pass per process.  Usage (via gpurun): [CFG=c3] [STEPS=5] [CALIB=0] [BENCH=0] bash tools/gpu_pmc_calib.sh <tag>
 set -e
 TAG=${1:-calib}
 CFG=${CFG:-c3}
@@ -10,6 +10,7 @@ STEPS=${STEPS:-5}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+if [ "${CALIB:-1}" = 1 ]; then
 tools/pmc_calib > $OUT/calib_alg.txt
 P1="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
 P2="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"
@@ -22,8 +23,9 @@ for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   timeout -s KILL 60 rocprofv3 --pmc $P --kernel-trace -f csv -d $OUT/calib_p$i -o run -- tools/pmc_calib > /dev/null 2> $OUT/calib_p$i.err
   echo "calib pass $i ok"
 done
+fi
 [ "${BENCH:-1}" = 1 ] || exit 0
-B="bench.py --config $CFG --no-cpu-baseline --parity-configs= --steps $STEPS --warmup 2"
+B="bench.py --config $CFG --no-cpu-baseline --parity-configs= --no-pipeline --no-sharded --steps $STEPS --warmup 2"
 i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
