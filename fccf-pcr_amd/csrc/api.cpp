@@ -817,8 +817,8 @@ extern "C" int fccf_stage_fine_verify(fccf_ctx* c, const float* s1, int64_t n1, 
     const size_t nk = (size_t)E * (u1 + u2);
     const size_t af1 = aggr_floats(u1), af2 = aggr_floats(u2);
     const size_t need = 12 * ((size_t)u1 + u2) + 4 * af1 + 12 * (size_t)E * u2 + 4 * E * af2 +
-                        sizeof(OctState) * (E + 2) + (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 +
-                        sizeof(m44) * E + 64 + sort_scratch_bytes((uint32_t)nk) + 40 * 256 +
+                        sizeof(OctState) * (E + 2) + (3 * 8 + 3 * 4 + 4 + 8) * (nk + 1) + 64 * 5 +
+                        sizeof(m44) * E + 64 + sort_scratch_bytes((uint32_t)nk) + 48 * 256 +
                         exact_sum_bytes(E, u1 + u2) + 256;
     c->arena2.ensure(need);
     c->arena2.reset();
@@ -834,8 +834,11 @@ extern "C" int fccf_stage_fine_verify(fccf_ctx* c, const float* s1, int64_t n1, 
     fb.state = a.take_n<OctState>(E + 1);
     fb.k0 = a.take_n<uint64_t>(nk);
     fb.k1 = a.take_n<uint64_t>(nk);
+    fb.k2 = a.take_n<uint64_t>(nk);
     fb.v0 = a.take_n<uint32_t>(nk);
     fb.v1 = a.take_n<uint32_t>(nk);
+    fb.v2 = a.take_n<uint32_t>(nk);
+    fb.pts = a.take_n<uint32_t>(MAX_EVAL);
     fb.starts = a.take_n<uint32_t>(nk + 1);
     fb.term = a.take_n<float>(nk + 1);
     fb.range = a.take_n<uint32_t>(2 * MAX_EVAL);

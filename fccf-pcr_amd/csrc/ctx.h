@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -253,6 +254,9 @@ struct fccf_ctx {
   fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)
   fccf::Group* group = nullptr;  // RCCL rank of a sharded registration (group.cpp), or none
   bool debug = false;
+  // face-code radix passes (x 8 bits) the cloud stage launches: three until a scene's
+  // 1 m octree needs a fourth digit (FACE_DEEP in a cloud's mailbox), then four
+  std::atomic<int> face_fast_bits{24};
   bool grow_device = false;  // K4 region growing on the GPU (grow.hip) instead of the host
   bool lm_device = false;    // quick_verify + LM on the GPU (verify.hip) instead of the host pool
   bool cluster_device = false;  // transform_cluster's seeds, sort and averaging on the GPU (cluster.hip)

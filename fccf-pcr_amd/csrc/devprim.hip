@@ -328,19 +328,29 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B4<RsRing<K>> R2, B4<const ui
 // the bits the fast_passes launched passes of the device plan covered.
 // Slow (one CU) but a single launch that exits at once in the common case, where
 // the launches of never-needed fast passes would each cost a kernel boundary.
+// copy_home (a sort with a third buffer, which launches no copy-back kernel): the one
+// plan that still ends outside buffer 0 -- a single active pass, 0 -> 1 -- is copied
+// home here, by this one workgroup (tiny key widths only: nbits <= RS_MAXW).
 template <class K>
 __global__ void __launch_bounds__(ST) k_rs_tail(B4<K*> k02, B4<uint32_t*> v02, B4<K*> k12, B4<uint32_t*> v12,
                                                 B4<const uint32_t*> d_n2, B4<const uint32_t*> d_nbits2,
-                                                int fast_passes, B4<const uint32_t*> need2) {
+                                                int fast_passes, B4<const uint32_t*> need2, int copy_home) {
   KT();
   const int e = blockIdx.y;
   const uint32_t nbits = *d_nbits2[e], n = *d_n2[e];
+  K* kb[2] = {k02[e], k12[e]};
+  uint32_t* vb[2] = {v02[e], v12[e]};
+  if (copy_home && rs_active(nbits, fast_passes) == 1u) {
+    for (uint32_t i = threadIdx.x; i < n; i += ST) {
+      kb[0][i] = kb[1][i];
+      if (vb[0]) vb[0][i] = vb[1][i];
+    }
+    __syncthreads();
+  }
   const RsPlan pl = rs_plan(nbits);
   const uint32_t lo_bit = pl.passes <= (uint32_t)fast_passes ? nbits : (uint32_t)fast_passes * pl.width;
   if (lo_bit >= nbits || n < 2) return;
   if (need2[e] && *need2[e] == 0u) return;
-  K* kb[2] = {k02[e], k12[e]};
-  uint32_t* vb[2] = {v02[e], v12[e]};
   __shared__ uint32_t run_ofs[256], cnt[256], tex[256], tcnt[256];
   __shared__ uint32_t wcnt[SW][256];
   __shared__ uint32_t sh[SW];
@@ -487,12 +497,16 @@ void radix_sort(B4<K*> k0, B4<uint32_t*> v0, B4<K*> k1, B4<uint32_t*> v1, B4<con
     const double eb = 2.0 * (sizeof(K) + (v0[0] ? 4 : 0));  // algorithmic bytes per element
     FCCF_LAUNCH("k_rs_scatter", (d_n[0], eb, nbatch > 1 ? d_n[1] : nullptr, eb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
   }
-  if (fast_passes) {
+  // With a third buffer every plan but a single pass ends in buffer 0 (an even pass
+  // count by ping-pong, three passes by rotation), so no copy-back kernel is launched
+  // (a dependent launch, ~5 us, that exited at once); the tail copies that one case home.
+  const bool three = k2[0] != nullptr;
+  if (fast_passes && !three) {
     const uint32_t g = min(nb * 8u, 2048u);
     k_rs_copyback<K><<<dim3(g, nbatch), 256, 0, st>>>(R, d_n, d_nbits, fast_passes);
   }
-  if (fast_bits < (int)(8 * sizeof(K)))
-    k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_passes, tail_need);
+  if (fast_bits < (int)(8 * sizeof(K)) || (three && fast_passes))
+    k_rs_tail<K><<<dim3(1, nbatch), ST, 0, st>>>(k0, v0, k1, v1, d_n, d_nbits, fast_passes, tail_need, three ? 1 : 0);
 }
 
 // ---------------------------------------------------------------- segments / scan

@@ -447,7 +447,8 @@ __global__ void __launch_bounds__(256) k_compact_planar(B4<FaceBufs> fb, B4<VoxR
   if (pm && blockIdx.x == 0 && threadIdx.x < 8) {
     const uint32_t i = threadIdx.x & 3u;
     if (threadIdx.x < 4) pm->sc[ce][i] = sc2[e][i];
-    else if (i == 1) pm->fsc[ce][1] = B.vgp ? B.vgp->sort_err | (B.vgp->redo ? VG_REDO : 0u) : 0u;  // both passes' sort flags, redo
+    else if (i == 1)  // both passes' sort flags, redo, deep face codes
+      pm->fsc[ce][1] = (B.vgp ? B.vgp->sort_err | (B.vgp->redo ? VG_REDO : 0u) : 0u) | (*B.nbits > 27u ? FACE_DEEP : 0u);
     else pm->fsc[ce][i] = B.nleaf[i];
   }
   // the cloud stage's device spans: the stamps of main's pass, the driver's pass and the
@@ -708,19 +709,20 @@ void face_planar_scan(uint32_t cap, B4<FaceBufs> b, hipStream_t st, int nbatch) 
 }
 
 void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b,
-                         hipStream_t st, int nbatch) {
+                         hipStream_t st, int nbatch, int fast_bits) {
   face_codes(xyz, d_n, cap, res, b, st, nbatch);
   const B4<uint32_t*> nbits = pick(b, [](const FaceBufs& f) { return f.nbits; });
   const B4<uint64_t*> c0 = pick(b, [](const FaceBufs& f) { return f.c0; }), c1 = pick(b, [](const FaceBufs& f) { return f.c1; });
   const B4<uint32_t*> v0 = pick(b, [](const FaceBufs& f) { return f.v0; }), v1 = pick(b, [](const FaceBufs& f) { return f.v1; });
   // codes are 3 bits per octree level (+1): the device plan takes 3 passes of <= 9-bit
-  // digits up to depth 8 (extents up to ~256 x face_voxel_size; c3: depth 6, 19 bits)
-  // and 4 passes of 8 bits at depth 9-10 (~1 km at 1 m voxels, outdoor scans), so four
-  // fast passes are launched: at depth <= 8 the fourth exits at once (~6 us of no-op
-  // launches per registration), and only trees deeper than 10 levels reach the
-  // single-workgroup tail launch.  With the third buffer a three-pass sort ends in
-  // (c0, v0) without a copy-back; a four-pass sort ends there by ping-pong.
-  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B4<const uint32_t*>(nbits), 32, true,
+  // digits up to depth 8 (extents up to ~256 x face_voxel_size; c3-c5: depth 6, 19
+  // bits) and 4 passes of 8 bits at depth 9-10 (~1 km at 1 m voxels, outdoor scans).
+  // The pipeline launches three (fast_bits 24) until a scene needs the fourth
+  // (FACE_DEEP, then 32 for the ctx): a fourth pass that exits at once still costs three
+  // dependent launches (~15 us per cloud stage).  Digits past the launched passes are
+  // sorted by the single-workgroup tail, exactly.  With the third buffer a three-pass
+  // sort ends in (c0, v0) by rotation and a two- or four-pass one by ping-pong.
+  radix_sort_u64(c0, v0, c1, v1, d_n, cap, B4<const uint32_t*>(nbits), fast_bits, true,
                  pick(b, [](const FaceBufs& f) { return f.ss; }), st, nbatch, B4<const uint32_t*>(nullptr),
                  pick(b, [](const FaceBufs& f) { return f.c2; }), pick(b, [](const FaceBufs& f) { return f.v2; }));
   segment_heads_u64(B4<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),

@@ -6,9 +6,15 @@
 // each occupied leaf in DFS (Morton) order: s/t counts and the sequential float sums
 //   allinvec += s + t ;  similar += (s+t) * (min/max)   (if s >= 1 and t >= 1)
 // score = similar / allinvec.  The S1 half of the octree bound replay is shared by
-// all evaluations.  Sort key = (e | morton | is_target); counts are exact integers,
-// the two float sums run in the reference's leaf order (one lane per evaluation).
+// all evaluations.  Each workgroup counts its tile's points per leaf in an LDS hash
+// (the residual clouds come in 1 m leaf order, so a tile of 2048 points holds a few
+// hundred 0.5 m leaves) and emits one entry per leaf: key (e | morton), value
+// (source | target << 16).  The entries are sorted by key, every leaf's entries summed
+// -- counts are exact integers, so neither the tiles nor the entry order change them --
+// and the float sum runs in the reference's leaf order (one lane per evaluation).
 #define KT_TU 5  // ktrace.h source tag
+#include <algorithm>
+
 #include "probe.h"
 #include "kernels.h"
 #include "match.h"
@@ -41,9 +47,11 @@ __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ 
   }
 }
 
-// scal: [0] total keys, [1] nbits, [3] shift = 3*Dmax+1, [4] n1, [5] n2, [6] E
+// scal: [0] leaf entries (counted by k_fv_entries), [1] nbits = 3*Dmax + eb, [3] shift
+// = 3*Dmax + 1 (the is_target bit of the per-point layout kept: the key of a leaf is
+// (e << (shift-1)) | morton), [4] n1, [5] n2, [6] E; pts[e] = 0
 __global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict__ scal, uint32_t* __restrict__ range,
-                          uint32_t n1, uint32_t n2, int E) {
+                          uint32_t* __restrict__ pts, uint32_t n1, uint32_t n2, int E) {
   KT();
   if (threadIdx.x != 0) return;
   uint32_t D = 0;
@@ -51,50 +59,108 @@ __global__ void k_fv_bits(const OctState* __restrict__ st, uint32_t* __restrict_
     if (st[e].defined && st[e].depth > D) D = st[e].depth;
   uint32_t eb = 1;
   while ((1u << eb) <= (uint32_t)E) ++eb;
-  scal[0] = (uint32_t)E * (n1 + n2);
+  scal[0] = 0u;
   scal[2] = 0u;  // segment count (stays 0 when there are no keys)
   for (int i = 0; i < 2 * MAX_EVAL; ++i) range[i] = 0u;
+  for (int i = 0; i < MAX_EVAL; ++i) pts[i] = 0u;
   scal[3] = 3u * D + 1u;
-  scal[1] = 3u * D + 1u + eb;
+  scal[1] = 3u * D + eb;
   scal[4] = n1;
   scal[5] = n2;
   scal[6] = (uint32_t)E;
 }
 
-__global__ void __launch_bounds__(256) k_fv_keys(const float* __restrict__ s1, const float* __restrict__ s2t,
-                                                 const OctState* __restrict__ st, const uint32_t* __restrict__ scal,
-                                                 double res, uint64_t* __restrict__ keys) {
+// Exclusive scan over the 256 threads of a block; sh needs 4 u32.
+__device__ __forceinline__ uint32_t fv_scan_256(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint32_t wp = 0;
+  for (uint32_t w = 0; w < wave; ++w) wp += sh[w];
+  const uint32_t tot = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  *total = tot;
+  return wp + x - v;
+}
+
+// One workgroup per (tile of FV_TILE points of the fused cloud S1 ++ T_e S2, evaluation
+// e): every finite point's leaf counted in an LDS hash (open addressing, FV_SLOTS = 2 x
+// FV_TILE slots: it never fills), then the tile's leaves appended to the entry list at
+// an offset taken with one atomic, and the tile's finite points added to pts[e].
+constexpr uint32_t FV_TILE = 2048, FV_SLOTS = 4096;
+constexpr unsigned long long FV_EMPTY = ~0ull;
+__global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1, const float* __restrict__ s2t,
+                                                    const OctState* __restrict__ st, uint32_t* __restrict__ scal,
+                                                    double res, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                    uint32_t* __restrict__ pts) {
   KT();
+  __shared__ unsigned long long hk[FV_SLOTS];
+  __shared__ uint32_t hc[FV_SLOTS];
+  __shared__ uint32_t sh[4], sbase;
   const int e = blockIdx.y;
+  const uint32_t n1 = scal[4], n2 = scal[5], shift = scal[3] - 1u;
+  const uint32_t n = n1 + n2, i0 = blockIdx.x * FV_TILE;
+  if (i0 >= n) return;
   const OctState S = st[e];
-  const uint32_t n1 = scal[4], n2 = scal[5], shift = scal[3];
-  const uint32_t n = n1 + n2;
-  uint64_t* out = keys + (size_t)e * n;
   const float* b = s2t + (size_t)e * 3 * n2;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  for (uint32_t j = threadIdx.x; j < FV_SLOTS; j += 256) {
+    hk[j] = FV_EMPTY;
+    hc[j] = 0u;
+  }
+  __syncthreads();
+  uint32_t fin = 0;
+  for (uint32_t j = 0; j < FV_TILE / 256; ++j) {
+    const uint32_t i = i0 + j * 256 + threadIdx.x;
+    if (i >= n) break;
     const bool tgt = i >= n1;
     const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
-    uint64_t k = ~(uint64_t)0;
-    if (finite3(p[0], p[1], p[2]))
-      k = ((uint64_t)e << shift) | (oct_code(S, res, p[0], p[1], p[2]) << 1) | (tgt ? 1ull : 0ull);
-    out[i] = k;
+    if (!finite3(p[0], p[1], p[2])) continue;
+    ++fin;
+    const unsigned long long key = ((unsigned long long)e << shift) | oct_code(S, res, p[0], p[1], p[2]);
+    uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52);  // 12 bits: FV_SLOTS
+    for (;;) {
+      const unsigned long long old = atomicCAS(&hk[h], FV_EMPTY, key);
+      if (old == FV_EMPTY || old == key) break;
+      h = (h + 1u) & (FV_SLOTS - 1u);
+    }
+    atomicAdd(&hc[h], tgt ? 0x10000u : 1u);
+  }
+  __syncthreads();
+  // the occupied slots, compacted: FV_SLOTS / 256 consecutive slots per thread
+  constexpr uint32_t PER = FV_SLOTS / 256;
+  uint32_t occ = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) occ += hk[threadIdx.x * PER + q] != FV_EMPTY ? 1u : 0u;
+  uint32_t tot, ftot;
+  uint32_t pos = fv_scan_256(occ, sh, &tot);
+  fv_scan_256(fin, sh, &ftot);
+  if (threadIdx.x == 0) {
+    sbase = atomicAdd(&scal[0], tot);
+    if (ftot) atomicAdd(&pts[e], ftot);
+  }
+  __syncthreads();
+  pos += sbase;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t j = threadIdx.x * PER + q;
+    if (hk[j] == FV_EMPTY) continue;
+    keys[pos] = hk[j];
+    vals[pos] = hc[j];
+    ++pos;
   }
 }
 
-__global__ void __launch_bounds__(256) k_fv_leafkeys(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ scal,
-                                                     uint64_t* __restrict__ vk) {
-  KT();
-  const uint32_t n = scal[0];
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint64_t k = keys[i];
-    vk[i] = k == ~(uint64_t)0 ? k : (k >> 1);
-  }
-}
-
-// Per leaf: source/target counts (exact) and the similar_num term (:830-835):
-// (s+t)*(min/max) when both are >= 1, else +0.0f (adding +0 leaves the float
-// sum unchanged).  Also the per-evaluation segment ranges.
-__global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vk,
+// Per leaf (a run of equal keys among the sorted entries): source/target counts, the
+// sums of its entries' counts (exact), and the similar_num term (:830-835):
+// (s+t)*(min/max) when both are >= 1, else +0.0f (adding +0 leaves the float sum
+// unchanged).  Also the per-evaluation segment ranges.
+__global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                    const uint32_t* __restrict__ starts,
                                                    const uint32_t* __restrict__ scal, float* __restrict__ term,
                                                    uint32_t* __restrict__ range) {
@@ -102,31 +168,28 @@ __global__ void __launch_bounds__(256) k_fv_counts(const uint64_t* __restrict__ 
   const uint32_t ns = scal[2], sh = scal[3] - 1u;
   for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
     const uint32_t b = starts[s], e = starts[s + 1];
-    // keys of one leaf differ only in the is_target bit and are sorted, so the
-    // source points come first: the split is found by binary search
-    uint32_t lo = b, hi = e;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (keys[mid] & 1ull) hi = mid;
-      else lo = mid + 1;
+    uint32_t src = 0, tg = 0;
+    for (uint32_t j = b; j < e; ++j) {
+      const uint32_t c = vals[j];
+      src += c & 0xFFFFu;
+      tg += c >> 16;
     }
-    const uint32_t src = lo - b;
-    const float sn = (float)src, tn = (float)((e - b) - src);
+    const float sn = (float)src, tn = (float)tg;
     float t = 0.f;
     if (sn >= 1.f && tn >= 1.f) {
       const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
       t = (sn + tn) * (mn / mx);
     }
     term[s] = t;
-    const uint32_t ev = (uint32_t)(vk[b] >> sh);
-    if (s == 0 || (uint32_t)(vk[starts[s - 1]] >> sh) != ev) range[2 * ev] = s;
-    if (s + 1 == ns || (uint32_t)(vk[starts[s + 1]] >> sh) != ev) range[2 * ev + 1] = s + 1;
+    const uint32_t ev = (uint32_t)(keys[b] >> sh);
+    if (s == 0 || (uint32_t)(keys[starts[s - 1]] >> sh) != ev) range[2 * ev] = s;
+    if (s + 1 == ns || (uint32_t)(keys[starts[s + 1]] >> sh) != ev) range[2 * ev + 1] = s + 1;
   }
 }
 
 // count of leaves per evaluation (exact_sum input) and allinvec: the float sum of
 // integer counts is exact below 2^24, so it equals the integer point count.
-__global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __restrict__ range,
+__global__ void k_fv_ranges(const uint32_t* __restrict__ pts_e, uint32_t* __restrict__ range,
                             uint32_t* __restrict__ nseg_e, float* __restrict__ all, uint32_t* __restrict__ scal, int E) {
   KT();
   const int e = threadIdx.x;
@@ -134,7 +197,7 @@ __global__ void k_fv_ranges(const uint32_t* __restrict__ starts, uint32_t* __res
   const uint32_t f = range[2 * e], l = range[2 * e + 1];
   nseg_e[e] = l - f;
   nseg_e[MAX_EVAL + e] = f;  // first leaf of evaluation e (exact_sum offsets)
-  const uint32_t pts = l > f ? starts[l] - starts[f] : 0u;
+  const uint32_t pts = pts_e[e];
   if (pts >= (1u << 24)) atomicOr(&scal[7], 1u);  // float allinvec would round: unsupported size
   all[e] = (float)pts;
 }
@@ -172,17 +235,17 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   sd.state = sizeof(OctState);
   block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
   octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, sd);
-  k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, n1, n2, E);
-  const uint32_t n = (uint32_t)E * (n1 + n2);
-  k_fv_keys<<<dim3(grid_for(n1 + n2, 256, 1024), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0);
-  // (e | morton | is_target): 4 fast passes cover depth <= 9 with <= 15 evaluations.
-  // Keys only: the counts below read the sorted keys, never a permutation.
-  radix_sort_u64(b.k0, B4<uint32_t*>(nullptr), b.k1, B4<uint32_t*>(nullptr), b.scal, n, b.scal + 1, 32, false, b.ss,
-                 st);
-  k_fv_leafkeys<<<grid_for(n), 256, 0, st>>>(b.k0, b.scal, b.k1);
-  segment_heads_u64(b.k1, b.scal, n, b.starts, b.scal + 2, b.ss, st);
-  FCCF_LAUNCH("k_fv_counts", (b.scal, 16.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.k1, b.starts, b.scal, b.term, b.range);
-  k_fv_ranges<<<1, 64, 0, st>>>(b.starts, b.range, b.nseg_e, b.all, b.scal, E);
+  k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, b.pts, n1, n2, E);
+  const uint32_t n = (uint32_t)E * (n1 + n2);  // the entry count's bound (one per point)
+  k_fv_entries<<<dim3(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0,
+                                                                          b.pts);
+  // (e | morton) entries with their counts: 4 fast passes cover depth <= 9 with <= 15
+  // evaluations; a third buffer, so no copy-back launch
+  radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 32, false, b.ss, st, 1, B4<const uint32_t*>(nullptr),
+                 B4<uint64_t*>(b.k2), B4<uint32_t*>(b.v2));
+  segment_heads_u64(b.k0, b.scal, n, b.starts, b.scal + 2, b.ss, st);
+  FCCF_LAUNCH("k_fv_counts", (b.scal, 12.0, b.scal + 2, 12.0), k_fv_counts, grid_for(n), 256, 0, st, b.k0, b.v0, b.starts, b.scal, b.term, b.range);
+  k_fv_ranges<<<1, 64, 0, st>>>(b.pts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
   k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E, b.scal, mail);
 }

@@ -162,6 +162,10 @@ const void* vg_entry_kernel();
 enum { VG_GENERAL = 0, VG_PRESORTED = 1, VG_OPTIMISTIC = 2 };
 constexpr uint32_t VG_REDO = 0x80000000u;       // CloudMail::fsc[k][1]: the optimistic pass must be redone
 constexpr uint32_t VG_FORCE_REDO = 0x10000u;    // test hook bit (fccf_debug_inject_sort_fault)
+// CloudMail::fsc[k][1]: the cloud's face codes are wider than three 9-bit radix digits
+// (a 1 m octree deeper than 8 levels): a cloud stage that launched three passes sorted
+// the rest in the single-workgroup tail, and the ctx launches four from then on
+constexpr uint32_t FACE_DEEP = 0x40000000u;
 constexpr uint32_t IS_POISON_XYZS = 0x20000u;   // test hook bit: sorted points filled with NaN before each sort
 void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_n, uint32_t cap, float leaf, B4<float*> out,
                 B4<uint32_t*> d_m, B4<VGBufs> b, hipStream_t st, int presorted = VG_GENERAL, int nbatch = 1,
@@ -223,8 +227,11 @@ struct FaceBufs {
 
 // Octree leaves (Morton order) of each cloud of the batch.  Batched clouds must be
 // carved identically: every pointer of cloud 1 sits `stride` bytes after cloud 0's.
+// fast_bits: 8 x the device-wide radix passes launched for the face codes (24: three
+// <= 9-bit digits, octrees up to depth 8; 32: four, depth 10; deeper codes finish in the
+// single-workgroup tail either way)
 void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, B4<FaceBufs> b,
-                         hipStream_t st, int nbatch = 1);
+                         hipStream_t st, int nbatch = 1, int fast_bits = 32);
 // Row P (the face stage sharded by Morton range of 1 m leaves, group.cpp
 // face_voxels_sharded): the codes of every point; this rank's points (in input order)
 // and their sort into leaf order; the fit of its leaves into views of the full arrays;

@@ -82,8 +82,9 @@ struct FineBufs {
   float* s2t;          // E * n2 * 3
   float* aggr2;        // E * blocks(n2) * 6
   OctState* state;     // E + 1 (slot E = after S1)
-  uint64_t *k0, *k1;   // E * (n1 + n2)
-  uint32_t *v0, *v1;
+  uint64_t *k0, *k1, *k2;  // E * (n1 + n2): leaf entries' keys (three sort buffers)
+  uint32_t *v0, *v1, *v2;  // their point counts (source | target << 16)
+  uint32_t* pts;           // MAX_EVAL: finite points per evaluation (allinvec)
   uint32_t* starts;    // E * (n1 + n2) + 1
   float* term;         // per leaf similar_num term
   uint32_t* range;     // per evaluation: first leaf, end leaf (2 * MAX_EVAL)

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <vector>
 
@@ -179,7 +180,7 @@ void seg_downsample(CloudWS* w, int nc, float leaf, hipStream_t st, int mode) {
              sc(3), vg, st, mode, nc);  // driver :1377-1387
 }
 // PG: row P, the face stage sharded over a group's ranks by Morton range (group.cpp)
-void seg_faces(CloudWS* w, int nc, const fccf_params& P, hipStream_t st, Group* PG = nullptr) {
+void seg_faces(CloudWS* w, int nc, const fccf_params& P, hipStream_t st, Group* PG = nullptr, int fast_bits = 32) {
   const uint32_t cap = w[0].cap;
   const B4<FaceBufs> fb = all_of<FaceBufs>(w, nc, [](const CloudWS& c) { return c.fb; });
   const B4<const uint32_t*> m2 = all_of<const uint32_t*>(w, nc, [](const CloudWS& c) { return (const uint32_t*)c.sc + 3; });
@@ -190,7 +191,7 @@ void seg_faces(CloudWS* w, int nc, const fccf_params& P, hipStream_t st, Group* 
     return;
   }
   face_voxels_prepare(all_of<const float*>(w, nc, [](const CloudWS& c) { return (const float*)c.ds2; }), m2, cap,
-                      (double)P.face_voxel_size, fb, st, nc);
+                      (double)P.face_voxel_size, fb, st, nc, fast_bits);
   face_voxels_fit(m2, cap, P.voxel_point_threshold, P.curvature_threshold,
                   all_of<float*>(w, nc, [](const CloudWS& c) { return c.resid; }), fb, st, nc);
 }
@@ -250,7 +251,17 @@ struct HostTrace {
     line += b;
   }
   void flush() {
-    if (on) std::fprintf(stderr, "host trace:%s\n", line.c_str());
+    if (on) {
+      // absolute start, for merging with a rocprofv3 kernel trace (tools/critical_path.py):
+      // steady_clock is CLOCK_MONOTONIC; the BOOTTIME offset is printed beside it
+      timespec m, b;
+      clock_gettime(CLOCK_MONOTONIC, &m);
+      clock_gettime(CLOCK_BOOTTIME, &b);
+      const long long off = ((long long)b.tv_sec - m.tv_sec) * 1000000000LL + (b.tv_nsec - m.tv_nsec);
+      std::fprintf(stderr, "host trace t0_mono_ns=%lld boot_minus_mono_ns=%lld:%s\n",
+                   (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count(), off,
+                   line.c_str());
+    }
     line.clear();
   }
 };
@@ -406,9 +417,9 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     uint32_t cap;
     int32_t pairs;
     float leaf, fvs, vpt, ct, fine_res;
-    uint32_t zero;
+    int32_t face_bits;
   } key = {cg.arena.base, cg.arena.cap, capmax, P, leaf, Pa.face_voxel_size, Pa.voxel_point_threshold,
-           Pa.curvature_threshold, Pa.fine_verify_voxel_size, 0u};
+           Pa.curvature_threshold, Pa.fine_verify_voxel_size, c->face_fast_bits.load()};
   static_assert(sizeof key == 8 + 8 + 4 + 4 + 5 * 4 + 4, "graph key without padding");
   // The inputs (caller-owned device clouds, or the staged copies of host arrays) are
   // read in place: their pointers and counts are patched into pass 1's entry kernel
@@ -446,7 +457,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     }
     exact_sum_n(d2, n2, nc, 3, 3, cen, true, xs, ss);  // compute3DCentroid (:473)
     HIP_CHECK(hipEventRecord(cg.ev[7], ss));
-    seg_faces(w, nc, Pa, st0, PG);
+    seg_faces(w, nc, Pa, st0, PG, key.face_bits);
     HIP_CHECK(hipStreamWaitEvent(st0, cg.ev[7], 0));
     face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
                        all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), st0, nc, cmail,
@@ -542,7 +553,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (fsc[0][2] > CloudMail::REC_CAP || fsc[1][2] > CloudMail::REC_CAP) HIP_CHECK(hipStreamSynchronize(st0));
   // K1's sort checks its invariants on the device (IS_FAULT_*): a violation means the
   // VoxelGrid order may not be std::sort's, so no transform is returned
-  if ((fsc[0][1] | fsc[1][1]) & ~VG_REDO)
+  if ((fsc[0][1] | fsc[1][1]) & FACE_DEEP) c->face_fast_bits = 32;  // (sticky: the next stages launch four passes)
+  if ((fsc[0][1] | fsc[1][1]) & ~(VG_REDO | FACE_DEEP))
     throw Error(FCCF_E_INTERNAL, "VoxelGrid: K1 sort invariant violated (flags cloud 0: " + std::to_string(fsc[0][1]) +
                                      ", cloud 1: " + std::to_string(fsc[1][1]) + ")");
   {  // device spans of the cloud stage: its kernels' s_memrealtime stamps (100 MHz)
@@ -907,8 +919,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     const size_t nk = (size_t)E * (n1 + n2);
     const size_t af2 = aggr_floats(n2);
     const size_t need = 12 * (size_t)E * n2 + 4 * E * af2 + sizeof(OctState) * (E + 1) +
-                        (2 * 8 + 2 * 4 + 4 + 8) * (nk + 1) + 64 * 4 + sizeof(m44) * E + 64 +
-                        sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 32 * 256 +
+                        (3 * 8 + 3 * 4 + 4 + 8) * (nk + 1) + 64 * 5 + sizeof(m44) * E + 64 +
+                        sort_scratch_bytes((uint32_t)std::max<size_t>(nk, 1)) + 40 * 256 +
                         exact_sum_bytes(E, n1 + n2) + 256;
     a3.ensure(need);
     a3.reset();
@@ -918,8 +930,11 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     fb.state = a3.take_n<OctState>(E + 1);
     fb.k0 = a3.take_n<uint64_t>(nk);
     fb.k1 = a3.take_n<uint64_t>(nk);
+    fb.k2 = a3.take_n<uint64_t>(nk);
     fb.v0 = a3.take_n<uint32_t>(nk);
     fb.v1 = a3.take_n<uint32_t>(nk);
+    fb.v2 = a3.take_n<uint32_t>(nk);
+    fb.pts = a3.take_n<uint32_t>(MAX_EVAL);
     fb.starts = a3.take_n<uint32_t>(nk + 1);
     fb.term = a3.take_n<float>(nk + 1);
     fb.range = a3.take_n<uint32_t>(2 * MAX_EVAL);

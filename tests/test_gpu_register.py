@@ -284,10 +284,12 @@ def test_sort_invariant_flag_fails_registration(ctx, oracle, fccf, bit):
 
 def test_outdoor_extent_face_sort_stays_on_fast_passes(ctx, oracle, fccf):
     """A scene ~120 m across (the first-point-anchored 1 m octree grows to depth 9:
-    28-bit face codes, about 500 x face_voxel_size of root cell) is sorted by the four
-    device-wide radix passes, not the single-workgroup tail: bitwise parity, and the
+    28-bit face codes, about 500 x face_voxel_size of root cell).  The cloud stage
+    launches three face-code radix passes until a scene needs a fourth digit: the first
+    registration sorts it in the single-workgroup tail (bitwise parity), flags the
+    cloud (FACE_DEEP) and the ctx launches four device-wide passes from then on, so the
     face stage's device span stays well under a millisecond (the tail path over the
-    whole cloud would take several)."""
+    whole cloud takes several)."""
     src, tar, _ = fccf.synth_pair(400_000, (120.0, 90.0, 8.0))
     run = oracle.Run(src, tar, 0.1, oracle.INTROSORT)
     assert run.get("oct1", np.float64)[3] == 9 and run.get("oct2", np.float64)[3] == 9  # depth

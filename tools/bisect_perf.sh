@@ -13,4 +13,8 @@ for i in $(seq $N); do
   echo "head pairs2: $(tail -1 gpurun_out/bis_head.txt)"
   FCCF_PAIR_BATCH=1 timeout -k 10 120 python -u tools/quick_perf.py > gpurun_out/bis_head1.txt 2>&1 || { tail -5 gpurun_out/bis_head1.txt; exit 1; }
   echo "head pairs1: $(tail -1 gpurun_out/bis_head1.txt)"
+  if [ -n "$HEAD_ENV" ]; then  # one more variant of the working build, e.g. HEAD_ENV=FCCF_WAIT=sync
+    env $HEAD_ENV timeout -k 10 120 python -u tools/quick_perf.py > gpurun_out/bis_headv.txt 2>&1 || { tail -5 gpurun_out/bis_headv.txt; exit 1; }
+    echo "head $HEAD_ENV: $(tail -1 gpurun_out/bis_headv.txt)"
+  fi
 done
