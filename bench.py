@@ -526,9 +526,9 @@ def main():
     for _ in range(args.warmup):
         T, st = reg()
     if pipelined and args.warmup:
-        # four pairs: both stage groups of the batch (two pairs per cloud stage, groups on
-        # alternating workspaces) capture their graphs here, not in the timed batch
-        batch(4)
+        # eight pairs: both stage groups of the batch (up to four pairs per cloud stage,
+        # groups on alternating workspaces) capture their graphs here, not in the timed batch
+        batch(8)
     barrier(dist)
     t0 = time.perf_counter()
     Ks = 0

@@ -855,12 +855,15 @@ extern "C" int fccf_stage_fine_verify(fccf_ctx* c, const float* s1, int64_t n1, 
     HIP_CHECK(hipMemcpyAsync(dn1, &u1, 4, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipMemcpyAsync(fb.T, T, sizeof(m44) * E, hipMemcpyHostToDevice, st));
     octree_replay(d1, dn1, u1, (double)voxel, aggr1, st1, st);
-    fine_verify_batch(d1, u1, st1, d2, u2, E, (double)voxel, fb, st, nullptr);
-    HIP_CHECK(hipGetLastError());
     uint32_t err = 0;
-    HIP_CHECK(hipMemcpyAsync(scores, fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&err, fb.scal + 7, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    for (int mode = fine_mode_env(c->fine_sorted.load() ? 1 : 0);; mode = FV_LEAVES_SORTED) {
+      fine_verify_batch(d1, u1, st1, d2, u2, E, (double)voxel, fb, st, nullptr, mode, fine_lds_cap_env());
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpyAsync(scores, fb.scores, 4 * (size_t)E, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipMemcpyAsync(&err, fb.scal + 7, 4, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+      if (!(err & FV_ERR_LDS) || mode == FV_LEAVES_SORTED) break;  // (more leaves than the LDS form holds: sorted)
+    }
     if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
   });
 }

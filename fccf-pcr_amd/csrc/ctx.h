@@ -236,13 +236,13 @@ struct fccf_ctx {
                                      // fork/join inside the one-graph cloud stage (capture-internal)
     hipEvent_t tev[6] = {};          // timing: [4] fine start, [5] fine done (fccf_stats::dev_ms[3]);
                                      // the cloud stage's spans are device stamps (CloudMail::stamp)
-    fccf::CachedGraph g_seg[2];      // slot 2G: the group's cloud stage of one / two pairs (VoxelGrid passes,
-                                     // centroids, faces), one graph per pair count
+    fccf::CachedGraph g_seg[4];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs (VoxelGrid
+                                     // passes, centroids, faces), one graph per pair count
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
-  } cs[4];
+  } cs[8];                           // two stage groups of up to PAIRS_MAX pair slots (pipeline.cpp)
   hipStream_t sa[3] = {};            // cloud stage streams (sa[1]: fine verification)
   hipStream_t sb = nullptr;          // matching, copies, stage exports
   fccf::Arena arena2;  // matching (and the stage exports)
@@ -257,6 +257,9 @@ struct fccf_ctx {
   // face-code radix passes (x 8 bits) the cloud stage launches: three until a scene's
   // 1 m octree needs a fourth digit (FACE_DEEP in a cloud's mailbox), then four
   std::atomic<int> face_fast_bits{24};
+  // fine verification in the sorted leaf form (FV_LEAVES_SORTED): set once an evaluation
+  // had more leaves than the LDS form holds (FV_ERR_LDS)
+  std::atomic<bool> fine_sorted{false};
   bool grow_device = false;  // K4 region growing on the GPU (grow.hip) instead of the host
   bool lm_device = false;    // quick_verify + LM on the GPU (verify.hip) instead of the host pool
   bool cluster_device = false;  // transform_cluster's seeds, sort and averaging on the GPU (cluster.hip)

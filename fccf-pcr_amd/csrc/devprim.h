@@ -33,21 +33,38 @@ size_t sort_scratch_bytes(uint32_t cap);
 SortScratch sort_scratch_carve(void* base, uint32_t cap);
 
 // Per-problem arguments of a batched launch: problem e = blockIdx.y uses v[e].
-// The primitives below run `nbatch` (1 to 4) independent problems -- the clouds of
-// one registration, or of two registrations that a pipelined batch runs together --
+// The primitives below run `nbatch` (1 to BMAX) independent problems -- the clouds of
+// one registration, or of the registrations that a pipelined batch runs together --
 // in the same launches (a kernel boundary costs ~1.7 us on gfx950 and two streams of
 // dependent kernels interfere, so one stream of batched launches is the fast shape).
-// A single value converts to a batch of one.
-constexpr int BMAX = 4;
+// A single value converts to a batch of one; entries past the ones given repeat the
+// last (never read: problems past nbatch do not run).
+constexpr int BMAX = 8;
 template <class T>
 struct B4 {
   T v[BMAX];
   B4() = default;
-  __host__ __device__ B4(T a) : v{a, a, a, a} {}
-  __host__ __device__ B4(T a, T b) : v{a, b, b, b} {}
-  __host__ __device__ B4(T a, T b, T c, T d) : v{a, b, c, d} {}
+  __host__ __device__ B4(T a) {
+    for (int i = 0; i < BMAX; ++i) v[i] = a;
+  }
+  __host__ __device__ B4(T a, T b) {
+    v[0] = a;
+    for (int i = 1; i < BMAX; ++i) v[i] = b;
+  }
+  __host__ __device__ B4(T a, T b, T c, T d) {
+    v[0] = a;
+    v[1] = b;
+    v[2] = c;
+    for (int i = 3; i < BMAX; ++i) v[i] = d;
+  }
+  // the first n of a[] (n >= 1)
+  __host__ __device__ B4(const T* a, int n) {
+    for (int i = 0; i < BMAX; ++i) v[i] = a[i < n ? i : n - 1];
+  }
   template <class U>
-  __host__ __device__ B4(const B4<U>& o) : v{o.v[0], o.v[1], o.v[2], o.v[3]} {}
+  __host__ __device__ B4(const B4<U>& o) {
+    for (int i = 0; i < BMAX; ++i) v[i] = o.v[i];
+  }
   // (an index into the kernel argument: ROCm 7.2 reads the selected entry from the
   // kernarg segment with scalar loads -- no scratch copy, fewer SGPRs than a select
   // chain, which on structs of four entries made the compiler spill to scratch; an

@@ -124,19 +124,11 @@ struct RsRing {
 // no reference to a part of it either, which would make the compiler store it to scratch)
 template <class K>
 __device__ __forceinline__ K* ring_key(const B4<RsRing<K>>& R2, int e, int i) {
-  K* a = i == 0 ? R2.v[0].k[0] : (i == 1 ? R2.v[0].k[1] : R2.v[0].k[2]);
-  K* b = i == 0 ? R2.v[1].k[0] : (i == 1 ? R2.v[1].k[1] : R2.v[1].k[2]);
-  K* c = i == 0 ? R2.v[2].k[0] : (i == 1 ? R2.v[2].k[1] : R2.v[2].k[2]);
-  K* d = i == 0 ? R2.v[3].k[0] : (i == 1 ? R2.v[3].k[1] : R2.v[3].k[2]);
-  return (e & 2) ? ((e & 1) ? d : c) : ((e & 1) ? b : a);
+  return R2.v[e].k[i];
 }
 template <class K>
 __device__ __forceinline__ uint32_t* ring_val(const B4<RsRing<K>>& R2, int e, int i) {
-  uint32_t* a = i == 0 ? R2.v[0].v[0] : (i == 1 ? R2.v[0].v[1] : R2.v[0].v[2]);
-  uint32_t* b = i == 0 ? R2.v[1].v[0] : (i == 1 ? R2.v[1].v[1] : R2.v[1].v[2]);
-  uint32_t* c = i == 0 ? R2.v[2].v[0] : (i == 1 ? R2.v[2].v[1] : R2.v[2].v[2]);
-  uint32_t* d = i == 0 ? R2.v[3].v[0] : (i == 1 ? R2.v[3].v[1] : R2.v[3].v[2]);
-  return (e & 2) ? ((e & 1) ? d : c) : ((e & 1) ? b : a);
+  return R2.v[e].v[i];
 }
 __device__ __forceinline__ uint32_t rs_active(uint32_t nbits, int fast_passes) {
   return min(rs_plan(nbits).passes, (uint32_t)fast_passes);

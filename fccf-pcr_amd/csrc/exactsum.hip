@@ -134,13 +134,16 @@ struct XsIn {
   const uint32_t* off;
   const uint32_t* cnt;
   int multi;
-  const float* dp[4];
-  const uint32_t* cp[4];
+  const float* dp[BMAX];
+  const uint32_t* cp[BMAX];
 };
 
 template <class T>
-__device__ __forceinline__ T sel4(const T (&a)[4], int b) {  // a select, not an index (see B4)
-  return b == 0 ? a[0] : (b == 1 ? a[1] : (b == 2 ? a[2] : a[3]));
+__device__ __forceinline__ T sel4(const T (&a)[BMAX], int b) {  // a select chain, not a dynamic index
+  T r = a[0];
+#pragma unroll
+  for (int q = 1; q < BMAX; ++q) r = b == q ? a[q] : r;
+  return r;
 }
 
 __device__ __forceinline__ uint32_t prob_n(const XsIn& in, int b) {
@@ -520,10 +523,10 @@ void exact_sum(const float* data, int S, int K, const uint32_t* off, const uint3
 
 void exact_sum_n(const float* const* data, const uint32_t* const* cnt, int nprob, int S, int K, float* out, bool divide,
                  XsBufs x, hipStream_t st) {
-  if (nprob < 1 || nprob > 4) throw Error(FCCF_E_INTERNAL, "exact_sum_n: 1 to 4 arrays");
+  if (nprob < 1 || nprob > BMAX) throw Error(FCCF_E_INTERNAL, "exact_sum_n: 1 to BMAX arrays");
   XsIn in{};
   in.multi = 1;
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < BMAX; ++b) {
     in.dp[b] = data[b < nprob ? b : nprob - 1];
     in.cp[b] = cnt[b < nprob ? b : nprob - 1];
   }

@@ -506,7 +506,9 @@ size_t byte_stride(const B4<T*>& p, int nbatch) {
 }
 template <class F>
 auto pick(const B4<FaceBufs>& b, F get) -> B4<decltype(get(b[0]))> {
-  return B4<decltype(get(b[0]))>(get(b[0]), get(b[1]), get(b[2]), get(b[3]));
+  B4<decltype(get(b[0]))> r;
+  for (int e = 0; e < BMAX; ++e) r.v[e] = get(b[e]);
+  return r;
 }
 }  // namespace
 

@@ -14,6 +14,7 @@
 // and the float sum runs in the reference's leaf order (one lane per evaluation).
 #define KT_TU 5  // ktrace.h source tag
 #include <algorithm>
+#include <cstdlib>
 
 #include "probe.h"
 #include "kernels.h"
@@ -28,11 +29,14 @@ namespace {
 __global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ s2, uint32_t n2,
                                                       const m44* __restrict__ T, float* __restrict__ s2t,
                                                       const OctState* __restrict__ s1_state, OctState* __restrict__ st,
-                                                      uint32_t* __restrict__ scal, uint32_t n1) {
+                                                      uint32_t* __restrict__ scal, uint32_t n1,
+                                                      uint32_t* __restrict__ ecnt, uint32_t* __restrict__ pts) {
   KT();
   const int e = blockIdx.y;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st[e] = *s1_state;
+    ecnt[e] = 0u;  // (the LDS form's per-evaluation entry counts and point counts)
+    pts[e] = 0u;
     if (e == 0) {
       scal[4] = n1;
       scal[5] = n2;
@@ -95,16 +99,18 @@ __device__ __forceinline__ uint32_t fv_scan_256(uint32_t v, uint32_t* sh, uint32
 // an offset taken with one atomic, and the tile's finite points added to pts[e].
 constexpr uint32_t FV_TILE = 2048, FV_SLOTS = 4096;
 constexpr unsigned long long FV_EMPTY = ~0ull;
+// ecnt (the LDS form): evaluation e's entries go to its own region keys[e * (n1 + n2) ..]
+// with their count in ecnt[e], and the key is the morton code alone.
 __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1, const float* __restrict__ s2t,
                                                     const OctState* __restrict__ st, uint32_t* __restrict__ scal,
                                                     double res, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                    uint32_t* __restrict__ pts) {
+                                                    uint32_t* __restrict__ pts, uint32_t* __restrict__ ecnt) {
   KT();
   __shared__ unsigned long long hk[FV_SLOTS];
   __shared__ uint32_t hc[FV_SLOTS];
   __shared__ uint32_t sh[4], sbase;
   const int e = blockIdx.y;
-  const uint32_t n1 = scal[4], n2 = scal[5], shift = scal[3] - 1u;
+  const uint32_t n1 = scal[4], n2 = scal[5], shift = ecnt ? 63u : scal[3] - 1u;
   const uint32_t n = n1 + n2, i0 = blockIdx.x * FV_TILE;
   if (i0 >= n) return;
   const OctState S = st[e];
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
     const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
     if (!finite3(p[0], p[1], p[2])) continue;
     ++fin;
-    const unsigned long long key = ((unsigned long long)e << shift) | oct_code(S, res, p[0], p[1], p[2]);
+    const unsigned long long key = (ecnt ? 0ull : (unsigned long long)e << shift) | oct_code(S, res, p[0], p[1], p[2]);
     uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52);  // 12 bits: FV_SLOTS
     for (;;) {
       const unsigned long long old = atomicCAS(&hk[h], FV_EMPTY, key);
@@ -141,7 +147,7 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
   uint32_t pos = fv_scan_256(occ, sh, &tot);
   fv_scan_256(fin, sh, &ftot);
   if (threadIdx.x == 0) {
-    sbase = atomicAdd(&scal[0], tot);
+    sbase = ecnt ? (uint32_t)e * n + atomicAdd(&ecnt[e], tot) : atomicAdd(&scal[0], tot);
     if (ftot) atomicAdd(&pts[e], ftot);
   }
   __syncthreads();
@@ -153,6 +159,144 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
     keys[pos] = hk[j];
     vals[pos] = hc[j];
     ++pos;
+  }
+}
+
+// The LDS form, one 1024-thread workgroup per evaluation e: its entries merged into an
+// LDS table (leaf code -> source, target counts; FV_LDS_SLOTS = 2 x FV_LDS_MAX slots),
+// the leaves compacted, each leaf's term (:830-835) placed at its rank in code order
+// (the count of smaller codes: U^2 LDS-broadcast compares, ~1400 leaves at c2-c5), and
+// the terms summed in that order by one lane -- the reference's sequential
+// similar_num -- then score = similar_num / allinvec.  More than lds_cap
+// leaves: FV_ERR_LDS, no score (the caller reruns in the sorted form).
+constexpr uint32_t FV_LDS_SLOTS = 2 * FV_LDS_MAX;
+__global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                  const uint32_t* __restrict__ ecnt, const uint32_t* __restrict__ pts,
+                                                  uint32_t* __restrict__ scal, float* __restrict__ scores,
+                                                  FineMail* __restrict__ mail, uint32_t lds_cap) {
+  KT();
+  __shared__ unsigned long long hk[FV_LDS_SLOTS];
+  __shared__ uint32_t hs[FV_LDS_SLOTS], ht[FV_LDS_SLOTS];
+  __shared__ float term[FV_LDS_MAX];  // the leaves' terms in code order
+  __shared__ uint32_t snu, sover;
+  const int e = blockIdx.x;
+  const uint32_t n = scal[4] + scal[5], m = ecnt[e];
+  const uint64_t* __restrict__ ke = keys + (size_t)e * n;
+  const uint32_t* __restrict__ ve = vals + (size_t)e * n;
+  for (uint32_t j = threadIdx.x; j < FV_LDS_SLOTS; j += 1024) {
+    hk[j] = FV_EMPTY;
+    hs[j] = 0u;
+    ht[j] = 0u;
+  }
+  if (threadIdx.x == 0) {
+    snu = 0u;
+    sover = 0u;
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < m; j += 1024) {
+    const unsigned long long key = ke[j];
+    const uint32_t c = ve[j];
+    uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 51);  // 13 bits: FV_LDS_SLOTS
+    bool ok = false;
+    for (uint32_t probe = 0; probe < FV_LDS_SLOTS; ++probe) {
+      const unsigned long long old = atomicCAS(&hk[h], FV_EMPTY, key);
+      if (old == FV_EMPTY) {
+        if (atomicAdd(&snu, 1u) >= lds_cap) sover = 1u;
+        ok = true;
+        break;
+      }
+      if (old == key) {
+        ok = true;
+        break;
+      }
+      h = (h + 1u) & (FV_LDS_SLOTS - 1u);
+    }
+    if (!ok) {
+      sover = 1u;
+      continue;
+    }
+    atomicAdd(&hs[h], c & 0xFFFFu);
+    atomicAdd(&ht[h], c >> 16);
+  }
+  __syncthreads();
+  if (sover) {  // (uniform) more leaves than the LDS form takes
+    if (threadIdx.x == 0) atomicOr(&scal[7], FV_ERR_LDS);  // (k_fv_mail_err copies the word to the mailbox)
+    return;
+  }
+  // the U occupied slots compacted to [0, U) in place (every thread reads its slots
+  // before the barrier, then writes)
+  const uint32_t U = snu;
+  {
+    constexpr uint32_t PER = FV_LDS_SLOTS / 1024;
+    unsigned long long k8[PER];
+    uint32_t s8[PER], t8[PER], occ = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t j = threadIdx.x * PER + q;
+      k8[q] = hk[j];
+      s8[q] = hs[j];
+      t8[q] = ht[j];
+      occ += k8[q] != FV_EMPTY ? 1u : 0u;
+    }
+    __shared__ uint32_t wsum[16];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t x = occ;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t pos = x - occ;
+    for (uint32_t w = 0; w < wave; ++w) pos += wsum[w];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q)
+      if (k8[q] != FV_EMPTY) {
+        hk[pos] = k8[q];
+        hs[pos] = s8[q];
+        ht[pos] = t8[q];
+        ++pos;
+      }
+  }
+  __syncthreads();
+  // each leaf's place in code order: the number of smaller codes (the codes are
+  // distinct after the merge; every thread reads the same code at the same time, an
+  // LDS broadcast), and its term (:830-835) written there
+  for (uint32_t i = threadIdx.x; i < U; i += 1024) {
+    const unsigned long long key = hk[i];
+    uint32_t rank = 0;
+    uint32_t j = 0;
+    for (; j + 4 <= U; j += 4) {
+      const unsigned long long a = hk[j], b = hk[j + 1], c = hk[j + 2], d = hk[j + 3];
+      rank += (a < key ? 1u : 0u) + (b < key ? 1u : 0u) + (c < key ? 1u : 0u) + (d < key ? 1u : 0u);
+    }
+    for (; j < U; ++j) rank += hk[j] < key ? 1u : 0u;
+    const float sn = (float)hs[i], tn = (float)ht[i];
+    float t = 0.f;
+    if (sn >= 1.f && tn >= 1.f) {
+      const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
+      t = (sn + tn) * (mn / mx);
+    }
+    term[rank] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float similar = 0.f;  // similar_num += term, leaf by leaf (a sequential float sum)
+    uint32_t i = 0;
+    for (; i + 8 <= U; i += 8) {
+      float t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = term[i + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) similar += t[q];
+    }
+    for (; i < U; ++i) similar += term[i];
+    const uint32_t p = pts[e];
+    if (p >= (1u << 24)) atomicOr(&scal[7], FV_ERR_POINTS);  // float allinvec would round: unsupported size
+    const float sc = similar / (float)p;
+    scores[e] = sc;
+    if (mail) mail->scores[e] = sc;
   }
 }
 
@@ -214,6 +358,12 @@ __global__ void k_fv_score(const float* __restrict__ similar, const float* __res
   if (mail && e == 0) mail->err = scal[7];
 }
 
+// the LDS form's error word into the mailbox (k_fv_score writes it in the sorted form)
+__global__ void k_fv_mail_err(const uint32_t* __restrict__ scal, FineMail* __restrict__ mail) {
+  KT();
+  if (threadIdx.x == 0) mail->err = scal[7];
+}
+
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
   uint32_t g = (cap + per - 1) / per;
   return g < 1 ? 1 : (g > mx ? mx : g);
@@ -222,11 +372,11 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 }  // namespace
 
 void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
-                       double res, FineBufs b, hipStream_t st, FineMail* mail) {
+                       double res, FineBufs b, hipStream_t st, FineMail* mail, int mode, uint32_t lds_cap) {
   if (E <= 0) return;
   const size_t astride = aggr_floats(n2);
   k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
-                                                                  n1);
+                                                                  n1, b.nseg_e, b.pts);
   // scal[5] holds n2 for the device-count interfaces
   uint32_t* d_n2 = b.scal + 5;
   SeqStrides sd;  // evaluation e: its own transformed S2 copy, aggregates and state; shared count
@@ -235,10 +385,19 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   sd.state = sizeof(OctState);
   block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
   octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, sd);
+  const dim3 ge(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E);
+  if (mode == FV_LEAVES_LDS) {
+    // the leaves of each evaluation merged, sorted and summed in LDS: two launches
+    // after the octrees instead of ~20 (scal[7] was zeroed by k_fv_transform)
+    k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, b.nseg_e);
+    k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail,
+                                  std::min<uint32_t>(lds_cap, FV_LDS_MAX));
+    if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, mail);
+    return;
+  }
   k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, b.pts, n1, n2, E);
   const uint32_t n = (uint32_t)E * (n1 + n2);  // the entry count's bound (one per point)
-  k_fv_entries<<<dim3(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E), 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0,
-                                                                          b.pts);
+  k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, nullptr);
   // (e | morton) entries with their counts: 4 fast passes cover depth <= 9 with <= 15
   // evaluations; a third buffer, so no copy-back launch
   radix_sort_u64(b.k0, b.v0, b.k1, b.v1, b.scal, n, b.scal + 1, 32, false, b.ss, st, 1, B4<const uint32_t*>(nullptr),
@@ -248,6 +407,16 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   k_fv_ranges<<<1, 64, 0, st>>>(b.pts, b.range, b.nseg_e, b.all, b.scal, E);
   exact_sum(b.term, 1, 1, b.nseg_e + MAX_EVAL, b.nseg_e, E, b.similar, false, b.xs, st);  // similar_num, leaf order
   k_fv_score<<<1, 64, 0, st>>>(b.similar, b.all, b.scores, E, b.scal, mail);
+}
+
+int fine_mode_env(int sticky_sorted) {
+  const char* e = std::getenv("FCCF_FINE_SORTED");
+  return (sticky_sorted || (e && e[0] == '1')) ? FV_LEAVES_SORTED : FV_LEAVES_LDS;
+}
+uint32_t fine_lds_cap_env() {
+  const char* e = std::getenv("FCCF_FINE_LDS_CAP");
+  const long v = e ? std::atol(e) : (long)FV_LDS_MAX;
+  return v < 1 ? 1u : (v > (long)FV_LDS_MAX ? FV_LDS_MAX : (uint32_t)v);
 }
 
 }  // namespace fccf

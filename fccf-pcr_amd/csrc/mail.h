@@ -49,9 +49,9 @@ struct FineMail {
 };
 
 struct HostMail {
-  CloudMail clouds[4];  // per pair slot; a stage group's two slots are adjacent (k_compact_planar)
+  CloudMail clouds[8];  // per pair slot; a stage group's slots are adjacent (k_compact_planar)
   MatchMail match;
-  FineMail fine[4];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
+  FineMail fine[8];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
 };
 
 }  // namespace fccf

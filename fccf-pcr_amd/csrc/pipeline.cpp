@@ -93,6 +93,17 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 
 namespace {
 
+// Pairs per cloud stage: a stage group's clouds (2 per pair) share every launch of the
+// stage (blockIdx.y), so PAIRS_MAX = BMAX / 2; two stage groups alternate, each with
+// PAIRS_MAX slots (ctx CloudSets, mailboxes).  FCCF_PAIR_BATCH=1..PAIRS_MAX overrides
+// the default.
+constexpr int PAIRS_MAX = BMAX / 2;
+constexpr int PAIRS_DEFAULT = 4;
+static_assert(sizeof(((fccf_ctx*)nullptr)->cs) / sizeof(((fccf_ctx*)nullptr)->cs[0]) == 2 * PAIRS_MAX, "slots");
+static_assert(sizeof(HostMail::clouds) / sizeof(CloudMail) == 2 * PAIRS_MAX, "cloud mailboxes");
+static_assert(sizeof(HostMail::fine) / sizeof(FineMail) == 2 * PAIRS_MAX, "fine mailboxes");
+static_assert(Group::SLOTS == 2 * PAIRS_MAX, "group fine buffers per slot");
+
 // ------------------------------------------------------------ per-cloud device state
 struct CloudWS {
   uint32_t cap = 0;
@@ -148,7 +159,7 @@ template <class T, class F>
 B4<T> all_of(const CloudWS* w, int nc, F get) {
   T v[BMAX];
   for (int e = 0; e < BMAX; ++e) v[e] = get(w[e < nc ? e : nc - 1]);
-  return B4<T>(v[0], v[1], v[2], v[3]);
+  return B4<T>(v, BMAX);
 }
 
 // main's VoxelGrid pass (:1668-1678) over the inputs xin (n points each), its
@@ -160,7 +171,7 @@ void seg_pass1(CloudWS* w, int nc, const float* const* xin, const uint32_t* n, f
   const B4<VGBufs> vg = all_of<VGBufs>(w, nc, [](const CloudWS& c) { return c.vg; });
   const float* x[BMAX];
   for (int e = 0; e < BMAX; ++e) x[e] = xin[e < nc ? e : nc - 1];
-  voxel_grid(B4<const float*>(x[0], x[1], x[2], x[3]), sc(0), cap, leaf,
+  voxel_grid(B4<const float*>(x, BMAX), sc(0), cap, leaf,
              all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1; }), sc(1), vg, st, false, nc,
              all_of<float*>(w, nc, [](const CloudWS& c) { return c.ds1f; }), n, entry);
 }
@@ -270,6 +281,14 @@ struct HostTrace {
 // first half (growing ... fine-verify launch) of the same pair.
 struct PhaseB {
   fccf_stats S;
+  FineBufs fb{};  // this pair's fine-verification buffers and inputs (a rerun in the sorted form)
+  struct {
+    const float* s1;
+    const OctState* s1_state;
+    const float* s2;
+    uint32_t n1, n2;
+    float res;
+  } fine_in{};
   std::vector<TS> ctv[3];
   std::vector<int64_t> counts;
   int E = 0, E_loc = 0, analyse_max = 0;  // E_loc: this rank's block of the E fine evaluations
@@ -299,7 +318,7 @@ struct PipeSet {
   // other than the inputs are set only when that graph is captured) and the centroid
   // sums' scratch
   int group_pairs = 0;
-  VGEntry entry[2];
+  VGEntry entry[PAIRS_MAX];
   XsBufs xs;
 };
 
@@ -346,9 +365,11 @@ struct PairIn {
 };
 void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float leaf, const fccf_params& Pa,
                           bool exact2 = false) {
-  if (P < 1 || P > 2 || (P > 1 && c->group)) throw Error(FCCF_E_INTERNAL, "cloud stage: 1 pair, or 2 without a group");
-  auto& cg = c->cs[2 * G];  // the group's arena, stage graphs and fork/join events
-  PipeSet& gs = pset(c, 2 * G);
+  if (P < 1 || P > PAIRS_MAX || (P > 1 && c->group))
+    throw Error(FCCF_E_INTERNAL, "cloud stage: 1 pair, or up to PAIRS_MAX without a group");
+  const int S0 = PAIRS_MAX * G;  // the group's first slot
+  auto& cg = c->cs[S0];          // the group's arena, stage graphs and fork/join events
+  PipeSet& gs = pset(c, S0);
   const int nc = 2 * P;
   hipStream_t st0 = c->sa[0], ss = c->sa[2];
   // both clouds get the larger capacity (all clouds of a stage, in fact), so their
@@ -358,7 +379,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     capmax = (uint32_t)std::max<int64_t>(capmax, std::max(in[j].n_src, in[j].n_tar));
   // the previous pairs on these slots may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for them
-  for (int j = 0; j < 2; ++j) guarded_stream_wait(st0, c->cs[2 * G + j].ev[3]);  // (recorded on the fine stream)
+  for (int j = 0; j < PAIRS_MAX; ++j) guarded_stream_wait(st0, c->cs[S0 + j].ev[3]);  // (recorded on the fine stream)
   cg.arena.ensure(nc * cloud_bytes(capmax, false) + exact_sum_bytes(3 * nc, capmax) + (1 << 20));
   cg.arena.reset();
   float* cen = cg.arena.take_n<float>(3 * BMAX + 4);
@@ -374,7 +395,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   const float* xin[BMAX] = {};
   uint32_t nv[BMAX] = {};
   for (int j = 0; j < P; ++j) {
-    PipeSet& ps = pset(c, 2 * G + j);
+    PipeSet& ps = pset(c, S0 + j);
     ps.t_enq = clk::now();
     ps.in_src = in[j].src;
     ps.in_tar = in[j].tar;
@@ -406,7 +427,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
       ps.w[k] = x;
     }
     // host inputs: staged by stage_inputs() into the slot's inarena on the copy stream
-    if (in[j].staged) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[2 * G + j].ev_in, 0));
+    if (in[j].staged) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[S0 + j].ev_in, 0));
   }
   gs.group_pairs = P;
   // (graph keys are compared bytewise: no padding bytes, or their stack garbage forces
@@ -431,8 +452,8 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
       x[e] = xin[e < nc ? e : nc - 1];
       n[e] = e < nc ? nv[e] : 0u;
     }
-    gs.entry[P - 1].xyz = B4<const float*>(x[0], x[1], x[2], x[3]);
-    gs.entry[P - 1].n = B4<uint32_t>(n[0], n[1], n[2], n[3]);
+    gs.entry[P - 1].xyz = B4<const float*>(x, BMAX);
+    gs.entry[P - 1].n = B4<uint32_t>(n, BMAX);
   }
   VGEntry& entry = gs.entry[P - 1];
   entry.bind();
@@ -442,7 +463,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   // device spans come from s_memrealtime stamps the stage's kernels write (no timing
   // events, which would split the graph: four graphs with events between them were
   // 0.04 ms per registration slower).
-  CloudMail* cmail = &host_mail(c)->clouds[2 * G];  // (slots 2G, 2G + 1 adjacent); never allocated inside the capture
+  CloudMail* cmail = &host_mail(c)->clouds[S0];  // (the group's slots adjacent); never allocated inside the capture
   const XsBufs xs = gs.xs;
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
@@ -464,8 +485,8 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
   }, vg_entry_kernel(), entry.args, DG != nullptr || exact2);
   for (int j = 0; j < P; ++j) {
-    auto& cs = c->cs[2 * G + j];
-    PipeSet& ps = pset(c, 2 * G + j);
+    auto& cs = c->cs[S0 + j];
+    PipeSet& ps = pset(c, S0 + j);
     // external signal for stage_inputs (this slot's inputs have been read): after the graph
     HIP_CHECK(hipEventRecord(cs.ev[0], st0));
     HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
@@ -483,20 +504,21 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   HIP_CHECK(hipGetLastError());
 }
 
-// One pair on slot s (s even: its group's first slot)
+// One pair on slot s (a group's first slot)
 void clouds_enqueue(fccf_ctx* c, int s, const float* src, int64_t n_src, const float* tar, int64_t n_tar,
                     bool staged, float leaf, const fccf_params& P, bool exact2 = false) {
   const PairIn in{src, tar, n_src, n_tar, staged};
-  clouds_enqueue_group(c, s / 2, 1, &in, leaf, P, exact2);
+  clouds_enqueue_group(c, s / PAIRS_MAX, 1, &in, leaf, P, exact2);
 }
 
 // The redo of slot s's stage group (VG_REDO): the same pairs, exact second pass
 void clouds_redo(fccf_ctx* c, int s, const fccf_params& P) {
-  const int G = s / 2;
-  const int np = pset(c, 2 * G).group_pairs;
-  PairIn in[2];
+  const int G = s / PAIRS_MAX;
+  const int S0 = PAIRS_MAX * G;
+  const int np = pset(c, S0).group_pairs;
+  PairIn in[PAIRS_MAX];
   for (int j = 0; j < np; ++j) {
-    const PipeSet& ps = pset(c, 2 * G + j);
+    const PipeSet& ps = pset(c, S0 + j);
     in[j] = PairIn{ps.in_src, ps.in_tar, ps.in_nsrc, ps.in_ntar, ps.staged};
   }
   clouds_enqueue_group(c, G, np, in, pset(c, s).leaf, P, true);
@@ -950,6 +972,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     FineMail& fm = host_mail(c)->fine[s];
     std::memcpy(fm.T, evals.data() + flo, sizeof(m44) * E);  // pinned staging: async H2D
     HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, sf));
+    // the leaf form: LDS per evaluation unless the ctx met an evaluation with more leaves
+    // than it holds (sticky), or the group's sharded gather reads the sorted form's words
+    const int fmode = FG ? FV_LEAVES_SORTED : fine_mode_env(c->fine_sorted.load() ? 1 : 0);
+    const uint32_t fcap = fine_lds_cap_env();
     struct {
       const void* base;
       size_t acap;
@@ -957,15 +983,20 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       uint32_t n1, n2;
       int32_t E;
       float res;
-    } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size};
-    static_assert(sizeof fkey == 5 * 8 + 4 * 4, "graph key without padding");
+      int32_t mode;
+      uint32_t cap;
+    } fkey = {a3.base, a3.cap, w[0].resid, w[1].resid, w[0].fstate, n1, n2, E, P.fine_verify_voxel_size, fmode, fcap};
+    static_assert(sizeof fkey == 5 * 8 + 6 * 4, "graph key without padding");
+    // what phase_b2 needs to rerun the batch in the sorted form (FV_ERR_LDS)
+    pb.fb = fb;
+    pb.fine_in = {w[0].resid, w[0].fstate, w[1].resid, n1, n2, P.fine_verify_voxel_size};
     ht.mark("fine_setup");
     // S1 octree bounds replayed (after the clouds); ev[5]'s stream may be capturing the next pair's clouds
     guarded_stream_wait(sf, c->cs[s].ev[5]);
     HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
-                        &fm);
+                        &fm, fmode, fcap);
     });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
@@ -1009,9 +1040,21 @@ void phase_b2(fccf_ctx* c, int s) {
     if (c->group && c->group->n > 1) {  // every rank's block, gathered in rank order
       group_fine_scores(c->group, s, E, scores.data(), &err);
     } else {
-      const FineMail& fm = host_mail(c)->fine[s];
-      std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
+      FineMail& fm = host_mail(c)->fine[s];
       err = fm.err;
+      if (err & FV_ERR_LDS) {
+        // an evaluation had more leaves than the LDS form holds: the batch again in the
+        // sorted form, eagerly, and the ctx keeps that form (the scores are the same)
+        c->fine_sorted = true;
+        hipStream_t sf = c->sa[1];
+        const auto& fi = pb.fine_in;
+        fine_verify_batch(fi.s1, fi.n1, fi.s1_state, fi.s2, fi.n2, E, (double)fi.res, pb.fb, sf, &fm, FV_LEAVES_SORTED);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(sf));
+        err = fm.err;
+        ++S.fine_reruns;
+      }
+      std::memcpy(scores.data(), fm.scores, 4 * (size_t)E);
     }
     if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
     if (pb.E_loc > 0) {
@@ -1319,16 +1362,16 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
   } join_guard{c};
   if (c->group) order_reset(c->group);
-  // Pairs per cloud stage: two -- both pairs' four clouds in the same launches, so the
-  // sort's dependent rounds and the face stage's small launches are paid once for both
-  // (DESIGN.md §7) -- unless a group is attached (its sharded sort gathers one pair's
-  // slices), a probe runs (its launch records count one pair), or FCCF_PAIR_BATCH=1.
+  // Pairs per cloud stage: four -- their eight clouds in the same launches, so the
+  // sort's dependent rounds and the face stage's small launches are paid once for all
+  // (DESIGN.md §12) -- unless a group is attached (its sharded sort gathers one pair's
+  // slices) or a probe runs (its launch records count one pair); FCCF_PAIR_BATCH=1..4.
   const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
-  const bool one_pair = pb_env && pb_env[0] == '1';
-  const int PP = (c->group || c->probe.on() || one_pair) ? 1 : 2;
+  const int pp_env = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
+  const int PP = (c->group || c->probe.on()) ? 1 : std::max(1, std::min(PAIRS_MAX, pp_env));
   const int ng = (n + PP - 1) / PP;  // stage groups; group g uses slots 2 (g & 1) + j
   auto cnt = [&](int g) { return std::min(PP, n - g * PP); };
-  auto slot = [&](int i) { return 2 * ((i / PP) & 1) + i % PP; };
+  auto slot = [&](int i) { return PAIRS_MAX * ((i / PP) & 1) + i % PP; };
   // Host inputs: group g+1's clouds are staged on the copy stream at the start of
   // group g (from the helper thread: the pageable copy blocks its caller), so the host
   // link works while group g's cloud stage runs.
@@ -1344,7 +1387,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   };
   auto enq_group = [c, n_src, n_tar, on_device, leaf, &P, dsrc, dtar, cnt, PP](int g) {
     HIP_CHECK(hipSetDevice(c->device));  // a no-op after the first call on the helper thread
-    PairIn pin[2];
+    PairIn pin[PAIRS_MAX];
     for (int j = 0; j < cnt(g); ++j) {
       const int i = g * PP + j;
       pin[j] = PairIn{dsrc(i), dtar(i), n_src[i], n_tar[i], !on_device};

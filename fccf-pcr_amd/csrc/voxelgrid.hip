@@ -390,7 +390,11 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
                 const uint32_t* n_in, VGEntry* entry) {
   const B4<const uint32_t*> d_n(d_nw);
   // one field of every problem's buffers (entries past nbatch repeat the caller's last)
-  auto F = [&](auto get) { return B4<decltype(get(b[0]))>(get(b[0]), get(b[1]), get(b[2]), get(b[3])); };
+  auto F = [&](auto get) {
+    B4<decltype(get(b[0]))> r;
+    for (int e = 0; e < BMAX; ++e) r.v[e] = get(b[e]);
+    return r;
+  };
   const B4<VGParams*> P = F([](const VGBufs& v) { return v.params; });
   const B4<uint32_t*> k0 = F([](const VGBufs& v) { return v.k0; }), v0 = F([](const VGBufs& v) { return v.v0; });
   const B4<uint32_t*> k1 = F([](const VGBufs& v) { return v.k1; }), v1 = F([](const VGBufs& v) { return v.v1; });

@@ -98,6 +98,9 @@ typedef struct fccf_stats {
   /* appended in round 4 */
   int32_t shard_ranks;           /* ranks of the attached group (1: no group)      */
   uint32_t sharded;              /* FCCF_SHARDED_* stages this call split over them */
+  int64_t fine_reruns;           /* fine verifications rerun in the sorted leaf form
+                                    (an evaluation with more 0.5 m leaves than the
+                                    LDS form holds; the scores are the same)      */
 } fccf_stats;
 /* fccf_stats.sharded bits */
 enum {

@@ -330,8 +330,9 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
     groups of two pairs, the last one single for an odd count; pipeline.cpp
     clouds_enqueue_group).  Pairs of different sizes within a group, single
     registrations between batches (the one-pair and two-pair stages lay the workspace
-    out differently, so their cached graphs must never be mixed), and the one-pair
-    form (FCCF_PAIR_BATCH=1) must all give the oracle's T bit for bit."""
+    out differently, so their cached graphs must never be mixed), and the other stage
+    forms (FCCF_PAIR_BATCH=1, 3, 4: up to eight clouds per launch) must all give the
+    oracle's T bit for bit."""
     base_src, base_tar, _ = fccf.synth_pair(90_000)
 
     def make_pairs(seed):  # the same sizes (so the same cached stage graphs), new points
@@ -359,7 +360,47 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
     Tb, _ = ctx.register_batch(pairs[:2], 0.1)  # one group of two
     for T, ref in zip(Tb, refs[:2]):
         np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
-    monkeypatch.setenv("FCCF_PAIR_BATCH", "1")
-    Tb1, _ = ctx.register_batch(pairs, 0.1)
-    for T, ref in zip(Tb1, refs):
-        np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    for pp in ("1", "3", "4"):  # one pair per stage, and three or four (up to 8 clouds per launch)
+        monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
+        Tb1, sb1 = ctx.register_batch(pairs, 0.1)
+        for T, ref in zip(Tb1, refs):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"{pp} pairs per stage")
+        for x in sb1:
+            ms = x.as_dict()["ms"]
+            assert 0.0 < ms["downsample"] < 1000.0 and 0.0 < ms["voxelfit"] < 1000.0, (pp, ms)
+
+
+def test_fine_verify_leaf_forms_agree(fccf, oracle, monkeypatch):
+    """fine_verify (FCCF.cpp:785-839) in its two leaf forms: per evaluation in LDS
+    (default: the tile entries merged, sorted and summed by one workgroup) and sorted
+    device-wide (FCCF_FINE_SORTED=1, the fallback).  Scores bit-equal between the forms
+    through the stage export; a capacity below the scene's leaf count (FCCF_FINE_LDS_CAP)
+    makes the pipeline rerun the batch in the sorted form (fine_reruns = 1) with T still
+    bit-exact, and the ctx keeps the sorted form afterwards."""
+    src, tar, _ = fccf.synth_pair(100_000)
+    ref = oracle.Run(src, tar, 0.1, oracle.INTROSORT)
+    c = fccf.Ctx(0, debug=True)
+    try:
+        T, st = c.register(src, tar, 0.1)
+        np.testing.assert_array_equal(T.view(np.uint32), ref.T.view(np.uint32))
+        assert st.fine_reruns == 0
+        s1, s2 = c.debug("res1").reshape(-1, 3), c.debug("res2").reshape(-1, 3)
+        Ts = np.stack([np.eye(4, dtype=np.float32)] + [fv.reshape(-1, 18)[:, :16].reshape(-1, 4, 4)[0]
+                                                       for fv in (c.debug("fv0"), c.debug("fv2")) if fv.size])
+        a = c.fine_verify(s1, s2, Ts)
+        monkeypatch.setenv("FCCF_FINE_SORTED", "1")
+        b = c.fine_verify(s1, s2, Ts)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+        monkeypatch.delenv("FCCF_FINE_SORTED")
+        monkeypatch.setenv("FCCF_FINE_LDS_CAP", "16")
+        d = c.fine_verify(s1, s2, Ts)  # the export falls back by itself
+        np.testing.assert_array_equal(a.view(np.uint32), d.view(np.uint32))
+        T2, st2 = c.register(src, tar, 0.1)
+        np.testing.assert_array_equal(T2.view(np.uint32), ref.T.view(np.uint32))
+        assert st2.fine_reruns == 1
+        monkeypatch.delenv("FCCF_FINE_LDS_CAP")
+        T3, st3 = c.register(src, tar, 0.1)  # sticky: sorted from the start, no rerun
+        np.testing.assert_array_equal(T3.view(np.uint32), ref.T.view(np.uint32))
+        assert st3.fine_reruns == 0
+    finally:
+        c.close()

@@ -93,7 +93,11 @@ def report(trace_dir, host_log, out=None):
             cur = sp[1]
     xs = [x for x in ks if x[2].startswith("k_xs") and x[0] < cur]
     mk = dict(marks)
-    fine = span("k_fv_transform", "k_fv_score")
+    fv = [x for x in ks if x[2].startswith("k_fv_transform")]
+    fine = None
+    if fv:  # from the transform to the last k_fv_* kernel after it (k_fv_score / k_fv_mail_err)
+        last = [x for x in ks if x[2].startswith("k_fv") and x[0] >= fv[0][0]]
+        fine = (fv[0][0], last[-1][1])
     match = [x for x in ks if x[2].startswith("k_match")]
     out_lines.append(f"{'segment':34s} {'start':>8s} {'end':>8s} {'us':>8s}")
     first_k = ks[0][0] if ks else 0.0

@@ -17,7 +17,7 @@ ds, dt = ctx.upload(src), ctx.upload(tar)
 pair = ((ds, len(src)), (dt, len(tar)))
 for _ in range(3):
     ctx.register_device(ds, len(src), dt, len(tar), cfg["leaf"])
-ctx.register_batch([pair] * 3, cfg["leaf"], on_device=True)
+ctx.register_batch([pair] * 8, cfg["leaf"], on_device=True)  # both stage groups
 e, vg = [], []
 for _ in range(reps):
     a = time.perf_counter()
