@@ -526,9 +526,10 @@ def main():
     for _ in range(args.warmup):
         T, st = reg()
     if pipelined and args.warmup:
-        # eight pairs: both stage groups of the batch (up to four pairs per cloud stage,
-        # groups on alternating workspaces) capture their graphs here, not in the timed batch
-        batch(8)
+        # the timed batch's own shape: every stage group of it (up to four pairs per cloud
+        # stage, groups on alternating workspaces, a smaller last group) captures its
+        # graphs here, not in the timed batch
+        batch(args.steps)
     barrier(dist)
     t0 = time.perf_counter()
     Ks = 0

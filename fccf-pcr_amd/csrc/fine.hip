@@ -164,9 +164,9 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
 
 // The LDS form, one 1024-thread workgroup per evaluation e: its entries merged into an
 // LDS table (leaf code -> source, target counts; FV_LDS_SLOTS = 2 x FV_LDS_MAX slots),
-// the leaves compacted, each leaf's term (:830-835) placed at its rank in code order
-// (the count of smaller codes: U^2 LDS-broadcast compares, ~1400 leaves at c2-c5), and
-// the terms summed in that order by one lane -- the reference's sequential
+// the leaves compacted, each leaf's term (:830-835) formed, the (code, term) pairs
+// sorted by code (bitonic over the next power of two above the leaf count, ~1400 at
+// c2-c5), and the terms summed in that order by one lane -- the reference's sequential
 // similar_num -- then score = similar_num / allinvec.  More than lds_cap
 // leaves: FV_ERR_LDS, no score (the caller reruns in the sorted form).
 constexpr uint32_t FV_LDS_SLOTS = 2 * FV_LDS_MAX;
@@ -176,8 +176,8 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
                                                   FineMail* __restrict__ mail, uint32_t lds_cap) {
   KT();
   __shared__ unsigned long long hk[FV_LDS_SLOTS];
-  __shared__ uint32_t hs[FV_LDS_SLOTS], ht[FV_LDS_SLOTS];
-  __shared__ float term[FV_LDS_MAX];  // the leaves' terms in code order
+  __shared__ uint32_t hs[FV_LDS_SLOTS];
+  __shared__ __attribute__((aligned(16))) uint32_t ht[FV_LDS_SLOTS];
   __shared__ uint32_t snu, sover;
   const int e = blockIdx.x;
   const uint32_t n = scal[4] + scal[5], m = ecnt[e];
@@ -260,38 +260,64 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
       }
   }
   __syncthreads();
-  // each leaf's place in code order: the number of smaller codes (the codes are
-  // distinct after the merge; every thread reads the same code at the same time, an
-  // LDS broadcast), and its term (:830-835) written there
-  for (uint32_t i = threadIdx.x; i < U; i += 1024) {
-    const unsigned long long key = hk[i];
-    uint32_t rank = 0;
-    uint32_t j = 0;
-    for (; j + 4 <= U; j += 4) {
-      const unsigned long long a = hk[j], b = hk[j + 1], c = hk[j + 2], d = hk[j + 3];
-      rank += (a < key ? 1u : 0u) + (b < key ? 1u : 0u) + (c < key ? 1u : 0u) + (d < key ? 1u : 0u);
+  // each leaf's term (:830-835) beside its code (in ht, as float bits), slots up to the
+  // next power of two emptied, then a bitonic sort of (code, term) over those P2 slots:
+  // the terms end in code order in [0, U)
+  uint32_t P2 = 2;
+  while (P2 < U) P2 <<= 1;
+  for (uint32_t i = threadIdx.x; i < P2; i += 1024) {
+    if (i < U) {
+      const float sn = (float)hs[i], tn = (float)ht[i];
+      float t = 0.f;
+      if (sn >= 1.f && tn >= 1.f) {
+        const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
+        t = (sn + tn) * (mn / mx);
+      }
+      ht[i] = __float_as_uint(t);
+    } else {
+      hk[i] = FV_EMPTY;
     }
-    for (; j < U; ++j) rank += hk[j] < key ? 1u : 0u;
-    const float sn = (float)hs[i], tn = (float)ht[i];
-    float t = 0.f;
-    if (sn >= 1.f && tn >= 1.f) {
-      const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
-      t = (sn + tn) * (mn / mx);
-    }
-    term[rank] = t;
   }
   __syncthreads();
+  for (uint32_t k = 2; k <= P2; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P2; i += 1024) {
+        const uint32_t l = i ^ jj;
+        if (l > i) {
+          const unsigned long long a = hk[i], b = hk[l];
+          if (((i & k) == 0) ? a > b : a < b) {
+            hk[i] = b;
+            hk[l] = a;
+            const uint32_t t0 = ht[i];
+            ht[i] = ht[l];
+            ht[l] = t0;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
     float similar = 0.f;  // similar_num += term, leaf by leaf (a sequential float sum)
-    uint32_t i = 0;
-    for (; i + 8 <= U; i += 8) {
-      float t[8];
+    // groups of 16 terms read as four 16-byte loads, the next group's issued before the
+    // current one's adds (positions past U are masked)
+    const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(ht);
+    uint4 cur[4], nxt[4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t[q] = term[i + q];
+    for (int u = 0; u < 4; ++u) cur[u] = t4[u];
+    for (uint32_t g = 0; g < U; g += 16) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) similar += t[q];
+      for (int u = 0; u < 4; ++u) nxt[u] = t4[((g + 16) >> 2) + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (g + 4 * u + 0 < U) similar += __uint_as_float(cur[u].x);
+        if (g + 4 * u + 1 < U) similar += __uint_as_float(cur[u].y);
+        if (g + 4 * u + 2 < U) similar += __uint_as_float(cur[u].z);
+        if (g + 4 * u + 3 < U) similar += __uint_as_float(cur[u].w);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
     }
-    for (; i < U; ++i) similar += term[i];
     const uint32_t p = pts[e];
     if (p >= (1u << 24)) atomicOr(&scal[7], FV_ERR_POINTS);  // float allinvec would round: unsupported size
     const float sc = similar / (float)p;

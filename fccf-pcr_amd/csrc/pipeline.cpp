@@ -380,10 +380,14 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   // the previous pairs on these slots may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for them
   for (int j = 0; j < PAIRS_MAX; ++j) guarded_stream_wait(st0, c->cs[S0 + j].ev[3]);  // (recorded on the fine stream)
-  cg.arena.ensure(nc * cloud_bytes(capmax, false) + exact_sum_bytes(3 * nc, capmax) + (1 << 20));
+  // (the centroid scratch is carved for BMAX clouds whatever the pair count, so slot
+  // j's clouds sit at the same addresses in every stage form, and the per-slot graphs
+  // keyed by those addresses -- the S1 replay, fine verification -- keep replaying when
+  // a batch ends with a smaller group)
+  cg.arena.ensure(nc * cloud_bytes(capmax, false) + exact_sum_bytes(3 * BMAX, capmax) + (1 << 20));
   cg.arena.reset();
   float* cen = cg.arena.take_n<float>(3 * BMAX + 4);
-  gs.xs = exact_sum_carve(cg.arena.take(exact_sum_bytes(3 * nc, capmax)), 3 * nc, capmax);
+  gs.xs = exact_sum_carve(cg.arena.take(exact_sum_bytes(3 * BMAX, capmax)), 3 * BMAX, capmax);
   // Row D: with a group, large clouds shard their K1 sort after its first rounds
   // (introsort.hip, group.cpp); the stage then runs eagerly (a host step between the
   // sort and the gather of the sorted slices)

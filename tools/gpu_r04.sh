@@ -14,7 +14,7 @@ rc=$?; echo "tests rc=$rc: $(tail -1 $OUT/pytest_gpu.log)"; [ $rc -eq 0 ] || { g
 step ab
 bash tools/ab_pairs.sh | tee $OUT/ab_pairs.log || exit 1
 step bench_c3
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 python3 tools/bench_summary.py $OUT/bench.json 2>/dev/null | head -20
 for cfg in c4 c5; do
   step bench_$cfg
@@ -25,4 +25,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/stats -o run -
 step pmc
 BENCH=1 STEPS=5 bash tools/gpu_pmc_calib.sh $TAG/pmc || exit 1
 python3 tools/pmc_calib.py $OUT/pmc $OUT/pmc/pmc_calib.json
+python3 tools/pmc_traffic.py $OUT/pmc c3 $OUT/pmc/pmc_traffic.json > $OUT/pmc/pmc_traffic.txt
+rm -rf $OUT/pmc/bench_p? $OUT/pmc/calib_p? $OUT/stats/run_kernel_trace.csv  # (gpurun returns at most 64 MiB)
 echo done
