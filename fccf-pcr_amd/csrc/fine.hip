@@ -279,25 +279,38 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
     }
   }
   __syncthreads();
+  // bitonic network over P2 slots, one compare-exchange per thread per 2048 slots and
+  // stage.  Pair c = (i, i | jj) with i = c with a zero bit inserted at jj: for jj < 128
+  // the pairs of wave w's indices (c = 64 w + lane, + 1024 r) stay inside slots that only
+  // wave w touches, so those stages (56 of 66 at 2048 slots) need a wave barrier only;
+  // a stage of jj >= 128 is bracketed by workgroup barriers
   for (uint32_t k = 2; k <= P2; k <<= 1) {
     for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = threadIdx.x; i < P2; i += 1024) {
-        const uint32_t l = i ^ jj;
-        if (l > i) {
-          const unsigned long long a = hk[i], b = hk[l];
-          if (((i & k) == 0) ? a > b : a < b) {
-            hk[i] = b;
-            hk[l] = a;
-            const uint32_t t0 = ht[i];
-            ht[i] = ht[l];
-            ht[l] = t0;
-          }
+      if (jj >= 128) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      for (uint32_t c = threadIdx.x; c < P2 / 2; c += 1024) {
+        const uint32_t i = ((c & ~(jj - 1)) << 1) | (c & (jj - 1)), l = i | jj;
+        const unsigned long long a = hk[i], b = hk[l];
+        if (((i & k) == 0) ? a > b : a < b) {
+          hk[i] = b;
+          hk[l] = a;
+          const uint32_t t0 = ht[i];
+          ht[i] = ht[l];
+          ht[l] = t0;
         }
       }
-      __syncthreads();
+      if (jj >= 128) __syncthreads();
     }
   }
-  if (threadIdx.x == 0) {
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  if (lane == 0) {
     float similar = 0.f;  // similar_num += term, leaf by leaf (a sequential float sum)
     // groups of 16 terms read as four 16-byte loads, the next group's issued before the
     // current one's adds (positions past U are masked)
