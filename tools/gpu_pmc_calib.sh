@@ -10,13 +10,13 @@ STEPS=${STEPS:-5}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-if [ "${CALIB:-1}" = 1 ]; then
-tools/pmc_calib > $OUT/calib_alg.txt
 P1="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
 P2="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"
 P3="FETCH_SIZE"
 P4="WRITE_SIZE"
 P5="TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum TCC_BUBBLE_sum"
+if [ "${CALIB:-1}" = 1 ]; then
+tools/pmc_calib > $OUT/calib_alg.txt
 i=0
 for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   i=$((i+1))
@@ -30,5 +30,6 @@ i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace -f csv -d $OUT/bench_p$i -o run -- python3 -u $B > $OUT/bench_p$i.json 2> $OUT/bench_p$i.err
+  ls $OUT/bench_p$i/*counter_collection.csv > /dev/null || { echo "bench pass $i: no counters"; exit 1; }
   echo "bench pass $i ok"
 done
