@@ -41,7 +41,13 @@
 namespace fccf {
 namespace {
 
-constexpr uint32_t IS_TILE = 2048;   // elements per round tile (small clouds)
+#ifndef IS_TILE_VAL
+#define IS_TILE_VAL 2048
+#endif
+// elements per round tile (small clouds).  4096 (-DIS_TILE_VAL=4096) measured at four
+// pairs per stage: pipelined the same (0.865-0.871 vs 0.847-0.870 ms), single
+// registration slower (main VoxelGrid 0.83 vs 0.73 ms)
+constexpr uint32_t IS_TILE = IS_TILE_VAL;
 constexpr uint32_t IS_TILE_L = 4096;  // elements per round tile (large clouds: fewer workgroup latency chains)
 // clouds from this size plan each round once (k_is_count_plan; sharded sorts always):
 // c5 (10M) 7.93 ms per registration with it vs 10.6 without, c4 (5M) 3.98 vs 3.85
