@@ -455,7 +455,8 @@ def main():
     ap.add_argument("--probe-kernel", default="auto", help="kernel for the roofline object (auto = dominant)")
     ap.add_argument("--no-sharded", action="store_true",
                     help="N>1: skip the strong-scaling leg (one c4 / c5 registration by an RCCL group of ranks)")
-    ap.add_argument("--sharded-timeout", type=float, default=300.0, help="time limit of a strong-scaling child")
+    ap.add_argument("--sharded-timeout", type=float, default=180.0,
+                    help="time limit of a strong-scaling child (normally well under a minute)")
     ap.add_argument("--sharded-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--child-world", type=int, default=1, help=argparse.SUPPRESS)
