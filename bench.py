@@ -298,7 +298,7 @@ def sharded_child(args):
                 pair = ((ds, src.shape[0]), (dt, tar.shape[0]))
                 T0, _ = ctx.register_device(ds, src.shape[0], dt, tar.shape[0], leaf)  # unsharded reference
                 if rank == 0:
-                    ctx.register_batch([pair] * 2, leaf, on_device=True)  # warm
+                    ctx.register_batch([pair] * steps, leaf, on_device=True)  # warm: the timed batch's own shape
                     a = time.perf_counter()
                     ctx.register_batch([pair] * steps, leaf, on_device=True)
                     res["one_gpu_ms_per_registration"] = (time.perf_counter() - a) / steps * 1e3
