@@ -2600,8 +2600,15 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   FCCF_LAUNCH("k_is_block", (b[0].ctl + 20, 16.0, nbatch > 1 ? b[1].ctl + 20 : nullptr, 16.0, 0.0), k_is_block,
               dim3(IS_OWN_BLOCKS / nbatch, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
+  // dev: FCCF_IS_WAVE_GRID = workgroups per launch, split over the clouds (default
+  // IS_WAVE_BLOCKS per cloud)
+  static const int wave_grid = [] {
+    const char* s = std::getenv("FCCF_IS_WAVE_GRID");
+    return s ? std::atoi(s) : 0;
+  }();
+  const int wave_blocks = wave_grid > 0 ? std::max(1, wave_grid / nbatch) : IS_WAVE_BLOCKS;
   FCCF_LAUNCH("k_is_wave", (b[0].ctl + 19, 16.0, nbatch > 1 ? b[1].ctl + 19 : nullptr, 16.0, 0.0), k_is_wave,
-              dim3(IS_WAVE_BLOCKS, nbatch), IS_WT, 0, st, k0, v0, b);
+              dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
 }
 
