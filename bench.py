@@ -221,10 +221,11 @@ class _SelftestCtx:
         return self.register_device(0, 0, 0, 0, leaf)
 
 
-def pmc_traffic(kernel, config):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of the
-    same workload (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py from
-    rocprofv3 --pmc passes over this bench command), else None."""
+def pmc_traffic(kernel, config, width):
+    """HBM bytes per launch of `kernel` at launch width `width` (clouds per launch) from
+    the newest committed PMC summary of the same workload and shape
+    (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
+    passes), else None.  Summaries without a width are of single registrations (2)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
     for f in reversed(files):
@@ -232,7 +233,7 @@ def pmc_traffic(kernel, config):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("config", "c3") != config:
+        if d.get("config", "c3") != config or int(d.get("width", 2)) != width:
             continue
         # (the probe label names the kernel family: the sort's round kernels have a small-
         # and a large-cloud form, k_is_scatter_s / k_is_scatter, by symbol)
@@ -242,15 +243,31 @@ def pmc_traffic(kernel, config):
     return None
 
 
-def probe_pass(ctx, reg, kernel, steps):
+def probe_pass(ctx, run, kernel, reps=1):
+    """Every launch of `kernel` during `reps` calls of run() (a pipelined batch, or
+    single registrations), timed with HIP events on its own stream.  Returns the totals
+    (ms, launches, algorithmic bytes) and the same split by launch width (clouds per
+    batched launch: {width: (ms, launches, bytes)})."""
     ctx.set_probe(kernel)
-    reg()  # one untimed eager warm-up step
+    run()  # one untimed eager warm-up call of the same shape
     ctx.set_probe(kernel)  # resets the totals
-    for _ in range(steps):
-        reg()
+    for _ in range(reps):
+        run()
     ms, n, b = ctx.probe_read()
-    return ms, n, b
+    return ms, n, b, ctx.probe_read_widths()
 
+
+def width_table(widths):
+    """{width: {launches, avg_launch_us, algorithmic_bytes_per_launch, achieved_GBps, frac}}"""
+    out = {}
+    for w, (ms, n, b) in sorted(widths.items()):
+        gbs = (b / n) / (ms * 1e-3 / n) / 1e9 if ms > 0 else None
+        out[str(w)] = {"launches": n, "avg_launch_us": ms * 1e3 / n, "algorithmic_bytes_per_launch": b / n,
+                       "achieved_GBps": gbs, "frac": gbs / HBM_PEAK_GBS if gbs else None}
+    return out
+
+
+PROBE_BATCH = 8  # registrations per pre-pass window: two stage groups of four pairs
 
 SHARDED_PLAN = (("c4", 4), ("c5", 8))  # BASELINE configs[3]/[4]: the pair and its rank count (capped at N)
 
@@ -285,7 +302,8 @@ def sharded_child(args):
         try:
             if args.selftest:  # CPU stub (tests/test_dist.py): the merge logic only, no numbers
                 time.sleep(0.01)
-                res.update({"one_gpu_ms_per_registration": 2.0 if rank == 0 else None, "elapsed_s": 0.001 * steps,
+                res.update({"one_gpu_ms_per_registration": 2.0 if rank == 0 else None,
+                            "one_gpu_ms_per_registration_pp1": 2.5 if rank == 0 else None, "elapsed_s": 0.001 * steps,
                             "e2e_s": [0.002] * min(steps, 10), "parity": "selftest-stub",
                             "sharded": ["fine", "search", "sort"], "K": 100, "device_ms": {}})
                 raise StopIteration
@@ -302,6 +320,15 @@ def sharded_child(args):
                     a = time.perf_counter()
                     ctx.register_batch([pair] * steps, leaf, on_device=True)
                     res["one_gpu_ms_per_registration"] = (time.perf_counter() - a) / steps * 1e3
+                    # the same at one pair per cloud stage (round 4's group form), beside it
+                    os.environ["FCCF_PAIR_BATCH"] = "1"
+                    try:
+                        ctx.register_batch([pair] * steps, leaf, on_device=True)
+                        a = time.perf_counter()
+                        ctx.register_batch([pair] * steps, leaf, on_device=True)
+                        res["one_gpu_ms_per_registration_pp1"] = (time.perf_counter() - a) / steps * 1e3
+                    finally:
+                        del os.environ["FCCF_PAIR_BATCH"]
                     uid = F.group_unique_id()
                     with open(os.path.join(d, f"id_{cfg_name}.tmp"), "wb") as f:
                         f.write(uid)
@@ -391,10 +418,14 @@ def sharded_pass(dist, ws, rank, local, args, timeout_s):
             el = max(x["elapsed_s"] for x in rs)
             e2e = [max(v) for v in zip(*[x["e2e_s"] for x in rs])]
             one = rs[0].get("one_gpu_ms_per_registration")
+            one1 = rs[0].get("one_gpu_ms_per_registration_pp1")
             ms = el / args.steps * 1e3
+            # both sides batch four pairs per cloud stage (the group form does since round 5);
+            # the one-GPU figure at one pair per stage is reported beside it
             out[cfg_name] = {"ranks": ranks, "ms_per_registration": ms,
                              "e2e_ms_median": statistics.median(e2e) * 1e3,
                              "one_gpu_ms_per_registration": one,
+                             "one_gpu_ms_per_registration_pp1": one1,
                              "speedup_vs_one_gpu": one / ms if one else None,
                              "correspondences_per_s": rs[0]["K"] / (ms * 1e-3),
                              "sharded_stages": rs[0]["sharded"],
@@ -504,25 +535,27 @@ def main():
     def reg():
         return ctx.register_device(d_src, src.shape[0], d_tar, tar.shape[0], leaf)
 
-    # Untimed pre-pass: GPU time per step of every probed kernel (HIP events around
-    # each launch; probed calls launch eagerly, see csrc/probe.h).  The roofline
-    # kernel is the one with the most GPU time per step (or --probe-kernel).
-    table, probe = {}, None
-    if not args.selftest:
-        for k in PROBE_KERNELS:
-            ms, n, b = probe_pass(ctx, reg, k, 3)
-            if n:
-                table[k] = {"ms_per_step": ms / 3, "launches_per_step": n / 3, "avg_launch_us": ms * 1e3 / n,
-                            "algorithmic_bytes_per_launch": b / n,
-                            "achieved_GBps": (b / n) / (ms * 1e-3 / n) / 1e9 if ms > 0 else None}
-        ctx.set_probe(None)
-        probe = max(table, key=lambda k: table[k]["ms_per_step"]) if args.probe_kernel == "auto" else args.probe_kernel
-
     def batch(k):  # k pipelined registrations of the pair (fccf_register_batch)
         pair = ((d_src, src.shape[0]), (d_tar, tar.shape[0]))
         return ctx.register_batch([pair] * k, leaf, on_device=True)
 
     pipelined = not args.no_pipeline and not args.selftest
+    # Untimed pre-pass: GPU time per step of every probed kernel (HIP events around
+    # each launch; probed calls launch eagerly, see csrc/probe.h), in the timed region's
+    # own shape: a pipelined batch (four pairs per cloud stage, eight clouds per launch)
+    # of PROBE_BATCH registrations, or single registrations with --no-pipeline.  The
+    # roofline kernel is the one with the most GPU time per step (or --probe-kernel).
+    table, probe = {}, None
+    if not args.selftest:
+        pre, pre_steps = ((lambda: batch(PROBE_BATCH)), PROBE_BATCH) if pipelined else (reg, 1)
+        for k in PROBE_KERNELS:
+            ms, n, b, _ = probe_pass(ctx, pre, k, 1)
+            if n:
+                table[k] = {"ms_per_step": ms / pre_steps, "launches_per_step": n / pre_steps,
+                            "avg_launch_us": ms * 1e3 / n, "algorithmic_bytes_per_launch": b / n,
+                            "achieved_GBps": (b / n) / (ms * 1e-3 / n) / 1e9 if ms > 0 else None}
+        ctx.set_probe(None)
+        probe = max(table, key=lambda k: table[k]["ms_per_step"]) if args.probe_kernel == "auto" else args.probe_kernel
     batch_ms = None
     for _ in range(args.warmup):
         T, st = reg()
@@ -575,17 +608,29 @@ def main():
         if ws > 1 and not args.no_sharded else None
     roofline = None
     if probe:
-        # Probe window right after the timed region, same inputs: every launch of
-        # the roofline kernel timed with HIP events on its own stream.
-        pms, pn, pb = probe_pass(ctx, reg, probe, args.steps)
+        # Probe window right after the timed region, same inputs and the same shape (one
+        # pipelined batch of `steps` registrations, or `steps` single ones with
+        # --no-pipeline): every launch of the roofline kernel timed with HIP events on its
+        # own stream.  The figure is taken at the timed shape's launch width (the width
+        # with the most launches); the other widths, and the two-cloud launches of a single
+        # registration, are reported beside it.
+        run = (lambda: batch(args.steps)) if pipelined else (lambda: [reg() for _ in range(args.steps)])
+        pms, pn, pb, pw = probe_pass(ctx, run, probe, 1)
+        sms, sn, sb, sw = probe_pass(ctx, reg, probe, min(args.steps, 10)) if pipelined else (None, 0, None, {})
         ctx.set_probe(None)
         if pn:
-            avg_s = pms * 1e-3 / pn
-            achieved = (pb / pn) / avg_s / 1e9
+            w = max(pw, key=lambda x: pw[x][1])  # the timed shape's launch width
+            wms, wn, wb = pw[w]
+            avg_s = wms * 1e-3 / wn
+            achieved = (wb / wn) / avg_s / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe, args.config), "kernel": probe,
-                        "avg_launch_us": avg_s * 1e6, "algorithmic_bytes_per_launch": pb / pn,
-                        "launches_per_step": pn / args.steps}
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(probe, args.config, w),
+                        "kernel": probe, "launch_width": w, "avg_launch_us": avg_s * 1e6,
+                        "algorithmic_bytes_per_launch": wb / wn, "launches_per_step": pn / args.steps,
+                        "shape": "pipelined batch" if pipelined else "single registrations",
+                        "by_width": width_table(pw)}
+            if sn:
+                roofline["single_registration"] = dict(width_table(sw), traffic=pmc_traffic(probe, args.config, 2))
     # parity against the oracle, after every timed or probed run (other sizes re-capture graphs)
     parity = None
     if rank == 0 and not args.selftest:

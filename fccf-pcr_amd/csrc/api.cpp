@@ -106,8 +106,7 @@ extern "C" int fccf_ctx_set_debug(fccf_ctx* c, int on) {
 extern "C" int fccf_ctx_set_probe(fccf_ctx* c, const char* kernel) {
   if (!c) return FCCF_E_ARG;
   c->probe.target = kernel ? kernel : "";
-  c->probe.total_ms = c->probe.total_bytes = 0.0;
-  c->probe.launches = 0;
+  c->probe.clear_totals();
   c->probe.armed.clear();
   return FCCF_OK;
 }
@@ -117,6 +116,17 @@ extern "C" int fccf_probe_read(fccf_ctx* c, double* total_ms, int64_t* launches,
   *total_ms = c->probe.total_ms;
   *launches = c->probe.launches;
   *total_bytes = c->probe.total_bytes;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_probe_read_widths(fccf_ctx* c, int max_width, double* ms, int64_t* launches, double* bytes) {
+  if (!c || max_width < 1 || !ms || !launches || !bytes) return FCCF_E_ARG;
+  for (int w = 1; w <= max_width; ++w) {
+    const bool in = w <= fccf::Probe::WMAX;
+    ms[w - 1] = in ? c->probe.w_ms[w] : 0.0;
+    launches[w - 1] = in ? c->probe.w_launches[w] : 0;
+    bytes[w - 1] = in ? c->probe.w_bytes[w] : 0.0;
+  }
   return FCCF_OK;
 }
 
@@ -323,8 +333,14 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
   });
 }
 
+extern "C" int fccf_debug_graph_mismatch(fccf_ctx* c) {
+  if (!c) return FCCF_E_ARG;
+  c->graph_mismatch = true;
+  return FCCF_OK;
+}
+
 extern "C" int fccf_debug_inject_sort_fault(fccf_ctx* c, uint32_t bits) {
-  if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO | IS_POISON_XYZS))) return FCCF_E_ARG;
+  if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO | VG_FORCE_REDO_LATER | IS_POISON_XYZS))) return FCCF_E_ARG;
   return guarded(c, [&] {
     HIP_CHECK(hipDeviceSynchronize());  // no sort of this ctx in flight reads the word meanwhile
     HIP_CHECK(hipMemcpy(c->d_flags, &bits, 4, hipMemcpyHostToDevice));

@@ -113,6 +113,14 @@ inline void guarded_stream_wait(hipStream_t st, hipEvent_t ev) {
   HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
 }
 
+// The arguments of a patched kernel node that describe the workspace layout (every
+// argument but the per-call inputs): their indices in kernelParams and their sizes.
+struct PatchLayout {
+  int n = 0;
+  int idx[8] = {};
+  size_t size[8] = {};
+};
+
 struct CachedGraph {
   std::vector<uint8_t> key;
   hipGraphExec_t exec = nullptr;
@@ -123,6 +131,11 @@ struct CachedGraph {
   hipGraph_t graph = nullptr;
   hipGraphNode_t pnode = nullptr;
   hipKernelNodeParams pparams{};
+  // Replay check: the layout arguments' bytes as captured.  A replay whose patch
+  // carries other layout arguments -- a patch state shared by graphs of different
+  // layouts, the bug class of a device fault in round 4 -- fails with FCCF_E_INTERNAL
+  // before anything is launched (a memcmp of a few hundred bytes per replay).
+  std::vector<uint8_t> layout_bytes;
   void reset() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -130,15 +143,29 @@ struct CachedGraph {
     graph = nullptr;
     pnode = nullptr;
     key.clear();
+    layout_bytes.clear();
   }
   ~CachedGraph() { reset(); }
+  // whether run() with this key would replay (not capture)
+  bool replays(const void* k, size_t kn) const {
+    return exec && key.size() == kn && std::memcmp(key.data(), k, kn) == 0;
+  }
+  static std::vector<uint8_t> layout_of(void** pargs, const PatchLayout* lay) {
+    std::vector<uint8_t> b;
+    for (int i = 0; lay && i < lay->n; ++i) {
+      const uint8_t* a = (const uint8_t*)pargs[lay->idx[i]];
+      b.insert(b.end(), a, a + lay->size[i]);
+    }
+    return b;
+  }
   // body enqueues the work; pfunc/pargs (optional): the patched kernel and its
-  // current arguments (kernelParams layout: one pointer per argument).
+  // current arguments (kernelParams layout: one pointer per argument); lay: which of
+  // them must equal the captured ones at every replay.
   // eager: launch the body directly this call (work with a host step inside, e.g. the
   // sharded sort's gather)
   template <class F>
   void run(const void* k, size_t kn, hipStream_t st, F body, const void* pfunc = nullptr, void** pargs = nullptr,
-           bool eager = false) {
+           bool eager = false, const PatchLayout* lay = nullptr) {
     static const bool enabled = [] {
       const char* e = std::getenv("FCCF_GRAPHS");
       return !(e && e[0] == '0');
@@ -171,9 +198,13 @@ struct CachedGraph {
       }
       graph = g;
       if (pfunc) find_node(pfunc);
+      if (pfunc) layout_bytes = layout_of(pargs, lay);
       key.assign(kb, kb + kn);
       ++captures;
     } else if (pfunc) {
+      if (layout_of(pargs, lay) != layout_bytes)
+        throw Error(FCCF_E_INTERNAL, "graph replay: the patched entry arguments differ from the layout the graph "
+                                     "was captured with");
       hipKernelNodeParams np = pparams;
       np.kernelParams = pargs;
       np.extra = nullptr;
@@ -218,10 +249,11 @@ struct CachedGraph {
 struct fccf_ctx {
   int device = 0;
   // Pair slots.  A cloud stage (both VoxelGrid passes, centroid, face voxels) runs the
-  // clouds of one or two pairs in the same launches (a pipelined batch pairs them up:
-  // the sort's dependent rounds are paid once for four clouds); stage group G uses
-  // slots 2G and 2G + 1, and the group's shared resources (arena of its clouds, stage
-  // graph, fork/join events) live in slot 2G.  Two groups double-buffer, so a batch can
+  // clouds of up to PAIRS_MAX = 4 pairs in the same launches (a pipelined batch groups
+  // them: the sort's dependent rounds are paid once for eight clouds); stage group G
+  // uses slots PAIRS_MAX * G + j (j < PAIRS_MAX), and the group's shared resources (arena
+  // of its clouds, stage graphs, fork/join events) live in its first slot, PAIRS_MAX * G.
+  // Two groups double-buffer, so a batch can
   // run the next group's clouds while this group's later stages run.  Two groups never
   // run their cloud stages at the same time, so they share streams: sa[0] the batched
   // cloud stage, sa[2] the centroid sums, sa[1] fine verification, and sb for matching
@@ -267,6 +299,7 @@ struct fccf_ctx {
   uint32_t sort_stats[32] = {};  // IsBufs::ctl of the last fccf_debug_sort_keys
   uint32_t sort_rounds[4 * 24] = {};  // IsBufs::rounds (IS_RMAX records) of the last fccf_debug_sort_keys
   uint32_t* d_flags = nullptr;   // device words (zeroed at creation): [0] injected K1 sort faults (test hook)
+  bool graph_mismatch = false;   // test hook: the next cloud-stage replay patches a wrong layout argument
   std::map<std::string, std::vector<uint8_t>> dbg;
   std::string last_error;
 

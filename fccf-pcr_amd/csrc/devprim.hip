@@ -487,7 +487,9 @@ void radix_sort(B4<K*> k0, B4<uint32_t*> v0, B4<K*> k1, B4<uint32_t*> v1, B4<con
     k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(R, d_n, d_nbits, p, s, nb, fast_passes);
     k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
     const double eb = 2.0 * (sizeof(K) + (v0[0] ? 4 : 0));  // algorithmic bytes per element
-    FCCF_LAUNCH("k_rs_scatter", (d_n[0], eb, nbatch > 1 ? d_n[1] : nullptr, eb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
+    ProbeBytes pb;
+    for (int e = 0; e < nbatch; ++e) pb.add(d_n[e], eb);
+    FCCF_LAUNCH("k_rs_scatter", (pb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
   }
   // With a third buffer every plan but a single pass ends in buffer 0 (an even pass
   // count by ping-pong, three passes by rotation), so no copy-back kernel is launched

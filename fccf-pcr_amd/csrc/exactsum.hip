@@ -497,12 +497,14 @@ void exact_sum_in(const XsIn& in, int S, int K, int nprob, float* out, bool divi
   if (S == 3) {
     k_xs_csum<3><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);
-    // probe bytes: 12 B per element of every problem (separate arrays: the first two
-    // problems' counts; probed calls batch one pair)
-    const uint32_t* c1 = in.multi ? in.cp[0] : in.cnt;
-    const uint32_t* c2 = in.multi && nprob > 1 ? in.cp[1] : nullptr;
-    FCCF_LAUNCH("k_xs_chunk", (c1, 12.0, c2, 12.0, 0.0), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
-    FCCF_LAUNCH("k_xs_chain", (c1, 12.0, c2, 12.0, 0.0), k_xs_chain<3>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
+    // probe bytes: 12 B per element of every problem (separate arrays: one count each)
+    ProbeBytes pb;
+    if (in.multi)
+      for (int e = 0; e < nprob && e < BMAX; ++e) pb.add(in.cp[e], 12.0);
+    else
+      pb.add(in.cnt, 12.0);
+    FCCF_LAUNCH("k_xs_chunk", (pb), k_xs_chunk<3>, gc, 256, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC);
+    FCCF_LAUNCH("k_xs_chain", (pb), k_xs_chain<3>, rows, 64, 0, st, in, K, x.pre, x.ctab, x.cE, x.NC, out, divide);
   } else {
     k_xs_csum<1><<<gc, 256, 0, st>>>(in, K, x.pre, x.NC);
     k_xs_prefix<<<rows, 256, 0, st>>>(in, K, x.pre, x.NC);

@@ -730,15 +730,16 @@ void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t
   segment_heads_u64(B4<const uint64_t*>(c0), d_n, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
                     pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
                     st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
-  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
-  FCCF_LAUNCH("k_gather", (d_n[0], 28.0, n2, 28.0), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B4<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
+  ProbeBytes pb;
+  for (int e = 0; e < nbatch; ++e) pb.add(d_n[e], 28.0);
+  FCCF_LAUNCH("k_gather", (pb), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B4<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
 }
 
 void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float vpt, float cthr, B4<float*> resid_out,
                      B4<FaceBufs> b, hipStream_t st, int nbatch) {
-  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;
-  const uint32_t* l2 = nbatch > 1 ? b[1].nleaf : nullptr;
-  FCCF_LAUNCH("k_voxel_fit", (d_n[0], 12.0, b[0].nleaf, (double)sizeof(VoxRec) + 12.0, 0.0, n2, 12.0, l2, (double)sizeof(VoxRec) + 12.0), k_voxel_fit, dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st, b, vpt, cthr);
+  ProbeBytes pb;
+  for (int e = 0; e < nbatch; ++e) pb.add(d_n[e], 12.0).add(b[e].nleaf, (double)sizeof(VoxRec) + 12.0);
+  FCCF_LAUNCH("k_voxel_fit", (pb), k_voxel_fit, dim3(grid_for(cap, 4, VFIT_BLOCKS), nbatch), 256, 0, st, b, vpt, cthr);
   const B4<SortScratch> ss = pick(b, [](const FaceBufs& f) { return f.ss; });
   const B4<const uint32_t*> nleaf = pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.nleaf; });
   exclusive_scan2_u32(pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.flag_planar; }),

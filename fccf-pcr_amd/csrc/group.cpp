@@ -2,7 +2,7 @@
 // One process per GPU; every rank holds communicators created from one
 // ncclUniqueId that rank 0 made and the caller distributed out of band.
 //
-// What is sharded:
+// What is sharded (DESIGN.md §8):
 //  * K5, the coplane-pair correspondence search (FCCF.cpp:1410-1428): source pairs B1
 //    in contiguous blocks (shard_range); each rank tests its block against all target
 //    pairs on its GPU, then the per-type candidate lists are gathered in rank order:
@@ -12,16 +12,26 @@
 //    candidates of each type) in contiguous blocks; each rank scores its block on
 //    its GPU and the scores are all-gathered in rank order, so every rank fuses the
 //    same scores in the same order.
-// Everything else is replicated: every rank runs the cloud stage on the same inputs
-// (the VoxelGrid's std::sort order spans the whole cloud), growth,
-// selection, clustering and the LM are sequential and deterministic, so every rank
-// computes the same T with no further exchange.
+//  * D, K1's std::sort (:1668-1678): after the replicated first rounds each rank
+//    partitions and finishes only the segments in its range of the sort; the sorted
+//    slices are all-gathered in rank order (shard_gather_sorted), every cloud of a
+//    stage group in one exchange.
+//  * P, the 1 m face stage (:470-534): each rank fits its Morton range of leaves; leaf
+//    records, planar flags and residual points are all-gathered in rank order
+//    (face_voxels_sharded).
+// Everything else is replicated: growth, selection, clustering and the LM are
+// sequential and deterministic, so every rank computes the same T with no further
+// exchange.
 //
 // Transports: RCCL (RcclTransport: an all-gather-v is one ncclGroupStart/End of
 // per-root ncclBroadcasts), or virtual ranks (LocalTransport, test hook): n contexts
 // of one process on one device exchange through a shared device staging buffer under
 // host barriers -- the same gather logic with n > 1, where RCCL itself would refuse
 // two ranks on one GPU.
+//
+// Failure handling (Group::aborted): every host wait that may depend on a peer is
+// bounded and polls the transport's async error; a failing rank aborts its
+// communicators (ncclCommAbort), and every rank returns FCCF_E_RCCL within the bound.
 #include "group.h"
 
 #include <algorithm>
@@ -31,6 +41,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ctx.h"
@@ -64,18 +75,47 @@ struct NcclGroup {
 struct RcclTransport : Transport {
   Group* g;
   explicit RcclTransport(Group* g_) : g(g_) {}
+  ncclComm_t comm(int ch) {
+    if (!g->comm[ch]) throw Error(FCCF_E_RCCL, "group aborted: " + g->abort_why);
+    return g->comm[ch];
+  }
+  void bcasts(int ch, const GatherOp& op, hipStream_t st) {
+    ncclComm_t cm = comm(ch);
+    for (int r = 0; r < g->n; ++r) {
+      if (!op.counts[r]) continue;
+      char* dst = (char*)op.recv + op.offs[r];
+      NCCL_CHECK(ncclBroadcast(r == g->rank ? op.send : (const void*)dst, dst, op.counts[r], ncclUint8, r, cm, st));
+    }
+  }
   void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
                   hipStream_t st) override {
     NcclGroup grp;
-    for (int r = 0; r < g->n; ++r) {
-      if (!counts[r]) continue;
-      char* dst = (char*)recv + offs[r];
-      NCCL_CHECK(ncclBroadcast(r == g->rank ? send : (const void*)dst, dst, counts[r], ncclUint8, r, g->comm[ch], st));
-    }
+    bcasts(ch, GatherOp{send, recv, counts, offs}, st);
+    grp.end();
+  }
+  void allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st) override {
+    NcclGroup grp;
+    for (int i = 0; i < nops; ++i) bcasts(ch, ops[i], st);
     grp.end();
   }
   void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
-    NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, g->comm[ch], st));
+    NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm(ch), st));
+  }
+  int async_error() override {
+    for (ncclComm_t c : g->comm) {
+      if (!c) continue;
+      ncclResult_t r = ncclSuccess;
+      if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return (int)ncclInternalError;
+      if (r != ncclSuccess && r != ncclInProgress) return (int)r;
+    }
+    return 0;
+  }
+  void abort() override {
+    for (ncclComm_t& c : g->comm)
+      if (c) {
+        (void)ncclCommAbort(c);  // (also frees the communicator)
+        c = nullptr;
+      }
   }
 };
 
@@ -84,6 +124,7 @@ struct RcclTransport : Transport {
 // host threads of a rank, like the separate communicators of the RCCL form).
 struct LocalHub {
   int n;
+  std::atomic<bool> aborted{false};
   struct Chan {
     std::mutex m;
     std::condition_variable cv;
@@ -97,9 +138,19 @@ struct LocalHub {
     for (Chan& c : ch)
       if (c.stage) (void)hipFree(c.stage);
   }
-  void barrier(int k) {
+  void abort() {
+    aborted = true;
+    for (Chan& c : ch) {
+      std::lock_guard<std::mutex> lk(c.m);
+      c.cv.notify_all();
+    }
+  }
+  // bounded: a rank that never arrives (its call failed without aborting, a dead
+  // peer) ends the wait after timeout_s; an aborted hub ends it at once
+  void barrier(int k, double timeout_s) {
     Chan& c = ch[k];
     std::unique_lock<std::mutex> lk(c.m);
+    if (aborted) throw Error(FCCF_E_RCCL, "virtual-rank group aborted by a rank");
     const uint64_t my = c.gen;
     if (++c.arrived == n) {
       c.arrived = 0;
@@ -107,9 +158,12 @@ struct LocalHub {
       c.cv.notify_all();
       return;
     }
-    // bounded: a rank that never arrives (its call failed) ends the wait with an error
-    if (!c.cv.wait_for(lk, std::chrono::seconds(60), [&] { return c.gen != my; }))
-      throw Error(FCCF_E_RCCL, "virtual-rank group: a rank did not reach the collective");
+    const bool ok = c.cv.wait_for(lk, std::chrono::duration<double>(timeout_s),
+                                  [&] { return c.gen != my || aborted.load(); });
+    if (c.gen != my) return;
+    if (aborted) throw Error(FCCF_E_RCCL, "virtual-rank group aborted by a rank");
+    (void)ok;
+    throw Error(FCCF_E_RCCL, "virtual-rank group: a rank did not reach the collective within the time limit");
   }
 };
 
@@ -126,7 +180,7 @@ struct LocalTransport : Transport {
       std::lock_guard<std::mutex> lk(C.m);
       C.need = std::max(C.need, total);
     }
-    g->hub->barrier(ch);
+    g->hub->barrier(ch, g->timeout_s);
     if (g->rank == 0 && C.need > C.cap) {  // one rank grows the staging, between barriers
       if (C.stage) HIP_CHECK(hipFree(C.stage));
       C.stage = nullptr;
@@ -134,12 +188,12 @@ struct LocalTransport : Transport {
       if (hipMalloc((void**)&C.stage, C.need) != hipSuccess) throw Error(FCCF_E_OOM, "virtual-rank staging");
       C.cap = C.need;
     }
-    g->hub->barrier(ch);
+    g->hub->barrier(ch, g->timeout_s);
     if (counts[g->rank]) {  // (on st: the legacy null stream would also wait for the other ranks' streams)
       HIP_CHECK(hipMemcpyAsync(C.stage + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
       HIP_CHECK(hipStreamSynchronize(st));
     }
-    g->hub->barrier(ch);
+    g->hub->barrier(ch, g->timeout_s);
     // every rank's part except its own (in place: an all-gather-v may send from its recv buffer)
     for (int r = 0; r < g->n; ++r)
       if (r != g->rank && counts[r])
@@ -147,14 +201,94 @@ struct LocalTransport : Transport {
     if (counts[g->rank] && (const char*)send != (const char*)recv + offs[g->rank])
       HIP_CHECK(hipMemcpyAsync((char*)recv + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    g->hub->barrier(ch);  // (the staging is rewritten by the next collective)
+    g->hub->barrier(ch, g->timeout_s);  // (the staging is rewritten by the next collective)
   }
   void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
     std::vector<size_t> counts((size_t)g->n, bytes), offs((size_t)g->n);
     for (int r = 0; r < g->n; ++r) offs[(size_t)r] = (size_t)r * bytes;
     allgatherv(ch, send, recv, counts.data(), offs.data(), st);
   }
+  int async_error() override { return g->hub->aborted ? 1 : 0; }
+  void abort() override { g->hub->abort(); }
 };
+
+// ------------------------------------------------------------ failure handling
+
+void group_abort(Group* g, const std::string& why) {
+  if (!g) return;
+  bool was = false;
+  if (!g->aborted.compare_exchange_strong(was, true)) return;
+  g->abort_why = why;
+  // a dead peer (the silent test hook) leaves its transport alone: the others find
+  // out at their time limit
+  if (!g->fail_silent && g->tr) g->tr->abort();
+  order_abort(g);
+}
+
+void group_check(const Group* g) {
+  if (g && g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + g->abort_why + "); destroy and recreate it");
+}
+
+namespace {
+template <class Q>
+void bounded_wait(Group* g, Q query, const char* what) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (uint64_t k = 0;; ++k) {
+    const hipError_t e = query();
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) {
+      const std::string m = std::string(what) + ": " + hipGetErrorString(e);
+      group_abort(g, m);
+      throw Error(FCCF_E_HIP, m);
+    }
+    if (g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + g->abort_why + ")");
+    if ((k & 31) == 31) {
+      if (const int ae = g->tr->async_error()) {
+        const std::string m = std::string(what) + ": transport failed asynchronously (" + std::to_string(ae) + ")";
+        group_abort(g, m);
+        throw Error(FCCF_E_RCCL, m);
+      }
+      if (std::chrono::duration<double>(clk::now() - t0).count() > g->timeout_s) {
+        const std::string m = std::string(what) + ": no completion within the group's time limit (" +
+                              std::to_string(g->timeout_s) + " s)";
+        group_abort(g, m);
+        throw Error(FCCF_E_RCCL, m);
+      }
+    }
+    // spin briefly (these waits are on the registration's critical path), then yield
+    if (k < 4096) {
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    } else if (k < 65536) {
+      std::this_thread::yield();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+}
+}  // namespace
+
+void group_wait(Group* g, hipStream_t st) {
+  bounded_wait(g, [st] { return hipStreamQuery(st); }, "group stream wait");
+}
+
+void group_wait_event(Group* g, hipEvent_t ev, bool capture_lock) {
+  if (capture_lock)
+    bounded_wait(g, [ev] {
+      std::lock_guard<std::mutex> lk(capture_mutex());
+      return hipEventQuery(ev);
+    }, "group event wait");
+  else
+    bounded_wait(g, [ev] { return hipEventQuery(ev); }, "group event wait");
+}
+
+void group_fail_point(Group* g, int site) {
+  if (!g || g->fail_at != site) return;
+  g->fail_at = 0;
+  throw Error(FCCF_E_RCCL, "injected failure at collective site " + std::to_string(site));
+}
 
 void shard_range(int n, int rank, int world, int* lo, int* hi) {
   const int q = n / world, r = n % world;
@@ -166,6 +300,7 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
                              int64_t kpass_loc, QTd* const q_all[3], MCand* const c_all[3], size_t cap,
                              uint32_t tot_all[3], uint32_t* d_tot_all, int64_t* kpass_all, hipStream_t st) {
   const int n = g->n;
+  group_fail_point(g, GROUP_FAIL_MATCH);
   uint32_t* h = g->h_cnt;  // pinned: [0..3] this rank's counts, [4 ..] every rank's
   h[0] = tot_loc[0];
   h[1] = tot_loc[1];
@@ -174,7 +309,7 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
   HIP_CHECK(hipMemcpyAsync(g->d_cnt, h, 16, hipMemcpyHostToDevice, st));
   g->tr->allgather(CH_MATCH, g->d_cnt, g->d_cnt + 4, 16, st);
   HIP_CHECK(hipMemcpyAsync(h + 4, g->d_cnt + 4, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  group_wait(g, st);
   int64_t kp = 0;
   size_t off[3] = {0, 0, 0};
   std::vector<size_t> base((size_t)n * 3);
@@ -190,29 +325,35 @@ void group_gather_candidates(Group* g, QTd* const q_loc[3], MCand* const c_loc[3
     tot_all[t] = (uint32_t)off[t];
   }
   *kpass_all = kp;
-  // all-gather-v of each type's quaternion records and matrices, rank-ordered
-  std::vector<size_t> cnt((size_t)n), offs((size_t)n);
+  // all-gather-v of each type's quaternion records and matrices, rank-ordered: the six
+  // lists in one exchange
+  std::vector<size_t> cnt((size_t)n * 6), offs((size_t)n * 6);
+  GatherOp ops[6];
   for (int t = 0; t < 3; ++t) {
+    size_t* cq = cnt.data() + (size_t)n * (2 * t);
+    size_t* oq = offs.data() + (size_t)n * (2 * t);
+    size_t* cc = cnt.data() + (size_t)n * (2 * t + 1);
+    size_t* oc = offs.data() + (size_t)n * (2 * t + 1);
     for (int r = 0; r < n; ++r) {
-      cnt[(size_t)r] = (size_t)h[4 + 4 * r + t] * sizeof(QTd);
-      offs[(size_t)r] = base[(size_t)r * 3 + t] * sizeof(QTd);
+      cq[r] = (size_t)h[4 + 4 * r + t] * sizeof(QTd);
+      oq[r] = base[(size_t)r * 3 + t] * sizeof(QTd);
+      cc[r] = (size_t)h[4 + 4 * r + t] * sizeof(MCand);
+      oc[r] = base[(size_t)r * 3 + t] * sizeof(MCand);
     }
-    g->tr->allgatherv(CH_MATCH, q_loc[t], q_all[t], cnt.data(), offs.data(), st);
-    for (int r = 0; r < n; ++r) {
-      cnt[(size_t)r] = (size_t)h[4 + 4 * r + t] * sizeof(MCand);
-      offs[(size_t)r] = base[(size_t)r * 3 + t] * sizeof(MCand);
-    }
-    g->tr->allgatherv(CH_MATCH, c_loc[t], c_all[t], cnt.data(), offs.data(), st);
+    ops[2 * t] = GatherOp{q_loc[t], q_all[t], cq, oq};
+    ops[2 * t + 1] = GatherOp{c_loc[t], c_all[t], cc, oc};
   }
+  g->tr->allgatherv_multi(CH_MATCH, ops, 6, st);
   h[0] = tot_all[0];
   h[1] = tot_all[1];
   h[2] = tot_all[2];
   h[3] = 0;
   HIP_CHECK(hipMemcpyAsync(d_tot_all, h, 16, hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipStreamSynchronize(st));  // (h is reused by the next call)
+  group_wait(g, st);  // (h is reused by the next call)
 }
 
 void group_fine_gather(Group* g, int s, const float* d_scores, int E_loc, const uint32_t* d_err, hipStream_t st) {
+  group_fail_point(g, GROUP_FAIL_FINE);
   float* snd = g->d_fsend[s];
   HIP_CHECK(hipMemsetAsync(snd, 0, sizeof(float) * Group::FE_BLK, st));
   if (E_loc > 0) {
@@ -256,8 +397,14 @@ int shard_sort_r0(int n_ranks) {
 
 void cloud_gate(Group* g) {
   std::unique_lock<std::mutex> lk(g->om);
-  g->ocv.wait(lk, [&] { return g->order_abort || g->b1_issued >= g->cloud_need; });
-  if (g->order_abort) throw Error(FCCF_E_RCCL, "group: batch aborted before the sharded sort's gather");
+  const bool ok = g->ocv.wait_for(lk, std::chrono::duration<double>(g->timeout_s),
+                                  [&] { return g->order_abort || g->b1_issued >= g->cloud_need; });
+  if (g->order_abort) throw Error(FCCF_E_RCCL, "group: batch aborted before the cloud stage's gather");
+  if (!ok) {
+    lk.unlock();
+    group_abort(g, "the cloud stage's gather waited past the time limit for the previous pairs' phase B1");
+    throw Error(FCCF_E_RCCL, "group: order gate timed out");
+  }
 }
 
 void b1_done(Group* g) {
@@ -288,56 +435,65 @@ void order_abort(Group* g) {
   g->ocv.notify_all();
 }
 
-void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
+void shard_gather_sorted(Group* g, const B4<uint32_t*>& k0, const B4<uint32_t*>& v0, const B4<const uint32_t*>& bounds,
                          int nbatch, hipStream_t st) {
   const int n = g->n;
+  if (nbatch < 1 || nbatch > BMAX) throw Error(FCCF_E_INTERNAL, "sharded sort: 1 .. BMAX clouds per stage");
   for (int e = 0; e < nbatch; ++e)
     HIP_CHECK(hipMemcpyAsync(g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1), bounds[e], 4 * (size_t)(n + 1),
                              hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
-  cloud_gate(g);  // (the batch's helper thread: after the previous pair's B1 collectives)
-  std::vector<size_t> cnt((size_t)n), off((size_t)n);
+  group_wait(g, st);
+  cloud_gate(g);  // (the batch's helper thread: after the previous pairs' B1 collectives)
+  group_fail_point(g, GROUP_FAIL_CLOUD);
+  // every cloud's keys and values: one exchange of 2 x nbatch all-gather-v's
+  std::vector<size_t> cnt((size_t)n * nbatch), off((size_t)n * nbatch);
+  std::vector<GatherOp> ops;
   for (int e = 0; e < nbatch; ++e) {
     const uint32_t* b = g->h_bounds + (size_t)e * (IS_SHARD_MAX + 1);
+    size_t* ce = cnt.data() + (size_t)n * e;
+    size_t* oe = off.data() + (size_t)n * e;
     for (int r = 0; r < n; ++r) {
       if (b[r + 1] < b[r]) throw Error(FCCF_E_INTERNAL, "sharded sort: rank bounds out of order");
-      cnt[(size_t)r] = 4 * (size_t)(b[r + 1] - b[r]);
-      off[(size_t)r] = 4 * (size_t)b[r];
+      ce[r] = 4 * (size_t)(b[r + 1] - b[r]);
+      oe[r] = 4 * (size_t)b[r];
     }
     const size_t me = 4 * (size_t)b[g->rank];
-    g->tr->allgatherv(CH_CLOUD, (const char*)k0[e] + me, k0[e], cnt.data(), off.data(), st);
-    g->tr->allgatherv(CH_CLOUD, (const char*)v0[e] + me, v0[e], cnt.data(), off.data(), st);
+    ops.push_back(GatherOp{(const char*)k0[e] + me, k0[e], ce, oe});
+    ops.push_back(GatherOp{(const char*)v0[e] + me, v0[e], ce, oe});
   }
+  g->tr->allgatherv_multi(CH_CLOUD, ops.data(), (int)ops.size(), st);
 }
 
 void face_voxels_sharded(Group* g, B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, double res, float vpt,
                          float cthr, B4<float*> resid_out, B4<FaceBufs> b, hipStream_t st, int nbatch) {
   const int n = g->n;
-  if (nbatch > 2) throw Error(FCCF_E_INTERNAL, "sharded face stage: one pair per cloud stage");
+  if (nbatch < 1 || nbatch > BMAX) throw Error(FCCF_E_INTERNAL, "sharded face stage: 1 .. BMAX clouds per stage");
   face_codes(xyz, d_n, cap, res, b, st, nbatch);  // replicated: the octree bounds depend on every point in order
   face_shard_select(d_n, cap, b, g->rank, n, st, nbatch);
   face_shard_sort(xyz, cap, b, st, nbatch);
-  cloud_gate(g);  // (the batch's helper thread: after the previous pair's B1 collectives)
-  // the ranks' counts (cnt(e) = scalar k of cloud e), all-gathered: every rank's base
-  auto gather_counts = [&](int k, std::vector<uint32_t>& base, uint32_t tot[2]) {
-    for (int e = 0; e < 2; ++e)
-      HIP_CHECK(hipMemcpyAsync(g->d_fcnt + e, b[e < nbatch ? e : 0].nleaf + k, 4, hipMemcpyDeviceToDevice, st));
-    g->tr->allgather(CH_CLOUD, g->d_fcnt, g->d_fcnt + 4, 16, st);
-    HIP_CHECK(hipMemcpyAsync(g->h_fcnt, g->d_fcnt + 4, 16 * (size_t)n, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    base.assign(2 * (size_t)(n + 1), 0u);
-    for (int e = 0; e < 2; ++e) {
+  cloud_gate(g);  // (the batch's helper thread: after the previous pairs' B1 collectives)
+  // the ranks' counts of every cloud (cnt(e) = scalar k of cloud e; BMAX words per
+  // rank), all-gathered in one collective: every rank's base per cloud
+  const size_t W = BMAX;
+  auto gather_counts = [&](int k, std::vector<uint32_t>& base, uint32_t* tot) {
+    for (int e = 0; e < nbatch; ++e)
+      HIP_CHECK(hipMemcpyAsync(g->d_fcnt + e, b[e].nleaf + k, 4, hipMemcpyDeviceToDevice, st));
+    g->tr->allgather(CH_CLOUD, g->d_fcnt, g->d_fcnt + W, 4 * W, st);
+    HIP_CHECK(hipMemcpyAsync(g->h_fcnt, g->d_fcnt + W, 4 * W * (size_t)n, hipMemcpyDeviceToHost, st));
+    group_wait(g, st);
+    base.assign((size_t)nbatch * (n + 1), 0u);
+    for (int e = 0; e < nbatch; ++e) {
       uint32_t run = 0;
       for (int r = 0; r < n; ++r) {
         base[(size_t)e * (n + 1) + r] = run;
-        run += g->h_fcnt[4 * r + e];
+        run += g->h_fcnt[W * r + e];
       }
       base[(size_t)e * (n + 1) + n] = run;
       tot[e] = run;
     }
   };
   std::vector<uint32_t> lb, rb;
-  uint32_t ltot[2], rtot[2];
+  uint32_t ltot[BMAX] = {}, rtot[BMAX] = {};
   gather_counts(0, lb, ltot);  // leaves per rank
   // views of the full leaf arrays at this rank's first leaf
   B4<FaceBufs> bv = b;
@@ -353,15 +509,19 @@ void face_voxels_sharded(Group* g, B4<const float*> xyz, B4<const uint32_t*> d_n
   B4<float*> rv = resid_out;
   for (int e = 0; e < BMAX; ++e) rv.v[e] += 3 * (size_t)rb[(size_t)(e < nbatch ? e : 0) * (n + 1) + g->rank];
   face_shard_resid(cap, bv, rv, st, nbatch);
-  // rank-ordered all-gathers into the full arrays (in place: each rank's part is already there)
-  std::vector<size_t> cnt((size_t)n), off((size_t)n);
+  // rank-ordered all-gathers into the full arrays (in place: each rank's part is already
+  // there), four per cloud, every cloud's in one exchange
+  std::vector<size_t> cnt((size_t)n * 4 * nbatch), off((size_t)n * 4 * nbatch);
+  std::vector<GatherOp> ops;
   auto allgv = [&](void* base, const std::vector<uint32_t>& bs, int e, size_t unit) {
+    size_t* c = cnt.data() + (size_t)n * ops.size();
+    size_t* o = off.data() + (size_t)n * ops.size();
     for (int r = 0; r < n; ++r) {
       const size_t i = (size_t)e * (n + 1) + r;
-      cnt[(size_t)r] = unit * (bs[i + 1] - bs[i]);
-      off[(size_t)r] = unit * bs[i];
+      c[r] = unit * (bs[i + 1] - bs[i]);
+      o[r] = unit * bs[i];
     }
-    g->tr->allgatherv(CH_CLOUD, (const char*)base + off[(size_t)g->rank], base, cnt.data(), off.data(), st);
+    ops.push_back(GatherOp{(const char*)base + o[g->rank], base, c, o});
   };
   for (int e = 0; e < nbatch; ++e) {
     allgv(b[e].recs, lb, e, sizeof(VoxRec));
@@ -369,17 +529,18 @@ void face_voxels_sharded(Group* g, B4<const float*> xyz, B4<const uint32_t*> d_n
     allgv(b[e].resid_cnt, lb, e, 4);  // (read only by the debug dumps: a leaf's residual flag)
     allgv(resid_out[e], rb, e, 12);
   }
+  g->tr->allgatherv_multi(CH_CLOUD, ops.data(), (int)ops.size(), st);
   // the full counts where the unsharded stage leaves them: leaves (scalar 0), residual
   // points (3); then the planar offsets over every leaf (nplanar, scalar 2)
-  uint32_t* h = g->h_fcnt + 4 * (size_t)n;
+  uint32_t* h = g->h_fcnt + W * (size_t)n;
   for (int e = 0; e < nbatch; ++e) {
-    h[4 * e] = ltot[e];
-    h[4 * e + 1] = rtot[e];
-    HIP_CHECK(hipMemcpyAsync(b[e].nleaf, h + 4 * e, 4, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(b[e].nresid, h + 4 * e + 1, 4, hipMemcpyHostToDevice, st));
+    h[2 * e] = ltot[e];
+    h[2 * e + 1] = rtot[e];
+    HIP_CHECK(hipMemcpyAsync(b[e].nleaf, h + 2 * e, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemcpyAsync(b[e].nresid, h + 2 * e + 1, 4, hipMemcpyHostToDevice, st));
   }
   face_planar_scan(cap, b, st, nbatch);
-  HIP_CHECK(hipStreamSynchronize(st));  // (h is reused by the next call)
+  group_wait(g, st);  // (h is reused by the next call)
 }
 
 }  // namespace fccf
@@ -400,11 +561,13 @@ void group_alloc(Group& g) {
   if (hipMalloc((void**)&g.d_cnt, 16 * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
   if (hipHostMalloc((void**)&g.h_cnt, 16 * (n + 1), hipHostMallocDefault) != hipSuccess)
     throw Error(FCCF_E_OOM, "hipHostMalloc");
-  if (hipHostMalloc((void**)&g.h_bounds, 4 * 2 * (IS_SHARD_MAX + 1), hipHostMallocDefault) != hipSuccess)
+  if (hipHostMalloc((void**)&g.h_bounds, 4 * BMAX * (IS_SHARD_MAX + 1), hipHostMallocDefault) != hipSuccess)
     throw Error(FCCF_E_OOM, "hipHostMalloc");
-  if (hipMalloc((void**)&g.d_fcnt, 16 * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
-  if (hipHostMalloc((void**)&g.h_fcnt, 16 * (n + 1) + 64, hipHostMallocDefault) != hipSuccess)
+  if (hipMalloc((void**)&g.d_fcnt, 4 * BMAX * (n + 1)) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc");
+  if (hipHostMalloc((void**)&g.h_fcnt, 4 * BMAX * n + 4 * 2 * BMAX + 64, hipHostMallocDefault) != hipSuccess)
     throw Error(FCCF_E_OOM, "hipHostMalloc");
+  const char* te = std::getenv("FCCF_GROUP_TIMEOUT_S");
+  if (te && std::atof(te) > 0) g.timeout_s = std::atof(te);
   for (int s = 0; s < Group::SLOTS; ++s) {
     if (hipMalloc((void**)&g.d_fsend[s], sizeof(float) * Group::FE_BLK) != hipSuccess ||
         hipMalloc((void**)&g.d_frecv[s], sizeof(float) * Group::FE_BLK * n) != hipSuccess)
@@ -529,6 +692,18 @@ extern "C" int fccf_group_destroy(fccf_group* G) {
   group_free(G->g);
   delete G;
   return FCCF_OK;
+}
+
+extern "C" int fccf_debug_group_fail(fccf_group* G, int site, int silent) {
+  if (!G || site < 0 || site > GROUP_FAIL_CLOUD) return FCCF_E_ARG;
+  G->g.fail_at = site;
+  G->g.fail_silent = silent != 0;
+  return FCCF_OK;
+}
+
+extern "C" int fccf_group_aborted(const fccf_group* G) {
+  if (!G) return FCCF_E_ARG;
+  return G->g.aborted ? 1 : 0;
 }
 
 extern "C" int fccf_group_info(const fccf_group* G, int* n_ranks, int* rank) {

@@ -13,11 +13,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <string>
 
 #include "kernels.h"
 #include "match.h"
@@ -33,6 +35,14 @@ namespace fccf {
 // thread).
 enum { CH_MATCH = 0, CH_FINE = 1, CH_CLOUD = 2, CH_COUNT = 3 };
 
+// One rank-ordered all-gather-v of a batch of them (Transport::allgatherv_multi).
+struct GatherOp {
+  const void* send;
+  void* recv;
+  const size_t* counts;  // n_ranks entries
+  const size_t* offs;
+};
+
 struct Transport {
   virtual ~Transport() = default;
   // Rank-ordered all-gather-v on channel ch, in the order of stream st: rank r's
@@ -40,8 +50,18 @@ struct Transport {
   // device memory of the rank's device.
   virtual void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
                           hipStream_t st) = 0;
+  // Several all-gather-v's as one exchange (RCCL: one ncclGroupStart/End).
+  virtual void allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st) {
+    for (int i = 0; i < nops; ++i) allgatherv(ch, ops[i].send, ops[i].recv, ops[i].counts, ops[i].offs, st);
+  }
   // The same with equal blocks of `bytes`, rank r's at recv + r * bytes.
   virtual void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
+  // A non-zero code once the transport has failed asynchronously (RCCL:
+  // ncclCommGetAsyncError of any communicator; virtual ranks: the hub was aborted).
+  virtual int async_error() { return 0; }
+  // Ends every outstanding and future collective of this rank (RCCL: ncclCommAbort of
+  // the communicators, which also releases the kernels waiting in them).
+  virtual void abort() {}
 };
 
 struct LocalHub;  // group.cpp
@@ -61,9 +81,9 @@ struct Group {
   float* d_fsend[SLOTS] = {};
   float* d_frecv[SLOTS] = {};  // n x FE_BLK
   float* h_frecv[SLOTS] = {};  // pinned copies
-  uint32_t* h_bounds = nullptr;             // pinned: the sharded sort's rank bounds, per cloud (row D)
-  uint32_t* d_fcnt = nullptr;               // row P: this rank's 4 counts, then all ranks' (n x 4), device
-  uint32_t* h_fcnt = nullptr;               // ... their pinned copy, then 8 words of totals for the device
+  uint32_t* h_bounds = nullptr;             // pinned: the sharded sort's rank bounds, per cloud (row D; BMAX clouds)
+  uint32_t* d_fcnt = nullptr;               // row P: this rank's BMAX counts, then all ranks' (n x BMAX), device
+  uint32_t* h_fcnt = nullptr;               // ... their pinned copy, then 2 x BMAX words of totals for the device
   // One issue order of collectives per rank.  Communicators that are used concurrently
   // must see their collectives issued in the same order on every rank, or their kernels
   // can wait on each other across ranks.  The pipelined batch issues CH_MATCH and CH_FINE
@@ -76,7 +96,36 @@ struct Group {
   int64_t b1_issued = 0;   // pairs of the current batch whose phase-B1 collectives are issued
   int64_t cloud_need = 0;  // the next CH_CLOUD gather waits for b1_issued >= cloud_need
   bool order_abort = false;  // set on an error unwind: a waiting gather throws instead of hanging
+  // Failure handling.  Every host wait that may depend on a peer (a stream or event
+  // after a collective, the order gate, a virtual-rank barrier) is bounded by
+  // timeout_s (FCCF_GROUP_TIMEOUT_S, default 30) and polls the transport's async error;
+  // on an error, a timeout or any exception out of a registration with the group
+  // attached, the rank aborts the group (group_abort): its communicators are aborted,
+  // so kernels and waits of this rank end, and it returns FCCF_E_RCCL.  A peer blocked
+  // in a collective with the failed rank ends at its own bound the same way.  An
+  // aborted group fails every later call until it is destroyed (and recreated).
+  std::atomic<bool> aborted{false};
+  double timeout_s = 30.0;
+  std::string abort_why;
+  // test hook (fccf_debug_group_fail): fail this rank at a collective site
+  int fail_at = 0;          // GROUP_FAIL_* site, 0 = off
+  bool fail_silent = false; // the failing rank does not abort its transport (a dead peer)
 };
+// Collective sites of the failure-injection hook.
+enum { GROUP_FAIL_MATCH = 1, GROUP_FAIL_FINE = 2, GROUP_FAIL_CLOUD = 3 };
+// Aborts the group (idempotent; see Group::aborted).  why: the reason recorded.
+void group_abort(Group* g, const std::string& why);
+// Throws FCCF_E_RCCL when the group is aborted.
+void group_check(const Group* g);
+// Bounded waits for a stream / an event that may depend on peers (see Group::aborted):
+// return when complete; abort the group and throw FCCF_E_RCCL on an async transport
+// error or after the group's time limit, FCCF_E_HIP on a device error.
+// capture_lock: each poll under the pipeline's capture lock (ctx.h capture_mutex; an
+// event whose stream another thread may be capturing).
+void group_wait(Group* g, hipStream_t st);
+void group_wait_event(Group* g, hipEvent_t ev, bool capture_lock = false);
+// The failure-injection hook at site `site` (throws when armed for it).
+void group_fail_point(Group* g, int site);
 // The collective-order gate (see Group::om): blocks until b1_issued >= cloud_need, or
 // throws FCCF_E_RCCL when the batch is unwinding after an error.
 void cloud_gate(Group* g);
@@ -93,9 +142,10 @@ void order_abort(Group* g);
 bool shard_sort_enabled(const Group* g, uint32_t cap, int rounds);
 int shard_sort_r0(int n_ranks);
 // After a sharded sort: every rank's sorted slice [bounds[r], bounds[r+1]) of (k0, v0)
-// of each cloud, gathered in rank order into every rank's arrays.  bounds[e]: the
+// of each of the nbatch clouds (up to BMAX: every pair of a stage group), gathered in
+// rank order into every rank's arrays, all clouds in one exchange.  bounds[e]: the
 // device copy of cloud e's bounds (IsBufs::bounds).  Synchronises st (the bounds).
-void shard_gather_sorted(Group* g, uint32_t* const k0[2], uint32_t* const v0[2], const uint32_t* const bounds[2],
+void shard_gather_sorted(Group* g, const B4<uint32_t*>& k0, const B4<uint32_t*>& v0, const B4<const uint32_t*>& bounds,
                          int nbatch, hipStream_t st);
 
 // Row P (FCCF.cpp:470-534): the face stage of the batch's clouds (the

@@ -2565,29 +2565,40 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
   const char* pm = std::getenv("FCCF_IS_PLAN");
   const bool large = b[0].shard_n > 1 || (pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN));
+  // algorithmic bytes of a launch, summed over its clouds (probe.h)
+  auto pb_round = [&](int r, double per) {
+    ProbeBytes x;
+    for (int e = 0; e < nbatch; ++e) x.add(&b[e].rounds[r].pad, per);
+    return x;
+  };
+  auto pb_ctl = [&](int word, double per) {
+    ProbeBytes x;
+    for (int e = 0; e < nbatch; ++e) x.add(b[e].ctl + word, per);
+    return x;
+  };
   for (int r = 0; r < R; ++r) {
     const B4<uint32_t*> ki = (r & 1) ? k1 : k0, vi = (r & 1) ? v1 : v0;
     const B4<uint32_t*> ko = (r & 1) ? k0 : k1, vo = (r & 1) ? v0 : v1;
     if (large) {
       // algorithmic bytes: the key read, a 2-byte list entry written (x2: >= and <= lists share a unit)
       FCCF_LAUNCH("k_is_count_plan",
-                  (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
+                  (pb_round(r, 8.0)),
                   k_is_count_plan, dim3(maxtiles_l, nbatch), IS_TT, 8 * (size_t)segmax, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
       // algorithmic bytes: key + value read and written, plus a 2-byte list entry
       FCCF_LAUNCH("k_is_scatter",
-                  (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
+                  (pb_round(r, 18.0)),
                   k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), ko, vo, b, r, R);
     } else {
       FCCF_LAUNCH("k_is_count_plan",
-                  (&b[0].rounds[r].pad, 8.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 8.0, 0.0),
+                  (pb_round(r, 8.0)),
                   k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
       FCCF_LAUNCH("k_is_scatter",
-                  (&b[0].rounds[r].pad, 18.0, nbatch > 1 ? &b[1].rounds[r].pad : nullptr, 18.0, 0.0),
+                  (pb_round(r, 18.0)),
                   k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), ko, vo, b, r);
     }
@@ -2597,7 +2608,7 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // k_is_block: IS_OWN_BLOCKS workgroups (one per CU) split over the clouds, so both
   // clouds' items run at once and 8 CUs stay free for the small kernels of other
   // streams (matching, fine verification); profiles/r03r
-  FCCF_LAUNCH("k_is_block", (b[0].ctl + 20, 16.0, nbatch > 1 ? b[1].ctl + 20 : nullptr, 16.0, 0.0), k_is_block,
+  FCCF_LAUNCH("k_is_block", (pb_ctl(20, 16.0)), k_is_block,
               dim3(IS_OWN_BLOCKS / nbatch, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
   // dev: FCCF_IS_WAVE_GRID = workgroups per launch, split over the clouds (default
@@ -2607,7 +2618,7 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
     return s ? std::atoi(s) : 0;
   }();
   const int wave_blocks = wave_grid > 0 ? std::max(1, wave_grid / nbatch) : IS_WAVE_BLOCKS;
-  FCCF_LAUNCH("k_is_wave", (b[0].ctl + 19, 16.0, nbatch > 1 ? b[1].ctl + 19 : nullptr, 16.0, 0.0), k_is_wave,
+  FCCF_LAUNCH("k_is_wave", (pb_ctl(19, 16.0)), k_is_wave,
               dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
 }

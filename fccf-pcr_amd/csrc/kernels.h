@@ -150,6 +150,12 @@ struct VGEntry {
   void bind() {
     args[0] = &xyz; args[1] = &d_n; args[2] = &n; args[3] = &set_n; args[4] = &part; args[5] = &P;
   }
+  // the arguments fixed by the workspace layout (all but the inputs xyz and n), as
+  // CachedGraph's replay check reads them: {index in args, size}
+  static constexpr int LAYOUT_N = 4;
+  static constexpr int layout_idx[LAYOUT_N] = {1, 3, 4, 5};
+  static constexpr size_t layout_size[LAYOUT_N] = {sizeof(B4<uint32_t*>), sizeof(int), sizeof(B4<float*>),
+                                                   sizeof(B4<VGParams*>)};
 };
 const void* vg_entry_kernel();
 // One VoxelGrid pass per batch entry.  n_in (optional): the counts by value (see
@@ -162,6 +168,7 @@ const void* vg_entry_kernel();
 enum { VG_GENERAL = 0, VG_PRESORTED = 1, VG_OPTIMISTIC = 2 };
 constexpr uint32_t VG_REDO = 0x80000000u;       // CloudMail::fsc[k][1]: the optimistic pass must be redone
 constexpr uint32_t VG_FORCE_REDO = 0x10000u;    // test hook bit (fccf_debug_inject_sort_fault)
+constexpr uint32_t VG_FORCE_REDO_LATER = 0x40000u;  // the same for a stage group's later pairs only (clouds >= 2)
 // CloudMail::fsc[k][1]: the cloud's face codes are wider than three 9-bit radix digits
 // (a 1 m octree deeper than 8 levels): a cloud stage that launched three passes sorted
 // the rest in the single-workgroup tail, and the ctx launches four from then on

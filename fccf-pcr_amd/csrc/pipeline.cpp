@@ -352,8 +352,8 @@ Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   return {ds, dt};
 }
 
-// Phase A: enqueue the cloud device stage of the pairs in[0 .. P) (P = 1 or 2) of
-// stage group G, pair j on slot 2G + j (returns at once).  src/tar are device clouds
+// Phase A: enqueue the cloud device stage of the pairs in[0 .. P) (1 <= P <= PAIRS_MAX)
+// of stage group G, pair j on slot PAIRS_MAX * G + j (returns at once).  src/tar are device clouds
 // (staged ones wait for their slot's ev_in).  Per pair: cloud 0 = driver source = TAR
 // file; cloud 1 = driver target = SRC file (:1683).
 // exact2: the driver's pass as VG_PRESORTED, eagerly (the redo of a stage whose
@@ -365,8 +365,7 @@ struct PairIn {
 };
 void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float leaf, const fccf_params& Pa,
                           bool exact2 = false) {
-  if (P < 1 || P > PAIRS_MAX || (P > 1 && c->group))
-    throw Error(FCCF_E_INTERNAL, "cloud stage: 1 pair, or up to PAIRS_MAX without a group");
+  if (P < 1 || P > PAIRS_MAX) throw Error(FCCF_E_INTERNAL, "cloud stage: 1 .. PAIRS_MAX pairs");
   const int S0 = PAIRS_MAX * G;  // the group's first slot
   auto& cg = c->cs[S0];          // the group's arena, stage graphs and fork/join events
   PipeSet& gs = pset(c, S0);
@@ -469,6 +468,23 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   // 0.04 ms per registration slower).
   CloudMail* cmail = &host_mail(c)->clouds[S0];  // (the group's slots adjacent); never allocated inside the capture
   const XsBufs xs = gs.xs;
+  PatchLayout lay;
+  lay.n = VGEntry::LAYOUT_N;
+  for (int i = 0; i < lay.n; ++i) {
+    lay.idx[i] = VGEntry::layout_idx[i];
+    lay.size[i] = VGEntry::layout_size[i];
+  }
+  // test hook (fccf_debug_graph_mismatch): a replay patched with another layout's
+  // workspace pointer, which the replay check must refuse before anything runs
+  VGEntry wrong;
+  void** pargs = entry.args;
+  if (c->graph_mismatch && cg.g_seg[P - 1].replays(&key, sizeof key) && !(DG != nullptr || exact2)) {
+    c->graph_mismatch = false;
+    wrong = entry;
+    wrong.part.v[0] += 64;
+    wrong.bind();
+    pargs = wrong.args;
+  }
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
     seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
@@ -487,7 +503,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
                        all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), st0, nc, cmail,
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
-  }, vg_entry_kernel(), entry.args, DG != nullptr || exact2);
+  }, vg_entry_kernel(), pargs, DG != nullptr || exact2, &lay);
   for (int j = 0; j < P; ++j) {
     auto& cs = c->cs[S0 + j];
     PipeSet& ps = pset(c, S0 + j);
@@ -551,8 +567,12 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
   c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
-  {
-    // (under the capture lock: with two pairs per stage, the second pair's B1 runs while
+  if (c->group) {
+    // a sharded stage holds collectives: a bounded wait that aborts the group on a
+    // peer's failure (group.h), polled under the capture lock
+    group_wait_event(c->group, c->cs[s].ev[4], true);
+  } else {
+    // (under the capture lock: with several pairs per stage, a later pair's B1 runs while
     // the helper thread may be capturing the next stage on the stream ev[4] was recorded
     // on, and HIP refuses to synchronize such an event; ev[4] is complete by then)
     std::lock_guard<std::mutex> lk(capture_mutex());
@@ -563,13 +583,24 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   std::memcpy(fsc, cm.fsc, sizeof fsc);
   if ((fsc[0][1] | fsc[1][1]) & VG_REDO) {
     // the driver's pass found main's output out of leaf order (optimistic mode ran no
-    // sort): the stage again with the exact second pass, before the next pair is enqueued
+    // sort): the stage again with the exact second pass.  When a later pair of a stage
+    // group raises it, the first pair's B1 has already handed the next group's stage to
+    // the helper thread: join that first, so the redo's eager launches cannot land in a
+    // graph the helper is capturing (they queue behind that stage on sa[0]; rare)
+    c->enq.wait();
     clouds_redo(c, s, P);
-    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+    if (c->group) {
+      group_wait_event(c->group, c->cs[s].ev[4], true);
+    } else {
+      std::lock_guard<std::mutex> lk(capture_mutex());
+      HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+    }
     std::memcpy(sc, cm.sc, sizeof sc);
     std::memcpy(fsc, cm.fsc, sizeof fsc);
   }
-  if (ps.redone) ++S.stage_redos;  // (also the group's other pair, whose stage was redone with this one)
+  // (also a later pair of the group, whose stage was redone with this one; a pair whose
+  // B1 had finished before a later pair raised the redo keeps its count of 0)
+  if (ps.redone) ++S.stage_redos;
   guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
   std::vector<VoxRec> vox[2];
   for (int k = 0; k < 2; ++k) {
@@ -764,7 +795,9 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     if (cdev) cluster_launch(c, dq, dtot, drows, ccap, P, &mm, st0);
   }
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipStreamSynchronize(st0));  // totals, K_pass and candidate lists are in the mailbox
+  // totals, K_pass and candidate lists are in the mailbox
+  if (G) group_wait(G, st0);
+  else HIP_CHECK(hipStreamSynchronize(st0));
   std::vector<QTd> qraw[3];
   int64_t kpass = 0;
   if (G && K > 0) {
@@ -793,7 +826,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     }
     HIP_CHECK(hipGetLastError());
     for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
-    HIP_CHECK(hipStreamSynchronize(st0));
+    group_wait(G, st0);
   } else if (K > 0) {
     std::memcpy(tot, mm.tot, 12);
     kpass = mm.kpass;
@@ -1028,7 +1061,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
 
 // Phase B2: the fine scores of the pair on CloudSet s (launched by phase_b1), the
 // score sums over all types and fusion (:1539-1606).
-void phase_b2(fccf_ctx* c, int s) {
+// batch: the pair is part of a pipelined batch, where the stage group's arena (the
+// residual clouds and S1 octree state fine verification reads) may already be
+// recycled by a later stage group when this runs.  An evaluation past the LDS form's
+// capacity (FV_ERR_LDS) then cannot be rerun from that arena: phase_b2 returns true
+// without a result, and the batch registers the pair again after its last pair
+// (sorted form, sticky on the ctx).  A single registration reruns eagerly.
+bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   PipeSet& ps = pset(c, s);
   PhaseB& pb = ps.pb;
   fccf_stats& S = pb.S;
@@ -1038,14 +1077,21 @@ void phase_b2(fccf_ctx* c, int s) {
   float* T_out = pb.T_out;
   std::vector<float> scores(E, 0.f);
   if (E > 0) {
-    // (ev[3]'s stream is captured only by this thread)
-    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));  // scores and the error word are in the mailbox
+    // (ev[3]'s stream is captured only by this thread) scores and the error word are in
+    // the mailbox; with a group the fine stream holds the score gather: a bounded wait
+    if (c->group) group_wait_event(c->group, c->cs[s].ev[3]);
+    else HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));
     uint32_t err = 0;
     if (c->group && c->group->n > 1) {  // every rank's block, gathered in rank order
       group_fine_scores(c->group, s, E, scores.data(), &err);
     } else {
       FineMail& fm = host_mail(c)->fine[s];
       err = fm.err;
+      if ((err & FV_ERR_LDS) && batch) {
+        c->fine_sorted = true;
+        pb.ht.flush();
+        return true;
+      }
       if (err & FV_ERR_LDS) {
         // an evaluation had more leaves than the LDS form holds: the batch again in the
         // sorted form, eagerly, and the ctx keeps that form (the scores are the same)
@@ -1135,6 +1181,7 @@ void phase_b2(fccf_ctx* c, int s) {
     c->dbg_put("counts", counts);
   }
   if (pb.stats) *pb.stats = S;
+  return false;
 }
 
 void reset_capture_counts(fccf_ctx* c) {
@@ -1328,6 +1375,7 @@ void pipeline_release(fccf_ctx* c) {
 
 void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
                   float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
+  group_check(c->group);
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
   if (c->group) order_reset(c->group);
@@ -1345,6 +1393,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
                         const int64_t* n_tar, bool on_device, float leaf, const fccf_params& P, float* T_out,
                         fccf_stats* stats) {
   if (n <= 0) return;
+  group_check(c->group);
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
   // On an error (an exception out of a pair's phase B) the helper thread may still be
@@ -1355,9 +1404,11 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     bool armed = true;
     ~JoinOnUnwind() {
       if (!armed) return;
-      // a helper thread waiting at the group's collective-order gate for a B1 that will
-      // not come throws instead of hanging (Group::om)
-      if (c->group) order_abort(c->group);
+      // with a group, this rank will not finish the batch's collectives: abort the group
+      // (its communicators end, so neither the helper thread's collectives nor the device
+      // synchronisation below can wait for peers), and a helper thread waiting at the
+      // collective-order gate throws instead of hanging (Group::om)
+      if (c->group) group_abort(c->group, "a pipelined batch failed on this rank");
       try {
         c->enq.wait();
       } catch (...) {
@@ -1368,11 +1419,12 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   if (c->group) order_reset(c->group);
   // Pairs per cloud stage: four -- their eight clouds in the same launches, so the
   // sort's dependent rounds and the face stage's small launches are paid once for all
-  //  -- unless a group is attached (its sharded sort gathers one pair's
-  // slices) or a probe runs (its launch records count one pair); FCCF_PAIR_BATCH=1..4.
+  // (DESIGN.md §12); FCCF_PAIR_BATCH=1..4.  With a group the sharded stages gather
+  // every cloud of the stage in one exchange (group.cpp); a probe keeps the batch's own
+  // launch width (its byte counts sum over every cloud of a launch, probe.h).
   const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
   const int pp_env = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
-  const int PP = (c->group || c->probe.on()) ? 1 : std::max(1, std::min(PAIRS_MAX, pp_env));
+  const int PP = std::max(1, std::min(PAIRS_MAX, pp_env));
   const int ng = (n + PP - 1) / PP;  // stage groups; group g uses slots 2 (g & 1) + j
   auto cnt = [&](int g) { return std::min(PP, n - g * PP); };
   auto slot = [&](int i) { return PAIRS_MAX * ((i / PP) & 1) + i % PP; };
@@ -1398,6 +1450,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
     clouds_enqueue_group(c, g & 1, cnt(g), pin, leaf, P);
   };
+  std::vector<int> redo;  // pairs to register again after the batch (phase_b2)
   if (!on_device) stage_group(0);
   enq_group(0);
   // pair i: B1 (its clouds done -> the first pair of a group enqueues the next group's
@@ -1419,25 +1472,36 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
         if (c->probe.on()) {
           enq_group(g + 1);
         } else {
-          // with a group, the helper's sharded-sort gather (CH_CLOUD) waits until this
-          // pair's B1 has issued its CH_MATCH / CH_FINE collectives: one issue order per rank
-          if (c->group) order_need(c->group, i + 1);
+          // with a group, the helper's gathers of the next stage (CH_CLOUD) wait until
+          // every pair of this stage has issued its B1 collectives (CH_MATCH / CH_FINE):
+          // one issue order on every rank
+          if (c->group) order_need(c->group, (int64_t)g * PP + cnt(g));
           c->enq.submit([enq_group, g] { enq_group(g + 1); });  // (after the staging task, which submit() joins first)
         }
       });
-      if (i > 0) phase_b2(c, slot(i - 1));
+      if (i > 0 && phase_b2(c, slot(i - 1), true)) redo.push_back(i - 1);
     }
   }
   c->enq.wait();
-  phase_b2(c, slot(n - 1));
+  if (phase_b2(c, slot(n - 1), true)) redo.push_back(n - 1);
   join_guard.armed = false;
   if (c->group) order_reset(c->group);
+  // pairs whose fine verification overflowed the LDS form (phase_b2): registered again
+  // alone, now in the sorted form (the ctx keeps it), with the same result bits
+  for (int i : redo) {
+    fccf_stats* si = stats ? stats + i : nullptr;
+    run_register(c, src[i], n_src[i], tar[i], n_tar[i], on_device, leaf, P, T_out + 16 * (size_t)i, si);
+    if (si) ++si->fine_reruns;
+  }
 }
 
 }  // namespace fccf
 
 using namespace fccf;
 
+// With a group attached, a registration that fails on this rank leaves its peers in
+// collectives it will not join: the group is aborted (group.h), so every rank returns
+// an error within the group's time limit instead of hanging.
 template <class F>
 static int guarded2(fccf_ctx* c, F&& f) {
   try {
@@ -1446,10 +1510,13 @@ static int guarded2(fccf_ctx* c, F&& f) {
     return FCCF_OK;
   } catch (const Error& e) {
     c->last_error = e.what();
+    if (c->group) group_abort(c->group, e.what());
     return e.code;
   } catch (const std::bad_alloc&) {
+    if (c->group) group_abort(c->group, "out of host memory");
     return FCCF_E_OOM;
   } catch (...) {
+    if (c->group) group_abort(c->group, "internal error");
     return FCCF_E_INTERNAL;
   }
 }

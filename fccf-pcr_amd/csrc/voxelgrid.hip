@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256) k_vg_centroid(B4<const uint32_t*> d_n2, B
   // the caller's redo (nothing is output, the flag goes to the cloud mailbox)
   if (presorted == VG_OPTIMISTIC && !q.overflow && n) {
     const uint32_t* inj = inject2[e];
-    if (q.unsorted || (inj && (*inj & VG_FORCE_REDO))) {
+    if (q.unsorted || (inj && ((*inj & VG_FORCE_REDO) || ((*inj & VG_FORCE_REDO_LATER) && e >= 2)))) {
       if (gid == 0) {
         *d_m = 0u;
         P2[e]->redo = 1u;
@@ -418,13 +418,17 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
     *entry = en;
     entry->bind();
   }
-  const uint32_t* n2 = nbatch > 1 ? d_n[1] : nullptr;  // probe: second problem's counts (probed calls batch <= 2)
-  const uint32_t* m2 = nbatch > 1 ? d_m[1] : nullptr;
+  // probe: algorithmic bytes summed over the launch's clouds
+  ProbeBytes pb_keys, pb_cen;
+  for (int e = 0; e < nbatch; ++e) {
+    pb_keys.add(d_n[e], 16.0);
+    pb_cen.add(d_n[e], 16.0).add(d_m[e], 12.0);
+  }
   const B4<const uint32_t*> unsorted = F([](const VGBufs& v) { return (const uint32_t*)&v.params->unsorted; });
   // the keys kernel also derives the parameters (k_vg_params folded in): each of its
   // VG_KEY_BLOCKS blocks reduces the bbox partials itself, so its grid is kept small
   const dim3 gk(std::min(grid_for(cap), (uint32_t)VG_KEY_BLOCKS), nbatch);
-  FCCF_LAUNCH("k_vg_keys", (d_n[0], 16.0, n2, 16.0, 0.0), k_vg_keys, gk, 256, 0, st, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
+  FCCF_LAUNCH("k_vg_keys", (pb_keys), k_vg_keys, gk, 256, 0, st, d_n, P, k0, v0, presorted ? 1 : 0, F([](const VGBufs& v) { return (const float*)v.part; }), VG_BBOX_BLOCKS, leaf);
   // the first pass's sort also writes the points in sorted order (IsBufs::xyzs), so the
   // centroid reads each leaf's members contiguously; not for a sharded sort (each rank
   // finishes only its range, and the gather moves keys and values only)
@@ -438,13 +442,9 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
   const B4<const VGParams*> Pc(P);
   if (!presorted) {
     introsort_u32(k0, v0, k1, v1, d_n, Pc, cap, isb, st, nbatch, false);
-    if (b[0].is.shard_n > 1) {  // row D: every rank's sorted slice, gathered in rank order (one pair)
-      if (nbatch > 2) throw Error(FCCF_E_INTERNAL, "sharded sort: one pair per cloud stage");
-      uint32_t* const kk[2] = {k0[0], k0[1]};
-      uint32_t* const vv[2] = {v0[0], v0[1]};
-      const uint32_t* const bb[2] = {b[0].is.bounds, b[1].is.bounds};
-      shard_gather_sorted((Group*)b[0].is.shard_group, kk, vv, bb, nbatch, st);
-    }
+    if (b[0].is.shard_n > 1)  // row D: every rank's sorted slice of every cloud, gathered in rank order
+      shard_gather_sorted((Group*)b[0].is.shard_group, k0, v0,
+                          F([](const VGBufs& v) { return (const uint32_t*)v.is.bounds; }), nbatch, st);
     segment_heads_u32(B4<const uint32_t*>(k0), d_n, cap, 0xFFFFFFFFu, starts, nseg, ss, st, B4<uint32_t*>(nullptr),
                       nbatch);
   } else if (presorted == VG_PRESORTED) {  // usually already in leaf order: a sort and segmentation that run only if not
@@ -453,7 +453,7 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
                       nbatch, unsorted);
   }
   const B4<const uint32_t*> inj = F([](const VGBufs& v) { return v.is.inject; });
-  FCCF_LAUNCH("k_vg_centroid", (d_n[0], 16.0, d_m[0], 12.0, 0.0, n2, 16.0, m2, 12.0), k_vg_centroid, g, 256, 0, st, d_n, P, B4<const uint32_t*>(v0), B4<const uint32_t*>(starts), B4<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
+  FCCF_LAUNCH("k_vg_centroid", (pb_cen), k_vg_centroid, g, 256, 0, st, d_n, P, B4<const uint32_t*>(v0), B4<const uint32_t*>(starts), B4<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
 }
 
 }  // namespace fccf

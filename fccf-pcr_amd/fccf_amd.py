@@ -105,6 +105,10 @@ _sig("fccf_stage_fine_verify", ctypes.c_int, _P, _P, _I64, _P, _I64, _P, ctypes.
 _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
 _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
      ctypes.POINTER(ctypes.c_double))
+_sig("fccf_probe_read_widths", ctypes.c_int, _P, ctypes.c_int, _P, _P, _P)
+_sig("fccf_debug_graph_mismatch", ctypes.c_int, _P)
+_sig("fccf_debug_group_fail", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int)
+_sig("fccf_group_aborted", ctypes.c_int, _P)
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
 _sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
@@ -321,6 +325,11 @@ class Ctx:
                "fccf_debug_sort_keys", self._h)
         return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
 
+    def graph_mismatch(self):
+        """Test hook: the next cloud-stage graph replay is patched with a wrong layout
+        argument; that call must fail (FCCF_E_INTERNAL) before launching anything."""
+        _check(_lib.fccf_debug_graph_mismatch(self._h), "fccf_debug_graph_mismatch", self._h)
+
     def inject_sort_fault(self, bits: int):
         """Test hook: later K1 sorts raise these invariant flags (0 switches it off)."""
         _check(_lib.fccf_debug_inject_sort_fault(self._h, int(bits)), "fccf_debug_inject_sort_fault", self._h)
@@ -424,6 +433,16 @@ class Ctx:
         _check(_lib.fccf_probe_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "fccf_probe_read", self._h)
         return ms.value, n.value, b.value
 
+    def probe_read_widths(self, max_width=8):
+        """{width: (total_ms, launches, total_algorithmic_bytes)} since set_probe, per
+        launch width (clouds per batched launch), widths with launches only."""
+        ms = np.zeros(max_width, np.float64)
+        n = np.zeros(max_width, np.int64)
+        b = np.zeros(max_width, np.float64)
+        _check(_lib.fccf_probe_read_widths(self._h, max_width, ms.ctypes.data, n.ctypes.data, b.ctypes.data),
+               "fccf_probe_read_widths", self._h)
+        return {w + 1: (float(ms[w]), int(n[w]), float(b[w])) for w in range(max_width) if n[w]}
+
     def centroid(self, xyz):
         """compute3DCentroid (FCCF.cpp:473) of a dense cloud: float32[4] (x, y, z, 1)."""
         a = _f32(xyz)
@@ -482,6 +501,20 @@ class Group:
         n, r = ctypes.c_int(), ctypes.c_int()
         _check(_lib.fccf_group_info(self._h, ctypes.byref(n), ctypes.byref(r)), "fccf_group_info")
         return n.value, r.value
+
+    def aborted(self) -> bool:
+        """True once the group was aborted (a failed registration on this rank or a
+        peer's failure seen at the group's time limit); destroy and recreate it."""
+        r = _lib.fccf_group_aborted(self._h)
+        if r < 0:
+            _check(r, "fccf_group_aborted")
+        return bool(r)
+
+    def inject_failure(self, site: int, silent: bool = False):
+        """Test hook: fail this rank at collective site 1 (candidate gather), 2 (fine
+        scores) or 3 (sharded sort gather) of its next registration; silent: without
+        aborting the transport (a dead peer)."""
+        _check(_lib.fccf_debug_group_fail(self._h, int(site), 1 if silent else 0), "fccf_debug_group_fail")
 
     def match(self, F1, B1, F2, B2, params: Params | None = None):
         """The sharded search (fccf_group_stage_match): same result as Ctx.match over

@@ -94,13 +94,19 @@ typedef struct fccf_stats {
   /* appended in round 3 */
   int64_t stage_redos;           /* cloud stages redone because the driver's VoxelGrid
                                     input was not in leaf order; in a
-                                    batch, counted for every pair of the redone stage */
+                                    batch, counted for the pair that found it and the
+                                    later pairs of its stage group (an earlier pair of
+                                    the group had already finished its phase B1, with
+                                    a correct result, and counts 0) */
   /* appended in round 4 */
   int32_t shard_ranks;           /* ranks of the attached group (1: no group)      */
   uint32_t sharded;              /* FCCF_SHARDED_* stages this call split over them */
   int64_t fine_reruns;           /* fine verifications rerun in the sorted leaf form
                                     (an evaluation with more 0.5 m leaves than the
-                                    LDS form holds; the scores are the same)      */
+                                    LDS form holds; the scores are the same).  In a
+                                    pipelined batch such a pair is registered again
+                                    after the batch's last pair (its stage arena may
+                                    be recycled by then)                           */
 } fccf_stats;
 /* fccf_stats.sharded bits */
 enum {
@@ -267,6 +273,10 @@ int fccf_stage_fine_verify(fccf_ctx* ctx, const float* s1_xyz, int64_t n1, const
  * kernel NULL or "" switches the probe off.  Setting it resets the totals. */
 int fccf_ctx_set_probe(fccf_ctx* ctx, const char* kernel);
 int fccf_probe_read(fccf_ctx* ctx, double* total_ms, int64_t* launches, double* total_bytes);
+/* The same totals split by launch width w = 1..max_width (entry w - 1): the clouds one
+ * batched launch processes (grid.y of the cloud stage's kernels; a single registration
+ * launches two, a pipelined batch of four pairs per stage eight). */
+int fccf_probe_read_widths(fccf_ctx* ctx, int max_width, double* ms, int64_t* launches, double* bytes);
 
 /* Named intermediate of the last fccf_register call with debug on (see DESIGN.md
  * "Debug names").  Copies min(cap_bytes, size) bytes; *n_bytes = full size. */
@@ -301,11 +311,19 @@ int fccf_debug_sort_rounds(fccf_ctx* ctx, uint32_t out[96]);
  * fccf_register* then fails with FCCF_E_INTERNAL, as it does for a real violation.
  * Bit 0x10000 instead makes the pipeline's optimistic driver VoxelGrid pass report its
  * input as out of leaf order, so the registration redoes its cloud stage with the
- * exact second pass (fccf_stats.stage_redos; the result is unchanged).  Bit 0x20000
+ * exact second pass (fccf_stats.stage_redos; the result is unchanged); bit 0x40000 does
+ * the same for the later pairs of a pipelined batch's stage group only (their clouds
+ * share the launches with the group's first pair, which is not flagged).  Bit 0x20000
  * fills the first pass's sorted-point buffer with NaN before every sort, so a sorted
  * position that the sort's finish kernels fail to write turns into a NaN centroid
  * (a wrong result) instead of a stale point of an earlier call. */
 int fccf_debug_inject_sort_fault(fccf_ctx* ctx, uint32_t bits);
+/* Test hook: the next replay of a cached cloud-stage graph is patched with one
+ * workspace-layout argument that differs from the graph's capture (the bug class of a
+ * patch state shared by graphs of two layouts).  Every replay compares the patched
+ * entry kernel's layout arguments with the captured ones, so that call fails with
+ * FCCF_E_INTERNAL before anything is launched; the hook is consumed. */
+int fccf_debug_graph_mismatch(fccf_ctx* ctx);
 /* Forces a graph capture on one stream concurrent with another thread's wait on
  * an event last recorded on that stream (the pipelined batch's hazard, guarded by
  * the capture lock).  guard 1 = the product's guarded wait, 0 = an unguarded
@@ -335,6 +353,22 @@ int fccf_group_destroy(fccf_group* group);
  * calls must come from its own host thread, all ranks calling the same sequence. */
 int fccf_group_create_local(fccf_ctx* const* ctxs, int n, fccf_group** groups);
 int fccf_group_info(const fccf_group* group, int* n_ranks, int* rank);
+/* Failure handling: every host wait of a registration that may depend on a peer (a
+ * stream or event after a collective, the pipelined batch's collective-order gate, a
+ * virtual-rank barrier) is bounded by FCCF_GROUP_TIMEOUT_S seconds (environment at
+ * group creation, default 30) and polls ncclCommGetAsyncError.  A rank whose
+ * registration fails -- an error of its own, an asynchronous RCCL error or a timeout --
+ * aborts the group (ncclCommAbort of its communicators, which also ends the kernels
+ * waiting in them) and returns the error; its peers end at their bound the same way
+ * and return FCCF_E_RCCL.  An aborted group fails every later registration with
+ * FCCF_E_RCCL until fccf_group_destroy; then create a new one.
+ * fccf_group_aborted: 1 if aborted, 0 if not. */
+int fccf_group_aborted(const fccf_group* group);
+/* Test hook: this rank fails (FCCF_E_RCCL, "injected failure") when its next
+ * registration reaches collective site `site` (1 the candidate gather, 2 the fine-score
+ * gather, 3 the sharded sort's gather; 0 = off).  silent != 0: it does not abort its
+ * transport either (a peer that died), so the others find out at their time limit. */
+int fccf_debug_group_fail(fccf_group* group, int site, int silent);
 /* Stage export of the sharded search: fccf_stage_match's arguments without the
  * range; this rank searches its block, and every rank receives the whole lists. */
 int fccf_group_stage_match(fccf_group* group, const fccf_plane* F1, int nF1, const fccf_base* B1, int nB1,

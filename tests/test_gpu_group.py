@@ -310,3 +310,127 @@ def test_virtual_ranks_shard_the_face_stage_debug_exact(fccf, oracle, n, cfg, mo
             assert got is not None and got.shape == ref.shape, (r, name)
             assert np.array_equal(as_bits(got), as_bits(ref)), (r, name)
         np.testing.assert_array_equal(bits(T), bits(run.T))
+
+
+FCCF_E_RCCL = -3
+
+
+def test_single_rank_group_failure_aborts_and_recovers(fccf, pair):
+    """VERDICT r4 item 2 on a real RCCL communicator (one rank: the box has one GPU): a
+    registration that fails at the candidate gather aborts the group (ncclCommAbort of
+    its three communicators) and returns FCCF_E_RCCL; the aborted group fails the next
+    call at once; after fccf_group_destroy the ctx registers bit-exactly again, and a new
+    group works."""
+    import time
+    src, tar, leaf = pair
+    with fccf.Ctx(0) as ctx:
+        T0, _ = ctx.register(src, tar, leaf)
+        g = fccf.Group(ctx, fccf.group_unique_id(), 1, 0)
+        try:
+            g.inject_failure(1)
+            with pytest.raises(fccf.FCCFError) as e:
+                ctx.register(src, tar, leaf)
+            assert e.value.code == FCCF_E_RCCL and "injected" in str(e.value)
+            assert g.aborted()
+            a = time.perf_counter()
+            with pytest.raises(fccf.FCCFError) as e:
+                ctx.register_batch([(src, tar)] * 2, leaf)
+            assert e.value.code == FCCF_E_RCCL and time.perf_counter() - a < 5.0
+        finally:
+            g.close()
+        T1, _ = ctx.register(src, tar, leaf)
+        with fccf.Group(ctx, fccf.group_unique_id(), 1, 0) as g2:
+            T2, _ = ctx.register(src, tar, leaf)
+            assert not g2.aborted()
+    np.testing.assert_array_equal(bits(T1), bits(T0))
+    np.testing.assert_array_equal(bits(T2), bits(T0))
+
+
+@pytest.mark.parametrize("site,silent,batch", [(1, False, False), (2, False, True), (3, False, True), (1, True, False)])
+def test_virtual_rank_failure_ends_every_rank(fccf, pair, monkeypatch, site, silent, batch):
+    """three virtual ranks, rank 1 made to fail mid-registration at a
+    collective site (1 candidate gather, 2 fine-score gather, 3 sharded sort gather).  A
+    failing rank aborts the group, so every rank returns an error promptly; a silent
+    failure (a dead peer that aborts nothing) is found by the others at the group's
+    time limit (FCCF_GROUP_TIMEOUT_S=3 here).  No rank hangs; the groups are aborted,
+    refuse the next call at once, and after they are destroyed every ctx registers
+    bit-exactly."""
+    import time
+    src, tar, leaf = pair
+    with fccf.Ctx(0) as ctx:
+        T0, _ = ctx.register(src, tar, leaf)
+    monkeypatch.setenv("FCCF_GROUP_TIMEOUT_S", "3")
+    if site == 3:
+        monkeypatch.setenv("FCCF_SHARD_D_MIN", "0")
+    n = 3
+    ctxs = [fccf.Ctx(0) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+        groups[1].inject_failure(site, silent)
+
+        def work(r):
+            a = time.perf_counter()
+            try:
+                if batch:
+                    ctxs[r].register_batch([(src, tar)] * 3, leaf)
+                else:
+                    ctxs[r].register(src, tar, leaf)
+                return ("ok", time.perf_counter() - a, 0)
+            except fccf.FCCFError as e:
+                return ("err", time.perf_counter() - a, e.code)
+
+        out = _on_threads(work, n)
+        for r, (status, dt, code) in enumerate(out):
+            assert status == "err", (r, out)
+            assert code == FCCF_E_RCCL, (r, out)
+            assert dt < (12.0 if silent else 8.0), (r, out)
+        assert all(g.aborted() for g in groups)
+        a = time.perf_counter()
+        for cx in ctxs:
+            with pytest.raises(fccf.FCCFError):
+                cx.register(src, tar, leaf)
+        assert time.perf_counter() - a < 5.0
+        for g in groups:
+            g.close()
+        for cx in ctxs[:1]:
+            T, _ = cx.register(src, tar, leaf)
+            np.testing.assert_array_equal(bits(T), bits(T0))
+    finally:
+        for cx in ctxs:
+            cx.close()
+
+
+@pytest.mark.parametrize("n,cfg,npairs", [(2, "c2", 6), (3, "c3", 5)])
+def test_virtual_ranks_pair_batched_stages(fccf, oracle, monkeypatch, n, cfg, npairs):
+    """a group no longer forces one pair per cloud stage.  With rows D
+    and P sharded (FCCF_SHARD_D_MIN=0) and four pairs per stage (FCCF_PAIR_BATCH=4:
+    stage groups of 4 and the remainder), every cloud of a stage is gathered in one
+    exchange, and the next stage's gathers wait for all of this stage's phase-B1
+    collectives (one issue order per rank).  Every rank's T equals the oracle's bit for
+    bit."""
+    c = fccf.CONFIGS[cfg]
+    src, tar, _ = fccf.synth_pair(c["n"], c["room"])
+    leaf = c["leaf"]
+    rng = np.random.default_rng(17)
+    pairs = [(src, tar)]
+    for k in range(npairs - 1):
+        jit = rng.normal(0, 0.002, src.shape).astype(np.float32)
+        pairs.append(((src + jit).astype(np.float32), tar[: len(tar) - 1000 * (k + 1)]))
+    refs = [oracle.Run(s, t, leaf, oracle.INTROSORT).T.copy() for s, t in pairs]
+    monkeypatch.setenv("FCCF_SHARD_D_MIN", "0")
+    monkeypatch.setenv("FCCF_PAIR_BATCH", "4")
+    ctxs = [fccf.Ctx(0) for _ in range(n)]
+    try:
+        groups = fccf.local_groups(ctxs)
+        out = _on_threads(lambda r: ctxs[r].register_batch(pairs, leaf), n)
+        for g in groups:
+            g.close()
+    finally:
+        for cx in ctxs:
+            cx.close()
+    for Tb, sb in out:
+        for i, (T, ref) in enumerate(zip(Tb, refs)):
+            np.testing.assert_array_equal(bits(T), bits(ref), err_msg=f"pair {i}")
+        for st in sb:
+            assert st.shard_ranks == n
+            assert sorted(st.as_dict()["sharded"]) == ["faces", "fine", "search", "sort"], st.as_dict()["sharded"]

@@ -153,6 +153,32 @@ def test_graph_replay_with_new_data_and_sizes(ctx, oracle, fccf):
         np.testing.assert_array_equal(T.view(np.uint32), run.T.view(np.uint32))
 
 
+def test_graph_replay_layout_check(fccf, oracle):
+    """Every replay of the cached cloud-stage graph compares the patched entry kernel's
+    layout arguments (everything but the inputs) with the ones it was captured with
+    (CachedGraph).  A replay deliberately patched with a wrong
+    workspace pointer (fccf_debug_graph_mismatch) fails with FCCF_E_INTERNAL before
+    anything is launched, and the same ctx then replays correctly, bit-exact."""
+    src, tar, _ = fccf.synth_pair(60_000)
+    ref = oracle.Run(src, tar, 0.1, oracle.INTROSORT).T
+    FCCF_E_INTERNAL = -6
+    c = fccf.Ctx(0)
+    try:
+        T0, _ = c.register(src, tar, 0.1)  # captures
+        T1, st1 = c.register(src, tar, 0.1)  # replays
+        assert st1.graph_captures == 0
+        c.graph_mismatch()
+        with pytest.raises(fccf.FCCFError) as e:
+            c.register(src, tar, 0.1)
+        assert e.value.code == FCCF_E_INTERNAL and "graph replay" in str(e.value)
+        T2, st2 = c.register(src, tar, 0.1)  # the hook is consumed; the graph is intact
+        assert st2.graph_captures == 0
+        for T in (T0, T1, T2):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+    finally:
+        c.close()
+
+
 def test_probe_path_is_exact_and_counts_launches(ctx, oracle, fccf):
     """With a kernel probe on, the device stages launch eagerly (no graphs) and the
     probed launches go through hipExtLaunchKernelGGL; results must not change."""
@@ -323,6 +349,75 @@ def test_optimistic_driver_pass_redo(ctx, oracle, fccf):
     T2, st2 = ctx.register(src, tar, 0.1)  # the cached graphs are intact afterwards
     assert st2.stage_redos == 0
     np.testing.assert_array_equal(T2.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("pp", ["2", "4"])
+def test_redo_raised_by_a_later_pair_of_the_group(fccf, oracle, monkeypatch, pp):
+    """A stage group's later pair alone finds the driver pass's input out of leaf order
+    (test hook 0x40000: clouds >= 2 of the stage only), after the group's first pair has
+    already handed the next group's cloud stage to the helper thread.  The redo joins the
+    helper first, so its eager launches never land in a capture; every
+    T stays bit-exact, and the pairs from the flagged one on count the redo."""
+    monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
+    base_src, base_tar, _ = fccf.synth_pair(70_000)
+    rng = np.random.default_rng(31)
+    pairs = []
+    for k in range(6):
+        jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
+        pairs.append(((base_src + jit).astype(np.float32)[: 70_000 - 3000 * k], base_tar))
+    refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
+    c = fccf.Ctx(0)
+    try:
+        c.inject_sort_fault(0x40000)
+        try:
+            Tb, sb = c.register_batch(pairs, 0.1)
+        finally:
+            c.inject_sort_fault(0)
+        for T, ref in zip(Tb, refs):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+        # pair j >= 1 of each group found the flag (j = 1) or ran after the redo; the
+        # group's first pair had finished its phase B1 before it, with a correct result
+        got = [int(x.stage_redos) for x in sb]
+        assert got == [1 if i % int(pp) else 0 for i in range(len(pairs))], got
+        Tb2, sb2 = c.register_batch(pairs, 0.1)  # hook off: cached graphs intact, no redo
+        for T, ref in zip(Tb2, refs):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+        assert all(x.stage_redos == 0 for x in sb2)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("pp", ["1", "4"])
+def test_batch_fine_overflow_registers_the_pair_again(fccf, oracle, monkeypatch, pp):
+    """in a pipelined batch, fine verification past the LDS form's
+    capacity (FV_ERR_LDS, forced with FCCF_FINE_LDS_CAP=16) cannot be rerun from the stage
+    arena, which a later stage group may already be recycling; the pair is registered
+    again after the batch's last pair instead (sorted form, sticky).  Every T bit-exact
+    against the oracle, the overflowing pairs count fine_reruns = 1, and the pairs whose
+    phase B1 ran after the first overflow use the sorted form from the start."""
+    monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
+    monkeypatch.setenv("FCCF_FINE_LDS_CAP", "16")
+    base_src, base_tar, _ = fccf.synth_pair(80_000)
+    rng = np.random.default_rng(41)
+    pairs = []
+    for k in range(6):
+        jit = rng.normal(0, 0.002, base_src.shape).astype(np.float32)
+        pairs.append(((base_src + jit).astype(np.float32), base_tar[: 80_000 - 4000 * k]))
+    refs = [oracle.Run(s, t, 0.1, oracle.INTROSORT).T for s, t in pairs]
+    c = fccf.Ctx(0)
+    try:
+        Tb, sb = c.register_batch(pairs, 0.1)
+        for i, (T, ref) in enumerate(zip(Tb, refs)):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"pair {i}")
+        reruns = [int(x.fine_reruns) for x in sb]
+        assert reruns[0] == 1, reruns
+        assert set(reruns) <= {0, 1} and reruns[-1] == 0, reruns
+        Tb2, sb2 = c.register_batch(pairs, 0.1)  # sorted form from the start now
+        for T, ref in zip(Tb2, refs):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
+        assert all(x.fine_reruns == 0 for x in sb2)
+    finally:
+        c.close()
 
 
 def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monkeypatch):

@@ -2,7 +2,10 @@
 # PMC calibration: the request-size-bucketed L2->fabric counters
 # (TCC_EA0_RDREQ_32B/64B/128B, TCC_EA0_WRREQ/_64B) beside FETCH_SIZE / WRITE_SIZE, over
 # tools/pmc_calib (known bytes per access pattern) and over the bench command, one
-# counter pass per process.  Usage (via gpurun): [CFG=c3] [STEPS=5] [CALIB=0] [BENCH=0] bash tools/gpu_pmc_calib.sh <tag>
+# counter pass per process.  BATCH=1: the workload is tools/pmc_batch.py (pipelined
+# batches only, eight clouds per launch: the timed region's shape) instead of single
+# registrations of the bench command.
+# Usage (via gpurun): [CFG=c3] [STEPS=5] [CALIB=0] [BENCH=0] [BATCH=1] bash tools/gpu_pmc_calib.sh <tag>
 set -e
 TAG=${1:-calib}
 CFG=${CFG:-c3}
@@ -25,7 +28,11 @@ for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
 done
 fi
 [ "${BENCH:-1}" = 1 ] || exit 0
-B="bench.py --config $CFG --no-cpu-baseline --parity-configs= --no-pipeline --no-sharded --steps $STEPS --warmup 2"
+if [ "${BATCH:-0}" = 1 ]; then
+  B="tools/pmc_batch.py $CFG $STEPS"
+else
+  B="bench.py --config $CFG --no-cpu-baseline --parity-configs= --no-pipeline --no-sharded --steps $STEPS --warmup 2"
+fi
 i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))

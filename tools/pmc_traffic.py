@@ -2,7 +2,11 @@
 bench.py's roofline.traffic (tools/gpu_pmc_calib.sh writes the passes).
 
 Usage:
-  python tools/pmc_traffic.py PMC_DIR CONFIG OUT.json [MIN_FRAC]
+  python tools/pmc_traffic.py PMC_DIR CONFIG OUT.json [MIN_FRAC] [WIDTH]
+
+WIDTH (default 2): the clouds per launch of the workload's cloud-stage kernels -- 2 for
+single registrations (the bench command with --no-pipeline), 8 for tools/pmc_batch.py
+(four pairs per stage, the timed region's shape); recorded in OUT.json for bench.py.
 
 PMC_DIR holds bench_p1 .. bench_p4, one counter pass per process (rocprofv3 does not
 split counters over passes, and a pass holds at most 4 TCC counters):
@@ -67,6 +71,7 @@ def active_mean(vals, min_frac):
 def main():
     pmc_dir, config, out = sys.argv[1:4]
     min_frac = float(sys.argv[4]) if len(sys.argv) > 4 else 0.05
+    width = int(sys.argv[5]) if len(sys.argv) > 5 else 2
     passes = {}
     for i in range(1, 5):
         for k, cs in per_kernel(os.path.join(pmc_dir, f"bench_p{i}")).items():
@@ -76,7 +81,7 @@ def main():
     if os.path.exists(bj):
         for k, v in json.load(open(bj)).get("kernel_table", {}).items():
             alg[k] = v.get("algorithmic_bytes_per_launch")
-    res = {"config": config, "units": "bytes per launch (active launches)",
+    res = {"config": config, "width": width, "units": "bytes per launch (active launches)",
            "hbm_bytes_per_launch": "exact: calibrated request-size buckets (see tools/pmc_traffic.py)",
            "kernels": {}}
     for k, cs in sorted(passes.items()):
