@@ -35,6 +35,7 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
   for (auto& s : c->sa) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
   ok = ok && hipStreamCreateWithFlags(&c->sb, hipStreamNonBlocking) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->d_flags, 256) == hipSuccess && hipMemset(c->d_flags, 0, 256) == hipSuccess;
+  for (auto& e : c->ev_match) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (auto& cs : c->cs) {
     for (auto& e : cs.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (auto& e : cs.tev) ok = ok && hipEventCreate(&e) == hipSuccess;
@@ -51,7 +52,7 @@ extern "C" int fccf_ctx_create(fccf_ctx** out, int device) {
 extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   if (!c) return FCCF_E_ARG;
   (void)hipSetDevice(c->device);
-  (void)hipDeviceSynchronize();
+  (void)device_sync_guarded();
   // a group still attached is detached, not destroyed: its handle stays the caller's,
   // and fccf_group_destroy then only releases the communicator
   if (c->group) {
@@ -74,6 +75,8 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
     if (s) (void)hipStreamDestroy(s);
   if (c->sb) (void)hipStreamDestroy(c->sb);
   if (c->d_flags) (void)hipFree(c->d_flags);
+  for (auto& e : c->ev_match)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return FCCF_OK;
 }
@@ -342,7 +345,7 @@ extern "C" int fccf_debug_graph_mismatch(fccf_ctx* c) {
 extern "C" int fccf_debug_inject_sort_fault(fccf_ctx* c, uint32_t bits) {
   if (!c || (bits & ~(IS_FAULT_MASK | VG_FORCE_REDO | VG_FORCE_REDO_LATER | IS_POISON_XYZS))) return FCCF_E_ARG;
   return guarded(c, [&] {
-    HIP_CHECK(hipDeviceSynchronize());  // no sort of this ctx in flight reads the word meanwhile
+    HIP_CHECK(device_sync_guarded());  // no sort of this ctx in flight reads the word meanwhile
     HIP_CHECK(hipMemcpy(c->d_flags, &bits, 4, hipMemcpyHostToDevice));
   });
 }
@@ -924,6 +927,6 @@ void ktrace_register(void (*setter)(unsigned long long*)) { kt_setters().push_ba
 extern "C" int fccf_ktrace_arm(void* buf) {
   if (buf) (void)hipMemset(buf, 0, 8);
   for (auto f : fccf::kt_setters()) f((unsigned long long*)buf);
-  return hipDeviceSynchronize() == hipSuccess ? FCCF_OK : FCCF_E_HIP;
+  return device_sync_guarded() == hipSuccess ? FCCF_OK : FCCF_E_HIP;
 }
 #endif

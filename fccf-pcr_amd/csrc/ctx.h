@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <atomic>
 #include <mutex>
 #include <stdexcept>
@@ -105,6 +106,14 @@ struct MailBuf {
 inline std::mutex& capture_mutex() {
   static std::mutex m;
   return m;
+}
+
+// A device-wide synchronisation while another thread (the batch's helper, another
+// phase-B chain, another virtual rank's ctx) may be capturing a graph: HIP may
+// invalidate a capture that a concurrent device synchronisation meets.
+inline hipError_t device_sync_guarded() {
+  std::lock_guard<std::mutex> lk(capture_mutex());
+  return hipDeviceSynchronize();
 }
 
 // A wait on an event that another thread's stream may be capturing right now.
@@ -282,6 +291,16 @@ struct fccf_ctx {
   fccf::MailBuf mail;  // pipeline.cpp host_mail()
   fccf::Pool pool;
   fccf::AsyncTask enq;  // pipelined batch: enqueues the next pair's cloud stage
+  // A pipelined batch runs the phase B of alternate pairs on two host threads ("chains",
+  // pipeline.cpp): the calling thread and b1w, each with a pool of half the host threads
+  // (bpool, created on first use), its own matching scratch (arena2 / arena2b), pinned
+  // match mailbox (HostMail::match / match2) and completion event (ev_match).  The
+  // fine-verification launches of both chains share sa[1] under fine_mutex.
+  fccf::AsyncTask b1w;
+  std::unique_ptr<fccf::Pool> bpool[2];
+  fccf::Arena arena2b;
+  hipEvent_t ev_match[2] = {nullptr, nullptr};
+  std::mutex fine_mutex;
   fccf::Probe probe;
   fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)
   fccf::Group* group = nullptr;  // RCCL rank of a sharded registration (group.cpp), or none

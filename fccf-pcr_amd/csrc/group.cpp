@@ -182,6 +182,8 @@ struct LocalTransport : Transport {
     }
     g->hub->barrier(ch, g->timeout_s);
     if (g->rank == 0 && C.need > C.cap) {  // one rank grows the staging, between barriers
+      // (hipFree synchronises the device: not while another rank's thread captures a graph)
+      std::lock_guard<std::mutex> lk(capture_mutex());
       if (C.stage) HIP_CHECK(hipFree(C.stage));
       C.stage = nullptr;
       C.cap = 0;
@@ -686,7 +688,7 @@ extern "C" int fccf_group_destroy(fccf_group* G) {
   if (!G) return FCCF_E_ARG;
   if (G->g.ctx) {
     (void)hipSetDevice(G->g.ctx->device);
-    (void)hipDeviceSynchronize();
+    (void)device_sync_guarded();
     if (G->g.ctx->group == &G->g) G->g.ctx->group = nullptr;
   }
   group_free(G->g);

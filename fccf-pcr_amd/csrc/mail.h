@@ -50,7 +50,8 @@ struct FineMail {
 
 struct HostMail {
   CloudMail clouds[8];  // per pair slot; a stage group's slots are adjacent (k_compact_planar)
-  MatchMail match;
+  MatchMail match;      // phase-B chain 0 (pipeline.cpp Chain)
+  MatchMail match2;     // chain 1: a pipelined batch's second host thread
   FineMail fine[8];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
 };
 

@@ -14,6 +14,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -298,6 +301,22 @@ struct PhaseB {
   HostTrace ht;
 };
 
+// A phase-B chain: what one pair's phase B1 uses exclusively.  A pipelined batch runs
+// two chains on two host threads (alternate pairs), so two pairs' host stages (growth,
+// clustering, the LM) overlap; a single registration, or a batch whose ctx needs the
+// one-chain form (group, probe, debug, the device growth/LM forms), uses chain 0.  The
+// matching stream sb is shared: each chain waits for its own work by its event.
+struct Chain {
+  Pool* pool;
+  Arena* arena2;     // matching scratch
+  MatchMail* mm;     // pinned match mailbox
+  hipEvent_t ev;     // this chain's matching work on sb is complete
+  bool may_redo;     // the stage redo (VG_REDO) runs in place (one chain only)
+};
+
+struct BatchRestart {};  // two-chain batch: a stage needs its redo -> the batch again with one chain
+struct WorkerAborted {};  // two-chain batch: the other worker failed first
+
 // State of the registration whose clouds occupy CloudSet s.
 struct PipeSet {
   PhaseB pb;
@@ -552,7 +571,7 @@ void clouds_redo(fccf_ctx* c, int s, const fccf_params& P) {
 // pair, so fine verification overlaps the next pair's host stages.
 template <class AfterClouds>
 void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_stats* stats,
-              AfterClouds&& after_clouds) {
+              AfterClouds&& after_clouds, const Chain& ch) {
   fccf_stats S;
   std::memset(&S, 0, sizeof S);
   PipeSet& ps = pset(c, s);
@@ -566,7 +585,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // counts and planar records of both clouds: written by k_compact_planar into
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
-  c->pool.warm(1000);  // growing runs both clouds in parallel right after this wait
+  ch.pool->warm(1000);  // growing runs both clouds in parallel right after this wait
   if (c->group) {
     // a sharded stage holds collectives: a bounded wait that aborts the group on a
     // peer's failure (group.h), polled under the capture lock
@@ -581,6 +600,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
   std::memcpy(fsc, cm.fsc, sizeof fsc);
+  if (((fsc[0][1] | fsc[1][1]) & VG_REDO) && !ch.may_redo) throw BatchRestart();
   if ((fsc[0][1] | fsc[1][1]) & VG_REDO) {
     // the driver's pass found main's output out of leaf order (optimistic mode ran no
     // sort): the stage again with the exact second pass.  When a later pair of a stage
@@ -691,7 +711,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     const uint32_t nvv[2] = {fsc[0][2], fsc[1][2]};
     grow_groups_device(c, dv, nvv, P, st0, gg);
   }
-  c->pool.parallel_for(2, [&](int k) {  // the two clouds are independent
+  ch.pool->parallel_for(2, [&](int k) {  // the two clouds are independent
     g[k] = gdev ? select_groups(gg[k], vox[k].data(), P) : grow_and_select(vox[k].data(), (int)vox[k].size(), P);
     const auto tb = clk::now();
     base[k] = select_base(g[k].planes, g[k].theta, P, k + 1);
@@ -729,7 +749,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (g[0].planes.size() > (size_t)MAX_PLANES || g[1].planes.size() > (size_t)MAX_PLANES ||
       base[0].size() > (size_t)MAX_BASES || base[1].size() > (size_t)MAX_BASES)
     throw Error(FCCF_E_INTERNAL, "plane table capacity");
-  MatchMail& mm = host_mail(c)->match;
+  MatchMail& mm = *ch.mm;
   MatchIn& M = mm.M;  // built in pinned memory: the H2D below is a true async copy
   std::memset(&M, 0, sizeof M);
   for (int k = 0; k < 2; ++k) {
@@ -769,35 +789,38 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   const bool cbits_on = !(cbe && cbe[0] == '0');
   const bool cdev = c->cluster_device && cbits_on && K > 0;  // f3 on the device (cluster.hip)
   const size_t cl_bytes = cdev ? sizeof(uint64_t) * MatchMail::CB_CAP + 15 * 4 * ccap + 4096 : 0;
-  c->arena2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + lists * (G ? 2 : 1) + cl_bytes + (1 << 16));
-  c->arena2.reset();
-  MatchIn* dM = c->arena2.take_n<MatchIn>(1);
-  uint32_t* dcnt = c->arena2.take_n<uint32_t>(std::max(K, 1));
-  int32_t* dtype = c->arena2.take_n<int32_t>(std::max(K, 1));
-  uint32_t* doff = c->arena2.take_n<uint32_t>(std::max(K, 1));
-  uint32_t* dtot = c->arena2.take_n<uint32_t>(4);
+  Arena& a2 = *ch.arena2;
+  a2.ensure(sizeof(MatchIn) + 3 * 4 * (size_t)std::max(K, 1) + lists * (G ? 2 : 1) + cl_bytes + (1 << 16));
+  a2.reset();
+  MatchIn* dM = a2.take_n<MatchIn>(1);
+  uint32_t* dcnt = a2.take_n<uint32_t>(std::max(K, 1));
+  int32_t* dtype = a2.take_n<int32_t>(std::max(K, 1));
+  uint32_t* doff = a2.take_n<uint32_t>(std::max(K, 1));
+  uint32_t* dtot = a2.take_n<uint32_t>(4);
   MCand* dc[3];
   QTd* dq[3];
   for (int t = 0; t < 3; ++t) {
-    dc[t] = c->arena2.take_n<MCand>(ccap);
-    dq[t] = c->arena2.take_n<QTd>(ccap);
+    dc[t] = a2.take_n<MCand>(ccap);
+    dq[t] = a2.take_n<QTd>(ccap);
   }
   uint32_t tot[4] = {0, 0, 0, 0};
   HIP_CHECK(hipMemcpyAsync(dM, &M, sizeof M, hipMemcpyHostToDevice, st0));
   // (k_match_scan writes the totals whenever there are tests: only an empty search
   // needs them zeroed -- one runtime fill kernel fewer on the dependent chain)
   if (Kloc <= 0) HIP_CHECK(hipMemsetAsync(dtot, 0, 16, st0));
-  uint64_t* drows = cdev ? c->arena2.take_n<uint64_t>(MatchMail::CB_CAP) : nullptr;
+  uint64_t* drows = cdev ? a2.take_n<uint64_t>(MatchMail::CB_CAP) : nullptr;
   match_candidates(dM, Kloc, dcnt, dtype, doff, dtot, dc, dq, st0, &mm);
   const float cr2 = (float)((double)P.cluster_distance_threshold * (double)P.cluster_distance_threshold);
   if (cbits_on && K > 0 && !G) {
     cluster_bits(dq, dtot, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0, drows);
-    if (cdev) cluster_launch(c, dq, dtot, drows, ccap, P, &mm, st0);
+    if (cdev) cluster_launch(c, dq, dtot, drows, ccap, P, &mm, st0, nullptr, &a2);
   }
   HIP_CHECK(hipGetLastError());
-  // totals, K_pass and candidate lists are in the mailbox
-  if (G) group_wait(G, st0);
-  else HIP_CHECK(hipStreamSynchronize(st0));
+  // totals, K_pass and candidate lists are in the mailbox (sb may also carry the other
+  // chain's matching: this chain waits for its own work)
+  HIP_CHECK(hipEventRecord(ch.ev, st0));
+  if (G) group_wait_event(G, ch.ev);
+  else HIP_CHECK(hipEventSynchronize(ch.ev));
   std::vector<QTd> qraw[3];
   int64_t kpass = 0;
   if (G && K > 0) {
@@ -810,10 +833,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     MCand* ca[3];
     QTd* qa[3];
     for (int t = 0; t < 3; ++t) {
-      ca[t] = c->arena2.take_n<MCand>(ccap);
-      qa[t] = c->arena2.take_n<QTd>(ccap);
+      ca[t] = a2.take_n<MCand>(ccap);
+      qa[t] = a2.take_n<QTd>(ccap);
     }
-    uint32_t* dtot_all = c->arena2.take_n<uint32_t>(4);
+    uint32_t* dtot_all = a2.take_n<uint32_t>(4);
     group_gather_candidates(G, dq, dc, tl, kl, qa, ca, ccap, tot, dtot_all, &kpass, st0);
     for (int t = 0; t < 3; ++t) {
       dc[t] = ca[t];
@@ -822,7 +845,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     if (cbits_on) {
       cluster_bits(dq, dtot_all, cr2, make_cut(P.cluster_angel_threshold), P.cluster_number_threshold, &mm, st0,
                    drows);
-      if (cdev) cluster_launch(c, dq, dtot_all, drows, ccap, P, &mm, st0);
+      if (cdev) cluster_launch(c, dq, dtot_all, drows, ccap, P, &mm, st0, nullptr, &a2);
     }
     HIP_CHECK(hipGetLastError());
     for (int t = 0; t < 3; ++t) qraw[t] = d2h(dq[t], tot[t], st0);
@@ -892,7 +915,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       continue;
     }
     int64_t ncl = 0;
-    transform_cluster(qv, fine[t], cluster_num, P, &ncl, &c->pool, bits);
+    transform_cluster(qv, fine[t], cluster_num, P, &ncl, ch.pool, bits);
     counts.push_back(ncl);
     S.fine[t] = (int64_t)fine[t].size();
   }
@@ -922,7 +945,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       npairs[items[k].first][(size_t)items[k].second] = nps[k];
     }
   } else {
-    c->pool.parallel_for((int)items.size(), [&](int k) {  // independent per candidate
+    ch.pool->parallel_for((int)items.size(), [&](int k) {  // independent per candidate
       const int t = items[k].first, i = items[k].second;
       TS& r = res[t][i];
       r.T = T_from_qt(fine[t][i]);
@@ -971,6 +994,9 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (FG) shard_range(E, FG->rank, FG->n, &flo, &fhi);
   const int El = fhi - flo;
   hipStream_t sf = c->sa[1];
+  // the fine stream is shared by the chains: one chain's launch sequence (waits, graph
+  // replay or capture, event records) at a time
+  std::unique_lock<std::mutex> flk(c->fine_mutex);
   if (El > 0) {
     fccf::Arena& a3 = c->cs[s].arena3;
     const uint32_t n1 = (uint32_t)S.res1, n2 = (uint32_t)S.res2;
@@ -1044,6 +1070,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     group_fine_gather(FG, s, nullptr, 0, nullptr, sf);
     HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));
   }
+  flk.unlock();
   pb.S = S;
   for (int t = 0; t < 3; ++t) pb.ctv[t] = std::move(ctv[t]);
   pb.counts = std::move(counts);
@@ -1162,7 +1189,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   S.ms[FCCF_T_FUSE] = ms_since(t0);
   S.ms_total = ms_since(pb.t_all);
   if (c->probe.on()) {
-    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(device_sync_guarded());
     probe_collect(c->probe);
   }
   S.graph_captures = c->cs[s].g_fine.captures;
@@ -1324,16 +1351,17 @@ void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vect
 }
 
 void cluster_launch(fccf_ctx* c, QTd* const dq[3], const uint32_t* dtot, const uint64_t* drows, size_t ccap,
-                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num) {
+                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num, Arena* scratch) {
+  Arena& a2 = scratch ? *scratch : c->arena2;
   ClusterIn in{};
   ClusterOut out{};
   for (int t = 0; t < 3; ++t) {
     in.q[t] = dq[t];
-    out.cseed[t] = c->arena2.take_n<uint32_t>(ccap);
-    out.csize[t] = c->arena2.take_n<uint32_t>(ccap);
-    out.bx[t] = c->arena2.take_n<uint32_t>(ccap);
-    out.bid[t] = c->arena2.take_n<uint32_t>(ccap);
-    out.emit[t] = c->arena2.take_n<uint32_t>(ccap);
+    out.cseed[t] = a2.take_n<uint32_t>(ccap);
+    out.csize[t] = a2.take_n<uint32_t>(ccap);
+    out.bx[t] = a2.take_n<uint32_t>(ccap);
+    out.bid[t] = a2.take_n<uint32_t>(ccap);
+    out.emit[t] = a2.take_n<uint32_t>(ccap);
   }
   in.rows = drows;
   in.totals = dtot;
@@ -1373,6 +1401,16 @@ void pipeline_release(fccf_ctx* c) {
   }
 }
 
+// Chain k of nchains (see Chain).
+Chain chain_of(fccf_ctx* c, int k, int nchains) {
+  HostMail* hm = host_mail(c);
+  if (nchains <= 1) return Chain{&c->pool, &c->arena2, &hm->match, c->ev_match[0], true};
+  for (auto& p : c->bpool)
+    if (!p) p.reset(new Pool(std::max(1, c->pool.size() / 2)));
+  return k == 0 ? Chain{c->bpool[0].get(), &c->arena2, &hm->match, c->ev_match[0], false}
+                : Chain{c->bpool[1].get(), &c->arena2b, &hm->match2, c->ev_match[1], false};
+}
+
 void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
                   float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
   group_check(c->group);
@@ -1385,13 +1423,13 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
     tar = in.tar;
   }
   clouds_enqueue(c, 0, src, n_src, tar, n_tar, !on_device, leaf, P);
-  phase_b1(c, 0, P, T_out, stats, [] {});
+  phase_b1(c, 0, P, T_out, stats, [] {}, chain_of(c, 0, 1));
   phase_b2(c, 0);
 }
 
 void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src, const float* const* tar,
                         const int64_t* n_tar, bool on_device, float leaf, const fccf_params& P, float* T_out,
-                        fccf_stats* stats) {
+                        fccf_stats* stats, int nchains) {
   if (n <= 0) return;
   group_check(c->group);
   ProbeGuard probe_guard(&c->probe);
@@ -1413,7 +1451,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
         c->enq.wait();
       } catch (...) {
       }
-      (void)hipDeviceSynchronize();
+      (void)device_sync_guarded();
     }
   } join_guard{c};
   if (c->group) order_reset(c->group);
@@ -1425,7 +1463,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
   const int pp_env = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
   const int PP = std::max(1, std::min(PAIRS_MAX, pp_env));
-  const int ng = (n + PP - 1) / PP;  // stage groups; group g uses slots 2 (g & 1) + j
+  const int ng = (n + PP - 1) / PP;  // stage groups; group g uses slots PAIRS_MAX (g & 1) + j
   auto cnt = [&](int g) { return std::min(PP, n - g * PP); };
   auto slot = [&](int i) { return PAIRS_MAX * ((i / PP) & 1) + i % PP; };
   // Host inputs: group g+1's clouds are staged on the copy stream at the start of
@@ -1453,37 +1491,140 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   std::vector<int> redo;  // pairs to register again after the batch (phase_b2)
   if (!on_device) stage_group(0);
   enq_group(0);
-  // pair i: B1 (its clouds done -> the first pair of a group enqueues the next group's
-  // clouds -> host stages -> launch fine verification), then B2 of pair i-1, whose fine
-  // verification ran on the GPU during pair i's host stages
-  for (int g = 0; g < ng; ++g) {
-    c->enq.wait();  // this group's cloud stage is fully enqueued (its events recorded)
-    if (!on_device && g + 1 < ng) {
-      if (c->probe.on()) stage_group(g + 1);
-      else c->enq.submit([stage_group, g] { stage_group(g + 1); });
+  if (nchains <= 1) {
+    const Chain ch = chain_of(c, 0, 1);
+    // pair i: B1 (its clouds done -> the first pair of a group enqueues the next group's
+    // clouds -> host stages -> launch fine verification), then B2 of pair i-1, whose fine
+    // verification ran on the GPU during pair i's host stages
+    for (int g = 0; g < ng; ++g) {
+      c->enq.wait();  // this group's cloud stage is fully enqueued (its events recorded)
+      if (!on_device && g + 1 < ng) {
+        if (c->probe.on()) stage_group(g + 1);
+        else c->enq.submit([stage_group, g] { stage_group(g + 1); });
+      }
+      for (int j = 0; j < cnt(g); ++j) {
+        const int i = g * PP + j;
+        phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
+          if (j != 0 || g + 1 >= ng) return;
+          // the next group's cloud stage is enqueued from a helper thread while this
+          // thread runs the host stages (launches are ~60 us of host time); probed
+          // runs stay on this thread (the probe's launch records are not shared)
+          if (c->probe.on()) {
+            enq_group(g + 1);
+          } else {
+            // with a group, the helper's gathers of the next stage (CH_CLOUD) wait until
+            // every pair of this stage has issued its B1 collectives (CH_MATCH / CH_FINE):
+            // one issue order on every rank
+            if (c->group) order_need(c->group, (int64_t)g * PP + cnt(g));
+            c->enq.submit([enq_group, g] { enq_group(g + 1); });  // (after the staging task, which submit() joins first)
+          }
+        }, ch);
+        if (i > 0 && phase_b2(c, slot(i - 1), true)) redo.push_back(i - 1);
+      }
     }
-    for (int j = 0; j < cnt(g); ++j) {
-      const int i = g * PP + j;
-      phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
-        if (j != 0 || g + 1 >= ng) return;
-        // the next group's cloud stage is enqueued from a helper thread while this
-        // thread runs the host stages (launches are ~60 us of host time); probed
-        // runs stay on this thread (the probe's launch records are not shared)
-        if (c->probe.on()) {
-          enq_group(g + 1);
+    c->enq.wait();
+    if (phase_b2(c, slot(n - 1), true)) redo.push_back(n - 1);
+  } else {
+    // Two chains: pair i's phase B on worker i % 2 (this thread and c->b1w), each worker
+    // running B1 of its next pair before B2 of its previous one (fine verification
+    // overlaps).  The first pair of a group still enqueues the next group's stage, which
+    // recycles the slots of the group before: it waits until every pair of that group has
+    // finished B1 (B1 reads the slot's workspace; B2 does not).  The other worker's pairs
+    // of a group wait until the group's stage is enqueued.
+    struct Sync {
+      std::mutex m;
+      std::condition_variable cv;
+      int submitted = 1;   // groups whose cloud-stage enqueue has been handed to the helper
+      int ready = 0;       // groups whose cloud stage is fully enqueued
+      std::vector<int> b1; // per group: pairs whose phase B1 has finished
+      bool failed = false;
+    } sy;
+    sy.b1.assign((size_t)ng, 0);
+    auto wait_until = [&sy](auto pred) {
+      std::unique_lock<std::mutex> lk(sy.m);
+      sy.cv.wait(lk, [&] { return sy.failed || pred(); });
+      if (sy.failed) throw WorkerAborted();
+    };
+    auto update = [&sy](auto f) {
+      {
+        std::lock_guard<std::mutex> lk(sy.m);
+        f();
+      }
+      sy.cv.notify_all();
+    };
+    const Chain chains[2] = {chain_of(c, 0, 2), chain_of(c, 1, 2)};  // (creates the chain pools here)
+    auto worker = [&](int k) {
+      HIP_CHECK(hipSetDevice(c->device));
+      const Chain& ch = chains[k];
+      int pending = -1;  // this worker's pair whose B2 is still to run
+      for (int i = k; i < n; i += 2) {
+        const int g = i / PP, j = i % PP;
+        if (j == 0) {
+          wait_until([&] { return sy.submitted > g; });
+          c->enq.wait();  // group g's cloud stage is fully enqueued
+          update([&] { sy.ready = g + 1; });
+          if (!on_device && g + 1 < ng) {
+            // staging group g+1 re-records the input events of group g-1's slots, which
+            // that group's B1 reads (the H2D time): after it
+            if (g >= 1) wait_until([&] { return sy.b1[(size_t)g - 1] >= cnt(g - 1); });
+            c->enq.submit([stage_group, g] { stage_group(g + 1); });
+          }
         } else {
-          // with a group, the helper's gathers of the next stage (CH_CLOUD) wait until
-          // every pair of this stage has issued its B1 collectives (CH_MATCH / CH_FINE):
-          // one issue order on every rank
-          if (c->group) order_need(c->group, (int64_t)g * PP + cnt(g));
-          c->enq.submit([enq_group, g] { enq_group(g + 1); });  // (after the staging task, which submit() joins first)
+          wait_until([&] { return sy.ready > g; });
         }
-      });
-      if (i > 0 && phase_b2(c, slot(i - 1), true)) redo.push_back(i - 1);
+        phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [&] {
+          if (j != 0 || g + 1 >= ng) return;
+          if (g >= 1) wait_until([&] { return sy.b1[(size_t)g - 1] >= cnt(g - 1); });
+          c->enq.submit([enq_group, g] { enq_group(g + 1); });
+          update([&] { sy.submitted = g + 2; });
+        }, ch);
+        update([&] { ++sy.b1[(size_t)g]; });
+        if (pending >= 0 && phase_b2(c, slot(pending), true)) update([&] { redo.push_back(pending); });
+        pending = i;
+      }
+      if (pending >= 0 && phase_b2(c, slot(pending), true)) update([&] { redo.push_back(pending); });
+    };
+    auto guarded_worker = [&](int k) {
+      try {
+        worker(k);
+      } catch (...) {
+        update([&] { sy.failed = true; });
+        throw;
+      }
+    };
+    c->b1w.submit([&guarded_worker] { guarded_worker(1); });
+    std::exception_ptr err[2];
+    try {
+      guarded_worker(0);
+    } catch (...) {
+      err[0] = std::current_exception();
     }
+    try {
+      c->b1w.wait();  // (always joined before this frame unwinds)
+    } catch (...) {
+      err[1] = std::current_exception();
+    }
+    // the first failure counts (a stage redo before anything else: the batch reruns with
+    // one chain); the other worker's WorkerAborted only says it stopped
+    bool restart = false;
+    std::exception_ptr first;
+    for (auto& e : err) {
+      if (!e) continue;
+      try {
+        std::rethrow_exception(e);
+      } catch (const BatchRestart&) {
+        restart = true;
+      } catch (const WorkerAborted&) {
+      } catch (...) {
+        if (!first) first = e;
+      }
+    }
+    if (first) std::rethrow_exception(first);
+    if (restart) throw BatchRestart();
+    if (err[0] || err[1]) throw Error(FCCF_E_INTERNAL, "pipelined batch: a phase-B worker stopped");
+    c->enq.wait();
+    std::sort(redo.begin(), redo.end());
   }
-  c->enq.wait();
-  if (phase_b2(c, slot(n - 1), true)) redo.push_back(n - 1);
   join_guard.armed = false;
   if (c->group) order_reset(c->group);
   // pairs whose fine verification overflowed the LDS form (phase_b2): registered again
@@ -1493,6 +1634,28 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     run_register(c, src[i], n_src[i], tar[i], n_tar[i], on_device, leaf, P, T_out + 16 * (size_t)i, si);
     if (si) ++si->fine_reruns;
   }
+}
+
+// The batch with two phase-B chains where the ctx allows it (FCCF_B1_CHAINS=1 forces
+// one); a stage redo found by a two-chain batch (rare: an input out of leaf order after
+// main's VoxelGrid) reruns the whole batch with one chain, whose redo runs in place.
+void run_register_batch_any(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src,
+                            const float* const* tar, const int64_t* n_tar, bool on_device, float leaf,
+                            const fccf_params& P, float* T_out, fccf_stats* stats) {
+  const char* ce = std::getenv("FCCF_B1_CHAINS");
+  const int want = ce ? std::atoi(ce) : 2;
+  const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
+  const int pp = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
+  const bool two = want >= 2 && pp >= 2 && n >= 2 && !c->group && !c->probe.on() && !c->debug &&
+                   !c->grow_device && !c->lm_device;
+  if (two) {
+    try {
+      run_register_batch(c, n, src, n_src, tar, n_tar, on_device, leaf, P, T_out, stats, 2);
+      return;
+    } catch (const BatchRestart&) {
+    }
+  }
+  run_register_batch(c, n, src, n_src, tar, n_tar, on_device, leaf, P, T_out, stats, 1);
 }
 
 }  // namespace fccf
@@ -1555,5 +1718,5 @@ extern "C" int fccf_register_batch(fccf_ctx* c, int n, const float* const* src, 
   fccf_params P;
   if (params) P = *params;
   else fccf_params_default(&P);
-  return guarded2(c, [&] { run_register_batch(c, n, src, ns, tar, nt, on_device != 0, leaf, P, T, stats); });
+  return guarded2(c, [&] { run_register_batch_any(c, n, src, ns, tar, nt, on_device != 0, leaf, P, T, stats); });
 }

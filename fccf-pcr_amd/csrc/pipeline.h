@@ -82,7 +82,8 @@ void grow_groups_device(fccf_ctx* c, const VoxRec* const dvox[2], const uint32_t
 // (may be null): one value for all types instead of the one derived from the totals.
 struct MatchMail;
 void cluster_launch(fccf_ctx* c, QTd* const dq[3], const uint32_t* dtot, const uint64_t* drows, size_t ccap,
-                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num = nullptr);
+                    const fccf_params& P, MatchMail* mail, hipStream_t st, const int* cluster_num = nullptr,
+                    Arena* scratch = nullptr);
 std::vector<QT> cluster_results(const MatchMail& mm, int t);  // type t's averages (status 0)
 MatchMail* match_mail(fccf_ctx* c);
 void verify_items_device(fccf_ctx* c, const std::vector<QT>& qs, const std::vector<Plane>& F1,

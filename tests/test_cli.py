@@ -1,4 +1,5 @@
-"""The drop-in CLI `fccf src.ply tar.ply voxel` (reference main, FCCF.cpp:1646-1689)."""
+"""The drop-in CLI `FCCF src.ply tar.ply voxel` (reference main, FCCF.cpp:1646-1689; the
+executable keeps the reference's name, CMakeLists.txt:32, and is also built as `fccf`)."""
 import os
 import subprocess
 
@@ -6,11 +7,20 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLI = os.path.join(ROOT, "fccf-pcr_amd", "lib", "fccf")
+CLI = os.path.join(ROOT, "fccf-pcr_amd", "lib", "FCCF")
+CLI_LOWER = os.path.join(ROOT, "fccf-pcr_amd", "lib", "fccf")
 
 
-def run_cli(*args, timeout=300):
-    return subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+def run_cli(*args, timeout=300, exe=CLI):
+    return subprocess.run([exe, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+
+
+def test_cli_under_the_reference_name_and_lower_case():
+    """Both names run the same program (argv and stdout of the reference's ./FCCF)."""
+    for exe in (CLI, CLI_LOWER):
+        assert os.access(exe, os.X_OK), exe
+        r = run_cli("a.ply", exe=exe)
+        assert r.returncode == 1 and "usage" in r.stderr
 
 
 def eigen_text(T):

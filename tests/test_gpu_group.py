@@ -375,12 +375,12 @@ def test_virtual_rank_failure_ends_every_rank(fccf, pair, monkeypatch, site, sil
                     ctxs[r].register_batch([(src, tar)] * 3, leaf)
                 else:
                     ctxs[r].register(src, tar, leaf)
-                return ("ok", time.perf_counter() - a, 0)
+                return ("ok", time.perf_counter() - a, 0, "")
             except fccf.FCCFError as e:
-                return ("err", time.perf_counter() - a, e.code)
+                return ("err", time.perf_counter() - a, e.code, str(e))
 
         out = _on_threads(work, n)
-        for r, (status, dt, code) in enumerate(out):
+        for r, (status, dt, code, msg) in enumerate(out):
             assert status == "err", (r, out)
             assert code == FCCF_E_RCCL, (r, out)
             assert dt < (12.0 if silent else 8.0), (r, out)
