@@ -740,6 +740,58 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan(B4<const uint32_t*> K2,
   tile_prefix(W, r, dyn, sh64);
 }
 
+// The partitioned tile written out.  Scatter form (G = false): every element to its
+// destination, so a swapped element is a scattered 4-byte store into another tile's
+// lines (two of them: key and value), which other workgroups fill too.  Gather form
+// (G = true): the swap is an involution (L[k] <-> R[k]), so position p receives the
+// element at its partner position -- the element there before the round, with the
+// median-to-first swap applied at m -- and every workgroup writes its own tile's
+// positions, whole lines, coalesced; the partners are read instead (a window of a few
+// tiles, mostly L2 / Infinity-Cache hits).
+template <bool G, int TC>
+__device__ __forceinline__ void store_partitioned(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
+                                                  uint32_t* __restrict__ Ko, uint32_t* __restrict__ Vo,
+                                                  const uint32_t (&kk)[TC], const uint32_t (&vv)[TC],
+                                                  uint32_t (&dst)[TC], uint32_t a, uint32_t f, uint32_t l,
+                                                  uint32_t m, uint32_t kf, uint32_t vf, const IsBufs& W) {
+  if constexpr (!G) {
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      const uint32_t d = dst[c];
+      if (d == IS_NONE) continue;
+      if (d <= f || d >= l) {  // cannot happen; never write outside the segment
+        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
+        continue;
+      }
+      Ko[d] = kk[c];
+      Vo[d] = vv[c];
+    }
+  } else {
+    uint32_t gk[TC], gv[TC];
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {  // every partner load issued before the first store
+      const uint32_t p = a + c * IS_TT + threadIdx.x, d = dst[c];
+      gk[c] = kk[c];
+      gv[c] = vv[c];
+      if (d == IS_NONE || d == p) continue;
+      if (d <= f || d >= l) {  // cannot happen; never read outside the segment
+        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
+        dst[c] = IS_NONE;
+        continue;
+      }
+      gk[c] = d == m ? kf : K[d];
+      gv[c] = d == m ? vf : V[d];
+    }
+#pragma unroll
+    for (int c = 0; c < TC; ++c) {
+      if (dst[c] == IS_NONE) continue;
+      const uint32_t p = a + c * IS_TT + threadIdx.x;
+      Ko[p] = gk[c];
+      Vo[p] = gv[c];
+    }
+  }
+}
+
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin; the last workgroup plans round
 // r + 1 (if r + 1 < R).  The partners of a tile's swapped elements have contiguous
@@ -750,6 +802,7 @@ constexpr uint32_t IS_WIN = 256;  // prefix window in LDS (larger windows: binar
 #ifndef IS_SCATTER_MINB
 #define IS_SCATTER_MINB 1
 #endif
+template <bool G>
 __global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
                                                       B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r,
                                                       int R) {
@@ -875,17 +928,7 @@ __global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B4<const 
         dst[c] = au + W.gel[au + (x - (wg_n <= IS_WIN ? wing[u - wg_lo] : pre[u].x))];
       }
     }
-#pragma unroll
-    for (int c = 0; c < IS_TC_L; ++c) {
-      const uint32_t d = dst[c];
-      if (d == IS_NONE) continue;
-      if (d <= f || d >= l) {  // cannot happen; never write outside the segment
-        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
-        continue;
-      }
-      Ko[d] = kk[c];
-      Vo[d] = vv[c];
-    }
+    store_partitioned<G, IS_TC_L>(K, V, Ko, Vo, kk, vv, dst, a, f, l, m, s.kf, s.vf, W);
     cut = wave_min_u32(cut);
     if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
     __syncthreads();
@@ -1064,6 +1107,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B4<const uint32_t*> K
 
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
+template <bool G>
 __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
                                                       B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r) {
   KT();
@@ -1207,17 +1251,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2,
       dst[c] = au + W.gel[au + (x - preg[u])];
     }
   }
-#pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
-    const uint32_t d = dst[c];
-    if (d == IS_NONE) continue;
-    if (d <= f || d >= l) {  // cannot happen; never write outside the segment
-      is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
-      continue;
-    }
-    Ko[d] = kk[c];
-    Vo[d] = vv[c];
-  }
+  store_partitioned<G, IS_TC>(K, V, Ko, Vo, kk, vv, dst, a, f, l, m, s.kf, s.vf, W);
   IS_PH(3);  // destinations (list loads), stores issued
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
@@ -2565,6 +2599,10 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
   const char* pm = std::getenv("FCCF_IS_PLAN");
   const bool large = b[0].shard_n > 1 || (pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN));
+  // the rounds' store form (store_partitioned): FCCF_IS_GATHER=1 the gather form, 0 the
+  // scatter form (read per call, as FCCF_IS_PLAN; tests run the sort cases in both)
+  const char* gm = std::getenv("FCCF_IS_GATHER");
+  const bool gather = gm && gm[0] == '1';
   // algorithmic bytes of a launch, summed over its clouds (probe.h)
   auto pb_round = [&](int r, double per) {
     ProbeBytes x;
@@ -2587,20 +2625,24 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
       // algorithmic bytes: key + value read and written, plus a 2-byte list entry
-      FCCF_LAUNCH("k_is_scatter",
-                  (pb_round(r, 18.0)),
-                  k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st, B4<const uint32_t*>(ki),
-                  B4<const uint32_t*>(vi), ko, vo, b, r, R);
+      if (gather)
+        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter<true>, dim3(maxtiles_l, nbatch), IS_TT, 0, st,
+                    B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r, R);
+      else
+        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter<false>, dim3(maxtiles_l, nbatch), IS_TT, 0, st,
+                    B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r, R);
     } else {
       FCCF_LAUNCH("k_is_count_plan",
                   (pb_round(r, 8.0)),
                   k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
-      FCCF_LAUNCH("k_is_scatter",
-                  (pb_round(r, 18.0)),
-                  k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT, 8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki),
-                  B4<const uint32_t*>(vi), ko, vo, b, r);
+      if (gather)
+        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s<true>, dim3(maxtiles, nbatch), IS_TT,
+                    8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
+      else
+        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s<false>, dim3(maxtiles, nbatch), IS_TT,
+                    8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
     }
     step("scatter", r);
   }
