@@ -332,7 +332,7 @@ struct PipeSet {
   float leaf = 0.f;
   uint32_t sharded = 0;  // FCCF_SHARDED_* of the cloud stage (row D)
   bool redone = false;   // the stage (this pair's stage group) was redone (VG_REDO)
-  // (slot 2G only) the stage group's last stage: how many pairs, the entry kernel's
+  // (a group's first slot, PAIRS_MAX * G, only) the stage group's last stage: how many pairs, the entry kernel's
   // arguments (patched into g_seg[P - 1] per call; one per graph, because the fields
   // other than the inputs are set only when that graph is captured) and the centroid
   // sums' scratch
