@@ -28,11 +28,25 @@ namespace {
 // points each (all loads issued before use), quad shuffles for the sub-record,
 // then the wave / block reduction for the block record.
 // Batched over blockIdx.y = sequence e.
+// TF: fine verification's form (FvTransform): the points are read from tf.s2, moved by
+// tf.T[e] and written to tf.s2t's sequence e as they are loaded (xyz0 unused).
+template <bool TF>
 __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xyz0, const uint32_t* __restrict__ d_n0,
                                                     float* __restrict__ aggr0, SeqStrides sd,
                                                     uint32_t nbc, OctState* __restrict__ reset0,
-                                                    uint64_t* __restrict__ stamp) {
+                                                    uint64_t* __restrict__ stamp, FvTransform tf) {
   KT();
+  if (TF && blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t e = blockIdx.y;
+    *sd.at(tf.st, sd.state, e) = *tf.s1_state;
+    tf.ecnt[e] = 0u;
+    tf.pts[e] = 0u;
+    if (e == 0) {
+      tf.scal[4] = tf.n1;
+      tf.scal[5] = tf.n2;
+      tf.scal[7] = 0u;
+    }
+  }
   if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)  // the face stage starts
     *stamp = __builtin_amdgcn_s_memrealtime();
   if (reset0 && blockIdx.x == 0 && threadIdx.x == 0) {  // empty octree for k_oct_sim (sequence blockIdx.y)
@@ -45,18 +59,42 @@ __global__ void __launch_bounds__(256) k_block_aggr(const float* __restrict__ xy
   __shared__ float sh[4][6];
   const float* xyz = sd.at(xyz0, sd.xyz, blockIdx.y);
   float* aggr = sd.at(aggr0, sd.aggr, blockIdx.y);
-  const uint32_t n = *sd.at(d_n0, sd.n, blockIdx.y);
+  const uint32_t n = TF ? tf.n2 : *sd.at(d_n0, sd.n, blockIdx.y);
   float* sub = aggr + 6 * (size_t)nbc;
   const uint32_t t = threadIdx.x, sb = t >> 2, q = t & 3, lane = t & 63, w = t >> 6;
   const uint32_t p0 = blockIdx.x * AGGR_BLOCK + sb * AGGR_SUB + q * 16;
   const uint32_t last = n ? n - 1u : 0u;
   float v[16][3];
+  if constexpr (TF) {
+    const m44 M = tf.T[blockIdx.y];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const size_t i = min(p0 + k, last);
-    v[k][0] = xyz[3 * i];
-    v[k][1] = xyz[3 * i + 1];
-    v[k][2] = xyz[3 * i + 2];
+    for (int k = 0; k < 16; ++k) {
+      const size_t i = min(p0 + k, last);
+      v[k][0] = tf.s2[3 * i];
+      v[k][1] = tf.s2[3 * i + 1];
+      v[k][2] = tf.s2[3 * i + 2];
+    }
+    float* o = sd.at(tf.s2t, sd.xyz, blockIdx.y);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const f3 pt = tf_se3(M, v[k][0], v[k][1], v[k][2]);
+      v[k][0] = pt.x;
+      v[k][1] = pt.y;
+      v[k][2] = pt.z;
+      if (p0 + k < n) {
+        o[3 * (size_t)(p0 + k)] = pt.x;
+        o[3 * (size_t)(p0 + k) + 1] = pt.y;
+        o[3 * (size_t)(p0 + k) + 2] = pt.z;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const size_t i = min(p0 + k, last);
+      v[k][0] = xyz[3 * i];
+      v[k][1] = xyz[3 * i + 1];
+      v[k][2] = xyz[3 * i + 2];
+    }
   }
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
@@ -485,7 +523,15 @@ inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch,
                 SeqStrides sd, OctState* reset_state, uint64_t* stamp) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap), reset_state, stamp);
+  k_block_aggr<false><<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(xyz, d_n, aggr, sd, aggr_blocks(cap), reset_state, stamp,
+                                                                FvTransform{});
+}
+
+void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
+                          int batch, SeqStrides sd) {
+  const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
+  k_block_aggr<true><<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(tf.s2, d_n, aggr, sd, aggr_blocks(cap), nullptr, nullptr,
+                                                               tf);
 }
 
 void octree_sim(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, const float* aggr, OctState* state,

@@ -121,21 +121,43 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
   }
   __syncthreads();
   uint32_t fin = 0;
+  const uint32_t lane = threadIdx.x & 63u;
   for (uint32_t j = 0; j < FV_TILE / 256; ++j) {
+    if (i0 + j * 256 >= n) break;  // (uniform)
     const uint32_t i = i0 + j * 256 + threadIdx.x;
-    if (i >= n) break;
     const bool tgt = i >= n1;
-    const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
-    if (!finite3(p[0], p[1], p[2])) continue;
-    ++fin;
-    const unsigned long long key = (ecnt ? 0ull : (unsigned long long)e << shift) | oct_code(S, res, p[0], p[1], p[2]);
-    uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52);  // 12 bits: FV_SLOTS
-    for (;;) {
-      const unsigned long long old = atomicCAS(&hk[h], FV_EMPTY, key);
-      if (old == FV_EMPTY || old == key) break;
-      h = (h + 1u) & (FV_SLOTS - 1u);
+    bool act = i < n;
+    unsigned long long key = 0ull;
+    if (act) {
+      const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
+      const float x = p[0], y = p[1], z = p[2];
+      act = finite3(x, y, z);
+      if (act) key = (ecnt ? 0ull : (unsigned long long)e << shift) | oct_code(S, res, x, y, z);
     }
-    atomicAdd(&hc[h], tgt ? 0x10000u : 1u);
+    fin += act ? 1u : 0u;
+    // A wave's points lie in a few leaves (the clouds come in 1 m leaf order): one lane
+    // per distinct key inserts it and adds the wave's source and target counts, instead
+    // of every lane hitting the same few LDS slots with atomics.
+    const uint64_t tmask = __ballot(act && tgt);
+    uint64_t pending = __ballot(act);
+    while (pending) {
+      const uint32_t leader = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
+      const uint32_t klo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, (int)leader);
+      const uint32_t khi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), (int)leader);
+      const unsigned long long lk = ((unsigned long long)khi << 32) | klo;
+      const uint64_t same = __ballot(act && key == lk) & pending;
+      if (lane == leader) {
+        uint32_t h = (uint32_t)((lk * 0x9E3779B97F4A7C15ull) >> 52);  // 12 bits: FV_SLOTS
+        for (;;) {
+          const unsigned long long old = atomicCAS(&hk[h], FV_EMPTY, lk);
+          if (old == FV_EMPTY || old == lk) break;
+          h = (h + 1u) & (FV_SLOTS - 1u);
+        }
+        const uint32_t nt = (uint32_t)__popcll(same & tmask), ns = (uint32_t)__popcll(same) - nt;
+        atomicAdd(&hc[h], ns | (nt << 16));
+      }
+      pending &= ~same;
+    }
   }
   __syncthreads();
   // the occupied slots, compacted: FV_SLOTS / 256 consecutive slots per thread
@@ -414,15 +436,26 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
                        double res, FineBufs b, hipStream_t st, FineMail* mail, int mode, uint32_t lds_cap) {
   if (E <= 0) return;
   const size_t astride = aggr_floats(n2);
-  k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
-                                                                  n1, b.nseg_e, b.pts);
   // scal[5] holds n2 for the device-count interfaces
   uint32_t* d_n2 = b.scal + 5;
   SeqStrides sd;  // evaluation e: its own transformed S2 copy, aggregates and state; shared count
   sd.xyz = 12 * (size_t)n2;
   sd.aggr = 4 * astride;
   sd.state = sizeof(OctState);
-  block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
+  // T_e * S2, its block aggregates and each evaluation's octree start (from S1's bounds)
+  // in one launch (FCCF_FV_SPLIT=1: the former transform launch, then the aggregates)
+  static const bool split = [] {
+    const char* s = std::getenv("FCCF_FV_SPLIT");
+    return s && s[0] == '1';
+  }();
+  if (split) {
+    k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
+                                                                    n1, b.nseg_e, b.pts);
+    block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
+  } else {
+    FvTransform tf{s2, b.T, b.s2t, s1_state, b.state, b.scal, b.nseg_e, b.pts, n1, n2};
+    block_aggr_transform(tf, d_n2, n2, b.aggr2, st, E, sd);
+  }
   octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, sd);
   const dim3 ge(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E);
   if (mode == FV_LEAVES_LDS) {

@@ -285,6 +285,23 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
 void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st, int batch = 1,
                 SeqStrides sd = SeqStrides(), OctState* reset_state = nullptr,
                 uint64_t* stamp = nullptr);  // stamp: the face stage's start (FaceBufs::t_faces)
+// Fine verification's form of block_aggr (fine.hip, FCCF.cpp:785-839): sequence e's
+// points are T[e] * s2[i] (tf_se3), written to s2t + e * sd.xyz as they are aggregated,
+// and block (0, e) also starts evaluation e's octree from the state after S1 and clears
+// its per-evaluation counters (the work of a separate transform launch before).
+struct FvTransform {
+  const float* s2;  // the untransformed cloud (shared by the evaluations)
+  const m44* T;
+  float* s2t;       // per evaluation (sd.xyz stride)
+  const OctState* s1_state;
+  OctState* st;     // per evaluation (sd.state stride)
+  uint32_t* scal;   // [4] n1, [5] n2, [7] error word (evaluation 0's block 0)
+  uint32_t* ecnt;   // per-evaluation entry counts
+  uint32_t* pts;    // per-evaluation finite point counts
+  uint32_t n1, n2;  // (n2 also written to scal[5], the later launches' device count)
+};
+void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
+                          int batch, SeqStrides sd);
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
 constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
 // aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per
