@@ -99,19 +99,82 @@ inline void set_avg(Group& g) {  // the recompute's averages (:580-586)
 }
 }  // namespace
 
-// compare_normal's rejection (angle_gt) for voxels j0 .. j0+7 against the group
-// normal (ax, ay, az) with double norm na: written branch-free over SoA arrays so
-// the compiler vectorises it; every lane does exactly normal_cos_pre's operations.
-static inline void angle_skip8(const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
-                               const double* __restrict__ vn, int j0, float ax,
-                               float ay, float az, double na, AngleCut cut, bool skip[8]) {
-  for (int k = 0; k < 8; ++k) {
-    const float dp = (float)dot3d((double)ax, (double)ay, (double)az, (double)nx[j0 + k], (double)ny[j0 + k],
-                                  (double)nz[j0 + k]);
-    const float c = (float)((double)dp / (na * vn[j0 + k]));
-    skip[k] = angle_gt(c, cut);
+// Direction index of unit normals for region growing's scan: cube-map cells (face =
+// the dominant axis and its sign, then a DG x DG grid over the other two coordinates
+// divided by the dominant one), each with its voxels in ascending index, its mean
+// direction and angular radius.  candidates(a, after) lists, ascending, the voxels after
+// index `after` and not yet allocated in every cell whose cone could hold a direction
+// within `cone` of a -- cos(angle(a, center)) >= cos(cone + radius + slack) -- plus the
+// non-finite normals; an undefined a (not finite, or not of unit length) lists them all.
+namespace {
+struct DirIndex {
+  static constexpr int DG = 8, NC = 6 * DG * DG;  // cell NC: non-finite / zero normals
+  std::vector<int> idx;                  // voxels by cell, ascending within a cell
+  int beg[NC + 2], len[NC + 1];          // cell c: idx[beg[c], beg[c] + len[c]) (allocated ones dropped)
+  float cx[NC], cy[NC], cz[NC], ccos[NC];  // unit mean direction, cos(cone + radius + slack)
+  int used[NC], nused = 0;               // non-empty cells
+  DirIndex(const float* ux, const float* uy, const float* uz, int n, double cone) : idx(n) {
+    std::vector<uint16_t> cof(n);
+    int cnt[NC + 1] = {};
+    for (int j = 0; j < n; ++j) ++cnt[cof[j] = (uint16_t)cell_of(ux[j], uy[j], uz[j])];
+    beg[0] = 0;
+    for (int c = 0; c <= NC; ++c) {
+      beg[c + 1] = beg[c] + cnt[c];
+      len[c] = 0;
+    }
+    for (int j = 0; j < n; ++j) idx[beg[cof[j]] + len[cof[j]]++] = j;
+    for (int c = 0; c < NC; ++c) {
+      if (!len[c]) continue;
+      used[nused++] = c;
+      const int* l = idx.data() + beg[c];
+      double m[3] = {0, 0, 0};
+      for (int q = 0; q < len[c]; ++q) { m[0] += ux[l[q]]; m[1] += uy[l[q]]; m[2] += uz[l[q]]; }
+      const double r = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+      for (double& x : m) x /= r;
+      double mind = 1.0;  // cos of the cell's angular radius
+      for (int q = 0; q < len[c]; ++q) mind = std::min(mind, m[0] * ux[l[q]] + m[1] * uy[l[q]] + m[2] * uz[l[q]]);
+      const double lim = cone + std::acos(std::max(-1.0, std::min(1.0, mind))) + 1e-3;
+      cx[c] = (float)m[0]; cy[c] = (float)m[1]; cz[c] = (float)m[2];
+      ccos[c] = lim >= 3.14159265358979323846 ? -2.f : (float)std::cos(lim) - 1e-5f;
+    }
   }
-}
+  static int cell_of(float x, float y, float z) {
+    if (!(std::isfinite(x) && std::isfinite(y) && std::isfinite(z))) return NC;
+    const float ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
+    int f;
+    float s, t, m;
+    if (ax >= ay && ax >= az) { f = x < 0 ? 1 : 0; m = ax; s = y; t = z; }
+    else if (ay >= az) { f = y < 0 ? 3 : 2; m = ay; s = x; t = z; }
+    else { f = z < 0 ? 5 : 4; m = az; s = x; t = y; }
+    if (!(m > 0.f)) return NC;
+    auto q = [](float v) { return std::min(DG - 1, std::max(0, (int)((v + 1.f) * (0.5f * DG)))); };
+    return f * DG * DG + q(s / m) * DG + q(t / m);
+  }
+  void candidates(const float a[3], int after, const char* va, std::vector<int>& out) {
+    out.clear();
+    const bool ok = std::isfinite(a[0]) && std::isfinite(a[1]) && std::isfinite(a[2]) &&
+                    std::fabs(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] - 1.f) < 1e-3f;
+    auto take = [&](int c) {
+      // drop allocated voxels from the cell for good (they never return), keep the rest
+      int* l = idx.data() + beg[c];
+      int w = 0;
+      for (int q = 0; q < len[c]; ++q) {
+        const int j = l[q];
+        if (va[j]) continue;
+        l[w++] = j;
+        if (j > after) out.push_back(j);
+      }
+      len[c] = w;
+    };
+    for (int u = 0; u < nused; ++u) {
+      const int c = used[u];
+      if (len[c] && (!ok || a[0] * cx[c] + a[1] * cy[c] + a[2] * cz[c] >= ccos[c])) take(c);
+    }
+    take(NC);
+    std::sort(out.begin(), out.end());
+  }
+};
+}  // namespace
 
 std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& P) {
   // compare_normal(...) == !(theta > thr) == !angle_gt(cos, cut): no acos in the O(V^2) loops
@@ -119,21 +182,29 @@ std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& 
   std::vector<char> va(nv, 0);
   std::vector<Group> G;
   // stage 1 (:536-593): recompute-from-scratch == running sums in member order (App. B Q7)
-  // The predicate is `same && cop` with no side effects, so `cop` is evaluated only
-  // when `same` holds; voxel normal norms are computed once.  The scan for a seed
-  // visits the still-unallocated voxels in index order: they are kept as a compact
-  // SoA list (padded by 8), compacted after each seed, and the angle test runs
-  // eight of them at a time; after an accept the group's averages change, so the
-  // next block starts right after it.
-  std::vector<int> ui(nv + 8, 0);
-  std::vector<float> nx(nv + 8, 0.f), ny(nv + 8, 0.f), nz(nv + 8, 0.f);
-  std::vector<double> vn(nv + 8, 1.0), vnv(nv);
+  // The predicate is `same && cop` with no side effects, so `cop` is evaluated only when
+  // `same` holds.  A seed's scan visits the still-unallocated voxels in index order and
+  // every rejection leaves the state unchanged, so it may skip any voxel the exact angle
+  // test would reject: the scan visits only candidates, the voxels whose normals lie in
+  // direction buckets (cube-map cells, DirIndex) near the seed's normal, in index order.
+  // A voxel that passes the exact test against the group normal g lies within thr1 of g;
+  // while g stays within DRIFT of the anchor the candidates were chosen for, it lies
+  // within thr1 + DRIFT of the anchor, so its bucket is among those selected (bucket
+  // radius and rounding slack included); when g drifts further, the candidates are
+  // chosen again for the rest of the scan.  Non-finite or zero normals (NaN cosines,
+  // never rejected) are always candidates; an undefined group direction scans all.
+  std::vector<double> vnv(nv);
+  std::vector<float> ux(nv), uy(nv), uz(nv);
   for (int j = 0; j < nv; ++j) {
-    ui[j] = j;
-    nx[j] = vox[j].n[0]; ny[j] = vox[j].n[1]; nz[j] = vox[j].n[2];
-    vn[j] = vnv[j] = norm3d(vox[j].n[0], vox[j].n[1], vox[j].n[2]);
+    vnv[j] = norm3d(vox[j].n[0], vox[j].n[1], vox[j].n[2]);
+    const double r = vnv[j];
+    ux[j] = (float)(vox[j].n[0] / r); uy[j] = (float)(vox[j].n[1] / r); uz[j] = (float)(vox[j].n[2] / r);
   }
-  int nu = nv;  // unallocated voxels, ui[0..nu) ascending
+  constexpr double DRIFT = 0.1, SLACK = 5e-3;  // radians
+  const double theta1 = (double)P.normal_vector_threshold1 * (3.14159265358979323846 / 180.0);
+  DirIndex dix(ux.data(), uy.data(), uz.data(), nv, theta1 + DRIFT + SLACK);
+  const float cos_drift = (float)std::cos(DRIFT);
+  std::vector<int> cand;
   for (int i = 0; i < nv; ++i) {
     if (va[i]) continue;
     Group g;
@@ -143,46 +214,58 @@ std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& 
     g.fps = (float)vox[i].count;
     for (int a = 0; a < 3; ++a) { g.an[a] = vox[i].n[a]; g.ac[a] = vox[i].c[a]; }
     g.nan_ = vnv[i];
-    int p = 0;
-    while (p < nu) {
-      bool skip[8];
-      angle_skip8(nx.data(), ny.data(), nz.data(), vn.data(), p, g.an[0], g.an[1], g.an[2], g.nan_, cut1, skip);
-      const int pe = std::min(nu, p + 8);
-      int next = pe;
-      for (int q = p; q < pe; ++q) {
-        const int jj = ui[q];
-        if (va[jj] || skip[q - p]) continue;
-        const VoxRec& v = vox[jj];
-        if (compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]}, f3{v.n[0], v.n[1], v.n[2]},
-                          f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1, P.parameter_k1)) {
-          g.mem.push_back(jj);
-          va[jj] = 1;
-          add_member(g, v);
-          set_avg(g);
-          next = q + 1;
-          break;
-        }
-      }
-      p = next;
-    }
-    int w = 0;  // drop this seed's members from the list
-    for (int q = 0; q < nu; ++q) {
-      const int jj = ui[q];
+    g.mem.reserve(64);
+    float anc[3];
+    size_t k = 0;
+    auto choose = [&](int after) {  // candidates after index `after`, for the current g
+      const double r = g.nan_;
+      for (int a = 0; a < 3; ++a) anc[a] = (float)(g.an[a] / r);
+      dix.candidates(anc, after, va.data(), cand);
+      k = 0;
+    };
+    choose(i);
+    while (k < cand.size()) {
+      const int jj = cand[k++];
       if (va[jj]) continue;
-      ui[w] = jj; nx[w] = nx[q]; ny[w] = ny[q]; nz[w] = nz[q]; vn[w] = vn[q];
-      ++w;
+      const VoxRec& v = vox[jj];
+      if (angle_gt(normal_cos_pre(g.an[0], g.an[1], g.an[2], g.nan_, v.n[0], v.n[1], v.n[2], vnv[jj]), cut1)) continue;
+      if (compare_plane(f3{g.an[0], g.an[1], g.an[2]}, f3{g.ac[0], g.ac[1], g.ac[2]}, f3{v.n[0], v.n[1], v.n[2]},
+                        f3{v.c[0], v.c[1], v.c[2]}, P.parameter_l1, P.parameter_k1)) {
+        g.mem.push_back(jj);
+        va[jj] = 1;
+        add_member(g, v);
+        set_avg(g);
+        // drift: cos(anchor, g) >= cos(DRIFT), as anc . an >= cos(DRIFT) |an| (an of zero or
+        // non-finite length fails it: choose() then scans everything)
+        const float cd = anc[0] * g.an[0] + anc[1] * g.an[1] + anc[2] * g.an[2];
+        if (!(g.nan_ > 0.0 && cd >= cos_drift * (float)g.nan_)) choose(jj);
+      }
     }
-    nu = w;
     G.push_back(std::move(g));
   }
-  // stage 2 (:595-648): seeds never mark themselves allocated (Q6)
-  for (size_t i = 0; i < G.size(); ++i) {
+  // stage 2 (:595-648): seeds never mark themselves allocated (Q6).  The angle test is
+  // prefiltered as in stage 1: with unit group normals in float, cf = a.b is within ~1e-6
+  // of the exact cosine, so cf < cut2.gt - d and cf > -1 + d reject for sure (every
+  // other pair, NaN included, takes the exact test).  Only group i's normal changes
+  // during its sweeps.
+  const size_t ng = G.size();
+  std::vector<float> gx(ng), gy(ng), gz(ng);
+  auto unit_of = [&](size_t k) {
+    const double r = G[k].nan_;
+    gx[k] = (float)(G[k].an[0] / r); gy[k] = (float)(G[k].an[1] / r); gz[k] = (float)(G[k].an[2] / r);
+  };
+  for (size_t k = 0; k < ng; ++k) unit_of(k);
+  constexpr float PF_D = 1e-4f;
+  const float pf_hi = cut2.gt - PF_D, pf_lo = -1.0f + PF_D;
+  for (size_t i = 0; i < ng; ++i) {
     if (G[i].alloc) continue;
     bool newadd = true;
     while (newadd) {
       newadd = false;
-      for (size_t j = 0; j < G.size(); ++j) {
+      for (size_t j = 0; j < ng; ++j) {
         if (j == i || G[j].alloc) continue;
+        const float cf = gx[i] * gx[j] + gy[i] * gy[j] + gz[i] * gz[j];
+        if (cf < pf_hi && cf > pf_lo) continue;
         Group& a = G[i];
         Group& b = G[j];
         if (angle_gt(normal_cos_pre(a.an[0], a.an[1], a.an[2], a.nan_, b.an[0], b.an[1], b.an[2], b.nan_), cut2))
@@ -196,6 +279,7 @@ std::vector<GroupOut> grow_groups(const VoxRec* vox, int nv, const fccf_params& 
             add_member(a, vox[m]);
           }
           set_avg(a);
+          unit_of(i);
         }
       }
     }
