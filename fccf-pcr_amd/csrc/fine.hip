@@ -184,6 +184,89 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
   }
 }
 
+// Bitonic sort of P2 (a power of two, <= 4096) packed 64-bit keys held in registers by a
+// 1024-thread workgroup: element i lives in thread i % 1024, register slot i / 1024.
+// Compare-exchange partners i ^ jj in the same wave (jj < 64) swap by shuffles, partners
+// in other waves through LDS (xs: P2 u64, bracketed by workgroup barriers), partners in
+// the same thread (jj >= 1024) in registers: 15 of the 66 stages at 2048 keys touch LDS.
+template <int E>
+__device__ __forceinline__ void reg_bitonic(unsigned long long (&v)[E], uint32_t P2, unsigned long long* xs) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = 2; k <= P2; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      if (jj >= 1024) {
+        const uint32_t d = jj >> 10;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t rp = (uint32_t)r ^ d;
+          if ((uint32_t)r < rp && rp < (uint32_t)E) {
+            const bool asc = ((t + 1024u * r) & k) == 0;
+            const unsigned long long a = v[r], b = v[rp];
+            const bool sw = asc ? a > b : a < b;
+            v[r] = sw ? b : a;
+            v[rp] = sw ? a : b;
+          }
+        }
+      } else if (jj >= 64) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          if (i < P2) xs[i] = v[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          if (i < P2) {
+            const unsigned long long o = xs[i ^ jj];
+            const bool keep_min = ((i & k) == 0) == ((i & jj) == 0);
+            v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)v[r], (int)jj, 64);
+          const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(v[r] >> 32), (int)jj, 64);
+          const unsigned long long o = ((unsigned long long)ohi << 32) | olo;
+          const bool keep_min = ((i & k) == 0) == ((i & jj) == 0);
+          v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+        }
+      }
+    }
+  }
+}
+
+// similar_num (:830-835): the sequential float sum of the U terms in ht (float bits), by
+// one lane -- groups of 16 without per-term conditions, the next group's 16-byte LDS
+// loads issued before the current group's adds, then the tail
+__device__ __forceinline__ float seq_sum(const uint32_t* ht, uint32_t U) {
+  float s = 0.f;
+  const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(ht);
+  const uint32_t full = U & ~15u;
+  uint4 cur[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) cur[u] = t4[u];
+  for (uint32_t g = 0; g < full; g += 16) {
+    uint4 nxt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) nxt[u] = t4[((g + 16) >> 2) + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s += __uint_as_float(cur[u].x);
+      s += __uint_as_float(cur[u].y);
+      s += __uint_as_float(cur[u].z);
+      s += __uint_as_float(cur[u].w);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+  }
+  for (uint32_t g = full; g < U; ++g) s += __uint_as_float(ht[g]);
+  return s;
+}
+
 // The LDS form, one 1024-thread workgroup per evaluation e: its entries merged into an
 // LDS table (leaf code -> source, target counts; FV_LDS_SLOTS = 2 x FV_LDS_MAX slots),
 // the leaves compacted, each leaf's term (:830-835) formed, the (code, term) pairs
@@ -201,6 +284,8 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
   __shared__ uint32_t hs[FV_LDS_SLOTS];
   __shared__ __attribute__((aligned(16))) uint32_t ht[FV_LDS_SLOTS];
   __shared__ uint32_t snu, sover;
+  const bool force_net = (lds_cap >> 31) != 0u;  // (FV_LDS_NET: tests of the LDS network)
+  lds_cap &= 0x7FFFFFFFu;
   const int e = blockIdx.x;
   const uint32_t n = scal[4] + scal[5], m = ecnt[e];
   const uint64_t* __restrict__ ke = keys + (size_t)e * n;
@@ -283,10 +368,13 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
   }
   __syncthreads();
   // each leaf's term (:830-835) beside its code (in ht, as float bits), slots up to the
-  // next power of two emptied, then a bitonic sort of (code, term) over those P2 slots:
-  // the terms end in code order in [0, U)
+  // next power of two emptied, then the (code, term) pairs sorted by code over those P2
+  // slots: the terms end in code order in [0, U).  Codes of at most 32 bits (octrees up to
+  // depth 10, 512 m at 0.5 m leaves) travel packed with their term as one 64-bit key
+  // sorted in registers (reg_bitonic); deeper octrees take the LDS network.
   uint32_t P2 = 2;
   while (P2 < U) P2 <<= 1;
+  bool wide = false;
   for (uint32_t i = threadIdx.x; i < P2; i += 1024) {
     if (i < U) {
       const float sn = (float)hs[i], tn = (float)ht[i];
@@ -296,63 +384,73 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
         t = (sn + tn) * (mn / mx);
       }
       ht[i] = __float_as_uint(t);
+      wide = wide || (hk[i] >> 32) != 0ull;
     } else {
       hk[i] = FV_EMPTY;
     }
   }
-  __syncthreads();
-  // bitonic network over P2 slots, one compare-exchange per thread per 2048 slots and
-  // stage.  Pair c = (i, i | jj) with i = c with a zero bit inserted at jj: for jj < 128
-  // the pairs of wave w's indices (c = 64 w + lane, + 1024 r) stay inside slots that only
-  // wave w touches, so those stages (56 of 66 at 2048 slots) need a wave barrier only;
-  // a stage of jj >= 128 is bracketed by workgroup barriers
-  for (uint32_t k = 2; k <= P2; k <<= 1) {
-    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      if (jj >= 128) {
-        __syncthreads();
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      for (uint32_t c = threadIdx.x; c < P2 / 2; c += 1024) {
-        const uint32_t i = ((c & ~(jj - 1)) << 1) | (c & (jj - 1)), l = i | jj;
-        const unsigned long long a = hk[i], b = hk[l];
-        if (((i & k) == 0) ? a > b : a < b) {
-          hk[i] = b;
-          hk[l] = a;
-          const uint32_t t0 = ht[i];
-          ht[i] = ht[l];
-          ht[l] = t0;
+  wide = __syncthreads_or(wide || force_net ? 1 : 0) != 0;
+  if (!wide) {
+    unsigned long long v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = threadIdx.x + 1024u * r;
+      v[r] = i < U ? (hk[i] << 32) | ht[i] : ~0ull;
+    }
+    // (reg_bitonic's first LDS stage starts with a barrier: every key is loaded before
+    // hk is reused as its exchange buffer)
+    if (P2 <= 1024) {
+      unsigned long long a[1] = {v[0]};
+      reg_bitonic<1>(a, P2, hk);
+      v[0] = a[0];
+    } else if (P2 <= 2048) {
+      unsigned long long a[2] = {v[0], v[1]};
+      reg_bitonic<2>(a, P2, hk);
+      v[0] = a[0];
+      v[1] = a[1];
+    } else {
+      reg_bitonic<4>(v, P2, hk);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = threadIdx.x + 1024u * r;
+      if (i < U) ht[i] = (uint32_t)v[r];
+    }
+  } else {
+    // bitonic network over P2 slots in LDS, one compare-exchange per thread per 2048
+    // slots and stage.  Pair c = (i, i | jj) with i = c with a zero bit inserted at jj:
+    // for jj < 128 the pairs of wave w's indices (c = 64 w + lane, + 1024 r) stay inside
+    // slots that only wave w touches, so those stages need a wave barrier only; a stage
+    // of jj >= 128 is bracketed by workgroup barriers
+    for (uint32_t k = 2; k <= P2; k <<= 1) {
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        if (jj >= 128) {
+          __syncthreads();
+        } else {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        for (uint32_t c = threadIdx.x; c < P2 / 2; c += 1024) {
+          const uint32_t i = ((c & ~(jj - 1)) << 1) | (c & (jj - 1)), l = i | jj;
+          const unsigned long long a = hk[i], b = hk[l];
+          if (((i & k) == 0) ? a > b : a < b) {
+            hk[i] = b;
+            hk[l] = a;
+            const uint32_t t0 = ht[i];
+            ht[i] = ht[l];
+            ht[l] = t0;
+          }
+        }
+        if (jj >= 128) __syncthreads();
       }
-      if (jj >= 128) __syncthreads();
     }
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const uint32_t lane = threadIdx.x;
   if (lane == 0) {
-    float similar = 0.f;  // similar_num += term, leaf by leaf (a sequential float sum)
-    // groups of 16 terms read as four 16-byte loads, the next group's issued before the
-    // current one's adds (positions past U are masked)
-    const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(ht);
-    uint4 cur[4], nxt[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cur[u] = t4[u];
-    for (uint32_t g = 0; g < U; g += 16) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) nxt[u] = t4[((g + 16) >> 2) + u];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (g + 4 * u + 0 < U) similar += __uint_as_float(cur[u].x);
-        if (g + 4 * u + 1 < U) similar += __uint_as_float(cur[u].y);
-        if (g + 4 * u + 2 < U) similar += __uint_as_float(cur[u].z);
-        if (g + 4 * u + 3 < U) similar += __uint_as_float(cur[u].w);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-    }
+    const float similar = seq_sum(ht, U);  // similar_num += term, leaf by leaf
     const uint32_t p = pts[e];
     if (p >= (1u << 24)) atomicOr(&scal[7], FV_ERR_POINTS);  // float allinvec would round: unsupported size
     const float sc = similar / (float)p;
@@ -463,7 +561,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
     // after the octrees instead of ~20 (scal[7] was zeroed by k_fv_transform)
     k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, b.nseg_e);
     k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail,
-                                  std::min<uint32_t>(lds_cap, FV_LDS_MAX));
+                                  std::min<uint32_t>(lds_cap & ~FV_LDS_NET, FV_LDS_MAX) | (lds_cap & FV_LDS_NET));
     if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, mail);
     return;
   }
@@ -488,7 +586,8 @@ int fine_mode_env(int sticky_sorted) {
 uint32_t fine_lds_cap_env() {
   const char* e = std::getenv("FCCF_FINE_LDS_CAP");
   const long v = e ? std::atol(e) : (long)FV_LDS_MAX;
-  return v < 1 ? 1u : (v > (long)FV_LDS_MAX ? FV_LDS_MAX : (uint32_t)v);
+  const char* w = std::getenv("FCCF_FINE_LDS_NET");  // tests: the LDS network for every code width
+  return (v < 1 ? 1u : (v > (long)FV_LDS_MAX ? FV_LDS_MAX : (uint32_t)v)) | (w && w[0] == '1' ? FV_LDS_NET : 0u);
 }
 
 }  // namespace fccf

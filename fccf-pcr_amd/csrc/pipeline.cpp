@@ -212,8 +212,25 @@ void seg_faces(CloudWS* w, int nc, const fccf_params& P, hipStream_t st, Group* 
 // The residual cloud of the driver source is fine_verify's S1 (:788-805): its
 // octree bounds do not depend on any candidate, so they are replayed after the
 // clouds-done event, overlapping the host stages that produce the candidates.
-void seg_s1_replay(CloudWS* w, const fccf_params& P, hipStream_t st) {
-  octree_replay(w[0].resid, w[0].fb.nresid, w[0].cap, (double)P.fine_verify_voxel_size, w[0].faggr, w[0].fstate, st);
+// fine_verify's S1 octree bounds (cloud 0 of each pair) for the P pairs of a stage group
+// in one batched launch pair (block aggregates, bounds replay): pair j's cloud 0 is
+// w[2j], carved alike, so its fields sit at one byte stride from pair 0's
+void seg_s1_replay(CloudWS* w, int P, const fccf_params& Pa, hipStream_t st) {
+  SeqStrides sd;
+  if (P > 1) {
+    auto stride = [&](const void* a0, const void* a1) { return (size_t)((const char*)a1 - (const char*)a0); };
+    sd.xyz = stride(w[0].resid, w[2].resid);
+    sd.n = stride(w[0].fb.nresid, w[2].fb.nresid);
+    sd.aggr = stride(w[0].faggr, w[2].faggr);
+    sd.state = stride(w[0].fstate, w[2].fstate);
+    for (int j = 2; j < P; ++j)
+      if (stride(w[0].resid, w[2 * j].resid) != j * sd.xyz || stride(w[0].fb.nresid, w[2 * j].fb.nresid) != j * sd.n ||
+          stride(w[0].faggr, w[2 * j].faggr) != j * sd.aggr || stride(w[0].fstate, w[2 * j].fstate) != j * sd.state)
+        throw Error(FCCF_E_INTERNAL, "S1 replay: clouds not carved alike");
+  }
+  const double res = (double)Pa.fine_verify_voxel_size;
+  block_aggr(w[0].resid, w[0].fb.nresid, w[0].cap, w[0].faggr, st, P, sd, w[0].fstate);  // (also resets the states)
+  octree_sim(w[0].resid, w[0].fb.nresid, w[0].cap, res, w[0].faggr, w[0].fstate, st, P, sd);
 }
 
 // The ctx's pinned mailboxes (mail.h): allocated once, so graph-captured kernels may hold the pointer.
@@ -525,21 +542,23 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   }, vg_entry_kernel(), pargs, DG != nullptr || exact2, &lay);
   for (int j = 0; j < P; ++j) {
     auto& cs = c->cs[S0 + j];
-    PipeSet& ps = pset(c, S0 + j);
     // external signal for stage_inputs (this slot's inputs have been read): after the graph
     HIP_CHECK(hipEventRecord(cs.ev[0], st0));
     HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
-    // (keyed by the pointers the replay reads: the layout of a one-pair and a two-pair
-    // stage differ, and a replay with another layout's pointers reads a stale count)
-    struct {
-      const void *resid, *nresid, *aggr, *state;
-      uint32_t cap;
-      float res;
-    } rkey = {ps.w[0].resid, ps.w[0].fb.nresid, ps.w[0].faggr, ps.w[0].fstate, capmax, Pa.fine_verify_voxel_size};
-    static_assert(sizeof rkey == 4 * 8 + 4 + 4, "graph key without padding");
-    cs.g_rep.run(&rkey, sizeof rkey, st0, [&] { seg_s1_replay(ps.w, Pa, st0); });
-    HIP_CHECK(hipEventRecord(cs.ev[5], st0));  // S1 octree bounds (fine verification)
   }
+  // fine verification's S1 octree bounds of every pair of the group, after the clouds-done
+  // events (the host's phase B1 starts without them): one batched replay (keyed by the
+  // pointers it reads: the layouts of stages of different pair counts differ, and a
+  // replay with another layout's pointers reads a stale count)
+  struct {
+    const void *resid, *nresid, *aggr, *state;
+    uint32_t cap;
+    float res;
+    int32_t pairs, pad;
+  } rkey = {w[0].resid, w[0].fb.nresid, w[0].faggr, w[0].fstate, capmax, Pa.fine_verify_voxel_size, P, 0};
+  static_assert(sizeof rkey == 4 * 8 + 4 * 4, "graph key without padding");
+  cg.g_rep.run(&rkey, sizeof rkey, st0, [&] { seg_s1_replay(w, P, Pa, st0); });
+  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], st0));  // S1 octree bounds
   HIP_CHECK(hipGetLastError());
 }
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -26,6 +27,92 @@ constexpr int NPH = 8;
 
 __device__ __forceinline__ void stamp(unsigned long long* ph, int k) {
   if (threadIdx.x == 0) ph[blockIdx.x * NPH + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+
+// Bitonic sort of P2 (power of two, <= 4096) packed 64-bit keys held in registers:
+// element i lives in thread i % 1024, slot i / 1024.  Partners in the same wave swap by
+// shuffles, partners in other waves through LDS (xs, P2 u64), same-thread partners in
+// registers.
+template <int E>
+__device__ __forceinline__ void reg_bitonic(unsigned long long (&v)[E], uint32_t P2, unsigned long long* xs) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = 2; k <= P2; k <<= 1) {
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      if (jj >= 1024) {
+        const uint32_t d = jj >> 10;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t rp = (uint32_t)r ^ d;
+          if ((uint32_t)r < rp && rp < (uint32_t)E) {
+            const uint32_t i = t + 1024u * r;
+            const bool asc = (i & k) == 0;
+            const unsigned long long a = v[r], b = v[rp];
+            const bool sw = asc ? a > b : a < b;
+            v[r] = sw ? b : a;
+            v[rp] = sw ? a : b;
+          }
+        }
+      } else if (jj >= 64) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          if (i < P2) xs[i] = v[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          if (i < P2) {
+            const unsigned long long o = xs[i ^ jj];
+            const bool asc = (i & k) == 0, lower = (i & jj) == 0;
+            const bool keep_min = asc == lower;
+            v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t i = t + 1024u * r;
+          const uint32_t lo = (uint32_t)v[r], hi = (uint32_t)(v[r] >> 32);
+          const uint32_t olo = (uint32_t)__shfl_xor((int)lo, (int)jj, 64);
+          const uint32_t ohi = (uint32_t)__shfl_xor((int)hi, (int)jj, 64);
+          const unsigned long long o = ((unsigned long long)ohi << 32) | olo;
+          const bool asc = (i & k) == 0, lower = (i & jj) == 0;
+          const bool keep_min = asc == lower;
+          v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+        }
+      }
+    }
+  }
+}
+
+// similar_num: the sequential float sum of U terms (one lane), groups of 16 without
+// per-term conditions, the next group's loads issued before the current adds
+__device__ __forceinline__ float seq_sum(const uint32_t* ht, uint32_t U) {
+  float s = 0.f;
+  const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(ht);
+  const uint32_t full = U & ~15u;
+  uint4 cur[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) cur[u] = t4[u];
+  for (uint32_t g = 0; g < full; g += 16) {
+    uint4 nxt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) nxt[u] = t4[((g + 16) >> 2) + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s += __uint_as_float(cur[u].x);
+      s += __uint_as_float(cur[u].y);
+      s += __uint_as_float(cur[u].z);
+      s += __uint_as_float(cur[u].w);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+  }
+  for (uint32_t g = full; g < U; ++g) s += __uint_as_float(ht[g]);
+  return s;
 }
 
 // mode bit 0: skip the bitonic network (timing only); bit 1: one wave sums (no other change)
@@ -131,6 +218,41 @@ __global__ void __launch_bounds__(1024) k_eval(const uint64_t* __restrict__ keys
   }
   __syncthreads();
   stamp(ph, 4);
+  if (mode == 2) {  // packed (code << 32 | term) keys sorted in registers, then the sum
+    unsigned long long v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = threadIdx.x + 1024u * r;
+      v[r] = i < U ? (hk[i] << 32) | ht[i] : ~0ull;
+    }
+    __syncthreads();
+    unsigned long long* xs = hk;  // (the codes are in registers now)
+    if (P2 <= 1024) {
+      unsigned long long a[1] = {v[0]};
+      reg_bitonic<1>(a, P2, xs);
+      v[0] = a[0];
+    } else if (P2 <= 2048) {
+      unsigned long long a[2] = {v[0], v[1]};
+      reg_bitonic<2>(a, P2, xs);
+      v[0] = a[0];
+      v[1] = a[1];
+    } else {
+      reg_bitonic<4>(v, P2, xs);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t i = threadIdx.x + 1024u * r;
+      if (i < U) ht[i] = (uint32_t)v[r];
+    }
+    __syncthreads();
+    stamp(ph, 5);
+    if (threadIdx.x == 0) {
+      scores[e] = seq_sum(ht, U);
+      ph[blockIdx.x * NPH + 6] = __builtin_amdgcn_s_memrealtime();
+    }
+    return;
+  }
   if (!(mode & 1))
     for (uint32_t k = 2; k <= P2; k <<= 1) {
       for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
@@ -214,7 +336,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const char* names[] = {"init", "merge", "compact", "terms", "bitonic", "sum"};
-  for (int mode : {0, 1}) {
+  std::vector<float> sc0(E), sc2(E);
+  for (int mode : {0, 1, 2}) {
     for (int rep = 0; rep < 4; ++rep) {
       CK(hipMemset(dph, 0, 8 * NPH * E));
       CK(hipEventRecord(a, 0));
@@ -226,6 +349,13 @@ int main(int argc, char** argv) {
       std::vector<unsigned long long> ph(NPH * E);
       CK(hipMemcpy(ph.data(), dph, 8 * ph.size(), hipMemcpyDeviceToHost));
       if (rep < 3) continue;
+      if (mode == 0) CK(hipMemcpy(sc0.data(), ds, 4 * E, hipMemcpyDeviceToHost));
+      if (mode == 2) {
+        CK(hipMemcpy(sc2.data(), ds, 4 * E, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int q = 0; q < E; ++q) bad += std::memcmp(&sc0[q], &sc2[q], 4) != 0;
+        std::printf("mode 2 scores vs mode 0: %d of %d differ\n", bad, E);
+      }
       std::printf("mode %d (m %u, U %u, E %d): kernel %.1f us (events); per phase, us (workgroup 0 / max):", mode, m, U,
                   E, ms * 1e3);
       for (int k = 0; k < 6; ++k) {
