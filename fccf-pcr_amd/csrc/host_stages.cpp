@@ -866,6 +866,30 @@ void lm_solve(const float* pf, int P, double best[7]) {
 
 float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2, const fccf_params& P,
                    int* npairs) {
+  std::vector<float> pairs;
+  int np = 0;
+  const float score = quick_verify_pairs(T, F1, F2, P, pairs, &np);
+  if (npairs) *npairs = np;
+  if ((float)np >= P.required_optimize_plane) {
+    double b[7];
+    lm_solve(pairs.data(), np, b);
+    quick_verify_refine(T, b);
+  }
+  return score;
+}
+
+void quick_verify_refine(m44& T, const double b[7]) {
+  const m33 R = rot_from_quat(quatf{(float)b[3], (float)b[0], (float)b[1], (float)b[2]});
+  m44 dT = eye44();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) dT.m[i][j] = R.m[i][j];
+  dT.m[0][3] = (float)b[4]; dT.m[1][3] = (float)b[5]; dT.m[2][3] = (float)b[6];
+  T = mul44(dT, T);
+}
+
+float quick_verify_pairs(const m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2,
+                         const fccf_params& P, std::vector<float>& pairs, int* npairs) {
+  pairs.clear();
   int fs1 = 0, fs2 = 0;
   for (const Plane& f : F1) fs1 = (int)((float)fs1 + f.fps);
   for (const Plane& f : F2) fs2 = (int)((float)fs2 + f.fps);
@@ -875,7 +899,6 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
     c2[k] = tf_se3(T, F2[k].c[0], F2[k].c[1], F2[k].c[2]);
     n2[k] = tf_so3(T, F2[k].n[0], F2[k].n[1], F2[k].n[2]);
   }
-  std::vector<float> pairs;
   int np = 0;
   for (size_t i = 0; i < F1.size(); ++i) {
     const Plane& a = F1[i];
@@ -904,16 +927,6 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
     }
   }
   if (npairs) *npairs = np;
-  if ((float)np >= P.required_optimize_plane) {
-    double b[7];
-    lm_solve(pairs.data(), np, b);
-    const m33 R = rot_from_quat(quatf{(float)b[3], (float)b[0], (float)b[1], (float)b[2]});
-    m44 dT = eye44();
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) dT.m[i][j] = R.m[i][j];
-    dT.m[0][3] = (float)b[4]; dT.m[1][3] = (float)b[5]; dT.m[2][3] = (float)b[6];
-    T = mul44(dT, T);
-  }
   float score = 0;
   for (int k = 0; k < np; ++k) score = score + pairs[13 * k + 12];
   return score;

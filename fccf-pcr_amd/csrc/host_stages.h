@@ -70,6 +70,16 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
 
 // Ceres-1.14-style LM on plane pairs (13 floats each: p1 n1 p2 n2 w); best x = q(xyzw), t.
 void lm_solve(const float* pairs, int P, double best[7]);
+// lm_solve of n problems, `lanes` at a time, SIMD across the problems (lm_batch.cpp):
+// bit-identical to lm_solve per problem.  lanes 0: the widest the CPU runs (8 with
+// AVX-512, 4 with AVX2, else 1 = lm_solve; FCCF_LM_LANES overrides).
+void lm_solve_batch(const float* const* pairs, const int* P, int n, double (*best)[7], int lanes = 0);
+int lm_batch_lanes();
+// quick_verify split for batched LMs: the plane pairs (13 floats each) and their count
+// for T, and the score; then quick_verify_refine applies the LM result to T.
+float quick_verify_pairs(const m44& T, const std::vector<Plane>& F1, const std::vector<Plane>& F2,
+                         const fccf_params& P, std::vector<float>& pairs, int* npairs);
+void quick_verify_refine(m44& T, const double best[7]);
 
 struct High {
   QT qt;

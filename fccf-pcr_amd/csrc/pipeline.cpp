@@ -963,6 +963,40 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       r.score2 = 0.f;
       npairs[items[k].first][(size_t)items[k].second] = nps[k];
     }
+  } else if (lm_batch_lanes() > 1) {
+    // quick_verify in two parallel passes: every candidate's plane pairs and score, then
+    // the LMs of those with enough pairs in lane groups (lm_solve_batch: SIMD across the
+    // candidates, each lane bit-identical to lm_solve), about one group per pool thread
+    std::vector<std::vector<float>> qp(items.size());
+    ch.pool->parallel_for((int)items.size(), [&](int k) {
+      const int t = items[k].first, i = items[k].second;
+      TS& r = res[t][i];
+      r.T = T_from_qt(fine[t][i]);
+      r.score = quick_verify_pairs(r.T, g[0].planes, g[1].planes, P, qp[(size_t)k], &npairs[t][i]);
+      r.score2 = 0.f;
+    });
+    std::vector<int> lm;  // items whose pairs reach required_optimize_plane
+    for (size_t k = 0; k < items.size(); ++k)
+      if ((float)npairs[items[k].first][(size_t)items[k].second] >= P.required_optimize_plane) lm.push_back((int)k);
+    const int lanes = lm_batch_lanes(), nth = std::max(1, ch.pool->size());
+    const int per = std::max(1, std::min(lanes, ((int)lm.size() + nth - 1) / nth));
+    const int ngr = ((int)lm.size() + per - 1) / per;
+    ch.pool->parallel_for(ngr, [&](int gi) {
+      const int k0 = gi * per, cnt = std::min(per, (int)lm.size() - k0);
+      const float* pf[8];
+      int np[8];
+      double best[8][7];
+      for (int j = 0; j < cnt; ++j) {
+        const int k = lm[(size_t)(k0 + j)];
+        pf[j] = qp[(size_t)k].data();
+        np[j] = npairs[items[k].first][(size_t)items[k].second];
+      }
+      lm_solve_batch(pf, np, cnt, best, lanes);
+      for (int j = 0; j < cnt; ++j) {
+        const int k = lm[(size_t)(k0 + j)];
+        quick_verify_refine(res[items[k].first][(size_t)items[k].second].T, best[j]);
+      }
+    });
   } else {
     ch.pool->parallel_for((int)items.size(), [&](int k) {  // independent per candidate
       const int t = items[k].first, i = items[k].second;

@@ -302,6 +302,12 @@ int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exa
  * where |x| is beyond its argument reduction. */
 int fccf_debug_sincos(fccf_ctx* ctx, const double* x, int64_t n, double* s, double* c, uint32_t* ok);
 int fccf_debug_sort_stats(fccf_ctx* ctx, uint32_t out[32]);
+/* Test hook (host only, no ctx): quick_verify's LM (Ceres-style, FCCF.cpp:210-249) for n
+ * problems, pairs[13 * (sum of the P before i) ..] holding problem i's P[i] plane pairs
+ * (p1 n1 p2 n2 w), solved `lanes` problems at a time with SIMD across the problems
+ * (1 = the scalar form, 4 = AVX2, 8 = AVX-512; 0 = the widest the CPU runs); best:
+ * n x 7 doubles (q xyzw, t).  FCCF_E_ARG when the CPU lacks the lanes asked for. */
+int fccf_debug_lm_batch(const float* pairs, const int32_t* P, int32_t n, int32_t lanes, double* best);
 /* Test hook: the round records of the last fccf_debug_sort_keys, 24 x {segments
  * partitioned, their tiles, owned segments so far, elements partitioned}. */
 int fccf_debug_sort_rounds(fccf_ctx* ctx, uint32_t out[96]);

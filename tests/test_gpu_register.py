@@ -394,7 +394,7 @@ def test_batch_fine_overflow_registers_the_pair_again(fccf, oracle, monkeypatch,
     arena, which a later stage group may already be recycling; the pair is registered
     again after the batch's last pair instead (sorted form, sticky).  Every T bit-exact
     against the oracle, the overflowing pairs count fine_reruns = 1, and the pairs whose
-    phase B1 ran after the first overflow use the sorted form from the start."""
+    fine launch came after the first overflow was seen use the sorted form from the start."""
     monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
     monkeypatch.setenv("FCCF_FINE_LDS_CAP", "16")
     base_src, base_tar, _ = fccf.synth_pair(80_000)
@@ -409,9 +409,12 @@ def test_batch_fine_overflow_registers_the_pair_again(fccf, oracle, monkeypatch,
         Tb, sb = c.register_batch(pairs, 0.1)
         for i, (T, ref) in enumerate(zip(Tb, refs)):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"pair {i}")
+        # which pairs launch in the LDS form before the first overflow is seen depends on
+        # timing when two phase-B chains run (pipeline.cpp): at least one pair reruns,
+        # and the last pair's phase B1 follows an overflow seen by its own chain
         reruns = [int(x.fine_reruns) for x in sb]
-        assert reruns[0] == 1, reruns
-        assert set(reruns) <= {0, 1} and reruns[-1] == 0, reruns
+        assert max(reruns) == 1 and set(reruns) <= {0, 1}, reruns
+        assert reruns[-1] == 0, reruns
         Tb2, sb2 = c.register_batch(pairs, 0.1)  # sorted form from the start now
         for T, ref in zip(Tb2, refs):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
