@@ -2650,8 +2650,15 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // k_is_block: IS_OWN_BLOCKS workgroups (one per CU) split over the clouds, so both
   // clouds' items run at once and 8 CUs stay free for the small kernels of other
   // streams (matching, fine verification); profiles/r03r
+  // dev: FCCF_IS_BLOCK_GRID = block-kernel workgroups per launch, split over the clouds
+  // (default IS_OWN_BLOCKS: one per CU; its LDS leaves room for two per CU)
+  static const int block_grid = [] {
+    const char* s = std::getenv("FCCF_IS_BLOCK_GRID");
+    return s ? std::atoi(s) : 0;
+  }();
+  const int own_blocks = std::max(1, (block_grid > 0 ? block_grid : IS_OWN_BLOCKS) / nbatch);
   FCCF_LAUNCH("k_is_block", (pb_ctl(20, 16.0)), k_is_block,
-              dim3(IS_OWN_BLOCKS / nbatch, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+              dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
   // dev: FCCF_IS_WAVE_GRID = workgroups per launch, split over the clouds (default
   // IS_WAVE_BLOCKS per cloud)
