@@ -272,19 +272,23 @@ struct fccf_ctx {
     fccf::Arena arena3;              // fine verification scratch of the pair on this set
     fccf::Arena inarena;             // staged host inputs of the pair on this set (copy stream)
     hipEvent_t ev_in0 = nullptr, ev_in = nullptr;  // their copies started / done (timing: fccf_stats h2d)
-    hipEvent_t ev[8] = {};           // [0] downsample done, [2] centroids done, [3] fine verification done,
-                                     // [4] clouds done, [5] S1 replay done; [6]/[7] the centroid branch's
-                                     // fork/join inside the one-graph cloud stage (capture-internal)
+    hipEvent_t ev[8] = {};           // [0] inputs read (pass 1 done), [1] the stage's part A done (first slot
+                                     // of a group), [3] fine verification done, [4] clouds done, [5] S1
+                                     // replay done; [6]/[7] the centroid branch's fork/join inside part B
+                                     // (capture-internal)
     hipEvent_t tev[6] = {};          // timing: [4] fine start, [5] fine done (fccf_stats::dev_ms[3]);
                                      // the cloud stage's spans are device stamps (CloudMail::stamp)
-    fccf::CachedGraph g_seg[4];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs (VoxelGrid
-                                     // passes, centroids, faces), one graph per pair count
+    fccf::CachedGraph g_seg[4];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs, one graph
+                                     // per pair count: part A (the VoxelGrid passes; with a group attached,
+                                     // the whole stage)
+    fccf::CachedGraph g_segb[4];     // and part B (centroid sums beside the face voxels, orientation)
     fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
   } cs[8];                           // two stage groups of up to PAIRS_MAX pair slots (pipeline.cpp)
-  hipStream_t sa[3] = {};            // cloud stage streams (sa[1]: fine verification)
+  hipStream_t sa[4] = {};            // cloud stage streams: [0] part A, [2] part B, [3] B's centroid branch
+                                     // (a capture fork; replays schedule it), [1] fine verification
   hipStream_t sb = nullptr;          // matching, copies, stage exports
   fccf::Arena arena2;  // matching (and the stage exports)
   fccf::PinnedBuf pinned;

@@ -13,6 +13,9 @@
 //    (points of non-planar leaves, Morton then index order, :527-530).
 // Sums run over each leaf's points in ascending index, the reference's order.
 #define KT_TU 3  // ktrace.h source tag
+#include <algorithm>
+#include <cstdlib>
+
 #include "probe.h"
 #include "kernels.h"
 #include "mail.h"
@@ -684,7 +687,7 @@ void face_codes(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t cap, dou
   sd.n = byte_stride(d_n, nbatch);
   block_aggr(xyz[0], d_n[0], cap, aggr[0], st, nbatch, sd, oct[0], b[0].t_faces);  // also resets the octree states
   octree_sim(xyz[0], d_n[0], cap, res, aggr[0], oct[0], st, nbatch, sd);
-  k_oct_codes<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, d_n, B4<const OctState*>(oct), res,
+  k_oct_codes<<<dim3(grid_stream(cap, nbatch, 1024), nbatch), 256, 0, st>>>(xyz, d_n, B4<const OctState*>(oct), res,
                                                           pick(b, [](const FaceBufs& f) { return f.c0; }),
                                                           pick(b, [](const FaceBufs& f) { return f.nbits; }));
 }
@@ -725,7 +728,7 @@ void face_shard_sort(B4<const float*> xyz, uint32_t cap, B4<FaceBufs> b, hipStre
   segment_heads_u64(B4<const uint64_t*>(c1), nr, cap, pick(b, [](const FaceBufs& f) { return f.starts; }),
                     pick(b, [](const FaceBufs& f) { return f.nleaf; }), pick(b, [](const FaceBufs& f) { return f.ss; }),
                     st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
-  k_gather<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(xyz, B4<const uint32_t*>(v1), nr,
+  k_gather<<<dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st>>>(xyz, B4<const uint32_t*>(v1), nr,
                                                        pick(b, [](const FaceBufs& f) { return f.sp; }));
 }
 
@@ -743,7 +746,7 @@ void face_shard_fit(uint32_t cap, float vpt, float cthr, B4<FaceBufs> bv, hipStr
 
 // The rank's residual points into rout (already shifted to the rank's first residual point)
 void face_shard_resid(uint32_t cap, B4<FaceBufs> bv, B4<float*> rout, hipStream_t st, int nbatch) {
-  k_compact_resid<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(
+  k_compact_resid<<<dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st>>>(
       bv, pick(bv, [](const FaceBufs& f) { return (const uint32_t*)(f.nleaf + 11); }), rout);
 }
 
@@ -778,7 +781,7 @@ void face_voxels_prepare(B4<const float*> xyz, B4<const uint32_t*> d_n, uint32_t
                     st, pick(b, [](const FaceBufs& f) { return f.seg_of; }), nbatch);
   ProbeBytes pb;
   for (int e = 0; e < nbatch; ++e) pb.add(d_n[e], 28.0);
-  FCCF_LAUNCH("k_gather", (pb), k_gather, dim3(grid_for(cap), nbatch), 256, 0, st, xyz, B4<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
+  FCCF_LAUNCH("k_gather", (pb), k_gather, dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st, xyz, B4<const uint32_t*>(v0), d_n, pick(b, [](const FaceBufs& f) { return f.sp; }));
 }
 
 void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float vpt, float cthr, B4<float*> resid_out,
@@ -794,7 +797,17 @@ void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float vpt, float cth
                       pick(b, [](const FaceBufs& f) { return (const uint32_t*)f.resid_cnt; }),
                       pick(b, [](const FaceBufs& f) { return f.resid_off; }),
                       pick(b, [](const FaceBufs& f) { return f.nresid; }), nleaf, cap, ss, st, nbatch);
-  k_compact_resid<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, d_n, resid_out);
+  k_compact_resid<<<dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st>>>(b, d_n, resid_out);
+}
+
+uint32_t grid_stream(uint32_t cap, int nbatch, uint32_t per) {
+  static const int total = [] {
+    const char* e = std::getenv("FCCF_STREAM_GRID");
+    return e ? std::atoi(e) : 2048;
+  }();
+  uint32_t g = (cap + per - 1) / per;
+  const uint32_t mx = total > 0 ? std::max(64u, (uint32_t)total / (uint32_t)std::max(1, nbatch)) : 4096u;
+  return g < 1 ? 1 : (g > mx ? mx : g);
 }
 
 void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double res, float* aggr, OctState* state,
@@ -805,7 +818,7 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
 
 void face_voxels_orient(uint32_t cap, B4<VoxRec*> planar_out, B4<FaceBufs> b, hipStream_t st, int nbatch,
                         CloudMail* mail, B4<const uint32_t*> sc) {
-  k_compact_planar<<<dim3(grid_for(cap), nbatch), 256, 0, st>>>(b, planar_out, mail, sc);
+  k_compact_planar<<<dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st>>>(b, planar_out, mail, sc);
 }
 
 }  // namespace fccf

@@ -302,6 +302,12 @@ struct FvTransform {
 };
 void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
                           int batch, SeqStrides sd);
+// Grid of a streaming (grid-stride) launch over up to `cap` items per cloud, `per` items
+// per workgroup, `nbatch` clouds: about one chip-full of workgroups in all (FCCF_STREAM_GRID
+// workgroups per launch, default 2048; 0 = one workgroup per `per` items, up to 4096 per
+// cloud).  The face stage and the second VoxelGrid pass run on the downsampled clouds,
+// a third of `cap` or less, so a grid sized by `cap` is mostly workgroups with no work.
+uint32_t grid_stream(uint32_t cap, int nbatch, uint32_t per = 256);
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate
 constexpr uint32_t AGGR_SUB = 64;      // points per sub-aggregate (64 per block)
 // aggregates of one sequence: aggr_blocks(cap) block records, then 64 sub-records per

@@ -406,7 +406,23 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   auto& cg = c->cs[S0];          // the group's arena, stage graphs and fork/join events
   PipeSet& gs = pset(c, S0);
   const int nc = 2 * P;
-  hipStream_t st0 = c->sa[0], ss = c->sa[2];
+  // Split form (dev, FCCF_STAGE_SPLIT=1): the stage in two graphs, A the VoxelGrid passes
+  // (the sort) on sa[0] and B the centroid sums beside the face voxels, then the
+  // orientation, on sa[2], so that a next group's A queued on sa[0] can overlap this
+  // group's B.  B's centroid branch is forked onto sa[3]
+  // inside its capture (a replay schedules the branches itself).  With a group attached
+  // (collectives in the stage) everything stays on sa[0], as one chain.
+  hipStream_t st0 = c->sa[0];
+  // Measured slower in the pipelined batch (0.805-0.812 against 0.757-0.784 ms per
+  // registration, interleaved, with the next stage enqueued early): the
+  // overlapping face part stretches the phase-B chains' matching and fine kernels.  Off
+  // by default; FCCF_STAGE_SPLIT=1 (dev) turns it on.
+  static const bool split_env = [] {
+    const char* e = std::getenv("FCCF_STAGE_SPLIT");
+    return e && e[0] == '1';
+  }();
+  const bool split = split_env && !c->group;
+  hipStream_t sB = split ? c->sa[2] : st0, ss = split ? c->sa[3] : c->sa[2];
   // both clouds get the larger capacity (all clouds of a stage, in fact), so their
   // workspaces are laid out alike (batched launches address cloud e at a fixed offset)
   uint32_t capmax = 1;
@@ -415,6 +431,9 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   // the previous pairs on these slots may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for them
   for (int j = 0; j < PAIRS_MAX; ++j) guarded_stream_wait(st0, c->cs[S0 + j].ev[3]);  // (recorded on the fine stream)
+  // and the previous stage on these slots has finished its B part (the S1 replay is its
+  // last launch; B runs on another stream than this stage's A)
+  if (split) guarded_stream_wait(st0, cg.ev[5]);
   // (the centroid scratch is carved for BMAX clouds whatever the pair count, so slot
   // j's clouds sit at the same addresses in every stage form, and the per-slot graphs
   // keyed by those addresses -- the S1 replay, fine verification -- keep replaying when
@@ -521,10 +540,8 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     wrong.bind();
     pargs = wrong.args;
   }
-  cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
-    seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
-    seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
-    HIP_CHECK(hipEventRecord(cg.ev[6], st0));
+  auto part_b = [&] {
+    HIP_CHECK(hipEventRecord(cg.ev[6], sB));
     HIP_CHECK(hipStreamWaitEvent(ss, cg.ev[6], 0));
     const float* d2[BMAX];
     const uint32_t* n2[BMAX];
@@ -534,18 +551,28 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     }
     exact_sum_n(d2, n2, nc, 3, 3, cen, true, xs, ss);  // compute3DCentroid (:473)
     HIP_CHECK(hipEventRecord(cg.ev[7], ss));
-    seg_faces(w, nc, Pa, st0, PG, key.face_bits);
-    HIP_CHECK(hipStreamWaitEvent(st0, cg.ev[7], 0));
+    seg_faces(w, nc, Pa, sB, PG, key.face_bits);
+    HIP_CHECK(hipStreamWaitEvent(sB, cg.ev[7], 0));
     face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
-                       all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), st0, nc, cmail,
+                       all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), sB, nc, cmail,
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
-  }, vg_entry_kernel(), pargs, DG != nullptr || exact2, &lay);
+  };
+  const bool eager = DG != nullptr || exact2;
+  cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
+    seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
+    seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
+    if (!split) part_b();
+  }, vg_entry_kernel(), pargs, eager, &lay);
   for (int j = 0; j < P; ++j) {
-    auto& cs = c->cs[S0 + j];
-    // external signal for stage_inputs (this slot's inputs have been read): after the graph
-    HIP_CHECK(hipEventRecord(cs.ev[0], st0));
-    HIP_CHECK(hipEventRecord(cs.ev[4], st0));  // clouds done
+    // external signal for stage_inputs (this slot's inputs have been read): after pass 1
+    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[0], st0));
   }
+  if (split) {
+    HIP_CHECK(hipEventRecord(cg.ev[1], st0));  // the VoxelGrid passes done: B may start
+    HIP_CHECK(hipStreamWaitEvent(sB, cg.ev[1], 0));  // (sB is captured by this thread only)
+    cg.g_segb[P - 1].run(&key, sizeof key, sB, part_b, nullptr, nullptr, eager);
+  }
+  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[4], sB));  // clouds done
   // fine verification's S1 octree bounds of every pair of the group, after the clouds-done
   // events (the host's phase B1 starts without them): one batched replay (keyed by the
   // pointers it reads: the layouts of stages of different pair counts differ, and a
@@ -557,8 +584,8 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     int32_t pairs, pad;
   } rkey = {w[0].resid, w[0].fb.nresid, w[0].faggr, w[0].fstate, capmax, Pa.fine_verify_voxel_size, P, 0};
   static_assert(sizeof rkey == 4 * 8 + 4 * 4, "graph key without padding");
-  cg.g_rep.run(&rkey, sizeof rkey, st0, [&] { seg_s1_replay(w, P, Pa, st0); });
-  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], st0));  // S1 octree bounds
+  cg.g_rep.run(&rkey, sizeof rkey, sB, [&] { seg_s1_replay(w, P, Pa, sB); });
+  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], sB));  // S1 octree bounds
   HIP_CHECK(hipGetLastError());
 }
 
@@ -963,10 +990,15 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       r.score2 = 0.f;
       npairs[items[k].first][(size_t)items[k].second] = nps[k];
     }
-  } else if (lm_batch_lanes() > 1) {
-    // quick_verify in two parallel passes: every candidate's plane pairs and score, then
-    // the LMs of those with enough pairs in lane groups (lm_solve_batch: SIMD across the
-    // candidates, each lane bit-identical to lm_solve), about one group per pool thread
+  } else {
+    // quick_verify (:680-783) in two parallel passes: every candidate's plane pairs and
+    // its score, then the LMs.  The score is the pairs' importance sum under the
+    // candidate's own T, before its LM (:778-782), and score_range (:1233-1251) ranks by
+    // score alone; only the first analyse_max of each type are used afterwards (fine
+    // verification and fusion, :1496-1606), so only their LM results can reach the
+    // output: the LM runs for those (<= 3 x fine_verify_number), with T bit-identical
+    // to refining every candidate.  A debug ctx refines every candidate (its qv0-2
+    // intermediates hold every T).
     std::vector<std::vector<float>> qp(items.size());
     ch.pool->parallel_for((int)items.size(), [&](int k) {
       const int t = items[k].first, i = items[k].second;
@@ -975,11 +1007,30 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       r.score = quick_verify_pairs(r.T, g[0].planes, g[1].planes, P, qp[(size_t)k], &npairs[t][i]);
       r.score2 = 0.f;
     });
-    std::vector<int> lm;  // items whose pairs reach required_optimize_plane
+    std::vector<char> used(items.size(), c->debug ? 1 : 0);
+    if (!c->debug) {
+      size_t k0 = 0;  // items are type-major
+      for (int t = 0; t < 3; ++t) {
+        const size_t nt = fine[t].size();
+        std::vector<int> ord(nt);
+        for (size_t i = 0; i < nt; ++i) ord[i] = (int)i;
+        for (size_t i = 0; i + 1 < nt && (int)i < analyse_max; ++i)  // score_range's exchange sort
+          for (size_t j = i + 1; j < nt; ++j)
+            if (res[t][(size_t)ord[i]].score < res[t][(size_t)ord[j]].score) std::swap(ord[i], ord[j]);
+        for (size_t i = 0; i < nt && (int)i < analyse_max; ++i) used[k0 + (size_t)ord[i]] = 1;
+        k0 += nt;
+      }
+    }
+    std::vector<int> lm;  // candidates whose pairs reach required_optimize_plane and whose T is used
     for (size_t k = 0; k < items.size(); ++k)
-      if ((float)npairs[items[k].first][(size_t)items[k].second] >= P.required_optimize_plane) lm.push_back((int)k);
-    const int lanes = lm_batch_lanes(), nth = std::max(1, ch.pool->size());
-    const int per = std::max(1, std::min(lanes, ((int)lm.size() + nth - 1) / nth));
+      if (used[k] && (float)npairs[items[k].first][(size_t)items[k].second] >= P.required_optimize_plane)
+        lm.push_back((int)k);
+    // a thread per LM while the pool has threads for all of them; more LMs than threads:
+    // lane groups (lm_solve_batch: SIMD across candidates, each lane bit-identical to
+    // lm_solve), about one group per thread
+    const int nth = std::max(1, ch.pool->size());
+    const int lanes = (int)lm.size() > nth ? lm_batch_lanes() : 1;
+    const int per = lanes > 1 ? std::max(1, std::min(lanes, ((int)lm.size() + nth - 1) / nth)) : 1;
     const int ngr = ((int)lm.size() + per - 1) / per;
     ch.pool->parallel_for(ngr, [&](int gi) {
       const int k0 = gi * per, cnt = std::min(per, (int)lm.size() - k0);
@@ -996,14 +1047,6 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
         const int k = lm[(size_t)(k0 + j)];
         quick_verify_refine(res[items[k].first][(size_t)items[k].second].T, best[j]);
       }
-    });
-  } else {
-    ch.pool->parallel_for((int)items.size(), [&](int k) {  // independent per candidate
-      const int t = items[k].first, i = items[k].second;
-      TS& r = res[t][i];
-      r.T = T_from_qt(fine[t][i]);
-      r.score = quick_verify(r.T, g[0].planes, g[1].planes, P, &npairs[t][i]);
-      r.score2 = 0.f;
     });
   }
   for (int t = 0; t < 3; ++t) {
@@ -1247,6 +1290,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   }
   S.graph_captures = c->cs[s].g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
+  for (auto& g : c->cs[s].g_segb) S.graph_captures += g.captures;
   S.graph_captures += c->cs[s].g_rep.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
@@ -1267,6 +1311,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
 void reset_capture_counts(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.captures = 0;
+    for (auto& g : cs.g_segb) g.captures = 0;
     cs.g_rep.captures = 0;
     cs.g_fine.captures = 0;
   }

@@ -400,7 +400,7 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
   const B4<uint32_t*> k1 = F([](const VGBufs& v) { return v.k1; }), v1 = F([](const VGBufs& v) { return v.v1; });
   const B4<uint32_t*> starts = F([](const VGBufs& v) { return v.starts; }), nseg = F([](const VGBufs& v) { return v.nseg; });
   const B4<SortScratch> ss = F([](const VGBufs& v) { return v.ss; });
-  const dim3 g(grid_for(cap), nbatch);
+
   VGEntry en;
   en.xyz = xyz;
   en.d_n = d_nw;
@@ -453,7 +453,7 @@ void voxel_grid(B4<const float*> xyz, B4<uint32_t*> d_nw, uint32_t cap, float le
                       nbatch, unsorted);
   }
   const B4<const uint32_t*> inj = F([](const VGBufs& v) { return v.is.inject; });
-  FCCF_LAUNCH("k_vg_centroid", (pb_cen), k_vg_centroid, g, 256, 0, st, d_n, P, B4<const uint32_t*>(v0), B4<const uint32_t*>(starts), B4<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
+  FCCF_LAUNCH("k_vg_centroid", (pb_cen), k_vg_centroid, dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st, d_n, P, B4<const uint32_t*>(v0), B4<const uint32_t*>(starts), B4<const uint32_t*>(nseg), out, d_m, presorted, out_copy, inj, xyzs);
 }
 
 }  // namespace fccf
