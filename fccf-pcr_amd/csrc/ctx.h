@@ -13,6 +13,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fccf.h"
@@ -120,6 +121,38 @@ inline hipError_t device_sync_guarded() {
 inline void guarded_stream_wait(hipStream_t st, hipEvent_t ev) {
   std::lock_guard<std::mutex> lk(capture_mutex());
   HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
+}
+
+// A host wait on a pinned mailbox flag that a stage's last kernel sets after a
+// system-scope fence (mail.h): polled for up to spin_us.  The runtime's event wait
+// polls only briefly and then sleeps on an interrupt, and the thread woke 18-35 us
+// after a ~1 ms cloud stage or a ~0.1 ms fine verification had ended (hipEventQuery
+// polling did not shorten it; profiles/r05k, r05l).  Returns false when the flag was
+// not seen in time (or FCCF_SPIN_US=0): the caller then waits on the stage's event.
+// keep (optional) runs about every 200 us of polling: the caller keeps its pool's
+// workers spinning for the parallel work that follows the wait.
+template <class Keep = void (*)()>
+inline bool mail_wait(const uint32_t* flag, double spin_us, Keep keep = nullptr) {
+  static const double env = [] {
+    const char* v = std::getenv("FCCF_SPIN_US");
+    return v && *v ? std::atof(v) : -1.0;
+  }();
+  if (env >= 0.0) spin_us = env;
+  if (spin_us <= 0.0) return false;
+  const auto t0 = std::chrono::steady_clock::now();
+  double next_keep = 200.0;
+  for (uint32_t it = 0;; ++it) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != 0u) return true;
+    if ((it & 63u) == 63u) {
+      const double el = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (el > spin_us) return false;
+      if (el > next_keep) {
+        if constexpr (!std::is_pointer<Keep>::value) keep();
+        next_keep = el + 200.0;
+      }
+    }
+    for (int i = 0; i < 8; ++i) __builtin_ia32_pause();
+  }
 }
 
 // The arguments of a patched kernel node that describe the workspace layout (every

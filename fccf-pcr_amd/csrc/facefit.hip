@@ -514,6 +514,15 @@ __global__ void __launch_bounds__(256) k_compact_planar(B4<FaceBufs> fb, B4<VoxR
   }
 }
 
+// The stage's mailboxes are complete: every record and count was written by the
+// kernels before this one on the stream; the flag follows them to host memory after a
+// system-scope fence, and phase B1 polls it instead of sleeping in an event wait.
+__global__ void k_mail_done(CloudMail* __restrict__ mail, int npairs) {
+  KT();
+  __threadfence_system();
+  if ((int)threadIdx.x < npairs) __hip_atomic_store(&mail[threadIdx.x].done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
   uint32_t g = (cap + per - 1) / per;
@@ -531,9 +540,9 @@ void block_aggr(const float* xyz, const uint32_t* d_n, uint32_t cap, float* aggr
 }
 
 void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
-                          int batch, SeqStrides sd) {
+                          int batch, SeqStrides sd, uint64_t* stamp) {
   const uint32_t nb = (cap + AGGR_BLOCK - 1) / AGGR_BLOCK;
-  k_block_aggr<true><<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(tf.s2, d_n, aggr, sd, aggr_blocks(cap), nullptr, nullptr,
+  k_block_aggr<true><<<dim3(nb ? nb : 1, batch), 256, 0, st>>>(tf.s2, d_n, aggr, sd, aggr_blocks(cap), nullptr, stamp,
                                                                tf);
 }
 
@@ -819,6 +828,7 @@ void octree_replay(const float* xyz, const uint32_t* d_n, uint32_t cap, double r
 void face_voxels_orient(uint32_t cap, B4<VoxRec*> planar_out, B4<FaceBufs> b, hipStream_t st, int nbatch,
                         CloudMail* mail, B4<const uint32_t*> sc) {
   k_compact_planar<<<dim3(grid_stream(cap, nbatch), nbatch), 256, 0, st>>>(b, planar_out, mail, sc);
+  if (mail) k_mail_done<<<1, 64, 0, st>>>(mail, (nbatch + 1) / 2);
 }
 
 }  // namespace fccf

@@ -515,12 +515,28 @@ __global__ void k_fv_score(const float* __restrict__ similar, const float* __res
     if (mail) mail->scores[e] = sc;
   }
   if (mail && e == 0) mail->err = scal[7];
+  if (mail) {  // the mailbox is complete: its flag after a system-scope fence (phase B2 polls it)
+    __syncthreads();
+    if (e == 0) {
+      __threadfence_system();
+      __hip_atomic_store(&mail->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
-// the LDS form's error word into the mailbox (k_fv_score writes it in the sorted form)
-__global__ void k_fv_mail_err(const uint32_t* __restrict__ scal, FineMail* __restrict__ mail) {
+// the LDS form's scores (again: this kernel's own writes then precede the flag) and
+// error word into the mailbox, then its flag (k_fv_score does this in the sorted form)
+__global__ void k_fv_mail_err(const uint32_t* __restrict__ scal, const float* __restrict__ scores, int E,
+                              FineMail* __restrict__ mail) {
   KT();
+  if (threadIdx.x == 0) mail->stamp[1] = __builtin_amdgcn_s_memrealtime();
+  if ((int)threadIdx.x < E) mail->scores[threadIdx.x] = scores[threadIdx.x];
   if (threadIdx.x == 0) mail->err = scal[7];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&mail->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 inline uint32_t grid_for(uint32_t cap, uint32_t per = 256, uint32_t mx = 4096) {
@@ -552,7 +568,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
     block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
   } else {
     FvTransform tf{s2, b.T, b.s2t, s1_state, b.state, b.scal, b.nseg_e, b.pts, n1, n2};
-    block_aggr_transform(tf, d_n2, n2, b.aggr2, st, E, sd);
+    block_aggr_transform(tf, d_n2, n2, b.aggr2, st, E, sd, mail ? &mail->stamp[0] : nullptr);
   }
   octree_sim(b.s2t, d_n2, n2, res, b.aggr2, b.state, st, E, sd);
   const dim3 ge(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E);
@@ -562,7 +578,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
     k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, b.nseg_e);
     k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail,
                                   std::min<uint32_t>(lds_cap & ~FV_LDS_NET, FV_LDS_MAX) | (lds_cap & FV_LDS_NET));
-    if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, mail);
+    if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, b.scores, E, mail);
     return;
   }
   k_fv_bits<<<1, 64, 0, st>>>(b.state, b.scal, b.range, b.pts, n1, n2, E);

@@ -301,7 +301,7 @@ struct FvTransform {
   uint32_t n1, n2;  // (n2 also written to scal[5], the later launches' device count)
 };
 void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
-                          int batch, SeqStrides sd);
+                          int batch, SeqStrides sd, uint64_t* stamp = nullptr);
 // Grid of a streaming (grid-stride) launch over up to `cap` items per cloud, `per` items
 // per workgroup, `nbatch` clouds: about one chip-full of workgroups in all (FCCF_STREAM_GRID
 // workgroups per launch, default 2048; 0 = one workgroup per `per` items, up to 4096 per

@@ -20,6 +20,9 @@ struct CloudMail {                     // one per pair slot (fccf_ctx::cs)
                                        // planar leaves, residual points
   uint64_t stamp[4];                   // s_memrealtime (100 MHz) when main's pass, the driver's pass,
                                        // the face stage and its last kernel started (fccf_stats dev_ms)
+  uint32_t done;                       // 1 once the stage's records and counts are in this mailbox
+                                       // (k_mail_done; the host clears it before the stage's launch)
+  uint32_t pad_[3];
   VoxRec rec[2][REC_CAP];              // oriented planar records, Morton order
 };
 
@@ -46,6 +49,9 @@ struct FineMail {
   m44 T[MAX_EVAL];                     // host staging of the evaluated transforms (H2D source)
   float scores[MAX_EVAL];
   uint32_t err;                        // fine_verify scal[7]
+  uint32_t done;                       // 1 once scores and err are here (cleared before the launch)
+  uint32_t pad_;
+  uint64_t stamp[2];                   // s_memrealtime: the launch's first and last kernels started
 };
 
 struct HostMail {

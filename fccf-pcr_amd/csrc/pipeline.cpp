@@ -557,6 +557,7 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
                        all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), sB, nc, cmail,
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
   };
+  for (int j = 0; j < P; ++j) __atomic_store_n(&cmail[j].done, 0u, __ATOMIC_RELAXED);  // (set by k_mail_done)
   const bool eager = DG != nullptr || exact2;
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
@@ -640,8 +641,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     // (under the capture lock: with several pairs per stage, a later pair's B1 runs while
     // the helper thread may be capturing the next stage on the stream ev[4] was recorded
     // on, and HIP refuses to synchronize such an event; ev[4] is complete by then)
-    std::lock_guard<std::mutex> lk(capture_mutex());
-    HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+    if (!mail_wait(&cm.done, 5000.0, [&] { ch.pool->warm(400); })) {
+      std::lock_guard<std::mutex> lk(capture_mutex());
+      HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+    }
   }
   uint32_t sc[2][4], fsc[2][4];
   std::memcpy(sc, cm.sc, sizeof sc);
@@ -688,7 +691,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     S.ms[FCCF_T_DOWNSAMPLE] = d[0] + d[1];
     S.ms[FCCF_T_VOXELFIT] = d[2];
     float h = 0.f;  // the staged host inputs' copy (complete before pass 1 started)
-    if (ps.staged) HIP_CHECK(hipEventElapsedTime(&h, c->cs[s].ev_in0, c->cs[s].ev_in));
+    if (ps.staged) {  // (the mailbox flag does not make the runtime see ev_in complete)
+      HIP_CHECK(hipEventSynchronize(c->cs[s].ev_in));
+      HIP_CHECK(hipEventElapsedTime(&h, c->cs[s].ev_in0, c->cs[s].ev_in));
+    }
     S.ms[FCCF_T_H2D] = h;
   }
   S.m1_tar = sc[0][1];
@@ -1007,6 +1013,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
       r.score = quick_verify_pairs(r.T, g[0].planes, g[1].planes, P, qp[(size_t)k], &npairs[t][i]);
       r.score2 = 0.f;
     });
+    ht.mark("vpairs");
     std::vector<char> used(items.size(), c->debug ? 1 : 0);
     if (!c->debug) {
       size_t k0 = 0;  // items are type-major
@@ -1129,6 +1136,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
                                (uint32_t)std::max<size_t>(nk, 1));
     fb.xs = exact_sum_carve(a3.take(exact_sum_bytes(E, n1 + n2)), E, n1 + n2);
     FineMail& fm = host_mail(c)->fine[s];
+    __atomic_store_n(&fm.done, 0u, __ATOMIC_RELAXED);  // (set by the launch's last kernel)
+    fm.stamp[0] = fm.stamp[1] = 0;
     std::memcpy(fm.T, evals.data() + flo, sizeof(m44) * E);  // pinned staging: async H2D
     HIP_CHECK(hipMemcpyAsync(fb.T, fm.T, sizeof(m44) * E, hipMemcpyHostToDevice, sf));
     // the leaf form: LDS per evaluation unless the ctx met an evaluation with more leaves
@@ -1203,7 +1212,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
     // (ev[3]'s stream is captured only by this thread) scores and the error word are in
     // the mailbox; with a group the fine stream holds the score gather: a bounded wait
     if (c->group) group_wait_event(c->group, c->cs[s].ev[3]);
-    else HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));
+    else if (!mail_wait(&host_mail(c)->fine[s].done, 3000.0)) HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));
     uint32_t err = 0;
     if (c->group && c->group->n > 1) {  // every rank's block, gathered in rank order
       group_fine_scores(c->group, s, E, scores.data(), &err);
@@ -1231,8 +1240,16 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
     }
     if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
     if (pb.E_loc > 0) {
+      // the device span from the launch's own stamps (100 MHz) when both were written
+      // (the LDS form without a rerun), else from the timing events around the launch
+      const FineMail& fm = host_mail(c)->fine[s];
       float d = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
+      if (!c->group && fm.stamp[0] && fm.stamp[1] >= fm.stamp[0]) {
+        d = (float)((double)(fm.stamp[1] - fm.stamp[0]) * 1e-5);
+      } else {
+        HIP_CHECK(hipEventSynchronize(c->cs[s].tev[5]));
+        HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
+      }
       S.dev_ms[3] = d;
     }
   }

@@ -117,7 +117,8 @@ def report(trace_dir, host_log, out=None):
             out_lines.append(f"{'  fine verification (device)':34s} {fine[0]:8.1f} {fine[1]:8.1f} {fine[1] - fine[0]:8.1f}")
         label = {"clouds": "host wakes (clouds done)", "next_enq": "host: next-pair enqueue (batch only)",
                  "grow": "host: region growing", "match": "host+device: matching", "cluster": "host: clustering",
-                 "verify": "host: quick_verify + LM", "fine_setup": "host: fine setup",
+                 "vpairs": "host: quick_verify pairs + scores",
+                 "verify": "host: LM (top per type)", "fine_setup": "host: fine setup",
                  "fine_launched": "host: fine launch", "fine": "host wakes (fine scores)"}.get(k, k)
         out_lines.append(f"{label:34s} {host_prev:8.1f} {v:8.1f} {v - host_prev:8.1f}")
         host_prev = v
