@@ -184,61 +184,6 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
   }
 }
 
-// Bitonic sort of P2 (a power of two, <= 4096) packed 64-bit keys held in registers by a
-// 1024-thread workgroup: element i lives in thread i % 1024, register slot i / 1024.
-// Compare-exchange partners i ^ jj in the same wave (jj < 64) swap by shuffles, partners
-// in other waves through LDS (xs: P2 u64, bracketed by workgroup barriers), partners in
-// the same thread (jj >= 1024) in registers: 15 of the 66 stages at 2048 keys touch LDS.
-template <int E>
-__device__ __forceinline__ void reg_bitonic(unsigned long long (&v)[E], uint32_t P2, unsigned long long* xs) {
-  const uint32_t t = threadIdx.x;
-  for (uint32_t k = 2; k <= P2; k <<= 1) {
-    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-      if (jj >= 1024) {
-        const uint32_t d = jj >> 10;
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          const uint32_t rp = (uint32_t)r ^ d;
-          if ((uint32_t)r < rp && rp < (uint32_t)E) {
-            const bool asc = ((t + 1024u * r) & k) == 0;
-            const unsigned long long a = v[r], b = v[rp];
-            const bool sw = asc ? a > b : a < b;
-            v[r] = sw ? b : a;
-            v[rp] = sw ? a : b;
-          }
-        }
-      } else if (jj >= 64) {
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          const uint32_t i = t + 1024u * r;
-          if (i < P2) xs[i] = v[r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          const uint32_t i = t + 1024u * r;
-          if (i < P2) {
-            const unsigned long long o = xs[i ^ jj];
-            const bool keep_min = ((i & k) == 0) == ((i & jj) == 0);
-            v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          const uint32_t i = t + 1024u * r;
-          const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)v[r], (int)jj, 64);
-          const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(v[r] >> 32), (int)jj, 64);
-          const unsigned long long o = ((unsigned long long)ohi << 32) | olo;
-          const bool keep_min = ((i & k) == 0) == ((i & jj) == 0);
-          v[r] = keep_min ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
-        }
-      }
-    }
-  }
-}
-
 // similar_num (:830-835): the sequential float sum of the U terms in ht (float bits), by
 // one lane -- groups of 16 without per-term conditions, the next group's 16-byte LDS
 // loads issued before the current group's adds, then the tail
@@ -269,24 +214,29 @@ __device__ __forceinline__ float seq_sum(const uint32_t* ht, uint32_t U) {
 
 // The LDS form, one 1024-thread workgroup per evaluation e: its entries merged into an
 // LDS table (leaf code -> source, target counts; FV_LDS_SLOTS = 2 x FV_LDS_MAX slots),
-// the leaves compacted, each leaf's term (:830-835) formed, the (code, term) pairs
-// sorted by code (bitonic over the next power of two above the leaf count, ~1400 at
-// c2-c5), and the terms summed in that order by one lane -- the reference's sequential
-// similar_num -- then score = similar_num / allinvec.  More than lds_cap
-// leaves: FV_ERR_LDS, no score (the caller reruns in the sorted form).
+// each leaf's term (:830-835) formed, the nonzero terms placed in code order by rank
+// (c3: ~1700 leaves, ~900 nonzero terms per evaluation), and summed in that order by
+// one lane -- the reference's sequential similar_num -- then score = similar_num /
+// allinvec.  More than lds_cap leaves: FV_ERR_LDS, no score (the caller reruns in the
+// sorted form).
 constexpr uint32_t FV_LDS_SLOTS = 2 * FV_LDS_MAX;
 __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                   const uint32_t* __restrict__ ecnt, const uint32_t* __restrict__ pts,
                                                   uint32_t* __restrict__ scal, float* __restrict__ scores,
                                                   FineMail* __restrict__ mail, uint32_t lds_cap) {
   KT();
-  __shared__ unsigned long long hk[FV_LDS_SLOTS];
-  __shared__ uint32_t hs[FV_LDS_SLOTS];
-  __shared__ __attribute__((aligned(16))) uint32_t ht[FV_LDS_SLOTS];
-  __shared__ uint32_t snu, sover;
-  const bool force_net = (lds_cap >> 31) != 0u;  // (FV_LDS_NET: tests of the LDS network)
-  lds_cap &= 0x7FFFFFFFu;
+  __shared__ __attribute__((aligned(16))) unsigned long long hk[FV_LDS_SLOTS];
+  __shared__ __attribute__((aligned(16))) uint32_t hs[FV_LDS_SLOTS];
+  __shared__ uint32_t ht[FV_LDS_SLOTS];
+  __shared__ uint32_t snu, snz, sover;
   const int e = blockIdx.x;
+#ifdef FV_PHASES
+  unsigned long long fvt[8];  // dev (make VAR=fvph EXTRA=-DFV_PHASES): thread 0's phase stamps, printed for e = 0
+#define FV_PH(k) do { if (threadIdx.x == 0) fvt[k] = __builtin_amdgcn_s_memtime(); } while (0)
+  FV_PH(0);
+#else
+#define FV_PH(k) do {} while (0)
+#endif
   const uint32_t n = scal[4] + scal[5], m = ecnt[e];
   const uint64_t* __restrict__ ke = keys + (size_t)e * n;
   const uint32_t* __restrict__ ve = vals + (size_t)e * n;
@@ -297,9 +247,11 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
   }
   if (threadIdx.x == 0) {
     snu = 0u;
+    snz = 0u;
     sover = 0u;
   }
   __syncthreads();
+  FV_PH(1);
   for (uint32_t j = threadIdx.x; j < m; j += 1024) {
     const unsigned long long key = ke[j];
     const uint32_t c = ve[j];
@@ -326,136 +278,108 @@ __global__ void __launch_bounds__(1024) k_fv_eval(const uint64_t* __restrict__ k
     atomicAdd(&ht[h], c >> 16);
   }
   __syncthreads();
+  FV_PH(2);
   if (sover) {  // (uniform) more leaves than the LDS form takes
     if (threadIdx.x == 0) atomicOr(&scal[7], FV_ERR_LDS);  // (k_fv_mail_err copies the word to the mailbox)
     return;
   }
-  // the U occupied slots compacted to [0, U) in place (every thread reads its slots
-  // before the barrier, then writes)
-  const uint32_t U = snu;
+  // Each occupied leaf's term (:830-835).  Only the leaves with both counts >= 1 have a
+  // nonzero term; the others add +0.0f to a sum that is never -0, which leaves it
+  // unchanged, so only the Z nonzero terms are ordered and summed.  They are appended
+  // in any order as (code, term) to the front of hk / ht (every thread reads its slots
+  // before the barrier, then writes), and each one's place in code order is its rank:
+  // the number of smaller codes among the Z (codes are distinct, one slot per leaf),
+  // found by sorted 64-pair chunks and binary searches.
   {
     constexpr uint32_t PER = FV_LDS_SLOTS / 1024;
     unsigned long long k8[PER];
-    uint32_t s8[PER], t8[PER], occ = 0;
+    uint32_t s8[PER], t8[PER];
 #pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-      const uint32_t j = threadIdx.x * PER + q;
+    for (uint32_t q = 0; q < PER; ++q) {  // (all loads first: an empty slot has counts 0)
+      const uint32_t j = q * 1024 + threadIdx.x;  // (consecutive lanes, consecutive slots)
       k8[q] = hk[j];
       s8[q] = hs[j];
       t8[q] = ht[j];
-      occ += k8[q] != FV_EMPTY ? 1u : 0u;
     }
-    __shared__ uint32_t wsum[16];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t x = occ;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t pos = x - occ;
-    for (uint32_t w = 0; w < wave; ++w) pos += wsum[w];
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q)
-      if (k8[q] != FV_EMPTY) {
-        hk[pos] = k8[q];
-        hs[pos] = s8[q];
-        ht[pos] = t8[q];
-        ++pos;
-      }
-  }
-  __syncthreads();
-  // each leaf's term (:830-835) beside its code (in ht, as float bits), slots up to the
-  // next power of two emptied, then the (code, term) pairs sorted by code over those P2
-  // slots: the terms end in code order in [0, U).  Codes of at most 32 bits (octrees up to
-  // depth 10, 512 m at 0.5 m leaves) travel packed with their term as one 64-bit key
-  // sorted in registers (reg_bitonic); deeper octrees take the LDS network.
-  uint32_t P2 = 2;
-  while (P2 < U) P2 <<= 1;
-  bool wide = false;
-  for (uint32_t i = threadIdx.x; i < P2; i += 1024) {
-    if (i < U) {
-      const float sn = (float)hs[i], tn = (float)ht[i];
-      float t = 0.f;
+    for (uint32_t q = 0; q < PER; ++q) {
+      const float sn = (float)s8[q], tn = (float)t8[q];
+      t8[q] = 0u;
       if (sn >= 1.f && tn >= 1.f) {
         const float mn = sn < tn ? sn : tn, mx = sn > tn ? sn : tn;
-        t = (sn + tn) * (mn / mx);
-      }
-      ht[i] = __float_as_uint(t);
-      wide = wide || (hk[i] >> 32) != 0ull;
-    } else {
-      hk[i] = FV_EMPTY;
-    }
-  }
-  wide = __syncthreads_or(wide || force_net ? 1 : 0) != 0;
-  if (!wide) {
-    unsigned long long v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t i = threadIdx.x + 1024u * r;
-      v[r] = i < U ? (hk[i] << 32) | ht[i] : ~0ull;
-    }
-    // (reg_bitonic's first LDS stage starts with a barrier: every key is loaded before
-    // hk is reused as its exchange buffer)
-    if (P2 <= 1024) {
-      unsigned long long a[1] = {v[0]};
-      reg_bitonic<1>(a, P2, hk);
-      v[0] = a[0];
-    } else if (P2 <= 2048) {
-      unsigned long long a[2] = {v[0], v[1]};
-      reg_bitonic<2>(a, P2, hk);
-      v[0] = a[0];
-      v[1] = a[1];
-    } else {
-      reg_bitonic<4>(v, P2, hk);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t i = threadIdx.x + 1024u * r;
-      if (i < U) ht[i] = (uint32_t)v[r];
-    }
-  } else {
-    // bitonic network over P2 slots in LDS, one compare-exchange per thread per 2048
-    // slots and stage.  Pair c = (i, i | jj) with i = c with a zero bit inserted at jj:
-    // for jj < 128 the pairs of wave w's indices (c = 64 w + lane, + 1024 r) stay inside
-    // slots that only wave w touches, so those stages need a wave barrier only; a stage
-    // of jj >= 128 is bracketed by workgroup barriers
-    for (uint32_t k = 2; k <= P2; k <<= 1) {
-      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-        if (jj >= 128) {
-          __syncthreads();
-        } else {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        for (uint32_t c = threadIdx.x; c < P2 / 2; c += 1024) {
-          const uint32_t i = ((c & ~(jj - 1)) << 1) | (c & (jj - 1)), l = i | jj;
-          const unsigned long long a = hk[i], b = hk[l];
-          if (((i & k) == 0) ? a > b : a < b) {
-            hk[i] = b;
-            hk[l] = a;
-            const uint32_t t0 = ht[i];
-            ht[i] = ht[l];
-            ht[l] = t0;
-          }
-        }
-        if (jj >= 128) __syncthreads();
+        t8[q] = __float_as_uint((sn + tn) * (mn / mx));  // > 0
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q)
+      if (t8[q]) {
+        const uint32_t o = atomicAdd(&snz, 1u);
+        hk[o] = k8[q];
+        ht[o] = t8[q];
+      }
   }
   __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const uint32_t lane = threadIdx.x;
-  if (lane == 0) {
-    const float similar = seq_sum(ht, U);  // similar_num += term, leaf by leaf
+  FV_PH(3);
+  const uint32_t Z = snz, nch = (Z + 63) / 64;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  // chunks of 64 pairs sorted by code in registers (a wave's bitonic network over
+  // shuffles), written back in place; pads (past Z) carry the empty code, above every
+  // real one, so each chunk's valid pairs come first
+  for (uint32_t c = wv; c < nch; c += 16) {
+    const uint32_t i = c * 64 + lane;
+    unsigned long long v = i < Z ? hk[i] : FV_EMPTY;
+    uint32_t t = i < Z ? ht[i] : 0u;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+        const uint32_t olo = (uint32_t)__shfl_xor((int)(uint32_t)v, (int)jj, 64);
+        const uint32_t ohi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), (int)jj, 64);
+        const uint32_t ot = (uint32_t)__shfl_xor((int)t, (int)jj, 64);
+        const unsigned long long o = ((unsigned long long)ohi << 32) | olo;
+        const bool keep_min = ((lane & k) == 0) == ((lane & jj) == 0);
+        const bool take = keep_min ? o < v : o > v;
+        v = take ? o : v;
+        t = take ? ot : t;
+      }
+    hk[i] = v;
+    ht[i] = t;
+  }
+  __syncthreads();
+  FV_PH(4);
+  // each pair's place in code order: its lane in its sorted chunk plus, per other chunk,
+  // the count of smaller codes there (a branchless binary search over the 64 entries)
+  for (uint32_t c = wv; c < nch; c += 16) {
+    const uint32_t i = c * 64 + lane;
+    if (i >= Z) continue;
+    const unsigned long long key = hk[i];
+    uint32_t r = lane;
+    for (uint32_t d = 0; d < nch; ++d) {
+      if (d == c) continue;
+      const unsigned long long* __restrict__ A = hk + d * 64;
+      uint32_t pos = 0;
+#pragma unroll
+      for (uint32_t st = 32; st > 0; st >>= 1) pos += A[pos + st - 1] < key ? st : 0u;
+      pos += A[pos] < key ? 1u : 0u;
+      r += pos;
+    }
+    hs[r] = ht[i];  // the terms in code order in hs[0, Z)
+  }
+  __syncthreads();
+  FV_PH(5);
+  if (threadIdx.x == 0) {
+    const float similar = seq_sum(hs, Z);  // similar_num += term, leaf by leaf
     const uint32_t p = pts[e];
     if (p >= (1u << 24)) atomicOr(&scal[7], FV_ERR_POINTS);  // float allinvec would round: unsupported size
     const float sc = similar / (float)p;
     scores[e] = sc;
     if (mail) mail->scores[e] = sc;
+#ifdef FV_PHASES
+    FV_PH(6);
+    if (e == 0) printf("fv_eval e0 m %u U %u Z %u | init %llu merge %llu terms %llu chunks %llu search %llu sum %llu (s_memtime ticks)\n", m, snu, Z,
+                       fvt[1] - fvt[0], fvt[2] - fvt[1], fvt[3] - fvt[2], fvt[4] - fvt[3], fvt[5] - fvt[4], fvt[6] - fvt[5]);
+#endif
   }
 }
 
@@ -576,8 +500,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
     // the leaves of each evaluation merged, sorted and summed in LDS: two launches
     // after the octrees instead of ~20 (scal[7] was zeroed by k_fv_transform)
     k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, b.nseg_e);
-    k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail,
-                                  std::min<uint32_t>(lds_cap & ~FV_LDS_NET, FV_LDS_MAX) | (lds_cap & FV_LDS_NET));
+    k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail, std::min<uint32_t>(lds_cap, FV_LDS_MAX));
     if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, b.scores, E, mail);
     return;
   }
@@ -602,8 +525,7 @@ int fine_mode_env(int sticky_sorted) {
 uint32_t fine_lds_cap_env() {
   const char* e = std::getenv("FCCF_FINE_LDS_CAP");
   const long v = e ? std::atol(e) : (long)FV_LDS_MAX;
-  const char* w = std::getenv("FCCF_FINE_LDS_NET");  // tests: the LDS network for every code width
-  return (v < 1 ? 1u : (v > (long)FV_LDS_MAX ? FV_LDS_MAX : (uint32_t)v)) | (w && w[0] == '1' ? FV_LDS_NET : 0u);
+  return v < 1 ? 1u : (v > (long)FV_LDS_MAX ? FV_LDS_MAX : (uint32_t)v);
 }
 
 }  // namespace fccf

@@ -113,15 +113,13 @@ void cluster_bits(QTd* const q[3], const uint32_t* totals, float r2, AngleCut cc
 constexpr int FV_LEAVES_LDS = 0, FV_LEAVES_SORTED = 1;
 constexpr uint32_t FV_ERR_POINTS = 1u, FV_ERR_LDS = 2u;  // error word bits (scal[7], FineMail::err)
 constexpr uint32_t FV_LDS_MAX = 4096;                    // leaves per evaluation in the LDS form
-constexpr uint32_t FV_LDS_NET = 1u << 31;                // lds_cap flag: sort in the LDS network (tests)
 struct FineMail;
 void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, const float* s2, uint32_t n2, int E,
                        double res, FineBufs b,
                        hipStream_t st, FineMail* mail = nullptr, int mode = FV_LEAVES_LDS,
                        uint32_t lds_cap = FV_LDS_MAX);
 // the leaf-form for this call: FCCF_FINE_SORTED=1 forces the sorted form, FCCF_FINE_LDS_CAP
-// lowers the LDS form's capacity (tests of the fallback), FCCF_FINE_LDS_NET=1 sorts the
-// LDS form's leaves in its LDS network even when their codes fit the register form
+// lowers the LDS form's capacity (tests of the fallback)
 int fine_mode_env(int sticky_sorted);
 uint32_t fine_lds_cap_env();
 

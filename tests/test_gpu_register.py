@@ -470,8 +470,8 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
 
 def test_fine_verify_leaf_forms_agree(fccf, oracle, monkeypatch):
     """fine_verify (FCCF.cpp:785-839) in its two leaf forms: per evaluation in LDS
-    (default: the tile entries merged, sorted -- in registers, or in the LDS network with
-    FCCF_FINE_LDS_NET=1 -- and summed by one workgroup) and sorted
+    (default: the tile entries merged, the nonzero terms placed in code order by rank and
+    summed by one workgroup) and sorted
     device-wide (FCCF_FINE_SORTED=1, the fallback).  Scores bit-equal between the forms
     through the stage export; a capacity below the scene's leaf count (FCCF_FINE_LDS_CAP)
     makes the pipeline rerun the batch in the sorted form (fine_reruns = 1) with T still
@@ -487,12 +487,6 @@ def test_fine_verify_leaf_forms_agree(fccf, oracle, monkeypatch):
         Ts = np.stack([np.eye(4, dtype=np.float32)] + [fv.reshape(-1, 18)[:, :16].reshape(-1, 4, 4)[0]
                                                        for fv in (c.debug("fv0"), c.debug("fv2")) if fv.size])
         a = c.fine_verify(s1, s2, Ts)
-        # the LDS form's two leaf orderings: packed keys in registers (codes of <= 32
-        # bits, the default here) and the LDS network (deeper octrees)
-        monkeypatch.setenv("FCCF_FINE_LDS_NET", "1")
-        n = c.fine_verify(s1, s2, Ts)
-        np.testing.assert_array_equal(a.view(np.uint32), n.view(np.uint32))
-        monkeypatch.delenv("FCCF_FINE_LDS_NET")
         monkeypatch.setenv("FCCF_FINE_SORTED", "1")
         b = c.fine_verify(s1, s2, Ts)
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
