@@ -632,7 +632,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // counts and planar records of both clouds: written by k_compact_planar into
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
-  ch.pool->warm(1000);  // growing runs both clouds in parallel right after this wait
+  // growing runs both clouds in parallel right after this wait: one worker besides this
+  // thread (FCCF_WARM_N: dev A/B of the count)
+  static const int warm_n = [] {
+    const char* v = std::getenv("FCCF_WARM_N");
+    return v && *v ? std::atoi(v) : 1;
+  }();
+  ch.pool->warm(1000, warm_n);
   if (c->group) {
     // a sharded stage holds collectives: a bounded wait that aborts the group on a
     // peer's failure (group.h), polled under the capture lock
@@ -641,7 +647,11 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     // (under the capture lock: with several pairs per stage, a later pair's B1 runs while
     // the helper thread may be capturing the next stage on the stream ev[4] was recorded
     // on, and HIP refuses to synchronize such an event; ev[4] is complete by then)
-    if (!mail_wait(&cm.done, 5000.0, [&] { ch.pool->warm(400); })) {
+    static const bool keep_warm = [] {
+      const char* v = std::getenv("FCCF_SPIN_WARM");  // dev A/B
+      return !(v && v[0] == '0');
+    }();
+    if (!mail_wait(&cm.done, 5000.0, [&] { if (keep_warm) ch.pool->warm(400, warm_n); })) {
       std::lock_guard<std::mutex> lk(capture_mutex());
       HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
     }

@@ -35,7 +35,7 @@ class Pool {
     }
     const char* s = std::getenv("FCCF_POOL_SPIN_US");
     spin_us_ = s ? std::atoi(s) : 500;
-    for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    for (int i = 1; i < n; ++i) workers_.emplace_back([this, i] { loop(i - 1); });
   }
   ~Pool() {
     {
@@ -46,11 +46,14 @@ class Pool {
     for (auto& t : workers_) t.join();
   }
   int size() const { return (int)workers_.size() + 1; }
-  // Wakes sleeping workers and keeps every worker spinning for `us` microseconds,
-  // so a parallel_for issued within that window starts on all threads at once
-  // (call it before a wait whose end is followed by parallel work).
-  void warm(int us) {
+  // Wakes sleeping workers and keeps the first `nw` workers (all by default) spinning
+  // for `us` microseconds, so a parallel_for issued within that window starts on those
+  // threads at once (call it before a wait whose end is followed by parallel work).
+  // Spinning threads take CPU time from the caller's other threads: keep nw to what the
+  // next parallel_for needs.
+  void warm(int us, int nw = 1 << 30) {
     if (workers_.empty()) return;
+    warm_n_.store(nw, std::memory_order_relaxed);
     warm_until_.store(now_us() + us, std::memory_order_relaxed);
     warm_gen_.fetch_add(1, std::memory_order_release);
     {
@@ -101,7 +104,7 @@ class Pool {
       w = word_.load(std::memory_order_acquire);
     }
   }
-  void loop() {
+  void loop(int id) {
     uint64_t seen = 0;
     while (true) {
       int64_t until = now_us() + spin_us_;
@@ -109,10 +112,16 @@ class Pool {
       int k = 0;
       while (((w = word_.load(std::memory_order_acquire)) >> 32) == seen && !quit_.load()) {
         relax();
-        if ((++k & 255) == 0 && now_us() > std::max(until, warm_until_.load(std::memory_order_relaxed))) {
+        if ((++k & 255) == 0 &&
+            now_us() > std::max(until, id < warm_n_.load(std::memory_order_relaxed)
+                                           ? warm_until_.load(std::memory_order_relaxed)
+                                           : int64_t(0))) {
           std::unique_lock<std::mutex> g(m_);
           const uint64_t wg = warm_gen_.load();
-          cv_.wait(g, [&] { return quit_.load() || (word_.load() >> 32) != seen || warm_gen_.load() != wg; });
+          cv_.wait(g, [&] {  // (a warm() wakes only the workers it keeps spinning)
+            return quit_.load() || (word_.load() >> 32) != seen ||
+                   (warm_gen_.load() != wg && id < warm_n_.load(std::memory_order_relaxed));
+          });
           until = now_us() + spin_us_;
         }
       }
@@ -129,6 +138,7 @@ class Pool {
   std::atomic<bool> quit_{false};
   std::atomic<int64_t> warm_until_{0};
   std::atomic<uint64_t> warm_gen_{0};
+  std::atomic<int> warm_n_{1 << 30};
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<int> n_{0};
   uint64_t job_ = 0;

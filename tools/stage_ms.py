@@ -23,5 +23,9 @@ for _ in range(reps):
     e2e.append((time.perf_counter() - a) * 1e3)
     ms.append(st.as_dict()["ms"])
 keys = ms[0].keys()
+g = sorted(m["grow"] for m in ms)
+e = sorted(e2e)
+q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))]
+print(f"spread: grow p10 {q(g, .1):.4f} p50 {q(g, .5):.4f} p90 {q(g, .9):.4f}; e2e p10 {q(e, .1):.3f} p90 {q(e, .9):.3f}")
 print(f"e2e {statistics.median(e2e):.3f} ms | " + " ".join(f"{k} {statistics.median(m[k] for m in ms):.4f}" for k in keys),
       flush=True)
