@@ -570,14 +570,15 @@ def main():
     if pipelined:
         # exactly K registrations, pair i+1's cloud stage overlapping pair i's later stages
         Tb, sts = batch(args.steps)
-        T, st = Tb[-1], sts[-1]
-        Ks = sum(x.K for x in sts)
-        batch_ms = {k: statistics.mean(x.as_dict()["ms"][k] for x in sts) for k in sts[0].as_dict()["ms"]}
     else:
         for _ in range(args.steps):
             T, st = reg()  # returns after T is on host
             Ks += st.K
     elapsed = time.perf_counter() - t0
+    if pipelined:  # (the per-registration stats are read after the clock stops)
+        T, st = Tb[-1], sts[-1]
+        Ks = sum(x.K for x in sts)
+        batch_ms = {k: statistics.mean(x.as_dict()["ms"][k] for x in sts) for k in sts[0].as_dict()["ms"]}
     barrier(dist)
     # latency: single registrations, one at a time (untimed for `value`)
     per, ref_win, stage_rl = [], [], None

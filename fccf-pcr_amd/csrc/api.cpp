@@ -63,7 +63,6 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.reset();
     for (auto& g : cs.g_segb) g.reset();
-    cs.g_rep.reset();
     cs.g_fine.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);

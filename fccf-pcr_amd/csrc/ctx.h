@@ -315,7 +315,6 @@ struct fccf_ctx {
                                      // per pair count: part A (the VoxelGrid passes; with a group attached,
                                      // the whole stage)
     fccf::CachedGraph g_segb[4];     // and part B (centroid sums beside the face voxels, orientation)
-    fccf::CachedGraph g_rep;         // fine_verify's S1 octree-bounds replay (after clouds done)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight

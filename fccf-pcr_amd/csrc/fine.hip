@@ -438,7 +438,10 @@ __global__ void k_fv_score(const float* __restrict__ similar, const float* __res
     scores[e] = sc;
     if (mail) mail->scores[e] = sc;
   }
-  if (mail && e == 0) mail->err = scal[7];
+  if (mail && e == 0) {
+    mail->err = scal[7];
+    mail->stamp[1] = __builtin_amdgcn_s_memrealtime();
+  }
   if (mail) {  // the mailbox is complete: its flag after a system-scope fence (phase B2 polls it)
     __syncthreads();
     if (e == 0) {
@@ -489,7 +492,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   if (split) {
     k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
                                                                     n1, b.nseg_e, b.pts);
-    block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd);
+    block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd, nullptr, mail ? &mail->stamp[0] : nullptr);
   } else {
     FvTransform tf{s2, b.T, b.s2t, s1_state, b.state, b.scal, b.nseg_e, b.pts, n1, n2};
     block_aggr_transform(tf, d_n2, n2, b.aggr2, st, E, sd, mail ? &mail->stamp[0] : nullptr);

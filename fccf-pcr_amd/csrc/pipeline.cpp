@@ -556,6 +556,9 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     face_voxels_orient(capmax, all_of<VoxRec*>(w, nc, [](const CloudWS& x) { return x.planar; }),
                        all_of<FaceBufs>(w, nc, [](const CloudWS& x) { return x.fb; }), sB, nc, cmail,
                        all_of<const uint32_t*>(w, nc, [](const CloudWS& x) { return (const uint32_t*)x.sc; }));
+    // fine verification's S1 octree bounds of every pair of the group: one batched replay
+    // after k_mail_done, so phase B1 (which polls the mailbox flag) starts without it
+    seg_s1_replay(w, P, Pa, sB);
   };
   for (int j = 0; j < P; ++j) __atomic_store_n(&cmail[j].done, 0u, __ATOMIC_RELAXED);  // (set by k_mail_done)
   const bool eager = DG != nullptr || exact2;
@@ -573,20 +576,10 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     HIP_CHECK(hipStreamWaitEvent(sB, cg.ev[1], 0));  // (sB is captured by this thread only)
     cg.g_segb[P - 1].run(&key, sizeof key, sB, part_b, nullptr, nullptr, eager);
   }
-  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[4], sB));  // clouds done
-  // fine verification's S1 octree bounds of every pair of the group, after the clouds-done
-  // events (the host's phase B1 starts without them): one batched replay (keyed by the
-  // pointers it reads: the layouts of stages of different pair counts differ, and a
-  // replay with another layout's pointers reads a stale count)
-  struct {
-    const void *resid, *nresid, *aggr, *state;
-    uint32_t cap;
-    float res;
-    int32_t pairs, pad;
-  } rkey = {w[0].resid, w[0].fb.nresid, w[0].faggr, w[0].fstate, capmax, Pa.fine_verify_voxel_size, P, 0};
-  static_assert(sizeof rkey == 4 * 8 + 4 * 4, "graph key without padding");
-  cg.g_rep.run(&rkey, sizeof rkey, sB, [&] { seg_s1_replay(w, P, Pa, sB); });
-  for (int j = 0; j < P; ++j) HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], sB));  // S1 octree bounds
+  for (int j = 0; j < P; ++j) {  // clouds done (and S1 octree bounds: the same point now)
+    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[4], sB));
+    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], sB));
+  }
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1171,13 +1164,13 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     ht.mark("fine_setup");
     // S1 octree bounds replayed (after the clouds); ev[5]'s stream may be capturing the next pair's clouds
     guarded_stream_wait(sf, c->cs[s].ev[5]);
-    HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));
+    if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));  // (otherwise the mailbox stamps time it)
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm, fmode, fcap);
     });
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
+    if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
     if (FG) group_fine_gather(FG, s, fb.scores, El, fb.scal + 7, sf);
     HIP_CHECK(hipEventRecord(c->cs[s].ev[3], sf));  // fine verification of this set's pair done
     ht.mark("fine_launched");
@@ -1250,12 +1243,12 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
     }
     if (err) throw Error(FCCF_E_INTERNAL, "fine_verify: >= 2^24 points in one evaluation");
     if (pb.E_loc > 0) {
-      // the device span from the launch's own stamps (100 MHz) when both were written
-      // (the LDS form without a rerun), else from the timing events around the launch
+      // the device span from the launch's own stamps (100 MHz; the timing events around
+      // the launch only with a group, whose sharded gather follows it on the stream)
       const FineMail& fm = host_mail(c)->fine[s];
       float d = 0.f;
-      if (!c->group && fm.stamp[0] && fm.stamp[1] >= fm.stamp[0]) {
-        d = (float)((double)(fm.stamp[1] - fm.stamp[0]) * 1e-5);
+      if (!(c->group && c->group->n > 1)) {  // (the events are recorded with a sharded fine stage only)
+        d = fm.stamp[0] && fm.stamp[1] >= fm.stamp[0] ? (float)((double)(fm.stamp[1] - fm.stamp[0]) * 1e-5) : 0.f;
       } else {
         HIP_CHECK(hipEventSynchronize(c->cs[s].tev[5]));
         HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
@@ -1318,7 +1311,6 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   S.graph_captures = c->cs[s].g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
   for (auto& g : c->cs[s].g_segb) S.graph_captures += g.captures;
-  S.graph_captures += c->cs[s].g_rep.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
   if (c->debug) {
@@ -1339,7 +1331,6 @@ void reset_capture_counts(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.captures = 0;
     for (auto& g : cs.g_segb) g.captures = 0;
-    cs.g_rep.captures = 0;
     cs.g_fine.captures = 0;
   }
 }

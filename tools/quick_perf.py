@@ -29,5 +29,5 @@ for _ in range(3):
     a = time.perf_counter()
     ctx.register_batch([pair] * reps, cfg["leaf"], on_device=True)
     pb.append((time.perf_counter() - a) / reps * 1e3)
-print(f"e2e {statistics.median(e):.3f} ms  vg_main {statistics.median(vg):.3f} ms  pipelined {min(pb):.3f} ms/reg",
-      flush=True)
+print(f"e2e {statistics.median(e):.3f} ms  vg_main {statistics.median(vg):.3f} ms  pipelined {min(pb):.3f} ms/reg"
+      f"  (batches: {' '.join(f'{x:.3f}' for x in pb)})", flush=True)
