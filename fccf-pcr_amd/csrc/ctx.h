@@ -133,11 +133,8 @@ inline void guarded_stream_wait(hipStream_t st, hipEvent_t ev) {
 // workers spinning for the parallel work that follows the wait.
 template <class Keep = void (*)()>
 inline bool mail_wait(const uint32_t* flag, double spin_us, Keep keep = nullptr) {
-  static const double env = [] {
-    const char* v = std::getenv("FCCF_SPIN_US");
-    return v && *v ? std::atof(v) : -1.0;
-  }();
-  if (env >= 0.0) spin_us = env;
+  const char* v = std::getenv("FCCF_SPIN_US");  // (read per wait: tests switch it)
+  if (v && *v) spin_us = std::atof(v);
   if (spin_us <= 0.0) return false;
   const auto t0 = std::chrono::steady_clock::now();
   double next_keep = 200.0;

@@ -503,3 +503,25 @@ def test_fine_verify_leaf_forms_agree(fccf, oracle, monkeypatch):
         assert st3.fine_reruns == 0
     finally:
         c.close()
+
+
+def test_mailbox_flags_and_event_waits_agree(ctx, oracle, fccf, monkeypatch):
+    """Phase B wakes on pinned mailbox flags that the stages' last kernels set after a
+    system-scope fence (k_mail_done, k_fv_mail_err; ctx.h mail_wait); FCCF_SPIN_US=0 takes
+    the event waits instead.  Both must read complete mailboxes: T bit-exact against the
+    oracle, single and batched, and the fine device span (from the mailbox stamps) set."""
+    src, tar, _ = fccf.synth_pair(80_000)
+    ref = oracle.Run(src, tar, 0.1, oracle.INTROSORT).T
+    for spin in ("", "0", "1"):  # default bound, event waits only, a 1 us bound (mostly events)
+        if spin:
+            monkeypatch.setenv("FCCF_SPIN_US", spin)
+        else:
+            monkeypatch.delenv("FCCF_SPIN_US", raising=False)
+        for _ in range(2):
+            T, st = ctx.register(src, tar, 0.1)
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"FCCF_SPIN_US={spin!r}")
+            assert 0.0 < st.dev_ms[3] < 1000.0, (spin, list(st.dev_ms))
+        Tb, sb = ctx.register_batch([(src, tar)] * 5, 0.1)
+        for T, x in zip(Tb, sb):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"batch, FCCF_SPIN_US={spin!r}")
+            assert 0.0 < x.dev_ms[3] < 1000.0, (spin, list(x.dev_ms))
