@@ -221,6 +221,7 @@ __global__ void __launch_bounds__(256) k_oct_codes(B4<const float*> xyz2, B4<con
   uint64_t* __restrict__ codes = codes2[e];
   uint32_t* __restrict__ d_nbits = d_nbits2[e];
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
+  const double inv = 1.0 / res;
   if (gid == 0) *d_nbits = S.defined ? 3u * S.depth + 1u : 1u;
   // four points per thread: three 16-byte loads, two 16-byte stores (aligned arena
   // buffers; a misaligned base takes the one-point loop for everything)
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(256) k_oct_codes(B4<const float*> xyz2, B4<con
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float x = p[3 * j], y = p[3 * j + 1], z = p[3 * j + 2];
-      k[j] = finite3(x, y, z) ? oct_code(S, res, x, y, z) : ~(uint64_t)0;
+      k[j] = finite3(x, y, z) ? oct_code(S, res, inv, x, y, z) : ~(uint64_t)0;
     }
     ulonglong2* o = reinterpret_cast<ulonglong2*>(codes + 4 * (size_t)q);
     o[0] = make_ulonglong2(k[0], k[1]);
@@ -242,7 +243,7 @@ __global__ void __launch_bounds__(256) k_oct_codes(B4<const float*> xyz2, B4<con
   }
   for (uint32_t i = 4 * nq + gid; i < n; i += gsz) {
     const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-    codes[i] = finite3(x, y, z) ? oct_code(S, res, x, y, z) : ~(uint64_t)0;
+    codes[i] = finite3(x, y, z) ? oct_code(S, res, inv, x, y, z) : ~(uint64_t)0;
   }
 }
 

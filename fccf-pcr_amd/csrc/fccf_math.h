@@ -262,7 +262,21 @@ FH bool oct_inside(const OctState& b, float x, float y, float z) {
 
 // Morton code of final leaf keys, x most significant within each level (DFS order
 // of getOccupiedVoxelCenters, child index (x<<2)|(y<<1)|z).
+// bit i of v (i < 21) to bit 3i
+FH uint64_t spread3(uint64_t v) {
+  v &= 0x1fffffull;
+  v = (v | v << 32) & 0x1f00000000ffffull;
+  v = (v | v << 16) & 0x1f0000ff0000ffull;
+  v = (v | v << 8) & 0x100f00f00f00f00full;
+  v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+  v = (v | v << 2) & 0x1249249249249249ull;
+  return v;
+}
 FH uint64_t morton_code(uint32_t kx, uint32_t ky, uint32_t kz, uint32_t depth) {
+  if (depth <= 21) {  // the loop below, as masked bit spreads (bit b of kx at 3b + 2)
+    const uint32_t mk = (uint32_t)((1ull << depth) - 1ull);
+    return (spread3(kx & mk) << 2) | (spread3(ky & mk) << 1) | spread3(kz & mk);
+  }
   uint64_t m = 0;
   for (int bit = (int)depth - 1; bit >= 0; --bit)
     m = (m << 3) | ((uint64_t)((kx >> bit) & 1u) << 2) | ((uint64_t)((ky >> bit) & 1u) << 1) | (uint64_t)((kz >> bit) & 1u);
@@ -272,6 +286,24 @@ FH uint64_t oct_code(const OctState& b, double res, float x, float y, float z) {
   const uint32_t kx = (uint32_t)(((double)x - b.min[0]) / res);
   const uint32_t ky = (uint32_t)(((double)y - b.min[1]) / res);
   const uint32_t kz = (uint32_t)(((double)z - b.min[2]) / res);
+  return morton_code(kx, ky, kz, b.depth);
+}
+// (uint32_t)(a / res), the key of an offset a from the octree's minimum, with inv = 1.0 /
+// res: the quotient through a multiplication (relative error below 2^-52) truncates the
+// same way as the IEEE division unless an integer lies within 2^-50 of it; there, and for
+// a <= 0, the division itself runs.  Bit-identical to the division form, without a
+// double-precision division per coordinate on the device.
+FH uint32_t key_div(double a, double res, double inv) {
+  const double q = a * inv;
+  const double f = floor(q);
+  const double m = q * 0x1p-50;
+  if (a > 0.0 && q - f > m && (f + 1.0) - q > m) return (uint32_t)f;
+  return (uint32_t)(a / res);
+}
+FH uint64_t oct_code(const OctState& b, double res, double inv, float x, float y, float z) {
+  const uint32_t kx = key_div((double)x - b.min[0], res, inv);
+  const uint32_t ky = key_div((double)y - b.min[1], res, inv);
+  const uint32_t kz = key_div((double)z - b.min[2], res, inv);
   return morton_code(kx, ky, kz, b.depth);
 }
 

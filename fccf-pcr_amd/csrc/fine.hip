@@ -114,6 +114,7 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
   const uint32_t n = n1 + n2, i0 = blockIdx.x * FV_TILE;
   if (i0 >= n) return;
   const OctState S = st[e];
+  const double inv = 1.0 / res;
   const float* b = s2t + (size_t)e * 3 * n2;
   for (uint32_t j = threadIdx.x; j < FV_SLOTS; j += 256) {
     hk[j] = FV_EMPTY;
@@ -132,7 +133,7 @@ __global__ void __launch_bounds__(256) k_fv_entries(const float* __restrict__ s1
       const float* p = tgt ? b + 3 * (i - n1) : s1 + 3 * i;
       const float x = p[0], y = p[1], z = p[2];
       act = finite3(x, y, z);
-      if (act) key = (ecnt ? 0ull : (unsigned long long)e << shift) | oct_code(S, res, x, y, z);
+      if (act) key = (ecnt ? 0ull : (unsigned long long)e << shift) | oct_code(S, res, inv, x, y, z);
     }
     fin += act ? 1u : 0u;
     // A wave's points lie in a few leaves (the clouds come in 1 m leaf order): one lane

@@ -74,3 +74,18 @@ def test_centroid_bitexact(ctx, n):
     else:
         want = np.array([_seq(xyz[:, k]) / np.float32(n) for k in range(3)] + [1], np.float32)
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (got, want)
+
+
+@pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"),
+                    reason="hipcc not available")
+def test_key_div_fuzz_host(tmp_path):
+    """Octree keys without a double division (fccf_math.h key_div, used by k_oct_codes and
+    k_fv_entries): the same integer as (uint32_t)(a / res) at and around every multiple
+    of res, for the reference's voxel sizes and random ones."""
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = tmp_path / "keydiv_fuzz"
+    subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-x", "hip", "--offload-arch=gfx950",
+                    os.path.join(HERE, "keydiv_fuzz.cpp"), "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
+    assert "mismatches 0" in r.stdout, r.stdout
+    assert r.returncode == 0
