@@ -363,6 +363,13 @@ PipeSet& pset(fccf_ctx* c, int s) {
   return *(PipeSet*)c->cs[s].ws;
 }
 
+// A stage group's events live on its first slot: one record per group at the stage's
+// end instead of one per pair (every record and cross-stream wait is a packet the
+// command processor handles between two stages' kernels).
+// ev[0]: the group's inputs have been read; ev[4]: clouds done (records, counts, S1
+// octree bounds); the slot's own ev[3] marks its fine verification.
+hipEvent_t group_event(fccf_ctx* c, int s, int k) { return c->cs[PAIRS_MAX * (s / PAIRS_MAX)].ev[k]; }
+
 // Host inputs of the pair for CloudSet s: both clouds copied into the set's input
 // arena on the ctx's copy stream (ingest.h; the runtime's pageable path), after the
 // previous pair on this set has finished reading it (its first pass, before ev[0]).
@@ -380,7 +387,7 @@ Staged stage_inputs(fccf_ctx* c, int s, const float* src, int64_t n_src, const f
   float* dt = cs.inarena.take_n<float>(3 * (size_t)n_tar);
   float* ds = cs.inarena.take_n<float>(3 * (size_t)n_src);
   hipStream_t su = c->ingest.su;
-  guarded_stream_wait(su, cs.ev[0]);
+  guarded_stream_wait(su, group_event(c, s, 0));
   HIP_CHECK(hipEventRecord(cs.ev_in0, su));
   if (n_tar) HIP_CHECK(hipMemcpyAsync(dt, tar, 12 * (size_t)n_tar, hipMemcpyHostToDevice, su));
   if (n_src) HIP_CHECK(hipMemcpyAsync(ds, src, 12 * (size_t)n_src, hipMemcpyHostToDevice, su));
@@ -430,10 +437,15 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     capmax = (uint32_t)std::max<int64_t>(capmax, std::max(in[j].n_src, in[j].n_tar));
   // the previous pairs on these slots may still be in fine verification, which reads
   // this workspace (residual clouds, S1 octree state): the stage waits for them
-  for (int j = 0; j < PAIRS_MAX; ++j) guarded_stream_wait(st0, c->cs[S0 + j].ev[3]);  // (recorded on the fine stream)
+  // (recorded on the fine stream; a wait on an event already complete -- the steady
+  // state, where those pairs finished long before -- is skipped: no packet)
+  for (int j = 0; j < PAIRS_MAX; ++j) {
+    std::lock_guard<std::mutex> lk(capture_mutex());
+    if (hipEventQuery(c->cs[S0 + j].ev[3]) != hipSuccess) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[S0 + j].ev[3], 0));
+  }
   // and the previous stage on these slots has finished its B part (the S1 replay is its
   // last launch; B runs on another stream than this stage's A)
-  if (split) guarded_stream_wait(st0, cg.ev[5]);
+  if (split) guarded_stream_wait(st0, cg.ev[4]);
   // (the centroid scratch is carved for BMAX clouds whatever the pair count, so slot
   // j's clouds sit at the same addresses in every stage form, and the per-slot graphs
   // keyed by those addresses -- the S1 replay, fine verification -- keep replaying when
@@ -567,19 +579,13 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
     if (!split) part_b();
   }, vg_entry_kernel(), pargs, eager, &lay);
-  for (int j = 0; j < P; ++j) {
-    // external signal for stage_inputs (this slot's inputs have been read): after pass 1
-    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[0], st0));
-  }
+  HIP_CHECK(hipEventRecord(cg.ev[0], st0));  // external signal for stage_inputs (the group's inputs have been read)
   if (split) {
     HIP_CHECK(hipEventRecord(cg.ev[1], st0));  // the VoxelGrid passes done: B may start
     HIP_CHECK(hipStreamWaitEvent(sB, cg.ev[1], 0));  // (sB is captured by this thread only)
     cg.g_segb[P - 1].run(&key, sizeof key, sB, part_b, nullptr, nullptr, eager);
   }
-  for (int j = 0; j < P; ++j) {  // clouds done (and S1 octree bounds: the same point now)
-    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[4], sB));
-    HIP_CHECK(hipEventRecord(c->cs[S0 + j].ev[5], sB));
-  }
+  HIP_CHECK(hipEventRecord(cg.ev[4], sB));  // clouds done, S1 octree bounds replayed
   HIP_CHECK(hipGetLastError());
 }
 
@@ -635,7 +641,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (c->group) {
     // a sharded stage holds collectives: a bounded wait that aborts the group on a
     // peer's failure (group.h), polled under the capture lock
-    group_wait_event(c->group, c->cs[s].ev[4], true);
+    group_wait_event(c->group, group_event(c, s, 4), true);
   } else {
     // (under the capture lock: with several pairs per stage, a later pair's B1 runs while
     // the helper thread may be capturing the next stage on the stream ev[4] was recorded
@@ -646,7 +652,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     }();
     if (!mail_wait(&cm.done, 5000.0, [&] { if (keep_warm) ch.pool->warm(400, warm_n); })) {
       std::lock_guard<std::mutex> lk(capture_mutex());
-      HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+      HIP_CHECK(hipEventSynchronize(group_event(c, s, 4)));
     }
   }
   uint32_t sc[2][4], fsc[2][4];
@@ -662,10 +668,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     c->enq.wait();
     clouds_redo(c, s, P);
     if (c->group) {
-      group_wait_event(c->group, c->cs[s].ev[4], true);
+      group_wait_event(c->group, group_event(c, s, 4), true);
     } else {
       std::lock_guard<std::mutex> lk(capture_mutex());
-      HIP_CHECK(hipEventSynchronize(c->cs[s].ev[4]));
+      HIP_CHECK(hipEventSynchronize(group_event(c, s, 4)));
     }
     std::memcpy(sc, cm.sc, sizeof sc);
     std::memcpy(fsc, cm.fsc, sizeof fsc);
@@ -673,7 +679,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // (also a later pair of the group, whose stage was redone with this one; a pair whose
   // B1 had finished before a later pair raised the redo keeps its count of 0)
   if (ps.redone) ++S.stage_redos;
-  guarded_stream_wait(st0, c->cs[s].ev[4]);  // (cheap: the capture lock is free in the steady state)
+  guarded_stream_wait(st0, group_event(c, s, 4));  // (cheap: the capture lock is free in the steady state)
   std::vector<VoxRec> vox[2];
   for (int k = 0; k < 2; ++k) {
     if (fsc[k][2] <= CloudMail::REC_CAP) vox[k].assign(cm.rec[k], cm.rec[k] + fsc[k][2]);
@@ -1162,8 +1168,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     pb.fb = fb;
     pb.fine_in = {w[0].resid, w[0].fstate, w[1].resid, n1, n2, P.fine_verify_voxel_size};
     ht.mark("fine_setup");
-    // S1 octree bounds replayed (after the clouds); ev[5]'s stream may be capturing the next pair's clouds
-    guarded_stream_wait(sf, c->cs[s].ev[5]);
+    // S1 octree bounds replayed (with the clouds); ev[4]'s stream may be capturing the next pair's clouds
+    guarded_stream_wait(sf, group_event(c, s, 4));
     if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));  // (otherwise the mailbox stamps time it)
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
