@@ -407,7 +407,7 @@ struct PairIn {
   bool staged;
 };
 void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float leaf, const fccf_params& Pa,
-                          bool exact2 = false) {
+                          bool exact2 = false, bool batch = false) {
   if (P < 1 || P > PAIRS_MAX) throw Error(FCCF_E_INTERNAL, "cloud stage: 1 .. PAIRS_MAX pairs");
   const int S0 = PAIRS_MAX * G;  // the group's first slot
   auto& cg = c->cs[S0];          // the group's arena, stage graphs and fork/join events
@@ -573,7 +573,18 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     seg_s1_replay(w, P, Pa, sB);
   };
   for (int j = 0; j < P; ++j) __atomic_store_n(&cmail[j].done, 0u, __ATOMIC_RELAXED);  // (set by k_mail_done)
-  const bool eager = DG != nullptr || exact2;
+  // A pipelined batch launches its stages eagerly from the helper thread; a single
+  // registration replays the graph.  A stage graph's launch holds the runtime for ~250 us
+  // of host time (profiles/r05ab), while the two phase-B chains launch their matching
+  // and fine kernels: in batches the eager stage read 0.664-0.671 against 0.706-0.716 ms
+  // per registration, and single registrations were ~15 us faster with the graph
+  // (profiles/r05ac).  FCCF_EAGER_STAGE=0 uses the graph everywhere, =2 launches eagerly
+  // everywhere (dev A/B).
+  static const int eager_env = [] {
+    const char* e = std::getenv("FCCF_EAGER_STAGE");
+    return e ? std::atoi(e) : 1;
+  }();
+  const bool eager = DG != nullptr || exact2 || eager_env >= 2 || (eager_env == 1 && batch);
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
     seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
@@ -1171,10 +1182,14 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     // S1 octree bounds replayed (with the clouds); ev[4]'s stream may be capturing the next pair's clouds
     guarded_stream_wait(sf, group_event(c, s, 4));
     if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));  // (otherwise the mailbox stamps time it)
+    static const bool fine_eager = [] {  // dev A/B: FCCF_EAGER_FINE=1 launches fine verification eagerly
+      const char* e = std::getenv("FCCF_EAGER_FINE");
+      return e && e[0] == '1';
+    }();
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm, fmode, fcap);
-    });
+    }, nullptr, nullptr, fine_eager);
     HIP_CHECK(hipGetLastError());
     if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
     if (FG) group_fine_gather(FG, s, fb.scores, El, fb.scal + 7, sf);
@@ -1608,7 +1623,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       const int i = g * PP + j;
       pin[j] = PairIn{dsrc(i), dtar(i), n_src[i], n_tar[i], !on_device};
     }
-    clouds_enqueue_group(c, g & 1, cnt(g), pin, leaf, P);
+    clouds_enqueue_group(c, g & 1, cnt(g), pin, leaf, P, false, true);
   };
   std::vector<int> redo;  // pairs to register again after the batch (phase_b2)
   if (!on_device) stage_group(0);
