@@ -1542,10 +1542,14 @@ void pipeline_release(fccf_ctx* c) {
 Chain chain_of(fccf_ctx* c, int k, int nchains) {
   HostMail* hm = host_mail(c);
   if (nchains <= 1) return Chain{&c->pool, &c->arena2, &hm->match, c->ev_match[0], true};
-  for (auto& p : c->bpool)
-    if (!p) p.reset(new Pool(std::max(1, c->pool.size() / 2)));
-  return k == 0 ? Chain{c->bpool[0].get(), &c->arena2, &hm->match, c->ev_match[0], false}
-                : Chain{c->bpool[1].get(), &c->arena2b, &hm->match2, c->ev_match[1], false};
+  for (int i = 0; i < 4; ++i)
+    if (!c->bpool[i]) c->bpool[i].reset(new Pool(std::max(1, c->pool.size() / (i < 2 ? 2 : 4))));
+  switch (k) {
+    case 0: return Chain{c->bpool[0].get(), &c->arena2, &hm->match, c->ev_match[0], false};
+    case 1: return Chain{c->bpool[1].get(), &c->arena2b, &hm->match2, c->ev_match[1], false};
+    case 2: return Chain{c->bpool[2].get(), &c->arena2c, &hm->match3, c->ev_match[2], false};
+    default: return Chain{c->bpool[3].get(), &c->arena2d, &hm->match4, c->ev_match[3], false};
+  }
 }
 
 void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
@@ -1689,12 +1693,32 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       }
       sy.cv.notify_all();
     };
-    const Chain chains[2] = {chain_of(c, 0, 2), chain_of(c, 1, 2)};  // (creates the chain pools here)
+    const Chain chains[4] = {chain_of(c, 0, 2), chain_of(c, 1, 2), chain_of(c, 2, 4), chain_of(c, 3, 4)};
+    // The last stage group drains with four chains: after its stage nothing else is left
+    // for the GPU, and its pairs' phase B would otherwise run two after two on each chain
+    // (FCCF_DRAIN4=0: two chains throughout, dev A/B)
+    static const bool drain4_env = [] {
+      const char* e = std::getenv("FCCF_DRAIN4");
+      return !(e && e[0] == '0');
+    }();
+    const int glast = ng - 1;
+    const bool drain4 = drain4_env && ng >= 2 && cnt(glast) >= 3;
+    auto drained = [&](int i) { return drain4 && i / PP == glast && i % PP >= 2; };  // pairs of workers 2, 3
     auto worker = [&](int k) {
       HIP_CHECK(hipSetDevice(c->device));
       const Chain& ch = chains[k];
       int pending = -1;  // this worker's pair whose B2 is still to run
+      if (k >= 2) {  // one pair of the last group: B1, then its B2
+        const int i = glast * PP + k;
+        if (i >= n) return;
+        wait_until([&] { return sy.ready > glast; });
+        phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [] {}, ch);
+        update([&] { ++sy.b1[(size_t)glast]; });
+        if (phase_b2(c, slot(i), true)) update([&] { redo.push_back(i); });
+        return;
+      }
       for (int i = k; i < n; i += 2) {
+        if (drained(i)) continue;
         const int g = i / PP, j = i % PP;
         if (j == 0) {
           wait_until([&] { return sy.submitted > g; });
@@ -1730,16 +1754,23 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       }
     };
     c->b1w.submit([&guarded_worker] { guarded_worker(1); });
-    std::exception_ptr err[2];
+    if (drain4) {
+      c->b1w2.submit([&guarded_worker] { guarded_worker(2); });
+      c->b1w3.submit([&guarded_worker] { guarded_worker(3); });
+    }
+    std::exception_ptr err[4];
     try {
       guarded_worker(0);
     } catch (...) {
       err[0] = std::current_exception();
     }
-    try {
-      c->b1w.wait();  // (always joined before this frame unwinds)
-    } catch (...) {
-      err[1] = std::current_exception();
+    AsyncTask* helpers[3] = {&c->b1w, &c->b1w2, &c->b1w3};
+    for (int h = 0; h < (drain4 ? 3 : 1); ++h) {
+      try {
+        helpers[h]->wait();  // (always joined before this frame unwinds)
+      } catch (...) {
+        err[h + 1] = std::current_exception();
+      }
     }
     // the first failure counts (a stage redo before anything else: the batch reruns with
     // one chain); the other worker's WorkerAborted only says it stopped
@@ -1758,7 +1789,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
     if (first) std::rethrow_exception(first);
     if (restart) throw BatchRestart();
-    if (err[0] || err[1]) throw Error(FCCF_E_INTERNAL, "pipelined batch: a phase-B worker stopped");
+    if (err[0] || err[1] || err[2] || err[3]) throw Error(FCCF_E_INTERNAL, "pipelined batch: a phase-B worker stopped");
     c->enq.wait();
     std::sort(redo.begin(), redo.end());
   }
