@@ -1678,9 +1678,11 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       int submitted = 1;   // groups whose cloud-stage enqueue has been handed to the helper
       int ready = 0;       // groups whose cloud stage is fully enqueued
       std::vector<int> b1; // per group: pairs whose phase B1 has finished
+      std::vector<char> b2;  // per pair: phase B2 has finished
       bool failed = false;
     } sy;
     sy.b1.assign((size_t)ng, 0);
+    sy.b2.assign((size_t)n, 0);
     auto wait_until = [&sy](auto pred) {
       std::unique_lock<std::mutex> lk(sy.m);
       sy.cv.wait(lk, [&] { return sy.failed || pred(); });
@@ -1697,10 +1699,8 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     // The last stage group drains with four chains: after its stage nothing else is left
     // for the GPU, and its pairs' phase B would otherwise run two after two on each chain
     // (FCCF_DRAIN4=0: two chains throughout, dev A/B)
-    static const bool drain4_env = [] {
-      const char* e = std::getenv("FCCF_DRAIN4");
-      return !(e && e[0] == '0');
-    }();
+    const char* d4e = std::getenv("FCCF_DRAIN4");  // (read per batch: tests switch it)
+    const bool drain4_env = !(d4e && d4e[0] == '0');
     const int glast = ng - 1;
     const bool drain4 = drain4_env && ng >= 2 && cnt(glast) >= 3;
     auto drained = [&](int i) { return drain4 && i / PP == glast && i % PP >= 2; };  // pairs of workers 2, 3
@@ -1712,6 +1712,9 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
         const int i = glast * PP + k;
         if (i >= n) return;
         wait_until([&] { return sy.ready > glast; });
+        // the slot's previous pair (two groups back) ran on worker 0 or 1: its B2 reads
+        // the slot's phase-B state and fine mailbox, which this B1 rewrites
+        if (i >= 2 * PP) wait_until([&] { return sy.b2[(size_t)(i - 2 * PP)] != 0; });
         phase_b1(c, slot(i), P, T_out + 16 * (size_t)i, stats ? stats + i : nullptr, [] {}, ch);
         update([&] { ++sy.b1[(size_t)glast]; });
         if (phase_b2(c, slot(i), true)) update([&] { redo.push_back(i); });
@@ -1740,10 +1743,22 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
           update([&] { sy.submitted = g + 2; });
         }, ch);
         update([&] { ++sy.b1[(size_t)g]; });
-        if (pending >= 0 && phase_b2(c, slot(pending), true)) update([&] { redo.push_back(pending); });
+        if (pending >= 0) {
+          const bool rd = phase_b2(c, slot(pending), true);
+          update([&] {
+            if (rd) redo.push_back(pending);
+            sy.b2[(size_t)pending] = 1;
+          });
+        }
         pending = i;
       }
-      if (pending >= 0 && phase_b2(c, slot(pending), true)) update([&] { redo.push_back(pending); });
+      if (pending >= 0) {
+        const bool rd = phase_b2(c, slot(pending), true);
+        update([&] {
+          if (rd) redo.push_back(pending);
+          sy.b2[(size_t)pending] = 1;
+        });
+      }
     };
     auto guarded_worker = [&](int k) {
       try {

@@ -525,3 +525,26 @@ def test_mailbox_flags_and_event_waits_agree(ctx, oracle, fccf, monkeypatch):
         for T, x in zip(Tb, sb):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"batch, FCCF_SPIN_US={spin!r}")
             assert 0.0 < x.dev_ms[3] < 1000.0, (spin, list(x.dev_ms))
+
+
+@pytest.mark.parametrize("drain4", ["1", "0"])
+def test_batch_drain_with_four_chains(ctx, oracle, fccf, monkeypatch, drain4):
+    """A batch whose last stage group holds three or four pairs drains with four phase-B
+    chains (pipeline.cpp; FCCF_DRAIN4=0: two).  Its third and fourth pairs reuse the
+    slots of pairs two groups back, whose phase B2 ran on the other workers.  Every T
+    equals the oracle's, for 11 pairs (groups 4 + 4 + 3) and 12 (4 + 4 + 4).  Distinct
+    pairs, so a result read from another pair's slot would show."""
+    monkeypatch.setenv("FCCF_DRAIN4", drain4)
+    base_src, base_tar, _ = fccf.synth_pair(40_000)
+    rng = np.random.default_rng(31)
+    pairs, refs = [], []
+    for k in range(12):
+        jit = rng.normal(0, 0.003, base_src.shape).astype(np.float32)
+        s, t = (base_src + jit).astype(np.float32), base_tar[: 34_000 + 500 * k]
+        pairs.append((s, t))
+        refs.append(oracle.Run(s, t, 0.1, oracle.INTROSORT).T)
+    for n in (11, 12):
+        Tb, sb = ctx.register_batch(pairs[:n], 0.1)
+        for i, (T, ref) in enumerate(zip(Tb, refs)):
+            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"n={n} pair {i}")
+        assert all(x.K > 0 for x in sb)
