@@ -31,7 +31,9 @@
 //              partitions, register-resident subtrees of <= 64, stable leaf sort).
 // HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); the block and wave
 // kernels read and write each element once more each (8 + 8 B).
-#define KT_TU 9  // ktrace.h source tag
+#ifndef KT_TU
+#define KT_TU 9  // ktrace.h source tag (introsort_b2.hip: 13)
+#endif
 #include <cstdio>
 #include <cstdlib>
 
@@ -2259,7 +2261,10 @@ __device__ bool distinct_keys(BlockLds& S, const uint32_t* K, uint32_t* T0, uint
 
 // One workgroup per remaining segment: the final children of the last round first
 // (they may exceed IS_LCAP), then the owned list, dequeued from ctl[1].
-__global__ void __launch_bounds__(IS_OT) k_is_block(B4<uint32_t*> K02, B4<uint32_t*> V02, B4<uint32_t*> K12,
+#ifndef IS_BLOCK_WPE
+#define IS_BLOCK_WPE 1
+#endif
+__global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_BLOCK_WPE))) k_is_block(B4<uint32_t*> K02, B4<uint32_t*> V02, B4<uint32_t*> K12,
                                                     B4<uint32_t*> V12, B4<IsBufs> W2, int R) {
   KT();
   __shared__ BlockLds S;
@@ -2503,6 +2508,17 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
 
 }  // namespace
 
+#ifdef IS_KERNEL_VARIANT
+// introsort_b2.hip: this file's kernels again with 512-thread block-kernel workgroups at
+// two per CU; only the block kernel's launch is taken from this form
+void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<IsBufs> b, int R,
+                        hipStream_t st, int nbatch) {
+  ProbeBytes pb;  // algorithmic bytes: each element's key and value read once and written once
+  for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0);
+  const int blocks = std::max(1, 2 * IS_OWN_BLOCKS / nbatch);
+  FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+}
+#else
 uint32_t introsort_tier() {
   static const uint32_t t = [] {
     const char* s = std::getenv("FCCF_IS_TIER");  // dev: round threshold (default 4096)
@@ -2657,8 +2673,19 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
     return s ? std::atoi(s) : 0;
   }();
   const int own_blocks = std::max(1, (block_grid > 0 ? block_grid : IS_OWN_BLOCKS) / nbatch);
-  FCCF_LAUNCH("k_is_block", (pb_ctl(20, 16.0)), k_is_block,
-              dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+  // Stage groups of three or four pairs (six or eight clouds per launch): the block
+  // kernel's second form, 512-thread workgroups at two per CU (introsort_b2.hip), whose
+  // items interleave their partition chains on each CU: pipelined 0.650-0.654 against
+  // 0.658-0.665 ms per registration; single registrations (two clouds: few items per
+  // workgroup) keep the 1024-thread form, 0.726 against 0.778 ms (profiles/r05ap).
+  // FCCF_IS_BLOCK_B2=0 / 1: never / always (dev, tests)
+  const char* b2e = std::getenv("FCCF_IS_BLOCK_B2");
+  const bool b2 = b2e ? b2e[0] == '1' : nbatch >= 6;
+  if (b2 && block_grid <= 0)
+    introsort_block_b2(k0, v0, k1, v1, b, R, st, nbatch);
+  else
+    FCCF_LAUNCH("k_is_block", (pb_ctl(20, 16.0)), k_is_block,
+                dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
   // dev: FCCF_IS_WAVE_GRID = workgroups per launch, split over the clouds (default
   // IS_WAVE_BLOCKS per cloud)
@@ -2671,6 +2698,8 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
               dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
 }
+
+#endif  // IS_KERNEL_VARIANT
 
 }  // namespace fccf
 

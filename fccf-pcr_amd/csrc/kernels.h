@@ -109,6 +109,9 @@ int introsort_rounds(uint32_t cap);
 // positions -- exactly as std::sort orders PCL's index vector of the finite points;
 // the result is left in (k0, v0) with the invalid keys after it.  (k1, v1) are the
 // other buffer.  exact_gate: sort only if P->unsorted (the presorted second pass).
+// k_is_block in its second form (introsort_b2.hip: 512-thread workgroups, two per CU)
+void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<IsBufs> b, int R,
+                        hipStream_t st, int nbatch);
 void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n,
                    B4<const VGParams*> P, uint32_t cap, B4<IsBufs> b, hipStream_t st, int nbatch, bool exact_gate);
 
