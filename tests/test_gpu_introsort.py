@@ -73,6 +73,22 @@ def test_sort_keys_equals_std_sort(ctx, fccf, oracle):
 
 
 @pytest.mark.gpu
+def test_block_kernel_second_form_equals_std_sort(ctx, fccf, oracle, monkeypatch):
+    """The block kernel's second form (introsort_b2.hip: 512-thread workgroups, two per CU;
+    stage groups of three or four pairs use it) forced for every sort (FCCF_IS_BLOCK_B2=1)
+    on every case and a c3 downsample, against the oracle's std::sort."""
+    monkeypatch.setenv("FCCF_IS_BLOCK_B2", "1")
+    bad = [name for name, k in _keys_cases(fccf, oracle).items()
+           if not np.array_equal(ctx.sort_keys(k), oracle.sort_pairs(k))]
+    assert not bad, bad
+    c = fccf.CONFIGS["c3"]
+    src, _, _ = fccf.synth_pair(c["n"], c["room"])
+    out = ctx.downsample(src, c["leaf"])
+    ref, _ = oracle.voxel_grid(src, c["leaf"], oracle.INTROSORT)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_sort_keys_exact_gate_equals_std_sort(ctx, fccf, oracle):
     """The presorted pass's single-workgroup form (no rounds) on the same cases."""
     bad = []
