@@ -339,7 +339,10 @@ constexpr uint32_t VFIT_BLOCKS = 512;  // 2048 waves per cloud; leaves are a few
 // LDS as (x, y, z, 1) so every lane computes term = p[i1] * p[i2] (the linear sums
 // use i2 = w = 1, and x * 1 == x exactly).  compute3DCentroid (:490) is the same
 // sequential x/y/z sum divided by n, i.e. accumulators 6..8 / n bit-for-bit.
-__global__ void __launch_bounds__(256) k_voxel_fit(B4<FaceBufs> fb, float vpt, float cthr) {
+#ifndef VFIT_WPE
+#define VFIT_WPE 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VFIT_WPE))) k_voxel_fit(B4<FaceBufs> fb, float vpt, float cthr) {
   KT();
   constexpr uint32_t VB = 256;  // points per LDS burst of a wave (four per lane)
   __shared__ __attribute__((aligned(16))) float pts[4][VB * 4];

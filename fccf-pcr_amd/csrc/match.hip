@@ -245,7 +245,10 @@ __global__ void __launch_bounds__(1024) k_match_scan(const MatchIn* __restrict__
   }
 }
 
-__global__ void __launch_bounds__(256) k_match_emit(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
+#ifndef EMIT_WPE
+#define EMIT_WPE 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EMIT_WPE))) k_match_emit(const MatchIn* __restrict__ Mp, const uint32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ type, const uint32_t* __restrict__ off,
                                                     MCand* __restrict__ c0, MCand* __restrict__ c1,
                                                     MCand* __restrict__ c2, QTd* __restrict__ q0,
