@@ -320,8 +320,9 @@ struct PhaseB {
 
 // A phase-B chain: what one pair's phase B1 uses exclusively.  A pipelined batch runs
 // two chains on two host threads (alternate pairs), so two pairs' host stages (growth,
-// clustering, the LM) overlap; a single registration, or a batch whose ctx needs the
-// one-chain form (group, probe, debug, the device growth/LM forms), uses chain 0.  The
+// clustering, the LM) overlap, and its last stage group drains with four (chains 2 and 3
+// on two more threads, quarter pools); a single registration, or a batch whose ctx needs
+// the one-chain form (group, probe, debug, the device growth/LM forms), uses chain 0.  The
 // matching stream sb is shared: each chain waits for its own work by its event.
 struct Chain {
   Pool* pool;
@@ -1666,7 +1667,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     c->enq.wait();
     if (phase_b2(c, slot(n - 1), true)) redo.push_back(n - 1);
   } else {
-    // Two chains: pair i's phase B on worker i % 2 (this thread and c->b1w), each worker
+    // Two chains (four in the drain, below): pair i's phase B on worker i % 2 (this thread and c->b1w), each worker
     // running B1 of its next pair before B2 of its previous one (fine verification
     // overlaps).  The first pair of a group still enqueues the next group's stage, which
     // recycles the slots of the group before: it waits until every pair of that group has
