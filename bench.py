@@ -267,7 +267,7 @@ def width_table(widths):
     return out
 
 
-PROBE_BATCH = 8  # registrations per pre-pass window: two stage groups of four pairs
+PROBE_BATCH = 10  # registrations per pre-pass window: two stage groups of five pairs
 
 SHARDED_PLAN = (("c4", 4), ("c5", 8))  # BASELINE configs[3]/[4]: the pair and its rank count (capped at N)
 
@@ -420,7 +420,7 @@ def sharded_pass(dist, ws, rank, local, args, timeout_s):
             one = rs[0].get("one_gpu_ms_per_registration")
             one1 = rs[0].get("one_gpu_ms_per_registration_pp1")
             ms = el / args.steps * 1e3
-            # both sides batch four pairs per cloud stage (the group form does since round 5);
+            # both sides batch five pairs per cloud stage (the group form does since round 5);
             # the one-GPU figure at one pair per stage is reported beside it
             out[cfg_name] = {"ranks": ranks, "ms_per_registration": ms,
                              "e2e_ms_median": statistics.median(e2e) * 1e3,
@@ -542,7 +542,7 @@ def main():
     pipelined = not args.no_pipeline and not args.selftest
     # Untimed pre-pass: GPU time per step of every probed kernel (HIP events around
     # each launch; probed calls launch eagerly, see csrc/probe.h), in the timed region's
-    # own shape: a pipelined batch (four pairs per cloud stage, eight clouds per launch)
+    # own shape: a pipelined batch (five pairs per cloud stage, ten clouds per launch)
     # of PROBE_BATCH registrations, or single registrations with --no-pipeline.  The
     # roofline kernel is the one with the most GPU time per step (or --probe-kernel).
     table, probe = {}, None
@@ -560,7 +560,7 @@ def main():
     for _ in range(args.warmup):
         T, st = reg()
     if pipelined and args.warmup:
-        # the timed batch's own shape: every stage group of it (up to four pairs per cloud
+        # the timed batch's own shape: every stage group of it (up to five pairs per cloud
         # stage, groups on alternating workspaces, a smaller last group) captures its
         # graphs here, not in the timed batch
         batch(args.steps)
@@ -593,6 +593,9 @@ def main():
             stage_rl = stage_roofline(st1)
     if not args.selftest:
         assert np.array_equal(T1.view(np.uint32), np.asarray(T).view(np.uint32)), "pipelined result differs"
+        if pipelined:  # every registration of the timed batch (the same pair), not only the last
+            assert all(np.array_equal(np.asarray(x).view(np.uint32), T1.view(np.uint32)) for x in Tb), \
+                "a pipelined registration's result differs"
     # PCIe-inclusive latency: the same registration from host arrays (fccf_register);
     # informational, never `value`
     per_host, h2d = [], []

@@ -288,8 +288,8 @@ struct CachedGraph {
 struct fccf_ctx {
   int device = 0;
   // Pair slots.  A cloud stage (both VoxelGrid passes, centroid, face voxels) runs the
-  // clouds of up to PAIRS_MAX = 4 pairs in the same launches (a pipelined batch groups
-  // them: the sort's dependent rounds are paid once for eight clouds); stage group G
+  // clouds of up to PAIRS_MAX = 5 pairs in the same launches (a pipelined batch groups
+  // them: the sort's dependent rounds are paid once for ten clouds); stage group G
   // uses slots PAIRS_MAX * G + j (j < PAIRS_MAX), and the group's shared resources (arena
   // of its clouds, stage graphs, fork/join events) live in its first slot, PAIRS_MAX * G.
   // Two groups double-buffer, so a batch can
@@ -308,14 +308,14 @@ struct fccf_ctx {
                                      // (capture-internal)
     hipEvent_t tev[6] = {};          // timing: [4] fine start, [5] fine done (fccf_stats::dev_ms[3]);
                                      // the cloud stage's spans are device stamps (CloudMail::stamp)
-    fccf::CachedGraph g_seg[4];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs, one graph
+    fccf::CachedGraph g_seg[5];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs, one graph
                                      // per pair count: part A (the VoxelGrid passes; with a group attached,
                                      // the whole stage)
-    fccf::CachedGraph g_segb[4];     // and part B (centroid sums beside the face voxels, orientation)
+    fccf::CachedGraph g_segb[5];     // and part B (centroid sums beside the face voxels, orientation)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight
-  } cs[8];                           // two stage groups of up to PAIRS_MAX pair slots (pipeline.cpp)
+  } cs[10];                           // two stage groups of up to PAIRS_MAX pair slots (pipeline.cpp)
   hipStream_t sa[4] = {};            // cloud stage streams: [0] part A, [2] part B, [3] B's centroid branch
                                      // (a capture fork; replays schedule it), [1] fine verification
   hipStream_t sb = nullptr;          // matching, copies, stage exports

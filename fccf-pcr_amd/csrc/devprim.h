@@ -39,7 +39,7 @@ SortScratch sort_scratch_carve(void* base, uint32_t cap);
 // dependent kernels interfere, so one stream of batched launches is the fast shape).
 // A single value converts to a batch of one; entries past the ones given repeat the
 // last (never read: problems past nbatch do not run).
-constexpr int BMAX = 8;
+constexpr int BMAX = 10;
 template <class T>
 struct B4 {
   T v[BMAX];

@@ -77,7 +77,7 @@ struct Group {
   // sharded fine verification, per pair slot s (the pipelined batch overlaps pairs):
   // this rank's block of scores + its error word (FE_BLK floats), all ranks' blocks
   static constexpr int FE_BLK = MAX_EVAL + 1;
-  static constexpr int SLOTS = 8;  // the ctx's pair slots (fccf_ctx::cs)
+  static constexpr int SLOTS = 10;  // the ctx's pair slots (fccf_ctx::cs)
   float* d_fsend[SLOTS] = {};
   float* d_frecv[SLOTS] = {};  // n x FE_BLK
   float* h_frecv[SLOTS] = {};  // pinned copies

@@ -2673,7 +2673,7 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
     return s ? std::atoi(s) : 0;
   }();
   const int own_blocks = std::max(1, (block_grid > 0 ? block_grid : IS_OWN_BLOCKS) / nbatch);
-  // Stage groups of three or four pairs (six or eight clouds per launch): the block
+  // Stage groups of three to five pairs (six to ten clouds per launch): the block
   // kernel's second form, 512-thread workgroups at two per CU (introsort_b2.hip), whose
   // items interleave their partition chains on each CU: pipelined 0.650-0.654 against
   // 0.658-0.665 ms per registration; single registrations (two clouds: few items per

@@ -55,12 +55,12 @@ struct FineMail {
 };
 
 struct HostMail {
-  CloudMail clouds[8];  // per pair slot; a stage group's slots are adjacent (k_compact_planar)
+  CloudMail clouds[10];  // per pair slot; a stage group's slots are adjacent (k_compact_planar)
   MatchMail match;      // phase-B chain 0 (pipeline.cpp Chain)
   MatchMail match2;     // chain 1: a pipelined batch's second host thread
   MatchMail match3;     // chains 2 and 3: the batch's last stage group (four chains)
   MatchMail match4;
-  FineMail fine[8];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
+  FineMail fine[10];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
 };
 
 }  // namespace fccf

@@ -101,7 +101,7 @@ namespace {
 // PAIRS_MAX slots (ctx CloudSets, mailboxes).  FCCF_PAIR_BATCH=1..PAIRS_MAX overrides
 // the default.
 constexpr int PAIRS_MAX = BMAX / 2;
-constexpr int PAIRS_DEFAULT = 4;
+constexpr int PAIRS_DEFAULT = 5;
 static_assert(sizeof(((fccf_ctx*)nullptr)->cs) / sizeof(((fccf_ctx*)nullptr)->cs[0]) == 2 * PAIRS_MAX, "slots");
 static_assert(sizeof(HostMail::clouds) / sizeof(CloudMail) == 2 * PAIRS_MAX, "cloud mailboxes");
 static_assert(sizeof(HostMail::fine) / sizeof(FineMail) == 2 * PAIRS_MAX, "fine mailboxes");
@@ -1597,9 +1597,9 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
   } join_guard{c};
   if (c->group) order_reset(c->group);
-  // Pairs per cloud stage: four -- their eight clouds in the same launches, so the
+  // Pairs per cloud stage: five -- their ten clouds in the same launches, so the
   // sort's dependent rounds and the face stage's small launches are paid once for all
-  // (DESIGN.md §12); FCCF_PAIR_BATCH=1..4.  With a group the sharded stages gather
+  // (DESIGN.md §12, §13); FCCF_PAIR_BATCH=1..5.  With a group the sharded stages gather
   // every cloud of the stage in one exchange (group.cpp); a probe keeps the batch's own
   // launch width (its byte counts sum over every cloud of a launch, probe.h).
   const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
@@ -1704,7 +1704,8 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     const bool drain4_env = !(d4e && d4e[0] == '0');
     const int glast = ng - 1;
     const bool drain4 = drain4_env && ng >= 2 && cnt(glast) >= 3;
-    auto drained = [&](int i) { return drain4 && i / PP == glast && i % PP >= 2; };  // pairs of workers 2, 3
+    // pairs 2 and 3 of the last group go to workers 2 and 3; a fifth stays with worker 0 or 1
+    auto drained = [&](int i) { return drain4 && i / PP == glast && (i % PP == 2 || i % PP == 3); };
     auto worker = [&](int k) {
       HIP_CHECK(hipSetDevice(c->device));
       const Chain& ch = chains[k];

@@ -433,7 +433,7 @@ class Ctx:
         _check(_lib.fccf_probe_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b)), "fccf_probe_read", self._h)
         return ms.value, n.value, b.value
 
-    def probe_read_widths(self, max_width=8):
+    def probe_read_widths(self, max_width=16):
         """{width: (total_ms, launches, total_algorithmic_bytes)} since set_probe, per
         launch width (clouds per batched launch), widths with launches only."""
         ms = np.zeros(max_width, np.float64)

@@ -75,7 +75,7 @@ def test_sort_keys_equals_std_sort(ctx, fccf, oracle):
 @pytest.mark.gpu
 def test_block_kernel_second_form_equals_std_sort(ctx, fccf, oracle, monkeypatch):
     """The block kernel's second form (introsort_b2.hip: 512-thread workgroups, two per CU;
-    stage groups of three or four pairs use it) forced for every sort (FCCF_IS_BLOCK_B2=1)
+    stage groups of three to five pairs use it) forced for every sort (FCCF_IS_BLOCK_B2=1)
     on every case and a c3 downsample, against the oracle's std::sort."""
     monkeypatch.setenv("FCCF_IS_BLOCK_B2", "1")
     bad = [name for name, k in _keys_cases(fccf, oracle).items()

@@ -429,7 +429,7 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
     clouds_enqueue_group).  Pairs of different sizes within a group, single
     registrations between batches (the one-pair and two-pair stages lay the workspace
     out differently, so their cached graphs must never be mixed), and the other stage
-    forms (FCCF_PAIR_BATCH=1, 3, 4: up to eight clouds per launch) must all give the
+    forms (FCCF_PAIR_BATCH=1, 3, 4, 5: up to ten clouds per launch) must all give the
     oracle's T bit for bit."""
     base_src, base_tar, _ = fccf.synth_pair(90_000)
 
@@ -458,7 +458,7 @@ def test_pair_batched_stages_equal_single_registrations(ctx, oracle, fccf, monke
     Tb, _ = ctx.register_batch(pairs[:2], 0.1)  # one group of two
     for T, ref in zip(Tb, refs[:2]):
         np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32))
-    for pp in ("1", "3", "4"):  # one pair per stage, and three or four (up to 8 clouds per launch)
+    for pp in ("1", "3", "4", "5"):  # one pair per stage, and three to five (up to 10 clouds per launch)
         monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
         Tb1, sb1 = ctx.register_batch(pairs, 0.1)
         for T, ref in zip(Tb1, refs):
@@ -528,22 +528,26 @@ def test_mailbox_flags_and_event_waits_agree(ctx, oracle, fccf, monkeypatch):
 
 
 @pytest.mark.parametrize("drain4", ["1", "0"])
-def test_batch_drain_with_four_chains(ctx, oracle, fccf, monkeypatch, drain4):
-    """A batch whose last stage group holds three or four pairs drains with four phase-B
-    chains (pipeline.cpp; FCCF_DRAIN4=0: two).  Its third and fourth pairs reuse the
-    slots of pairs two groups back, whose phase B2 ran on the other workers.  Every T
-    equals the oracle's, for 11 pairs (groups 4 + 4 + 3) and 12 (4 + 4 + 4).  Distinct
-    pairs, so a result read from another pair's slot would show."""
+@pytest.mark.parametrize("pp,ns", [("4", (11, 12)), ("5", (13, 14, 15))])
+def test_batch_drain_with_four_chains(ctx, oracle, fccf, monkeypatch, drain4, pp, ns):
+    """A batch whose last stage group holds three to five pairs drains with four phase-B
+    chains (pipeline.cpp; FCCF_DRAIN4=0: two).  Its third and fourth pairs go to the
+    drain's own workers and reuse the slots of pairs two groups back, whose phase B2 ran
+    on the other workers; a fifth stays with the first two workers.  Every T equals the
+    oracle's, for groups 4 + 4 + 3 and 4 + 4 + 4 at four pairs per stage, and 5 + 5 + 3,
+    5 + 5 + 4 and 5 + 5 + 5 at five (the default).  Distinct pairs, so a result read from
+    another pair's slot, or a pair left out, would show."""
     monkeypatch.setenv("FCCF_DRAIN4", drain4)
+    monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
     base_src, base_tar, _ = fccf.synth_pair(40_000)
     rng = np.random.default_rng(31)
     pairs, refs = [], []
-    for k in range(12):
+    for k in range(max(ns)):
         jit = rng.normal(0, 0.003, base_src.shape).astype(np.float32)
         s, t = (base_src + jit).astype(np.float32), base_tar[: 34_000 + 500 * k]
         pairs.append((s, t))
         refs.append(oracle.Run(s, t, 0.1, oracle.INTROSORT).T)
-    for n in (11, 12):
+    for n in ns:
         Tb, sb = ctx.register_batch(pairs[:n], 0.1)
         for i, (T, ref) in enumerate(zip(Tb, refs)):
             np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"n={n} pair {i}")

@@ -2,7 +2,7 @@
 # Round-5 roofline evidence (via gpurun): rocprofv3 kernel stats of the
 # exact bench command, per-kernel durations split by launch width (Grid_Size_Y = clouds per
 # launch), and the size-bucketed PMC traffic passes over tools/pmc_batch.py (pipelined
-# batches only: eight clouds per launch, the timed region's shape).
+# batches only: ten clouds per launch, the timed region's shape).
 # Usage: bash tools/gpu_prof_r05.sh <tag> [STATS=1] [PMC=1]
 set -o pipefail
 TAG=${1:-r05p}
@@ -20,9 +20,9 @@ if [ "${STATS:-1}" = 1 ]; then
 fi
 if [ "${PMC:-1}" = 1 ]; then
   step pmc
-  CALIB=0 BATCH=1 STEPS=${STEPS:-8} bash tools/gpu_pmc_calib.sh $TAG/pmc || exit 1
+  CALIB=0 BATCH=1 STEPS=${STEPS:-10} bash tools/gpu_pmc_calib.sh $TAG/pmc || exit 1
   cp $OUT/pmc/bench_p1.json $OUT/pmc/pmc_batch_p1.json
-  python3 tools/pmc_traffic.py $OUT/pmc c3 $OUT/pmc/pmc_traffic.json 0.05 8 > $OUT/pmc/pmc_traffic.txt
+  python3 tools/pmc_traffic.py $OUT/pmc c3 $OUT/pmc/pmc_traffic.json 0.05 10 > $OUT/pmc/pmc_traffic.txt
   cat $OUT/pmc/pmc_traffic.txt | head -12
   rm -rf $OUT/pmc/bench_p?
 fi

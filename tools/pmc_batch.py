@@ -1,5 +1,5 @@
 """PMC workload of the timed region's own shape: pipelined batches
-of one config's pair, four pairs per cloud stage (eight clouds per launch), and nothing
+of one config's pair, five pairs per cloud stage (ten clouds per launch), and nothing
 else -- no single registrations, whose two-cloud launches would mix into the per-kernel
 means.  Run under rocprofv3 --pmc (tools/gpu_pmc_calib.sh BATCH=1); prints one JSON line
 whose kernel_table carries the probe's algorithmic bytes per launch at that width, the
@@ -27,7 +27,7 @@ with F.Ctx(0) as ctx:
     table = {}
     for k in kernels:  # algorithmic bytes per launch at the batch's width (probe.h)
         ctx.set_probe(k)
-        ctx.register_batch(pairs[:4], cfg["leaf"], on_device=True)
+        ctx.register_batch(pairs[:10], cfg["leaf"], on_device=True)  # two full stage groups
         w = ctx.probe_read_widths()
         if w:
             width = max(w, key=lambda x: w[x][1])

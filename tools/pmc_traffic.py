@@ -5,8 +5,8 @@ Usage:
   python tools/pmc_traffic.py PMC_DIR CONFIG OUT.json [MIN_FRAC] [WIDTH]
 
 WIDTH (default 2): the clouds per launch of the workload's cloud-stage kernels -- 2 for
-single registrations (the bench command with --no-pipeline), 8 for tools/pmc_batch.py
-(four pairs per stage, the timed region's shape); recorded in OUT.json for bench.py.
+single registrations (the bench command with --no-pipeline), 10 for tools/pmc_batch.py
+(five pairs per stage, the timed region's shape; 8 in the summaries before r05au); recorded in OUT.json for bench.py.
 
 PMC_DIR holds bench_p1 .. bench_p4, one counter pass per process (rocprofv3 does not
 split counters over passes, and a pass holds at most 4 TCC counters):
