@@ -400,11 +400,12 @@ def test_virtual_rank_failure_ends_every_rank(fccf, pair, monkeypatch, site, sil
             cx.close()
 
 
-@pytest.mark.parametrize("n,cfg,npairs", [(2, "c2", 6), (3, "c3", 5)])
-def test_virtual_ranks_pair_batched_stages(fccf, oracle, monkeypatch, n, cfg, npairs):
+@pytest.mark.parametrize("n,cfg,npairs,pp", [(2, "c2", 6, "4"), (3, "c3", 5, "4"), (2, "c2", 7, "5")])
+def test_virtual_ranks_pair_batched_stages(fccf, oracle, monkeypatch, n, cfg, npairs, pp):
     """a group no longer forces one pair per cloud stage.  With rows D
-    and P sharded (FCCF_SHARD_D_MIN=0) and four pairs per stage (FCCF_PAIR_BATCH=4:
-    stage groups of 4 and the remainder), every cloud of a stage is gathered in one
+    and P sharded (FCCF_SHARD_D_MIN=0) and four or five pairs per stage (FCCF_PAIR_BATCH:
+    stage groups of that size and the remainder; five, ten clouds per exchange, is the
+    default the driver's sharded leg runs), every cloud of a stage is gathered in one
     exchange, and the next stage's gathers wait for all of this stage's phase-B1
     collectives (one issue order per rank).  Every rank's T equals the oracle's bit for
     bit."""
@@ -418,7 +419,7 @@ def test_virtual_ranks_pair_batched_stages(fccf, oracle, monkeypatch, n, cfg, np
         pairs.append(((src + jit).astype(np.float32), tar[: len(tar) - 1000 * (k + 1)]))
     refs = [oracle.Run(s, t, leaf, oracle.INTROSORT).T.copy() for s, t in pairs]
     monkeypatch.setenv("FCCF_SHARD_D_MIN", "0")
-    monkeypatch.setenv("FCCF_PAIR_BATCH", "4")
+    monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
     ctxs = [fccf.Ctx(0) for _ in range(n)]
     try:
         groups = fccf.local_groups(ctxs)
