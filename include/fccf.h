@@ -275,7 +275,8 @@ int fccf_ctx_set_probe(fccf_ctx* ctx, const char* kernel);
 int fccf_probe_read(fccf_ctx* ctx, double* total_ms, int64_t* launches, double* total_bytes);
 /* The same totals split by launch width w = 1..max_width (entry w - 1): the clouds one
  * batched launch processes (grid.y of the cloud stage's kernels; a single registration
- * launches two, a pipelined batch of four pairs per stage eight). */
+ * launches two, a pipelined batch of five pairs per stage ten; widths past 16 are not
+ * tallied). */
 int fccf_probe_read_widths(fccf_ctx* ctx, int max_width, double* ms, int64_t* launches, double* bytes);
 
 /* Named intermediate of the last fccf_register call with debug on (see DESIGN.md
