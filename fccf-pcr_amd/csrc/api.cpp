@@ -159,6 +159,24 @@ static int guarded(fccf_ctx* c, F&& f) {
   }
 }
 
+// The host-only stage exports (grow + selection + select_base, transform_cluster,
+// fusion): the product's host code, which needs no device, so ctx may be null there
+// (then no device form is selectable and no error message is kept).
+template <class F>
+static int host_guarded(fccf_ctx* c, F&& f) {
+  if (c) return guarded(c, f);
+  try {
+    f();
+    return FCCF_OK;
+  } catch (const Error& e) {
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    return FCCF_E_OOM;
+  } catch (...) {
+    return FCCF_E_INTERNAL;
+  }
+}
+
 extern "C" const char* fccf_ctx_last_error(fccf_ctx* c) { return c ? c->last_error.c_str() : ""; }
 
 namespace {
@@ -535,17 +553,17 @@ extern "C" int fccf_stage_voxel_planes(fccf_ctx* c, const float* xyz, int64_t n,
 extern "C" int fccf_stage_grow(fccf_ctx* c, const fccf_voxel* vox, int64_t nv, int side, const fccf_params* params,
                                fccf_plane* planes, int cap_planes, int* n_planes, double* theta, fccf_base* bases,
                                int cap_bases, int* n_bases) {
-  if (!c || (!vox && nv) || nv < 0 || nv > (int64_t)0x7FFFFFFF || (side != 1 && side != 2) || !n_planes ||
+  if ((!vox && nv) || nv < 0 || nv > (int64_t)0x7FFFFFFF || (side != 1 && side != 2) || !n_planes ||
       !n_bases || cap_planes < 0 || cap_bases < 0 || (cap_planes && !planes) || (cap_bases && !bases))
     return FCCF_E_ARG;
   fccf_params P;
   if (params) P = *params;
   else fccf_params_default(&P);
-  return guarded(c, [&] {
+  return host_guarded(c, [&] {
     std::vector<VoxRec> v((size_t)nv);
     if (nv) std::memcpy(v.data(), vox, sizeof(VoxRec) * (size_t)nv);
     GrowOut g;
-    if (c->grow_device && nv <= (int64_t)GROW_CAP) {  // K4 on the device (grow.hip)
+    if (c && c->grow_device && nv <= (int64_t)GROW_CAP) {  // K4 on the device (grow.hip)
       hipStream_t st = c->sb;
       VoxRec* d = nullptr;
       if (hipMalloc((void**)&d, sizeof(VoxRec) * (size_t)std::max<int64_t>(nv, 1)) != hipSuccess)
@@ -766,12 +784,12 @@ extern "C" int fccf_group_stage_match(fccf_group* g, const fccf_plane* F1, int n
 extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int cluster_num,
                                   const fccf_params* params, float* fine, int64_t cap, int64_t* n_fine,
                                   int64_t* n_clusters) {
-  if (!c || (!cand && n) || n < 0 || n > (int64_t)0x7FFFFFFF || cap < 0 || (cap && !fine) || !n_fine)
+  if ((!cand && n) || n < 0 || n > (int64_t)0x7FFFFFFF || cap < 0 || (cap && !fine) || !n_fine)
     return FCCF_E_ARG;
   fccf_params P;
   if (params) P = *params;
   else fccf_params_default(&P);
-  return guarded(c, [&] {
+  return host_guarded(c, [&] {
     std::vector<QT> in((size_t)n), out;
     for (int64_t i = 0; i < n; ++i) {
       m44 T;
@@ -781,7 +799,7 @@ extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int
     }
     int64_t ncl = 0;
     bool done = false;
-    if (c->cluster_device && n > 0) {  // f3: radius search, seeds, sort and averaging on the device
+    if (c && c->cluster_device && n > 0) {  // f3: radius search, seeds, sort and averaging on the device
       hipStream_t st = c->sb;
       MatchMail* mm = match_mail(c);
       const size_t nn = (size_t)n;
@@ -813,7 +831,7 @@ extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int
         done = true;
       }
     }
-    if (!done) transform_cluster(in, out, cluster_num, P, &ncl, &c->pool, nullptr);
+    if (!done) transform_cluster(in, out, cluster_num, P, &ncl, c ? &c->pool : nullptr, nullptr);
     *n_fine = (int64_t)out.size();
     if (n_clusters) *n_clusters = ncl;
     for (int64_t i = 0; i < std::min(*n_fine, cap); ++i) {
@@ -821,6 +839,36 @@ extern "C" int fccf_stage_cluster(fccf_ctx* c, const float* cand, int64_t n, int
       const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
       std::memcpy(fine + 8 * i, a, sizeof a);
     }
+  });
+}
+
+// Fusion (FCCF.cpp:1546-1606, host): the caller's ranked, verified candidates of the
+// three types (18 floats each: row-major T, quick_verify score, fine_verify score).
+extern "C" int fccf_stage_fuse(fccf_ctx* c, const float* const cand[3], const int64_t n[3], int analyse_max,
+                               float T[16], float high[24]) {
+  if (!cand || !n || !T || analyse_max < 0) return FCCF_E_ARG;
+  for (int t = 0; t < 3; ++t)
+    if (n[t] < 0 || (n[t] && !cand[t])) return FCCF_E_ARG;
+  return host_guarded(c, [&] {
+    std::vector<TS> ctv[3];
+    for (int t = 0; t < 3; ++t)
+      for (int64_t i = 0; i < n[t]; ++i) {
+        TS x;
+        const float* r = cand[t] + 18 * i;
+        std::memcpy(x.T.m, r, sizeof x.T.m);
+        x.score = r[16];
+        x.score2 = r[17];
+        ctv[t].push_back(x);
+      }
+    std::vector<High> tmp;
+    const m44 R = fuse_types(ctv, analyse_max, &tmp);
+    std::memcpy(T, R.m, sizeof R.m);
+    if (high)
+      for (int t = 0; t < 3; ++t) {
+        const High& h = tmp[(size_t)t];
+        const float a[8] = {h.qt.qw, h.qt.qx, h.qt.qy, h.qt.qz, h.qt.tx, h.qt.ty, h.qt.tz, h.score};
+        std::memcpy(high + 8 * t, a, sizeof a);
+      }
   });
 }
 

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -121,6 +122,22 @@ inline hipError_t device_sync_guarded() {
 inline void guarded_stream_wait(hipStream_t st, hipEvent_t ev) {
   std::lock_guard<std::mutex> lk(capture_mutex());
   HIP_CHECK(hipStreamWaitEvent(st, ev, 0));
+}
+
+// A host wait on an event whose stream another thread may be capturing (the fine stream
+// sa[1], which every phase-B chain captures g_fine on): each query under the capture
+// lock, the lock released between queries so that a capture can proceed.
+inline void guarded_event_sync(hipEvent_t ev) {
+  for (;;) {
+    hipError_t e;
+    {
+      std::lock_guard<std::mutex> lk(capture_mutex());
+      e = hipEventQuery(ev);
+    }
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
 }
 
 // A host wait on a pinned mailbox flag that a stage's last kernel sets after a

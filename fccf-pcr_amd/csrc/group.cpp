@@ -72,38 +72,57 @@ struct NcclGroup {
   }
 };
 
+// The communicators stay valid while a thread uses them: comm() is taken through a Use
+// (per channel: the abort flag checked and a user count raised under the channel's
+// mutex), and abort() frees a communicator (ncclCommAbort) only once no thread is
+// inside an enqueue on it -- at once when idle, otherwise by the last user leaving.
+// abort() never waits for a user, so it cannot hang behind an enqueue that waits for a
+// peer.  (the helper thread could use a communicator that abort had freed.)
 struct RcclTransport : Transport {
   Group* g;
+  struct Chan {
+    std::mutex m;
+    int users = 0;
+    bool pending = false;  // aborted while in use: the last user frees it
+  } chan[CH_COUNT];
+  std::atomic<bool> dead{false};
   explicit RcclTransport(Group* g_) : g(g_) {}
-  ncclComm_t comm(int ch) {
-    if (!g->comm[ch]) throw Error(FCCF_E_RCCL, "group aborted: " + g->abort_why);
-    return g->comm[ch];
-  }
-  void bcasts(int ch, const GatherOp& op, hipStream_t st) {
-    ncclComm_t cm = comm(ch);
-    for (int r = 0; r < g->n; ++r) {
-      if (!op.counts[r]) continue;
-      char* dst = (char*)op.recv + op.offs[r];
-      NCCL_CHECK(ncclBroadcast(r == g->rank ? op.send : (const void*)dst, dst, op.counts[r], ncclUint8, r, cm, st));
+  struct Use {
+    RcclTransport* t;
+    int ch;
+    ncclComm_t c;
+    Use(RcclTransport* t_, int ch_) : t(t_), ch(ch_) {
+      std::lock_guard<std::mutex> lk(t->chan[ch].m);
+      c = t->g->comm[ch];
+      if (t->dead || !c) throw Error(FCCF_E_RCCL, "group aborted: " + group_why(t->g));
+      ++t->chan[ch].users;
     }
+    ~Use() {
+      std::lock_guard<std::mutex> lk(t->chan[ch].m);
+      if (--t->chan[ch].users == 0 && t->chan[ch].pending) t->free_comm(ch);
+    }
+  };
+  void free_comm(int ch) {  // (the channel's mutex held, no user)
+    ncclComm_t& c = g->comm[ch];
+    if (c) (void)ncclCommAbort(c);  // (also frees the communicator)
+    c = nullptr;
+    chan[ch].pending = false;
   }
   void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
                   hipStream_t st) override {
-    NcclGroup grp;
-    bcasts(ch, GatherOp{send, recv, counts, offs}, st);
-    grp.end();
-  }
-  void allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st) override {
-    NcclGroup grp;
-    for (int i = 0; i < nops; ++i) bcasts(ch, ops[i], st);
-    grp.end();
+    GatherOp op{send, recv, counts, offs};
+    allgatherv_multi(ch, &op, 1, st);
   }
   void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
-    NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm(ch), st));
+    Use u(this, ch);
+    NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, u.c, st));
+    rx_bytes[ch] += (int64_t)bytes * (g->n - 1);
   }
   int async_error() override {
-    for (ncclComm_t c : g->comm) {
-      if (!c) continue;
+    for (int ch = 0; ch < CH_COUNT; ++ch) {
+      std::lock_guard<std::mutex> lk(chan[ch].m);
+      ncclComm_t c = g->comm[ch];
+      if (!c || chan[ch].pending) continue;
       ncclResult_t r = ncclSuccess;
       if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return (int)ncclInternalError;
       if (r != ncclSuccess && r != ncclInProgress) return (int)r;
@@ -111,11 +130,12 @@ struct RcclTransport : Transport {
     return 0;
   }
   void abort() override {
-    for (ncclComm_t& c : g->comm)
-      if (c) {
-        (void)ncclCommAbort(c);  // (also frees the communicator)
-        c = nullptr;
-      }
+    dead = true;
+    for (int ch = 0; ch < CH_COUNT; ++ch) {
+      std::lock_guard<std::mutex> lk(chan[ch].m);
+      if (chan[ch].users == 0) free_comm(ch);
+      else chan[ch].pending = true;
+    }
   }
 };
 
@@ -204,6 +224,8 @@ struct LocalTransport : Transport {
       HIP_CHECK(hipMemcpyAsync((char*)recv + offs[g->rank], send, counts[g->rank], hipMemcpyDeviceToDevice, st));
     HIP_CHECK(hipStreamSynchronize(st));
     g->hub->barrier(ch, g->timeout_s);  // (the staging is rewritten by the next collective)
+    for (int r = 0; r < g->n; ++r)
+      if (r != g->rank) rx_bytes[ch] += (int64_t)counts[r];
   }
   void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) override {
     std::vector<size_t> counts((size_t)g->n, bytes), offs((size_t)g->n);
@@ -214,21 +236,147 @@ struct LocalTransport : Transport {
   void abort() override { g->hub->abort(); }
 };
 
+// ------------------------------------------------------------ packed all-gather-v
+
+namespace {
+// Up to CP_MAX (src, dst, bytes) copies per launch, passed by value (kernel arguments):
+// blockIdx.y = copy, the x blocks stride over it in 16-byte words when src, dst and the
+// size allow, else in 4-byte words, else bytes (a uniform branch per copy).
+constexpr int CP_MAX = 64;
+struct CopyDesc {
+  const char* src;
+  char* dst;
+  uint64_t bytes;
+};
+struct CopyBatch {
+  int n;
+  CopyDesc d[CP_MAX];
+};
+
+__global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b) {
+  if ((int)blockIdx.y >= b.n) return;
+  const CopyDesc c = b.d[blockIdx.y];
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t al = (uint64_t)c.src | (uint64_t)c.dst | c.bytes;
+  if ((al & 15u) == 0) {
+    const uint4* s = (const uint4*)c.src;
+    uint4* d = (uint4*)c.dst;
+    for (uint64_t i = t; i < c.bytes / 16; i += stride) d[i] = s[i];
+  } else if ((al & 3u) == 0) {
+    const uint32_t* s = (const uint32_t*)c.src;
+    uint32_t* d = (uint32_t*)c.dst;
+    for (uint64_t i = t; i < c.bytes / 4; i += stride) d[i] = s[i];
+  } else {
+    for (uint64_t i = t; i < c.bytes; i += stride) c.dst[i] = c.src[i];
+  }
+}
+
+void copy_batch(const std::vector<CopyDesc>& v, hipStream_t st) {
+  for (size_t i = 0; i < v.size(); i += CP_MAX) {
+    CopyBatch b;
+    b.n = (int)std::min<size_t>(CP_MAX, v.size() - i);
+    uint64_t mx = 0;
+    for (int j = 0; j < b.n; ++j) {
+      b.d[j] = v[i + (size_t)j];
+      mx = std::max<uint64_t>(mx, b.d[j].bytes);
+    }
+    const unsigned gx = (unsigned)std::min<uint64_t>(64, std::max<uint64_t>(1, (mx / 16 + 4095) / 4096));
+    k_copy_batch<<<dim3(gx, (unsigned)b.n), 256, 0, st>>>(b);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// (the scratch of channel ch at >= the sizes; its previous use on st has finished first)
+char* grow(char*& p, size_t& cap, size_t need, hipStream_t st) {
+  if (need <= cap) return p;
+  HIP_CHECK(hipStreamSynchronize(st));
+  std::lock_guard<std::mutex> lk(capture_mutex());  // (hipFree may synchronise the device)
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  need = std::max(need, (size_t)1 << 20);
+  if (hipMalloc((void**)&p, need) != hipSuccess) throw Error(FCCF_E_OOM, "hipMalloc (all-gather scratch)");
+  cap = need;
+  return p;
+}
+}  // namespace
+
+Transport::~Transport() { free_scratch(); }
+
+void Transport::free_scratch() {
+  for (Scratch& s : scratch) {
+    if (s.pack) (void)hipFree(s.pack);
+    if (s.recv) (void)hipFree(s.recv);
+    s = Scratch{};
+  }
+}
+
+void Transport::allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st) {
+  const int n = n_ranks, me = my_rank;
+  if (nops <= 0) return;
+  // every rank's block: its parts of the ops, each 16-byte aligned; M = the largest block
+  std::vector<size_t> inner((size_t)n * nops);
+  size_t M = 0;
+  for (int r = 0; r < n; ++r) {
+    size_t o = 0;
+    for (int i = 0; i < nops; ++i) {
+      inner[(size_t)r * nops + i] = o;
+      o += pad16(ops[i].counts[r]);
+    }
+    M = std::max(M, o);
+  }
+  if (M == 0) return;
+  Scratch& S = scratch[ch];
+  char* pack = grow(S.pack, S.cap_pack, M, st);
+  char* recv = grow(S.recv, S.cap_recv, M * (size_t)n, st);
+  std::vector<CopyDesc> cp;
+  for (int i = 0; i < nops; ++i)
+    if (ops[i].counts[me])
+      cp.push_back(CopyDesc{(const char*)ops[i].send, pack + inner[(size_t)me * nops + i], ops[i].counts[me]});
+  copy_batch(cp, st);
+  allgather(ch, pack, recv, M, st);
+  cp.clear();
+  for (int i = 0; i < nops; ++i)
+    for (int r = 0; r < n; ++r) {
+      const size_t c = ops[i].counts[r];
+      if (!c) continue;
+      char* dst = (char*)ops[i].recv + ops[i].offs[r];
+      if (r == me) {
+        if ((const char*)ops[i].send != dst) cp.push_back(CopyDesc{(const char*)ops[i].send, dst, c});
+      } else {
+        cp.push_back(CopyDesc{recv + (size_t)r * M + inner[(size_t)r * nops + i], dst, c});
+      }
+    }
+  copy_batch(cp, st);
+}
+
 // ------------------------------------------------------------ failure handling
 
 void group_abort(Group* g, const std::string& why) {
   if (!g) return;
-  bool was = false;
-  if (!g->aborted.compare_exchange_strong(was, true)) return;
-  g->abort_why = why;
+  {
+    // the reason is written before the flag becomes visible: a reader that
+    // sees `aborted` and then takes why_m finds it complete
+    std::lock_guard<std::mutex> lk(g->why_m);
+    if (g->aborted.load(std::memory_order_acquire)) return;
+    g->abort_why = why;
+    g->aborted.store(true, std::memory_order_release);
+  }
   // a dead peer (the silent test hook) leaves its transport alone: the others find
   // out at their time limit
   if (!g->fail_silent && g->tr) g->tr->abort();
   order_abort(g);
 }
 
-void group_check(const Group* g) {
-  if (g && g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + g->abort_why + "); destroy and recreate it");
+std::string group_why(Group* g) {
+  std::lock_guard<std::mutex> lk(g->why_m);
+  return g->abort_why;
+}
+
+void group_check(Group* g) {
+  if (g && g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + group_why(g) + "); destroy and recreate it");
 }
 
 namespace {
@@ -244,7 +392,7 @@ void bounded_wait(Group* g, Q query, const char* what) {
       group_abort(g, m);
       throw Error(FCCF_E_HIP, m);
     }
-    if (g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + g->abort_why + ")");
+    if (g->aborted) throw Error(FCCF_E_RCCL, "group aborted (" + group_why(g) + ")");
     if ((k & 31) == 31) {
       if (const int ae = g->tr->async_error()) {
         const std::string m = std::string(what) + ": transport failed asynchronously (" + std::to_string(ae) + ")";
@@ -633,6 +781,8 @@ extern "C" int fccf_group_create(fccf_ctx* c, const uint8_t id[FCCF_GROUP_ID_BYT
     G->g.n = n_ranks;
     G->g.rank = rank;
     G->g.tr.reset(new RcclTransport(&G->g));
+    G->g.tr->n_ranks = n_ranks;
+    G->g.tr->my_rank = rank;
     group_alloc(G->g);
     c->group = &G->g;
     *out = G;
@@ -668,6 +818,8 @@ extern "C" int fccf_group_create_local(fccf_ctx* const* ctxs, int n, fccf_group*
       G->g.rank = r;
       G->g.hub = hub;
       G->g.tr.reset(new LocalTransport(&G->g));
+      G->g.tr->n_ranks = n;
+      G->g.tr->my_rank = r;
       group_alloc(G->g);
     }
   } catch (...) {
@@ -706,6 +858,12 @@ extern "C" int fccf_debug_group_fail(fccf_group* G, int site, int silent) {
 extern "C" int fccf_group_aborted(const fccf_group* G) {
   if (!G) return FCCF_E_ARG;
   return G->g.aborted ? 1 : 0;
+}
+
+extern "C" int fccf_group_bytes(const fccf_group* G, int64_t rx[3]) {
+  if (!G || !rx) return FCCF_E_ARG;
+  for (int c = 0; c < 3; ++c) rx[c] = G->g.tr ? G->g.tr->rx_bytes[c].load() : 0;
+  return FCCF_OK;
 }
 
 extern "C" int fccf_group_info(const fccf_group* G, int* n_ranks, int* rank) {

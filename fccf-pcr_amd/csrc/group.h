@@ -44,18 +44,31 @@ struct GatherOp {
 };
 
 struct Transport {
-  virtual ~Transport() = default;
+  virtual ~Transport();
   // Rank-ordered all-gather-v on channel ch, in the order of stream st: rank r's
   // counts[r] bytes (its `send`) land at recv + offs[r] on every rank.  Buffers are
   // device memory of the rank's device.
   virtual void allgatherv(int ch, const void* send, void* recv, const size_t* counts, const size_t* offs,
                           hipStream_t st) = 0;
-  // Several all-gather-v's as one exchange (RCCL: one ncclGroupStart/End).
-  virtual void allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st) {
-    for (int i = 0; i < nops; ++i) allgatherv(ch, ops[i].send, ops[i].recv, ops[i].counts, ops[i].offs, st);
-  }
+  // Several all-gather-v's as one exchange.  The default (both transports) is ONE
+  // all-gather of count-padded blocks: each rank packs its parts of every op into one
+  // block (16-byte aligned parts), the blocks (the largest rank's size) are all-gathered,
+  // and every rank's parts are copied to their places -- a pack and an unpack launch of
+  // a descriptor copy kernel around one collective (group.cpp allgatherv_packed).
+  virtual void allgatherv_multi(int ch, const GatherOp* ops, int nops, hipStream_t st);
   // The same with equal blocks of `bytes`, rank r's at recv + r * bytes.
   virtual void allgather(int ch, const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
+  // Bytes this rank received through collectives, per channel (fccf_stats.coll_bytes).
+  std::atomic<int64_t> rx_bytes[3] = {{0}, {0}, {0}};
+  // Device scratch of the packed all-gather-v, per channel (grown on demand; used only
+  // from the channel's one stream).
+  struct Scratch {
+    char* pack = nullptr;
+    char* recv = nullptr;
+    size_t cap_pack = 0, cap_recv = 0;
+  } scratch[3];
+  void free_scratch();
+  int n_ranks = 1, my_rank = 0;
   // A non-zero code once the transport has failed asynchronously (RCCL:
   // ncclCommGetAsyncError of any communicator; virtual ranks: the hub was aborted).
   virtual int async_error() { return 0; }
@@ -106,6 +119,9 @@ struct Group {
   // aborted group fails every later call until it is destroyed (and recreated).
   std::atomic<bool> aborted{false};
   double timeout_s = 30.0;
+  // why the group was aborted: written under why_m before `aborted` is set (group_abort),
+  // read through group_why
+  std::mutex why_m;
   std::string abort_why;
   // test hook (fccf_debug_group_fail): fail this rank at a collective site
   int fail_at = 0;          // GROUP_FAIL_* site, 0 = off
@@ -116,7 +132,9 @@ enum { GROUP_FAIL_MATCH = 1, GROUP_FAIL_FINE = 2, GROUP_FAIL_CLOUD = 3 };
 // Aborts the group (idempotent; see Group::aborted).  why: the reason recorded.
 void group_abort(Group* g, const std::string& why);
 // Throws FCCF_E_RCCL when the group is aborted.
-void group_check(const Group* g);
+void group_check(Group* g);
+// The recorded abort reason (a copy taken under the group's why_m).
+std::string group_why(Group* g);
 // Bounded waits for a stream / an event that may depend on peers (see Group::aborted):
 // return when complete; abort the group and throw FCCF_E_RCCL on an async transport
 // error or after the group's time limit, FCCF_E_HIP on a device error.

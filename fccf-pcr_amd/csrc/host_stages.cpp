@@ -954,4 +954,36 @@ m44 fuse_answer(const std::vector<High>& hs, float sum) {
   return T;
 }
 
+m44 fuse_types(const std::vector<TS> ctv[3], int analyse_max, std::vector<High>* tmp_out) {
+  // sums over every type's first analyse_max candidates (:1499-1541), before any type is
+  // normalised (App. B Q15)
+  float score1_sum = 0.f, score2_sum = 0.f;
+  for (int t = 0; t < 3; ++t)
+    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
+      score2_sum += ctv[t][i].score2;
+      score1_sum += ctv[t][i].score;
+    }
+  std::vector<High> tmp;
+  float best_best = 0.f;
+  for (int t = 0; t < 3; ++t) {
+    float bs = 0.f;
+    m44 bt = eye44();
+    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
+      const float sc = ctv[t][i].score / score1_sum + ctv[t][i].score2 / score2_sum;
+      if (sc > bs) { bs = sc; bt = ctv[t][i].T; }  // first best on ties (:1559)
+    }
+    if (best_best < bs) best_best = bs;
+    tmp.push_back({qt_from_T(bt), bs});
+  }
+  std::vector<High> hs;
+  float score_sum = 0.f;
+  for (const High& h : tmp)
+    if (h.score > best_best * 0.8) {  // (float * double: the cut in double, :1601)
+      hs.push_back(h);
+      score_sum += h.score;
+    }
+  if (tmp_out) *tmp_out = tmp;
+  return fuse_answer(hs, score_sum);
+}
+
 }  // namespace fccf

@@ -88,6 +88,13 @@ struct High {
 // weight_normal + fuse_answer (:1253-1368)
 m44 fuse_answer(const std::vector<High>& hs, float sum);
 
+struct TS { m44 T; float score, score2; };  // a verified candidate: T, quick score, fine score
+// The fusion of computer_transform_guess (:1546-1606): score1/score2 sums over the first
+// analyse_max candidates of every type (:1538-1540), each type's best normalised score
+// (:1548-1596, identity when a type has none), the types above 0.8 of the best
+// (:1599-1605) and fuse_answer.  tmp (may be null) receives the three per-type bests.
+m44 fuse_types(const std::vector<TS> ctv[3], int analyse_max, std::vector<High>* tmp);
+
 QT qt_from_T(const m44& T);
 m44 T_from_qt(const QT& q);
 

@@ -152,7 +152,13 @@ typedef Pt3* GPt3;
 __device__ __forceinline__ Pt3 load_xyz(const float* src, uint32_t v) { return ((GPt3c)(const Pt3*)src)[v]; }
 __device__ __forceinline__ void store_xyz(const IsBufs& W, uint32_t pos, const Pt3& q) { ((GPt3)(Pt3*)W.xyzs)[pos] = q; }
 __device__ __forceinline__ void put_xyz(const IsBufs& W, const float* __restrict__ src, uint32_t pos, uint32_t v) {
+#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 1
+  store_xyz(W, pos, load_xyz(src, pos));  // dev timing only: a coalesced source (wrong points)
+#elif defined(IS_XYZ_PROBE) && (IS_XYZ_PROBE == 2 || IS_XYZ_PROBE == 3)
+  (void)W; (void)src; (void)pos; (void)v;  // dev: no points here (3: k_is_xyz_gather after the finish kernels)
+#else
   store_xyz(W, pos, load_xyz(src, v));
+#endif
 }
 
 // The fence before a workgroup barrier that hands global-memory data between the waves
@@ -2506,6 +2512,19 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
   }
 }
 
+#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 3
+// dev: the sorted points in one streaming pass after the finish kernels (every position
+// reads its final value's point)
+__global__ void __launch_bounds__(256) k_is_xyz_gather(B4<uint32_t*> V02, B4<IsBufs> W2) {
+  const IsBufs W = W2[blockIdx.y];
+  if (!W.xyzs) return;
+  const uint32_t n = W.ctl[0];
+  const uint32_t* V = V02[blockIdx.y];
+  const float* src = W.vgp->src;
+  for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) store_xyz(W, p, load_xyz(src, V[p]));
+}
+#endif
+
 }  // namespace
 
 #ifdef IS_KERNEL_VARIANT
@@ -2697,6 +2716,9 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   FCCF_LAUNCH("k_is_wave", (pb_ctl(19, 16.0)), k_is_wave,
               dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
+#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 3
+  k_is_xyz_gather<<<dim3(2048, nbatch), 256, 0, st>>>(v0, b);
+#endif
 }
 
 #endif  // IS_KERNEL_VARIANT

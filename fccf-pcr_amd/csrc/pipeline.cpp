@@ -267,7 +267,6 @@ void dump_planes(fccf_ctx* c, const std::string& k, const std::vector<Plane>& F)
 
 namespace {
 
-struct TS { m44 T; float score, score2; };  // a verified candidate: T, quick score, fine score
 
 // FCCF_HOST_TRACE=1 (development): host timestamps of phase B, microseconds since
 // the pair's cloud stage was enqueued, printed to stderr when the pair finishes.
@@ -1234,10 +1233,13 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   float* T_out = pb.T_out;
   std::vector<float> scores(E, 0.f);
   if (E > 0) {
-    // (ev[3]'s stream is captured only by this thread) scores and the error word are in
-    // the mailbox; with a group the fine stream holds the score gather: a bounded wait
+    // scores and the error word are in the mailbox; with a group the fine stream holds the
+    // score gather: a bounded wait.  ev[3] is recorded on the fine stream sa[1], which the
+    // other phase-B chains capture g_fine on (a new capture whenever the pair sizes
+    // change), so the event fallback queries under the capture lock, as phase_b1 does
+    // for ev[4]
     if (c->group) group_wait_event(c->group, c->cs[s].ev[3]);
-    else if (!mail_wait(&host_mail(c)->fine[s].done, 3000.0)) HIP_CHECK(hipEventSynchronize(c->cs[s].ev[3]));
+    else if (!mail_wait(&host_mail(c)->fine[s].done, 3000.0)) guarded_event_sync(c->cs[s].ev[3]);
     uint32_t err = 0;
     if (c->group && c->group->n > 1) {  // every rank's block, gathered in rank order
       group_fine_scores(c->group, s, E, scores.data(), &err);
@@ -1272,7 +1274,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
       if (!(c->group && c->group->n > 1)) {  // (the events are recorded with a sharded fine stage only)
         d = fm.stamp[0] && fm.stamp[1] >= fm.stamp[0] ? (float)((double)(fm.stamp[1] - fm.stamp[0]) * 1e-5) : 0.f;
       } else {
-        HIP_CHECK(hipEventSynchronize(c->cs[s].tev[5]));
+        guarded_event_sync(c->cs[s].tev[5]);  // (sa[1]: see ev[3] above)
         HIP_CHECK(hipEventElapsedTime(&d, c->cs[s].tev[4], c->cs[s].tev[5]));
       }
       S.dev_ms[3] = d;
@@ -1285,15 +1287,12 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
 
   // ---------------- host: score sums (over all types) and fusion (:1539-1606)
   auto t0 = clk::now();
-  float score1_sum = 0.f, score2_sum = 0.f;
   {
     int e = 0;
     for (int t = 0; t < 3; ++t) {
       std::vector<float> fv;
       for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i, ++e) {
         ctv[t][i].score2 = scores[e];
-        score2_sum += ctv[t][i].score2;
-        score1_sum += ctv[t][i].score;
         for (int a = 0; a < 4; ++a)
           for (int b = 0; b < 4; ++b) fv.push_back(ctv[t][i].T.m[a][b]);
         fv.push_back(ctv[t][i].score);
@@ -1303,25 +1302,7 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
     }
   }
   std::vector<High> tmp;
-  float best_best = 0.f;
-  for (int t = 0; t < 3; ++t) {
-    float bs = 0.f;
-    m44 bt = eye44();
-    for (int i = 0; i < (int)ctv[t].size() && i < analyse_max; ++i) {
-      const float sc = ctv[t][i].score / score1_sum + ctv[t][i].score2 / score2_sum;
-      if (sc > bs) { bs = sc; bt = ctv[t][i].T; }
-    }
-    if (best_best < bs) best_best = bs;
-    tmp.push_back({qt_from_T(bt), bs});
-  }
-  std::vector<High> hs;
-  float score_sum = 0.f;
-  for (const High& h : tmp)
-    if (h.score > best_best * 0.8) {
-      hs.push_back(h);
-      score_sum += h.score;
-    }
-  const m44 T = fuse_answer(hs, score_sum);
+  const m44 T = fuse_types(ctv, analyse_max, &tmp);
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) T_out[4 * i + j] = T.m[i][j];
   S.ms[FCCF_T_FUSE] = ms_since(t0);

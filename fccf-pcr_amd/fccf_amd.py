@@ -101,6 +101,7 @@ _sig("fccf_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _
      ctypes.POINTER(_I64))
 _sig("fccf_stage_cluster", ctypes.c_int, _P, _P, _I64, ctypes.c_int, ctypes.POINTER(Params), _P, _I64,
      ctypes.POINTER(_I64), ctypes.POINTER(_I64))
+_sig("fccf_stage_fuse", ctypes.c_int, _P, ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.c_int, _P, _P)
 _sig("fccf_stage_fine_verify", ctypes.c_int, _P, _P, _I64, _P, _I64, _P, ctypes.c_int, ctypes.c_float, _P)
 _sig("fccf_ctx_set_probe", ctypes.c_int, _P, ctypes.c_char_p)
 _sig("fccf_probe_read", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64),
@@ -127,6 +128,7 @@ _sig("fccf_group_create", ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, ctyp
 _sig("fccf_group_create_local", ctypes.c_int, ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P))
 _sig("fccf_group_destroy", ctypes.c_int, _P)
 _sig("fccf_group_info", ctypes.c_int, _P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+_sig("fccf_group_bytes", ctypes.c_int, _P, ctypes.POINTER(_I64))
 _sig("fccf_group_stage_match", ctypes.c_int, _P, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int,
      ctypes.POINTER(Params), ctypes.POINTER(_P), ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64))
 _sig("fccf_synth_scene", ctypes.c_int, _I64, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
@@ -374,14 +376,7 @@ class Ctx:
     def grow(self, vox, side: int, params: Params | None = None):
         """Region growing, plane selection and select_base (FCCF.cpp:536-677, :429-468).
         side 1 = driver source, 2 = target.  Returns (PLANE_DTYPE[F], float64 theta[F], BASE_DTYPE[B])."""
-        v = np.ascontiguousarray(vox, VOXEL_DTYPE)
-        p = params if params is not None else default_params()
-        planes, theta, bases = np.zeros(64, PLANE_DTYPE), np.zeros(64, np.float64), np.zeros(2080, BASE_DTYPE)
-        nF, nB = ctypes.c_int(), ctypes.c_int()
-        _check(_lib.fccf_stage_grow(self._h, v.ctypes.data, len(v), int(side), ctypes.byref(p), planes.ctypes.data,
-                                    len(planes), ctypes.byref(nF), theta.ctypes.data, bases.ctypes.data, len(bases),
-                                    ctypes.byref(nB)), "fccf_stage_grow", self._h)
-        return planes[: nF.value].copy(), theta[: nF.value].copy(), bases[: nB.value].copy()
+        return stage_grow(vox, side, params, self._h)
 
     def match(self, F1, B1, F2, B2, b1_lo: int = 0, b1_hi: int = -1, params: Params | None = None):
         """Coplane-pair correspondence search + computer_transform (FCCF.cpp:1410-1428,
@@ -403,16 +398,11 @@ class Ctx:
     def cluster(self, cand, cluster_num: int, params: Params | None = None):
         """transform_cluster (FCCF.cpp:1040-1231) of one type's candidates (float32[n, 4, 4]).
         Returns (fused float32[m, 8] = qw qx qy qz tx ty tz allocated, clusters formed)."""
-        a = np.ascontiguousarray(np.asarray(cand, np.float32).reshape(-1, 16))
-        p = params if params is not None else default_params()
-        nf, ncl = _I64(), _I64()
-        _check(_lib.fccf_stage_cluster(self._h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p), None, 0,
-                                       ctypes.byref(nf), ctypes.byref(ncl)), "fccf_stage_cluster", self._h)
-        out = np.zeros((max(nf.value, 1), 8), np.float32)
-        _check(_lib.fccf_stage_cluster(self._h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p),
-                                       out.ctypes.data, nf.value, ctypes.byref(nf), ctypes.byref(ncl)),
-               "fccf_stage_cluster", self._h)
-        return out[: nf.value], ncl.value
+        return stage_cluster(cand, cluster_num, params, self._h)
+
+    def fuse(self, lists, analyse_max: int = 4):
+        """Fusion (FCCF.cpp:1546-1606): see stage_fuse."""
+        return stage_fuse(lists, analyse_max, self._h)
 
     def fine_verify(self, s1, s2, T, voxel: float = 0.5):
         """fine_verify (FCCF.cpp:785-839) of E <= 16 transforms T[E, 4, 4]: float32[E] scores."""
@@ -502,6 +492,13 @@ class Group:
         _check(_lib.fccf_group_info(self._h, ctypes.byref(n), ctypes.byref(r)), "fccf_group_info")
         return n.value, r.value
 
+    def rx_bytes(self):
+        """Bytes this rank has received through the group's collectives, per channel
+        (candidate gather, fine scores, cloud stage rows D and P), since creation."""
+        a = (_I64 * 3)()
+        _check(_lib.fccf_group_bytes(self._h, a), "fccf_group_bytes")
+        return [int(x) for x in a]
+
     def aborted(self) -> bool:
         """True once the group was aborted (a failed registration on this rank or a
         peer's failure seen at the group's time limit); destroy and recreate it."""
@@ -564,6 +561,55 @@ def local_groups(ctxs) -> list:
     out = (_P * n)()
     _check(_lib.fccf_group_create_local(hs, n, out), "fccf_group_create_local")
     return [Group._wrap(c, _P(out[i])) for i, c in enumerate(ctxs)]
+
+
+# The host-only stage exports (fccf_stage_grow / _cluster / _fuse run the product's host
+# C++; they need no GPU, so they can be called without a ctx, e.g. by the CPU tests).
+def stage_grow(vox, side: int, params: Params | None = None, h=None):
+    """Region growing, plane selection and select_base (FCCF.cpp:536-677, :429-468) of
+    VOXEL_DTYPE records.  Returns (PLANE_DTYPE[F], float64 theta[F], BASE_DTYPE[B])."""
+    v = np.ascontiguousarray(vox, VOXEL_DTYPE)
+    p = params if params is not None else default_params()
+    planes, theta, bases = np.zeros(64, PLANE_DTYPE), np.zeros(64, np.float64), np.zeros(2080, BASE_DTYPE)
+    nF, nB = ctypes.c_int(), ctypes.c_int()
+    _check(_lib.fccf_stage_grow(h, v.ctypes.data, len(v), int(side), ctypes.byref(p), planes.ctypes.data,
+                                len(planes), ctypes.byref(nF), theta.ctypes.data, bases.ctypes.data, len(bases),
+                                ctypes.byref(nB)), "fccf_stage_grow", h)
+    return planes[: nF.value].copy(), theta[: nF.value].copy(), bases[: nB.value].copy()
+
+
+def stage_cluster(cand, cluster_num: int, params: Params | None = None, h=None):
+    """transform_cluster (FCCF.cpp:1040-1231) of one type's candidates (float32[n, 4, 4]).
+    Returns (fused float32[m, 8] = qw qx qy qz tx ty tz allocated, clusters formed)."""
+    a = np.ascontiguousarray(np.asarray(cand, np.float32).reshape(-1, 16))
+    p = params if params is not None else default_params()
+    nf, ncl = _I64(), _I64()
+    _check(_lib.fccf_stage_cluster(h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p), None, 0,
+                                   ctypes.byref(nf), ctypes.byref(ncl)), "fccf_stage_cluster", h)
+    out = np.zeros((max(nf.value, 1), 8), np.float32)
+    _check(_lib.fccf_stage_cluster(h, a.ctypes.data, len(a), int(cluster_num), ctypes.byref(p),
+                                   out.ctypes.data, nf.value, ctypes.byref(nf), ctypes.byref(ncl)),
+           "fccf_stage_cluster", h)
+    return out[: nf.value], ncl.value
+
+
+def stage_fuse(lists, analyse_max: int = 4, h=None):
+    """Fusion of computer_transform_guess (FCCF.cpp:1546-1606).  lists: three sequences of
+    (T float32[4, 4], quick_verify score, fine_verify score) in score_range order.
+    Returns (T float32[4, 4], high float32[3, 8] = per-type best qw qx qy qz tx ty tz score)."""
+    recs, ptrs, ns = [], (_P * 3)(), (_I64 * 3)()
+    for t in range(3):
+        a = np.zeros((max(len(lists[t]), 1), 18), np.float32)
+        for i, (T, s1, s2) in enumerate(lists[t]):
+            a[i, :16] = np.asarray(T, np.float32).reshape(16)
+            a[i, 16], a[i, 17] = s1, s2
+        recs.append(a)
+        ptrs[t] = a.ctypes.data
+        ns[t] = len(lists[t])
+    T = np.zeros(16, np.float32)
+    high = np.zeros(24, np.float32)
+    _check(_lib.fccf_stage_fuse(h, ptrs, ns, int(analyse_max), T.ctypes.data, high.ctypes.data), "fccf_stage_fuse", h)
+    return T.reshape(4, 4), high.reshape(3, 8)
 
 
 def strerror(code: int) -> str:

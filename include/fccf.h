@@ -254,6 +254,17 @@ int fccf_stage_match(fccf_ctx* ctx, const fccf_plane* F1, int nF1, const fccf_ba
  * *n_clusters (may be NULL) = clusters formed. */
 int fccf_stage_cluster(fccf_ctx* ctx, const float* cand_rowmajor, int64_t n, int cluster_num,
                        const fccf_params* params, float* fine, int64_t cap, int64_t* n_fine, int64_t* n_clusters);
+/* Stage export: the fusion of computer_transform_guess (FCCF.cpp:1546-1606, host
+ * stage): cand[t] holds n[t] verified candidates of type t in score_range order, 18
+ * floats each (row-major 4x4 T, quick_verify score, fine_verify score).  The score
+ * sums run over the first analyse_max candidates of every type (:1538-1540), each
+ * type's best normalised score picks its T (identity when none), the types above 0.8
+ * of the best are fused (fuse_answer :1253-1368).  T receives the result; high (may be
+ * NULL) the three per-type bests, 8 floats each (qw qx qy qz tx ty tz score).
+ * fccf_stage_grow, fccf_stage_cluster and fccf_stage_fuse are host code: ctx may be
+ * NULL for them (no device form is selectable then). */
+int fccf_stage_fuse(fccf_ctx* ctx, const float* const cand[3], const int64_t n[3], int analyse_max, float T_rowmajor[16],
+                    float high[24]);
 
 /* Stage export: fine_verify (FCCF.cpp:785-839) of E <= 16 transforms on the GPU:
  * scores[e] = score of S2 transformed by T_e against S1 over the fine_verify_voxel
@@ -360,6 +371,12 @@ int fccf_group_destroy(fccf_group* group);
  * calls must come from its own host thread, all ranks calling the same sequence. */
 int fccf_group_create_local(fccf_ctx* const* ctxs, int n, fccf_group** groups);
 int fccf_group_info(const fccf_group* group, int* n_ranks, int* rank);
+/* Bytes this rank has received through the group's collectives since it was created,
+ * per channel: [0] the candidate gather (matching stream), [1] the fine scores, [2]
+ * the cloud stage's rows D and P (sorted slices, leaf records, residual points).  An
+ * all-gather-v is one all-gather of count-padded blocks, so the padding is included.
+ * The caller takes differences around the calls it measures (bench.py's group leg). */
+int fccf_group_bytes(const fccf_group* group, int64_t rx[3]);
 /* Failure handling: every host wait of a registration that may depend on a peer (a
  * stream or event after a collective, the pipelined batch's collective-order gate, a
  * virtual-rank barrier) is bounded by FCCF_GROUP_TIMEOUT_S seconds (environment at

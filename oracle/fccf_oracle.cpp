@@ -640,6 +640,7 @@ static void face_recompute(Face& f, const std::vector<Voxel>& vox) {
   f.an[0] = nx / s; f.an[1] = ny / s; f.an[2] = nz / s;
 }
 
+static void grow_select(const Params& P, FaceOut& out);
 static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
   const size_t n = npts(cloud);
   // compute3DCentroid (dense): sequential float sums / n
@@ -689,6 +690,13 @@ static void face_extrate(const Cloud& cloud, const Params& P, FaceOut& out) {
     out.vcurv.push_back(curv);
   }
 
+  grow_select(P, out);
+}
+
+// Region growing stages 1-2, range_face and the selection with roughness
+// (:536-677) over out.voxels; fills planes, theta and groups_all.
+static void grow_select(const Params& P, FaceOut& out) {
+  const std::vector<Voxel>& vox = out.voxels;
   // stage 1: greedy seed growth (:536-593)
   std::vector<char> valloc(vox.size(), 0);
   std::vector<Face> groth;
@@ -1454,6 +1462,40 @@ static double ms_since(clk::time_point t0) {
   return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
 }
 
+// The fusion (:1546-1606): every type's best normalised score over its first
+// analyse_max candidates (score1_sum / score2_sum over all types, App. B Q15), the
+// types above 0.8 of the best, fuse_answer.
+struct TS { M4f T; float score, score2; };
+static M4f fuse_stage(const std::vector<TS> ctv[3], int analyse_max, float score1_sum, float score2_sum,
+                      std::vector<High>& tmp) {
+  float best_best = 0;
+  for (int i = 0; i < 3; ++i) {
+    int analyse_sum = 0;
+    float bs = 0;
+    M4f bt = identity4();
+    for (auto& ts : ctv[i]) {
+      if (analyse_sum < analyse_max) {
+        analyse_sum++;
+        float s = ts.score / score1_sum + ts.score2 / score2_sum;
+        if (s > bs) { bs = s; bt = ts.T; }
+      }
+    }
+    if (best_best < bs) best_best = bs;
+    High h;
+    h.qt = qt_from_T(bt);
+    h.score = bs;
+    tmp.push_back(h);
+  }
+  std::vector<High> hs;
+  float score_sum = 0;
+  for (const High& h : tmp)
+    if (h.score > best_best * 0.8) {
+      hs.push_back(h);
+      score_sum += h.score;
+    }
+  return fuse_answer(hs, score_sum);
+}
+
 static void computer_transform_guess(Cloud source, Cloud target, float leaf, int order, const Params& P, M4f& best,
                                      orc_ctx* cx) {
   Store& st = cx->st;
@@ -1541,7 +1583,6 @@ static void computer_transform_guess(Cloud source, Cloud target, float leaf, int
   for (int i = 0; i < 3; ++i) st.put("cand" + std::to_string(i), flat(tv[i]));
 
   float score1_sum = 0, score2_sum = 0;
-  struct TS { M4f T; float score, score2; };
   std::vector<TS> ctv[3];
   const int analyse_max = (int)P.fine_verify_number;
   int64_t lm_solves = 0;
@@ -1608,38 +1649,13 @@ static void computer_transform_guess(Cloud source, Cloud target, float leaf, int
   }
   t0 = clk::now();
   std::vector<High> tmp;
-  float best_best = 0;
-  for (int i = 0; i < 3; ++i) {
-    int analyse_sum = 0;
-    float bs = 0;
-    M4f bt = identity4();
-    for (auto& ts : ctv[i]) {
-      if (analyse_sum < analyse_max) {
-        analyse_sum++;
-        float s = ts.score / score1_sum + ts.score2 / score2_sum;
-        if (s > bs) { bs = s; bt = ts.T; }
-      }
-    }
-    if (best_best < bs) best_best = bs;
-    High h;
-    h.qt = qt_from_T(bt);
-    h.score = bs;
-    tmp.push_back(h);
-  }
-  std::vector<High> hs;
-  float score_sum = 0;
-  for (const High& h : tmp)
-    if (h.score > best_best * 0.8) {
-      hs.push_back(h);
-      score_sum += h.score;
-    }
+  M4f T = fuse_stage(ctv, analyse_max, score1_sum, score2_sum, tmp);
   std::vector<float> hv;
   for (const High& h : tmp) {
     float a[8] = {h.qt.qw, h.qt.qx, h.qt.qy, h.qt.qz, h.qt.tx, h.qt.ty, h.qt.tz, h.score};
     hv.insert(hv.end(), a, a + 8);
   }
   st.put("high", hv);
-  M4f T = fuse_answer(hs, score_sum);
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 4; ++j) best.m[i][j] = T.m[i][j];
   cx->ms[7] += ms_since(t0);
@@ -1786,5 +1802,96 @@ extern "C" int orc_lm_refine(const float* pairs, int P, double q[4], double t[3]
   lm_solve(pf, b);
   for (int i = 0; i < 4; ++i) q[i] = b[i];
   for (int i = 0; i < 3; ++i) t[i] = b[4 + i];
+  return 0;
+}
+
+// ------------------------------------------------ single host stages (KAT inputs)
+extern "C" int orc_stage_grow(const orc_voxel* vox, int64_t nv, int side, float* planes, int cap_planes,
+                              int* n_planes, double* theta, int32_t* bases, int cap_bases, int* n_bases) {
+  if ((!vox && nv) || nv < 0 || (side != 1 && side != 2) || !n_planes || !n_bases) return -1;
+  Params P;
+  FaceOut out;
+  for (int64_t i = 0; i < nv; ++i) {
+    Voxel v;
+    for (int a = 0; a < 3; ++a) { v.c[a] = vox[i].c[a]; v.n[a] = vox[i].n[a]; }
+    v.size = vox[i].count;
+    out.voxels.push_back(v);
+  }
+  grow_select(P, out);
+  std::vector<Base> b;
+  std::vector<int> type;
+  select_base(out.planes, out.theta, P, b, type);
+  *n_planes = (int)out.planes.size();
+  *n_bases = (int)b.size();
+  for (int i = 0; i < *n_planes && i < cap_planes; ++i) {
+    const Face& f = out.planes[(size_t)i];
+    const float a[8] = {f.ac[0], f.ac[1], f.ac[2], f.an[0], f.an[1], f.an[2], f.fps, (float)f.members.size()};
+    std::memcpy(planes + 8 * i, a, sizeof a);
+    if (theta) theta[i] = out.theta[(size_t)i];
+  }
+  // type_index is shorter than the bases when a roughness is NaN (App. B Q5): positions
+  // past its end read as the side's sentinel, as the matching loop does (-1 / -2)
+  for (int k = 0; k < *n_bases && k < cap_bases; ++k) {
+    int32_t* r = bases + 4 * k;
+    r[0] = b[(size_t)k].i1;
+    r[1] = b[(size_t)k].i2;
+    std::memcpy(&r[2], &b[(size_t)k].angle, 4);
+    r[3] = (size_t)k < type.size() ? type[(size_t)k] : (side == 1 ? -1 : -2);
+  }
+  return 0;
+}
+
+extern "C" int orc_stage_cluster(const float* cand, int64_t n, int cluster_num, float* fine, int64_t cap,
+                                 int64_t* n_fine, int64_t* n_clusters) {
+  if ((!cand && n) || n < 0 || !n_fine) return -1;
+  Params P;
+  std::vector<QT> qv, out;
+  for (int64_t i = 0; i < n; ++i) {
+    M4f T;
+    std::memcpy(T.m, cand + 16 * i, sizeof T.m);
+    qv.push_back(qt_from_T(T));
+  }
+  int64_t ncl = 0;
+  transform_cluster(qv, out, cluster_num, P, &ncl);
+  *n_fine = (int64_t)out.size();
+  if (n_clusters) *n_clusters = ncl;
+  for (int64_t i = 0; i < *n_fine && i < cap; ++i) {
+    const QT& q = out[(size_t)i];
+    const float a[8] = {q.qw, q.qx, q.qy, q.qz, q.tx, q.ty, q.tz, q.alloc ? 1.f : 0.f};
+    std::memcpy(fine + 8 * i, a, sizeof a);
+  }
+  return 0;
+}
+
+extern "C" int orc_stage_fuse(const float* const cand[3], const int64_t n[3], int analyse_max, float T[16],
+                              float high[24]) {
+  if (!cand || !n || !T) return -1;
+  std::vector<TS> ctv[3];
+  float s1 = 0, s2 = 0;
+  for (int t = 0; t < 3; ++t)
+    for (int64_t i = 0; i < n[t]; ++i) {
+      TS x;
+      const float* r = cand[t] + 18 * i;
+      std::memcpy(x.T.m, r, sizeof x.T.m);
+      x.score = r[16];
+      x.score2 = r[17];
+      ctv[t].push_back(x);
+      if (i < analyse_max) {  // (:1538-1540: the first analyse_max of every type)
+        s2 += x.score2;
+        s1 += x.score;
+      }
+    }
+  std::vector<High> tmp;
+  const M4f R = fuse_stage(ctv, analyse_max, s1, s2, tmp);
+  M4f best = identity4();  // (the caller's matrix: rows 0-2 written, :1606 via fuse_answer)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) best.m[i][j] = R.m[i][j];
+  std::memcpy(T, best.m, sizeof best.m);
+  if (high)
+    for (int t = 0; t < 3; ++t) {
+      const High& h = tmp[(size_t)t];
+      const float a[8] = {h.qt.qw, h.qt.qx, h.qt.qy, h.qt.qz, h.qt.tx, h.qt.ty, h.qt.tz, h.score};
+      std::memcpy(high + 8 * t, a, sizeof a);
+    }
   return 0;
 }

@@ -70,6 +70,20 @@ void orc_rot_from_quat(const float q_wxyz[4], float R[9]);
  * as 13 floats each: p1[3] n1[3] p2[3] n2[3] weight.  Outputs q (x,y,z,w), t. */
 int orc_lm_refine(const float* pairs, int P, double q_xyzw[4], double t[3]);
 
+/* Single host stages for the known-answer tests (tests/test_host_kat.py), default
+ * parameters.  orc_voxel has fccf_voxel's layout. */
+typedef struct orc_voxel { float c[3], n[3]; int32_t count; float curvature; } orc_voxel;
+/* Region growing, range_face + selection and select_base (FCCF.cpp:536-677, :429-468):
+ * planes 8 floats each (c, n, fps, voxel count), theta per plane, bases 4 words each
+ * (i1, i2, angle bits, type; past type_index's end the side's sentinel -1 / -2). */
+int orc_stage_grow(const orc_voxel* vox, int64_t nv, int side, float* planes, int cap_planes, int* n_planes,
+                   double* theta, int32_t* bases, int cap_bases, int* n_bases);
+/* transform_cluster (:1040-1231) of n row-major candidates: 8 floats per fused one. */
+int orc_stage_cluster(const float* cand, int64_t n, int cluster_num, float* fine, int64_t cap, int64_t* n_fine,
+                      int64_t* n_clusters);
+/* The fusion (:1546-1606): cand[t] n[t] records of 18 floats (T, score, score2). */
+int orc_stage_fuse(const float* const cand[3], const int64_t n[3], int analyse_max, float T[16], float high[24]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,9 @@ def _load():
     lib.orc_acos_audit.argtypes = [P, ctypes.c_int]
     lib.orc_lm_refine.restype = ctypes.c_int
     lib.orc_lm_refine.argtypes = [P, ctypes.c_int, P, P]
+    lib.orc_stage_grow.argtypes = [P, I64, ctypes.c_int, P, ctypes.c_int, P, P, P, ctypes.c_int, P]
+    lib.orc_stage_cluster.argtypes = [P, I64, ctypes.c_int, P, I64, P, P]
+    lib.orc_stage_fuse.argtypes = [P, P, ctypes.c_int, P, P]
     return lib
 
 
@@ -158,3 +161,57 @@ def lm_refine(pairs):
     t = np.zeros(3)
     lib.orc_lm_refine(p.ctypes.data, p.shape[0], q.ctypes.data, t.ctypes.data)
     return q, t
+
+
+# ---- single host stages (the known-answer tests of tests/test_host_kat.py)
+VOXEL_DTYPE = np.dtype([("c", "<f4", 3), ("n", "<f4", 3), ("count", "<i4"), ("curvature", "<f4")])
+PLANE_DTYPE = np.dtype([("c", "<f4", 3), ("n", "<f4", 3), ("fps", "<f4"), ("nvox", "<i4")])
+BASE_DTYPE = np.dtype([("i1", "<i4"), ("i2", "<i4"), ("angle", "<f4"), ("type", "<i4")])
+
+
+def stage_grow(vox, side):
+    """Growth + selection + select_base (FCCF.cpp:536-677, :429-468): (planes, theta, bases)
+    with libfccf's record layouts."""
+    v = np.ascontiguousarray(vox, VOXEL_DTYPE)
+    pl = np.zeros((64, 8), np.float32)
+    th = np.zeros(64, np.float64)
+    bs = np.zeros((2080, 4), np.int32)
+    nF, nB = ctypes.c_int(), ctypes.c_int()
+    rc = lib.orc_stage_grow(v.ctypes.data, len(v), int(side), pl.ctypes.data, 64, ctypes.byref(nF), th.ctypes.data,
+                            bs.ctypes.data, 2080, ctypes.byref(nB))
+    assert rc == 0
+    planes = np.zeros(nF.value, PLANE_DTYPE)
+    planes["c"], planes["n"] = pl[: nF.value, 0:3], pl[: nF.value, 3:6]
+    planes["fps"], planes["nvox"] = pl[: nF.value, 6], pl[: nF.value, 7].astype(np.int32)
+    bases = np.ascontiguousarray(bs[: nB.value]).view(BASE_DTYPE).reshape(-1).copy()
+    return planes, th[: nF.value].copy(), bases
+
+
+def stage_cluster(cand, cluster_num):
+    """transform_cluster (FCCF.cpp:1040-1231): (fused float32[m, 8], clusters formed)."""
+    a = np.ascontiguousarray(np.asarray(cand, np.float32).reshape(-1, 16))
+    out = np.zeros((max(4 * len(a), 16), 8), np.float32)
+    nf, ncl = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib.orc_stage_cluster(a.ctypes.data, len(a), int(cluster_num), out.ctypes.data, len(out), ctypes.byref(nf),
+                               ctypes.byref(ncl))
+    assert rc == 0 and nf.value <= len(out)
+    return out[: nf.value].copy(), ncl.value
+
+
+def stage_fuse(lists, analyse_max=4):
+    """The fusion (FCCF.cpp:1546-1606): lists of (T, score, score2) per type -> (T, high[3, 8])."""
+    recs = []
+    ptrs = (ctypes.c_void_p * 3)()
+    ns = (ctypes.c_int64 * 3)()
+    for t in range(3):
+        a = np.zeros((max(len(lists[t]), 1), 18), np.float32)
+        for i, (T, s1, s2) in enumerate(lists[t]):
+            a[i, :16] = np.asarray(T, np.float32).reshape(16)
+            a[i, 16], a[i, 17] = s1, s2
+        recs.append(a)
+        ptrs[t] = a.ctypes.data
+        ns[t] = len(lists[t])
+    T = np.zeros(16, np.float32)
+    high = np.zeros(24, np.float32)
+    assert lib.orc_stage_fuse(ptrs, ns, int(analyse_max), T.ctypes.data, high.ctypes.data) == 0
+    return T.reshape(4, 4), high.reshape(3, 8)
