@@ -687,7 +687,26 @@ def main():
             out["sharded"] = sharded
         if roofline is not None:
             roofline["stage"] = stage_rl
+            tr = roofline["traffic"]
+            # over-fetch: calibrated L2-miss bytes per launch / algorithmic bytes per launch
+            roofline["traffic_over_algorithmic"] = tr / roofline["algorithmic_bytes_per_launch"] if tr else None
             out["roofline"] = roofline
+            # the sort's finish kernels beside the dominant one: honest
+            # algorithmic bytes (keys, values and, for the elements a kernel finishes, the
+            # sorted point gathered and written: DESIGN.md §14) and calibrated traffic, at
+            # the pre-pass's width (ten clouds per launch)
+            fk = {}
+            for k in ("k_is_wave", "k_is_block"):
+                if k in table:
+                    t = table[k]
+                    trk = pmc_traffic(k, args.config, PROBE_BATCH if pipelined else 2)
+                    fk[k] = {"avg_launch_us": t["avg_launch_us"],
+                             "algorithmic_bytes_per_launch": t["algorithmic_bytes_per_launch"],
+                             "achieved_GBps": t["achieved_GBps"],
+                             "frac": t["achieved_GBps"] / HBM_PEAK_GBS if t["achieved_GBps"] else None,
+                             "traffic": trk,
+                             "traffic_over_algorithmic": trk / t["algorithmic_bytes_per_launch"] if trk else None}
+            out["finish_kernels"] = fk
             out["kernel_table"] = {k: {a: (round(b, 4) if isinstance(b, float) else b) for a, b in v.items()}
                                    for k, v in table.items()}
         T_oracle = None

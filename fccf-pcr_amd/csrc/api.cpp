@@ -62,7 +62,6 @@ extern "C" int fccf_ctx_destroy(fccf_ctx* c) {
   pipeline_release(c);
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.reset();
-    for (auto& g : cs.g_segb) g.reset();
     cs.g_fine.reset();
     for (auto& e : cs.ev)
       if (e) (void)hipEventDestroy(e);
@@ -254,18 +253,6 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
     for (uint32_t i = 0; i < (uint32_t)n; ++i) iota[i] = i;
     if (n) HIP_CHECK(hipMemcpyAsync(b.v0, iota.data(), 4 * (size_t)n, hipMemcpyHostToDevice, st));
     k_sortkeys_params<<<1, 1024, 0, st>>>(b.k0, d_sc, b.params);
-    // FCCF_IS_WATCH=<seconds> (dev): progress records of the owner kernel in host-mapped
-    // memory, printed and the process ended if the sort has not finished by then
-    static const double watch = std::getenv("FCCF_IS_WATCH") ? std::atof(std::getenv("FCCF_IS_WATCH")) : 0.0;
-    uint32_t* prog = nullptr;
-    if (watch > 0) {
-      HIP_CHECK(hipStreamSynchronize(st));
-      HIP_CHECK(hipHostMalloc((void**)&prog, 4 * 32 * 512, hipHostMallocMapped | hipHostMallocCoherent));
-      std::memset(prog, 0xFF, 4 * 32 * 512);
-      uint32_t* dprog = nullptr;
-      HIP_CHECK(hipHostGetDevicePointer((void**)&dprog, prog, 0));
-      b.is.prog = dprog;
-    }
     // FCCF_IS_TRACE_OUT=<path> (dev): per block item / wave task timestamps (IsBufs::trace)
     static const char* tpath = std::getenv("FCCF_IS_TRACE_OUT");
     unsigned long long* dtr = nullptr;
@@ -319,24 +306,6 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
       (void)hipFree(dtr);
     }
     HIP_CHECK(hipGetLastError());
-    if (watch > 0) {
-      const auto t0 = std::chrono::steady_clock::now();
-      while (hipStreamQuery(st) == hipErrorNotReady) {
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > watch) {
-          for (int i = 0; i < 512; ++i) {
-            const uint32_t* r = prog + 32 * i;
-            if (r[6] == 9u || r[6] == 0xFFFFFFFFu) continue;
-            std::fprintf(stderr, "wg %d: entry %u sp %u top [%u, %u) d %u guard %u state %u x %u wgiter %u n %u waves", i,
-                         r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[24], r[25]);
-            for (int w = 0; w < 16; ++w) std::fprintf(stderr, " %u/%u", r[8 + w] & 0xFFFFu, r[8 + w] >> 16);
-            std::fprintf(stderr, "\n");
-          }
-          std::fflush(stderr);
-          std::_Exit(3);
-        }
-      }
-      (void)hipHostFree(prog);
-    }
     if (n) HIP_CHECK(hipMemcpyAsync(perm, b.v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(c->sort_stats, b.is.ctl, sizeof c->sort_stats, hipMemcpyDeviceToHost, st));
     static_assert(sizeof c->sort_rounds == sizeof(IsRound) * IS_RMAX, "sort_rounds size");

@@ -99,7 +99,7 @@ struct MailBuf {
 // One captured hipGraph, re-captured whenever its key (the workspace layout and
 // every launch argument that is not read from device memory) changes.  The
 // pipeline's sizes live in device memory, so a graph replays for any input that
-// fits the captured capacities.  FCCF_GRAPHS=0 launches eagerly instead.
+// fits the captured capacities.
 // A pipelined batch enqueues the next pair's cloud stage from a helper thread
 // while this thread waits on events of the current pair.  HIP rejects a wait on an
 // event whose recording stream is being captured at that moment, so graph captures
@@ -222,11 +222,7 @@ struct CachedGraph {
   template <class F>
   void run(const void* k, size_t kn, hipStream_t st, F body, const void* pfunc = nullptr, void** pargs = nullptr,
            bool eager = false, const PatchLayout* lay = nullptr) {
-    static const bool enabled = [] {
-      const char* e = std::getenv("FCCF_GRAPHS");
-      return !(e && e[0] == '0');
-    }();
-    if (!enabled || eager || (g_probe && g_probe->on())) {  // probed calls launch eagerly (probe.h)
+    if (eager || (g_probe && g_probe->on())) {  // probed calls launch eagerly (probe.h)
       body();
       return;
     }
@@ -328,7 +324,6 @@ struct fccf_ctx {
     fccf::CachedGraph g_seg[5];      // first slot of a group: its cloud stage of 1..PAIRS_MAX pairs, one graph
                                      // per pair count: part A (the VoxelGrid passes; with a group attached,
                                      // the whole stage)
-    fccf::CachedGraph g_segb[5];     // and part B (centroid sums beside the face voxels, orientation)
     fccf::CachedGraph g_fine;        // fine-verify batch (K7) of the pair on this set: one graph per
                                      // set, so alternating pairs in a batch replay instead of re-capturing
     void* ws = nullptr;              // pipeline.cpp state of the registration in flight

@@ -814,12 +814,9 @@ void face_voxels_fit(B4<const uint32_t*> d_n, uint32_t cap, float vpt, float cth
 }
 
 uint32_t grid_stream(uint32_t cap, int nbatch, uint32_t per) {
-  static const int total = [] {
-    const char* e = std::getenv("FCCF_STREAM_GRID");
-    return e ? std::atoi(e) : 2048;
-  }();
+  constexpr uint32_t total = 2048;  // (1024 / 4096 measured no better)
   uint32_t g = (cap + per - 1) / per;
-  const uint32_t mx = total > 0 ? std::max(64u, (uint32_t)total / (uint32_t)std::max(1, nbatch)) : 4096u;
+  const uint32_t mx = std::max(64u, total / (uint32_t)std::max(1, nbatch));
   return g < 1 ? 1 : (g > mx ? mx : g);
 }
 

@@ -24,33 +24,6 @@
 namespace fccf {
 namespace {
 
-// Block (0, e) also starts evaluation e's octree from the bounds after S1 (the fused
-// cloud is S1 ++ T_e S2), and block (0, 0) writes the scalars.
-__global__ void __launch_bounds__(256) k_fv_transform(const float* __restrict__ s2, uint32_t n2,
-                                                      const m44* __restrict__ T, float* __restrict__ s2t,
-                                                      const OctState* __restrict__ s1_state, OctState* __restrict__ st,
-                                                      uint32_t* __restrict__ scal, uint32_t n1,
-                                                      uint32_t* __restrict__ ecnt, uint32_t* __restrict__ pts) {
-  KT();
-  const int e = blockIdx.y;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st[e] = *s1_state;
-    ecnt[e] = 0u;  // (the LDS form's per-evaluation entry counts and point counts)
-    pts[e] = 0u;
-    if (e == 0) {
-      scal[4] = n1;
-      scal[5] = n2;
-      scal[7] = 0u;
-    }
-  }
-  const m44 M = T[e];
-  float* o = s2t + (size_t)e * 3 * n2;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += gridDim.x * 256) {
-    const f3 p = tf_se3(M, s2[3 * i], s2[3 * i + 1], s2[3 * i + 2]);
-    o[3 * i] = p.x; o[3 * i + 1] = p.y; o[3 * i + 2] = p.z;
-  }
-}
-
 // scal: [0] leaf entries (counted by k_fv_entries), [1] nbits = 3*Dmax + eb, [3] shift
 // = 3*Dmax + 1 (the is_target bit of the per-point layout kept: the key of a leaf is
 // (e << (shift-1)) | morton), [4] n1, [5] n2, [6] E; pts[e] = 0
@@ -485,16 +458,8 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   sd.aggr = 4 * astride;
   sd.state = sizeof(OctState);
   // T_e * S2, its block aggregates and each evaluation's octree start (from S1's bounds)
-  // in one launch (FCCF_FV_SPLIT=1: the former transform launch, then the aggregates)
-  static const bool split = [] {
-    const char* s = std::getenv("FCCF_FV_SPLIT");
-    return s && s[0] == '1';
-  }();
-  if (split) {
-    k_fv_transform<<<dim3(grid_for(n2, 256, 1024), E), 256, 0, st>>>(s2, n2, b.T, b.s2t, s1_state, b.state, b.scal,
-                                                                    n1, b.nseg_e, b.pts);
-    block_aggr(b.s2t, d_n2, n2, b.aggr2, st, E, sd, nullptr, mail ? &mail->stamp[0] : nullptr);
-  } else {
+  // in one launch
+  {
     FvTransform tf{s2, b.T, b.s2t, s1_state, b.state, b.scal, b.nseg_e, b.pts, n1, n2};
     block_aggr_transform(tf, d_n2, n2, b.aggr2, st, E, sd, mail ? &mail->stamp[0] : nullptr);
   }
@@ -502,7 +467,7 @@ void fine_verify_batch(const float* s1, uint32_t n1, const OctState* s1_state, c
   const dim3 ge(std::max<uint32_t>(1u, (n1 + n2 + FV_TILE - 1) / FV_TILE), E);
   if (mode == FV_LEAVES_LDS) {
     // the leaves of each evaluation merged, sorted and summed in LDS: two launches
-    // after the octrees instead of ~20 (scal[7] was zeroed by k_fv_transform)
+    // after the octrees instead of ~20 (scal[7] was zeroed by the transform launch)
     k_fv_entries<<<ge, 256, 0, st>>>(s1, b.s2t, b.state, b.scal, res, b.k0, b.v0, b.pts, b.nseg_e);
     k_fv_eval<<<E, 1024, 0, st>>>(b.k0, b.v0, b.nseg_e, b.pts, b.scal, b.scores, mail, std::min<uint32_t>(lds_cap, FV_LDS_MAX));
     if (mail) k_fv_mail_err<<<1, 64, 0, st>>>(b.scal, b.scores, E, mail);

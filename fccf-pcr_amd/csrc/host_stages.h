@@ -72,7 +72,7 @@ float quick_verify(m44& T, const std::vector<Plane>& F1, const std::vector<Plane
 void lm_solve(const float* pairs, int P, double best[7]);
 // lm_solve of n problems, `lanes` at a time, SIMD across the problems (lm_batch.cpp):
 // bit-identical to lm_solve per problem.  lanes 0: the widest the CPU runs (8 with
-// AVX-512, 4 with AVX2, else 1 = lm_solve; FCCF_LM_LANES overrides).
+// AVX-512, 4 with AVX2, else 1 = lm_solve).
 void lm_solve_batch(const float* const* pairs, const int* P, int n, double (*best)[7], int lanes = 0);
 int lm_batch_lanes();
 // quick_verify split for batched LMs: the plane pairs (13 floats each) and their count

@@ -28,8 +28,7 @@ Ingest::~Ingest() {
 
 void Ingest::init() {
   if (su) return;
-  const char* e = std::getenv("FCCF_INGEST_ROWS");
-  rows_per_slot = e ? std::max(1024L, std::atol(e)) : (256 << 10);  // 3 MB of xyz per slot
+  rows_per_slot = 256 << 10;  // 3 MB of xyz per slot
   HIP_CHECK(hipStreamCreateWithFlags(&su, hipStreamNonBlocking));
   for (int i = 0; i < NSLOT; ++i) {
     if (hipHostMalloc(&slot[i], 12 * (size_t)rows_per_slot, hipHostMallocDefault) != hipSuccess)
@@ -37,8 +36,7 @@ void Ingest::init() {
     HIP_CHECK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   }
   HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-  const char* t = std::getenv("FCCF_INGEST_THREADS");
-  pool.reset(new Pool(t ? std::atoi(t) : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
+  pool.reset(new Pool((int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()))));
 }
 
 int Ingest::upload_rows(float* dst, int64_t n, const std::function<int(int64_t, int64_t, float*)>& fill) {

@@ -152,13 +152,9 @@ typedef Pt3* GPt3;
 __device__ __forceinline__ Pt3 load_xyz(const float* src, uint32_t v) { return ((GPt3c)(const Pt3*)src)[v]; }
 __device__ __forceinline__ void store_xyz(const IsBufs& W, uint32_t pos, const Pt3& q) { ((GPt3)(Pt3*)W.xyzs)[pos] = q; }
 __device__ __forceinline__ void put_xyz(const IsBufs& W, const float* __restrict__ src, uint32_t pos, uint32_t v) {
-#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 1
-  store_xyz(W, pos, load_xyz(src, pos));  // dev timing only: a coalesced source (wrong points)
-#elif defined(IS_XYZ_PROBE) && (IS_XYZ_PROBE == 2 || IS_XYZ_PROBE == 3)
-  (void)W; (void)src; (void)pos; (void)v;  // dev: no points here (3: k_is_xyz_gather after the finish kernels)
-#else
+  // (a random 12-B load: one line each, overlapped by the finish kernels' LDS work;
+  // a separate gather pass cost 170 us per ten clouds and saved nothing, profiles/r06a)
   store_xyz(W, pos, load_xyz(src, v));
-#endif
 }
 
 // The fence before a workgroup barrier that hands global-memory data between the waves
@@ -748,55 +744,25 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan(B4<const uint32_t*> K2,
   tile_prefix(W, r, dyn, sh64);
 }
 
-// The partitioned tile written out.  Scatter form (G = false): every element to its
-// destination, so a swapped element is a scattered 4-byte store into another tile's
-// lines (two of them: key and value), which other workgroups fill too.  Gather form
-// (G = true): the swap is an involution (L[k] <-> R[k]), so position p receives the
-// element at its partner position -- the element there before the round, with the
-// median-to-first swap applied at m -- and every workgroup writes its own tile's
-// positions, whole lines, coalesced; the partners are read instead (a window of a few
-// tiles, mostly L2 / Infinity-Cache hits).
-template <bool G, int TC>
-__device__ __forceinline__ void store_partitioned(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
-                                                  uint32_t* __restrict__ Ko, uint32_t* __restrict__ Vo,
+// The partitioned tile written out: every element to its destination, so a swapped
+// element is a scattered 4-byte store into another tile's lines (two of them: key and
+// value), which other workgroups fill too.  (A gather form -- every position reading
+// its partner, whole tiles written coalesced -- measured no faster: pipelined
+// 0.770/0.768/0.808 against 0.787/0.794/0.770 ms, profiles/r05a/ab_gather.txt.)
+template <int TC>
+__device__ __forceinline__ void store_partitioned(uint32_t* __restrict__ Ko, uint32_t* __restrict__ Vo,
                                                   const uint32_t (&kk)[TC], const uint32_t (&vv)[TC],
-                                                  uint32_t (&dst)[TC], uint32_t a, uint32_t f, uint32_t l,
-                                                  uint32_t m, uint32_t kf, uint32_t vf, const IsBufs& W) {
-  if constexpr (!G) {
+                                                  const uint32_t (&dst)[TC], uint32_t f, uint32_t l, const IsBufs& W) {
 #pragma unroll
-    for (int c = 0; c < TC; ++c) {
-      const uint32_t d = dst[c];
-      if (d == IS_NONE) continue;
-      if (d <= f || d >= l) {  // cannot happen; never write outside the segment
-        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
-        continue;
-      }
-      Ko[d] = kk[c];
-      Vo[d] = vv[c];
+  for (int c = 0; c < TC; ++c) {
+    const uint32_t d = dst[c];
+    if (d == IS_NONE) continue;
+    if (d <= f || d >= l) {  // cannot happen; never write outside the segment
+      is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
+      continue;
     }
-  } else {
-    uint32_t gk[TC], gv[TC];
-#pragma unroll
-    for (int c = 0; c < TC; ++c) {  // every partner load issued before the first store
-      const uint32_t p = a + c * IS_TT + threadIdx.x, d = dst[c];
-      gk[c] = kk[c];
-      gv[c] = vv[c];
-      if (d == IS_NONE || d == p) continue;
-      if (d <= f || d >= l) {  // cannot happen; never read outside the segment
-        is_fault(W.ctl, W.err, IS_FAULT_SCATTER);
-        dst[c] = IS_NONE;
-        continue;
-      }
-      gk[c] = d == m ? kf : K[d];
-      gv[c] = d == m ? vf : V[d];
-    }
-#pragma unroll
-    for (int c = 0; c < TC; ++c) {
-      if (dst[c] == IS_NONE) continue;
-      const uint32_t p = a + c * IS_TT + threadIdx.x;
-      Ko[p] = gk[c];
-      Vo[p] = gv[c];
-    }
+    Ko[d] = kk[c];
+    Vo[d] = vv[c];
   }
 }
 
@@ -810,7 +776,6 @@ constexpr uint32_t IS_WIN = 256;  // prefix window in LDS (larger windows: binar
 #ifndef IS_SCATTER_MINB
 #define IS_SCATTER_MINB 1
 #endif
-template <bool G>
 __global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
                                                       B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r,
                                                       int R) {
@@ -936,7 +901,7 @@ __global__ void __launch_bounds__(IS_TT, IS_SCATTER_MINB) k_is_scatter(B4<const 
         dst[c] = au + W.gel[au + (x - (wg_n <= IS_WIN ? wing[u - wg_lo] : pre[u].x))];
       }
     }
-    store_partitioned<G, IS_TC_L>(K, V, Ko, Vo, kk, vv, dst, a, f, l, m, s.kf, s.vf, W);
+    store_partitioned<IS_TC_L>(Ko, Vo, kk, vv, dst, f, l, W);
     cut = wave_min_u32(cut);
     if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
     __syncthreads();
@@ -1115,7 +1080,6 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B4<const uint32_t*> K
 
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
-template <bool G>
 __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
                                                       B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r) {
   KT();
@@ -1259,7 +1223,7 @@ __global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2,
       dst[c] = au + W.gel[au + (x - preg[u])];
     }
   }
-  store_partitioned<G, IS_TC>(K, V, Ko, Vo, kk, vv, dst, a, f, l, m, s.kf, s.vf, W);
+  store_partitioned<IS_TC>(Ko, Vo, kk, vv, dst, f, l, W);
   IS_PH(3);  // destinations (list loads), stores issued
   cut = wave_min_u32(cut);
   if (lane == 0 && cut != IS_NONE) atomicMin(&scut, cut);
@@ -1308,19 +1272,15 @@ struct BlockLds {
 };
 static_assert(IS_LCAP <= 8192 && IS_WCAP <= 1024, "task packing: 13-bit offsets, 11-bit sizes, 8-bit depths");
 
-#ifndef IS_WLEVEL
-#define IS_WLEVEL 1  // wave tasks of > 64 elements partitioned level by level (wave_task_level)
-#endif
+// (wave tasks of > 64 elements are partitioned level by level, wave_task_level)
 
 // One wave's slice of the wave kernel
 struct WaveLds {
   uint32_t k[IS_WCAP], v[IS_WCAP];
-#if IS_WLEVEL
   uint16_t lg[IS_WCAP], ll[IS_WCAP];   // a level's >= / <= positions, in position order
   uint32_t cutv[IS_WCAP];              // per segment (at its first position): its cut, or its end
   uint64_t bw[2][IS_WC + 1];           // the level's >= / <= ballots per chunk
   uint32_t pc[2][IS_WC + 1];           // and their exclusive prefix counts
-#endif
   uint16_t xch[IS_WCAP / 2];
   uint32_t heads[IS_WCAP / 32];
   uint32_t stk[IS_STACK];
@@ -1648,7 +1608,6 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
   }
 }
 
-#if IS_WLEVEL
 // # of the level's >= (s = 0) / <= (s = 1) elements before position x (0 <= x <= 64 C)
 __device__ __forceinline__ uint32_t level_rank(const WaveLds& S, int s, uint32_t x) {
   const uint32_t c = x >> 6, bit = x & 63u;
@@ -1861,7 +1820,6 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       if (dpos[c] != IS_NONE) store_xyz(W, dpos[c], pt[c]);
   }
 }
-#endif
 
 // One partition of [f, l) (IS_WCAP < l - f <= IS_OT * C) in LDS by the whole block.
 template <int C>
@@ -2298,6 +2256,7 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
   uint32_t* const K1 = K12[e];
   uint32_t* const V1 = V12[e];
   uint32_t units = 0;  // elements this workgroup sorted in LDS (the block probe's unit count)
+  uint32_t xunits = 0;  // ... of which it finished itself (sorted points written: ctl[21])
   for (;;) {
     if (threadIdx.x == 0) {
       // look before taking: once the list is drained, leave without another atomic
@@ -2356,6 +2315,7 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
         // (free: std::sort's depth bounds the LDS stacks; its depth limit there is the
         // parallel rank sort, exact for distinct keys)
         lds_block(S, W, K, V, K0, V0, gf, len, gfree ? depth0(len) : gd);
+        if (W.xyzs) xunits += len - S.units;  // (S.units: its elements handed to wave tasks)
       } else if (gd == 0 && distinct_keys(S, K + gf, (buf ? K0 : K1) + gf, (buf ? V0 : V1) + gf, len)) {
         // depth exhausted, distinct keys: the order is unique; go on with free pivots
         if (threadIdx.x == 0) {
@@ -2377,8 +2337,10 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
             K0[gf + q] = K[gf + q];
             V0[gf + q] = V[gf + q];
           }
-        if (W.xyzs)
+        if (W.xyzs) {
           for (uint32_t q = threadIdx.x; q < len; q += IS_OT) put_xyz(W, W.vgp->src, gf + q, V[gf + q]);
+          xunits += len;
+        }
         __syncthreads();
       } else {
         if (S.son && threadIdx.x == 0) atomicAdd(&W.ctl[3], 1u);
@@ -2411,6 +2373,7 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
     }
   }
   if (threadIdx.x == 0 && units) atomicAdd(&W.ctl[20], units);
+  if (threadIdx.x == 0 && xunits) atomicAdd(&W.ctl[21], xunits);
 }
 
 // Every wave takes its share of the wave tasks: the subtree in its LDS slice,
@@ -2457,14 +2420,12 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
     if (lane < IS_WCAP / 32) S.heads[lane] = 0;
     wsync();
     const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
-#if IS_WLEVEL
     if (n > 64) {
       if (n <= 128) wave_task_level<2>(S, K, V, f, n, d, W, xsrc);
       else if (n <= 256) wave_task_level<4>(S, K, V, f, n, d, W, xsrc);
       else wave_task_level<IS_WC>(S, K, V, f, n, d, W, xsrc);
       if (S.son && lane == 0) atomicAdd(&S.lstat[2], 1u);
     } else
-#endif
     {
     wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
     wsync();
@@ -2512,18 +2473,6 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
   }
 }
 
-#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 3
-// dev: the sorted points in one streaming pass after the finish kernels (every position
-// reads its final value's point)
-__global__ void __launch_bounds__(256) k_is_xyz_gather(B4<uint32_t*> V02, B4<IsBufs> W2) {
-  const IsBufs W = W2[blockIdx.y];
-  if (!W.xyzs) return;
-  const uint32_t n = W.ctl[0];
-  const uint32_t* V = V02[blockIdx.y];
-  const float* src = W.vgp->src;
-  for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) store_xyz(W, p, load_xyz(src, V[p]));
-}
-#endif
 
 }  // namespace
 
@@ -2532,29 +2481,20 @@ __global__ void __launch_bounds__(256) k_is_xyz_gather(B4<uint32_t*> V02, B4<IsB
 // two per CU; only the block kernel's launch is taken from this form
 void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<IsBufs> b, int R,
                         hipStream_t st, int nbatch) {
-  ProbeBytes pb;  // algorithmic bytes: each element's key and value read once and written once
-  for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0);
+  ProbeBytes pb;  // algorithmic bytes: see introsort_u32 (block_probe_bytes)
+  for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0).add(b[e].ctl + 21, 24.0);
   const int blocks = std::max(1, 2 * IS_OWN_BLOCKS / nbatch);
   FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
 }
 #else
-uint32_t introsort_tier() {
-  static const uint32_t t = [] {
-    const char* s = std::getenv("FCCF_IS_TIER");  // dev: round threshold (default 4096)
-    const uint32_t v = s ? (uint32_t)std::atoi(s) : 4096u;
-    return v < 64u ? 64u : (v > IS_LCAP ? IS_LCAP : v);
-  }();
-  return t;
-}
+// the rounds split segments longer than this (8192 / 6144 / 2048 with 13-17 rounds
+// measured slower)
+uint32_t introsort_tier() { return 4096u; }
 uint32_t introsort_segmax(uint32_t cap) { return cap / introsort_tier() + 2; }
 uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
 uint32_t introsort_maxtiles_l(uint32_t cap) { return cap / IS_TILE_L + introsort_segmax(cap) + 1; }
 
 int introsort_rounds(uint32_t cap) {
-  static const int env = [] {
-    const char* s = std::getenv("FCCF_IS_ROUNDS");
-    return s ? std::atoi(s) : -1;
-  }();
   int r = 0;
   const uint32_t tier = introsort_tier();
   if (cap > tier) {
@@ -2563,7 +2503,6 @@ int introsort_rounds(uint32_t cap) {
     while ((uint64_t)tier << r < cap) ++r;
     r += 7;
   }
-  if (env >= 0) r = env;
   return r > IS_RMAX ? IS_RMAX : r;
 }
 
@@ -2606,7 +2545,6 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.shard_rank = 0;
   b.shard_r0 = 0;
   b.shard_group = nullptr;
-  b.prog = nullptr;
   b.trace = nullptr;
   b.tier = introsort_tier();
   b.stats = 0;
@@ -2634,19 +2572,20 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // FCCF_IS_PLAN=large|small overrides (tests run the sort cases in both)
   const char* pm = std::getenv("FCCF_IS_PLAN");
   const bool large = b[0].shard_n > 1 || (pm && pm[0] == 'l' ? true : (pm && pm[0] == 's' ? false : cap >= IS_LARGE_MIN));
-  // the rounds' store form (store_partitioned): FCCF_IS_GATHER=1 the gather form, 0 the
-  // scatter form (read per call, as FCCF_IS_PLAN; tests run the sort cases in both)
-  const char* gm = std::getenv("FCCF_IS_GATHER");
-  const bool gather = gm && gm[0] == '1';
   // algorithmic bytes of a launch, summed over its clouds (probe.h)
   auto pb_round = [&](int r, double per) {
     ProbeBytes x;
     for (int e = 0; e < nbatch; ++e) x.add(&b[e].rounds[r].pad, per);
     return x;
   };
-  auto pb_ctl = [&](int word, double per) {
+  auto pb_block = [&] {
     ProbeBytes x;
-    for (int e = 0; e < nbatch; ++e) x.add(b[e].ctl + word, per);
+    for (int e = 0; e < nbatch; ++e) x.add(b[e].ctl + 20, 16.0).add(b[e].ctl + 21, 24.0);
+    return x;
+  };
+  auto pb_wave = [&] {
+    ProbeBytes x;
+    for (int e = 0; e < nbatch; ++e) x.add(b[e].ctl + 19, b[e].xyzs ? 40.0 : 16.0);
     return x;
   };
   for (int r = 0; r < R; ++r) {
@@ -2660,38 +2599,29 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
       // algorithmic bytes: key + value read and written, plus a 2-byte list entry
-      if (gather)
-        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter<true>, dim3(maxtiles_l, nbatch), IS_TT, 0, st,
-                    B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r, R);
-      else
-        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter<false>, dim3(maxtiles_l, nbatch), IS_TT, 0, st,
-                    B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r, R);
+      FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter, dim3(maxtiles_l, nbatch), IS_TT, 0, st,
+                  B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r, R);
     } else {
       FCCF_LAUNCH("k_is_count_plan",
                   (pb_round(r, 8.0)),
                   k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B4<const uint32_t*>(ki),
                   B4<const uint32_t*>(vi), b, r);
       step("count", r);
-      if (gather)
-        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s<true>, dim3(maxtiles, nbatch), IS_TT,
-                    8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
-      else
-        FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s<false>, dim3(maxtiles, nbatch), IS_TT,
-                    8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
+      FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT,
+                  8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
     }
     step("scatter", r);
   }
-  // algorithmic bytes: each element's key and value read once and written once
+  // Algorithmic bytes of the finish kernels: each element's key and value read once and
+  // written once (16 B), and for the elements a kernel finishes while the sort writes
+  // sorted points (VoxelGrid's first pass), the point gathered from its original
+  // position and written at its final one (12 + 12 B): the wave kernel finishes every
+  // element of its tasks (ctl[19]), the block kernel the leaves it settles itself
+  // (ctl[21], of its ctl[20] LDS elements).
   // k_is_block: IS_OWN_BLOCKS workgroups (one per CU) split over the clouds, so both
   // clouds' items run at once and 8 CUs stay free for the small kernels of other
   // streams (matching, fine verification); profiles/r03r
-  // dev: FCCF_IS_BLOCK_GRID = block-kernel workgroups per launch, split over the clouds
-  // (default IS_OWN_BLOCKS: one per CU; its LDS leaves room for two per CU)
-  static const int block_grid = [] {
-    const char* s = std::getenv("FCCF_IS_BLOCK_GRID");
-    return s ? std::atoi(s) : 0;
-  }();
-  const int own_blocks = std::max(1, (block_grid > 0 ? block_grid : IS_OWN_BLOCKS) / nbatch);
+  const int own_blocks = std::max(1, IS_OWN_BLOCKS / nbatch);
   // Stage groups of three to five pairs (six to ten clouds per launch): the block
   // kernel's second form, 512-thread workgroups at two per CU (introsort_b2.hip), whose
   // items interleave their partition chains on each CU: pipelined 0.650-0.654 against
@@ -2700,25 +2630,17 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // FCCF_IS_BLOCK_B2=0 / 1: never / always (dev, tests)
   const char* b2e = std::getenv("FCCF_IS_BLOCK_B2");
   const bool b2 = b2e ? b2e[0] == '1' : nbatch >= 6;
-  if (b2 && block_grid <= 0)
+  if (b2)
     introsort_block_b2(k0, v0, k1, v1, b, R, st, nbatch);
   else
-    FCCF_LAUNCH("k_is_block", (pb_ctl(20, 16.0)), k_is_block,
+    FCCF_LAUNCH("k_is_block", (pb_block()), k_is_block,
                 dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
   step("block", R);
-  // dev: FCCF_IS_WAVE_GRID = workgroups per launch, split over the clouds (default
-  // IS_WAVE_BLOCKS per cloud)
-  static const int wave_grid = [] {
-    const char* s = std::getenv("FCCF_IS_WAVE_GRID");
-    return s ? std::atoi(s) : 0;
-  }();
-  const int wave_blocks = wave_grid > 0 ? std::max(1, wave_grid / nbatch) : IS_WAVE_BLOCKS;
-  FCCF_LAUNCH("k_is_wave", (pb_ctl(19, 16.0)), k_is_wave,
+  // (other wave grids at ten clouds per launch: no gain, profiles/r05au/ab_wave_grid_width10.txt)
+  const int wave_blocks = IS_WAVE_BLOCKS;
+  FCCF_LAUNCH("k_is_wave", (pb_wave()), k_is_wave,
               dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);
-#if defined(IS_XYZ_PROBE) && IS_XYZ_PROBE == 3
-  k_is_xyz_gather<<<dim3(2048, nbatch), 256, 0, st>>>(v0, b);
-#endif
 }
 
 #endif  // IS_KERNEL_VARIANT

@@ -79,7 +79,6 @@ struct IsBufs {
   uint32_t shard_n, shard_rank, shard_r0;
   uint32_t* bounds;     // IS_SHARD_MAX + 1
   void* shard_group;    // host only: the Group whose ranks gather the sorted slices
-  uint32_t* prog;       // dev: host-mapped progress records of k_is_own (null = off)
   unsigned long long* trace;  // dev (null = off): per block item / wave task {start, end, size, who},
                               // block records from 0 (count in ctl[24]), wave records from taskmax (ctl[25])
   uint32_t segmax, maxtiles, ownmax, taskmax;
@@ -306,9 +305,8 @@ struct FvTransform {
 void block_aggr_transform(const FvTransform& tf, const uint32_t* d_n, uint32_t cap, float* aggr, hipStream_t st,
                           int batch, SeqStrides sd, uint64_t* stamp = nullptr);
 // Grid of a streaming (grid-stride) launch over up to `cap` items per cloud, `per` items
-// per workgroup, `nbatch` clouds: about one chip-full of workgroups in all (FCCF_STREAM_GRID
-// workgroups per launch, default 2048; 0 = one workgroup per `per` items, up to 4096 per
-// cloud).  The face stage and the second VoxelGrid pass run on the downsampled clouds,
+// per workgroup, `nbatch` clouds: about one chip-full of workgroups in all (2048 per
+// launch).  The face stage and the second VoxelGrid pass run on the downsampled clouds,
 // a third of `cap` or less, so a grid sized by `cap` is mostly workgroups with no work.
 uint32_t grid_stream(uint32_t cap, int nbatch, uint32_t per = 256);
 constexpr uint32_t AGGR_BLOCK = 4096;  // points per block aggregate

@@ -411,11 +411,6 @@ __attribute__((target("avx2,bmi2"))) void lm_solve_x4(const float* const* pf, co
 }
 
 int lm_lanes_detect() {
-  const char* e = std::getenv("FCCF_LM_LANES");  // tests / A-B: 1 (scalar), 4, 8
-  if (e) {
-    const int v = std::atoi(e);
-    return v >= 8 ? 8 : (v >= 4 ? 4 : 1);
-  }
   __builtin_cpu_init();
   if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") && __builtin_cpu_supports("avx512vl"))
     return 8;

@@ -413,23 +413,9 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   auto& cg = c->cs[S0];          // the group's arena, stage graphs and fork/join events
   PipeSet& gs = pset(c, S0);
   const int nc = 2 * P;
-  // Split form (dev, FCCF_STAGE_SPLIT=1): the stage in two graphs, A the VoxelGrid passes
-  // (the sort) on sa[0] and B the centroid sums beside the face voxels, then the
-  // orientation, on sa[2], so that a next group's A queued on sa[0] can overlap this
-  // group's B.  B's centroid branch is forked onto sa[3]
-  // inside its capture (a replay schedules the branches itself).  With a group attached
-  // (collectives in the stage) everything stays on sa[0], as one chain.
+  // (the centroid sums run on sa[2] beside the face stage, forked inside the stage)
   hipStream_t st0 = c->sa[0];
-  // Measured slower in the pipelined batch (0.805-0.812 against 0.757-0.784 ms per
-  // registration, interleaved, with the next stage enqueued early): the
-  // overlapping face part stretches the phase-B chains' matching and fine kernels.  Off
-  // by default; FCCF_STAGE_SPLIT=1 (dev) turns it on.
-  static const bool split_env = [] {
-    const char* e = std::getenv("FCCF_STAGE_SPLIT");
-    return e && e[0] == '1';
-  }();
-  const bool split = split_env && !c->group;
-  hipStream_t sB = split ? c->sa[2] : st0, ss = split ? c->sa[3] : c->sa[2];
+  hipStream_t sB = st0, ss = c->sa[2];
   // both clouds get the larger capacity (all clouds of a stage, in fact), so their
   // workspaces are laid out alike (batched launches address cloud e at a fixed offset)
   uint32_t capmax = 1;
@@ -443,9 +429,6 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     std::lock_guard<std::mutex> lk(capture_mutex());
     if (hipEventQuery(c->cs[S0 + j].ev[3]) != hipSuccess) HIP_CHECK(hipStreamWaitEvent(st0, c->cs[S0 + j].ev[3], 0));
   }
-  // and the previous stage on these slots has finished its B part (the S1 replay is its
-  // last launch; B runs on another stream than this stage's A)
-  if (split) guarded_stream_wait(st0, cg.ev[4]);
   // (the centroid scratch is carved for BMAX clouds whatever the pair count, so slot
   // j's clouds sit at the same addresses in every stage form, and the per-slot graphs
   // keyed by those addresses -- the S1 replay, fine verification -- keep replaying when
@@ -458,9 +441,8 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   // (introsort.hip, group.cpp); the stage then runs eagerly (a host step between the
   // sort and the gather of the sorted slices)
   Group* const DG = shard_sort_enabled(c->group, capmax, introsort_rounds(capmax)) ? c->group : nullptr;
-  // Row P shards with row D (FCCF_SHARD_P=0 keeps the face stage whole)
-  const char* pe = std::getenv("FCCF_SHARD_P");
-  Group* const PG = (DG && capmax >= 8192 && !(pe && pe[0] == '0')) ? DG : nullptr;
+  // Row P shards with row D
+  Group* const PG = (DG && capmax >= 8192) ? DG : nullptr;
   CloudWS w[BMAX];
   const float* xin[BMAX] = {};
   uint32_t nv[BMAX] = {};
@@ -543,9 +525,17 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
   }
   // test hook (fccf_debug_graph_mismatch): a replay patched with another layout's
   // workspace pointer, which the replay check must refuse before anything runs
+  // A pipelined batch launches its stages eagerly from the helper thread; a single
+  // registration replays the graph.  A stage graph's launch holds the runtime for ~250 us
+  // of host time (profiles/r05ab), while the two phase-B chains launch their matching
+  // and fine kernels: in batches the eager stage read 0.664-0.671 against 0.706-0.716 ms
+  // per registration, and single registrations were ~15 us faster with the graph
+  // (profiles/r05ac).
+  const bool eager = DG != nullptr || exact2 || batch;
   VGEntry wrong;
   void** pargs = entry.args;
-  if (c->graph_mismatch && cg.g_seg[P - 1].replays(&key, sizeof key) && !(DG != nullptr || exact2)) {
+  // (armed only for a call that replays: an eager stage checks no layout)
+  if (c->graph_mismatch && !eager && cg.g_seg[P - 1].replays(&key, sizeof key)) {
     c->graph_mismatch = false;
     wrong = entry;
     wrong.part.v[0] += 64;
@@ -573,29 +563,12 @@ void clouds_enqueue_group(fccf_ctx* c, int G, int P, const PairIn* in, float lea
     seg_s1_replay(w, P, Pa, sB);
   };
   for (int j = 0; j < P; ++j) __atomic_store_n(&cmail[j].done, 0u, __ATOMIC_RELAXED);  // (set by k_mail_done)
-  // A pipelined batch launches its stages eagerly from the helper thread; a single
-  // registration replays the graph.  A stage graph's launch holds the runtime for ~250 us
-  // of host time (profiles/r05ab), while the two phase-B chains launch their matching
-  // and fine kernels: in batches the eager stage read 0.664-0.671 against 0.706-0.716 ms
-  // per registration, and single registrations were ~15 us faster with the graph
-  // (profiles/r05ac).  FCCF_EAGER_STAGE=0 uses the graph everywhere, =2 launches eagerly
-  // everywhere (dev A/B).
-  static const int eager_env = [] {
-    const char* e = std::getenv("FCCF_EAGER_STAGE");
-    return e ? std::atoi(e) : 1;
-  }();
-  const bool eager = DG != nullptr || exact2 || eager_env >= 2 || (eager_env == 1 && batch);
   cg.g_seg[P - 1].run(&key, sizeof key, st0, [&] {
     seg_pass1(w, nc, xin, nv, leaf, st0, &entry);
     seg_downsample(w, nc, leaf, st0, exact2 ? VG_PRESORTED : VG_OPTIMISTIC);
-    if (!split) part_b();
+    part_b();
   }, vg_entry_kernel(), pargs, eager, &lay);
   HIP_CHECK(hipEventRecord(cg.ev[0], st0));  // external signal for stage_inputs (the group's inputs have been read)
-  if (split) {
-    HIP_CHECK(hipEventRecord(cg.ev[1], st0));  // the VoxelGrid passes done: B may start
-    HIP_CHECK(hipStreamWaitEvent(sB, cg.ev[1], 0));  // (sB is captured by this thread only)
-    cg.g_segb[P - 1].run(&key, sizeof key, sB, part_b, nullptr, nullptr, eager);
-  }
   HIP_CHECK(hipEventRecord(cg.ev[4], sB));  // clouds done, S1 octree bounds replayed
   HIP_CHECK(hipGetLastError());
 }
@@ -643,11 +616,8 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
   // growing runs both clouds in parallel right after this wait: one worker besides this
-  // thread (FCCF_WARM_N: dev A/B of the count)
-  static const int warm_n = [] {
-    const char* v = std::getenv("FCCF_WARM_N");
-    return v && *v ? std::atoi(v) : 1;
-  }();
+  // thread (keeping more workers spinning slowed growth on the box)
+  constexpr int warm_n = 1;
   ch.pool->warm(1000, warm_n);
   if (c->group) {
     // a sharded stage holds collectives: a bounded wait that aborts the group on a
@@ -657,11 +627,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     // (under the capture lock: with several pairs per stage, a later pair's B1 runs while
     // the helper thread may be capturing the next stage on the stream ev[4] was recorded
     // on, and HIP refuses to synchronize such an event; ev[4] is complete by then)
-    static const bool keep_warm = [] {
-      const char* v = std::getenv("FCCF_SPIN_WARM");  // dev A/B
-      return !(v && v[0] == '0');
-    }();
-    if (!mail_wait(&cm.done, 5000.0, [&] { if (keep_warm) ch.pool->warm(400, warm_n); })) {
+    if (!mail_wait(&cm.done, 5000.0, [&] { ch.pool->warm(400, warm_n); })) {
       std::lock_guard<std::mutex> lk(capture_mutex());
       HIP_CHECK(hipEventSynchronize(group_event(c, s, 4)));
     }
@@ -1182,14 +1148,10 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
     // S1 octree bounds replayed (with the clouds); ev[4]'s stream may be capturing the next pair's clouds
     guarded_stream_wait(sf, group_event(c, s, 4));
     if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[4], sf));  // (otherwise the mailbox stamps time it)
-    static const bool fine_eager = [] {  // dev A/B: FCCF_EAGER_FINE=1 launches fine verification eagerly
-      const char* e = std::getenv("FCCF_EAGER_FINE");
-      return e && e[0] == '1';
-    }();
     c->cs[s].g_fine.run(&fkey, sizeof fkey, sf, [&] {
       fine_verify_batch(w[0].resid, n1, w[0].fstate, w[1].resid, n2, E, (double)P.fine_verify_voxel_size, fb, sf,
                         &fm, fmode, fcap);
-    }, nullptr, nullptr, fine_eager);
+    }, nullptr, nullptr, false);
     HIP_CHECK(hipGetLastError());
     if (FG) HIP_CHECK(hipEventRecord(c->cs[s].tev[5], sf));
     if (FG) group_fine_gather(FG, s, fb.scores, El, fb.scal + 7, sf);
@@ -1313,7 +1275,6 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
   }
   S.graph_captures = c->cs[s].g_fine.captures;
   for (auto& g : c->cs[s].g_seg) S.graph_captures += g.captures;
-  for (auto& g : c->cs[s].g_segb) S.graph_captures += g.captures;
   counts.push_back(S.lm_solves);
   counts.push_back(0);
   if (c->debug) {
@@ -1333,7 +1294,6 @@ bool phase_b2(fccf_ctx* c, int s, bool batch = false) {
 void reset_capture_counts(fccf_ctx* c) {
   for (auto& cs : c->cs) {
     for (auto& g : cs.g_seg) g.captures = 0;
-    for (auto& g : cs.g_segb) g.captures = 0;
     cs.g_fine.captures = 0;
   }
 }
@@ -1802,17 +1762,14 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
   }
 }
 
-// The batch with two phase-B chains where the ctx allows it (FCCF_B1_CHAINS=1 forces
-// one); a stage redo found by a two-chain batch (rare: an input out of leaf order after
+// The batch with two phase-B chains where the ctx allows it; a stage redo found by a two-chain batch (rare: an input out of leaf order after
 // main's VoxelGrid) reruns the whole batch with one chain, whose redo runs in place.
 void run_register_batch_any(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src,
                             const float* const* tar, const int64_t* n_tar, bool on_device, float leaf,
                             const fccf_params& P, float* T_out, fccf_stats* stats) {
-  const char* ce = std::getenv("FCCF_B1_CHAINS");
-  const int want = ce ? std::atoi(ce) : 2;
   const char* pb_env = std::getenv("FCCF_PAIR_BATCH");
   const int pp = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
-  const bool two = want >= 2 && pp >= 2 && n >= 2 && !c->group && !c->probe.on() && !c->debug &&
+  const bool two = pp >= 2 && n >= 2 && !c->group && !c->probe.on() && !c->debug &&
                    !c->grow_device && !c->lm_device;
   if (two) {
     try {

@@ -25,7 +25,7 @@ namespace fccf {
 // Algorithmic bytes of one launch: fixed + sum of per[i] * *cnt[i] (device-resident
 // unit counts, one term per problem of a batched launch).
 struct ProbeBytes {
-  static constexpr int MAXT = 16;
+  static constexpr int MAXT = 32;  // (two terms per cloud at ten clouds per launch)
   const uint32_t* cnt[MAXT] = {};
   double per[MAXT] = {};
   int n = 0;

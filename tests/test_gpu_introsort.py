@@ -126,15 +126,11 @@ def test_downsample_equals_reference_order(ctx, fccf, oracle, n, leaf, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("plan", ["large", "small"])
-@pytest.mark.parametrize("gather", ["0", "1"])
-def test_round_plan_forms_equal_std_sort(ctx, fccf, oracle, plan, gather, monkeypatch):
+def test_round_plan_forms_equal_std_sort(ctx, fccf, oracle, plan, monkeypatch):
     """Both forms of the rounds' plan (FCCF_IS_PLAN: once per round by the last
-    workgroups, the default from 2M points; or derived by every workgroup, below it)
-    and both store forms of the rounds (FCCF_IS_GATHER: swapped elements scattered to
-    their partners, or every position gathering its partner) on every case and on the
-    c3 keys, against the oracle's std::sort."""
+    workgroups, the default from 2M points; or derived by every workgroup, below it) on
+    every case and on the c3 keys, against the oracle's std::sort."""
     monkeypatch.setenv("FCCF_IS_PLAN", plan)
-    monkeypatch.setenv("FCCF_IS_GATHER", gather)
     cases = _keys_cases(fccf, oracle)
     c = fccf.CONFIGS["c3"]
     src, _, _ = fccf.synth_pair(c["n"], c["room"])
