@@ -261,9 +261,11 @@ def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
         groups = fccf.local_groups(ctxs)
 
         def work(r):
+            b0 = groups[r].rx_bytes()
             T, s = ctxs[r].register(src, tar, leaf)
+            b1 = groups[r].rx_bytes()
             Tb, sb = ctxs[r].register_batch([(src, tar)] * 2, leaf)
-            return T, s, Tb, sb
+            return T, s, Tb, sb, [y - x for x, y in zip(b0, b1)]
 
         out = _on_threads(work, n)
         for g in groups:
@@ -271,7 +273,11 @@ def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
     finally:
         for cx in ctxs:
             cx.close()
-    for T, s, Tb, sb in out:
+    for T, s, Tb, sb, rx in out:
+        # fccf_group_bytes: every channel exchanged; row D alone brings each rank the
+        # other ranks' sorted (key, value) slices of both clouds, ~(n-1)/n of 8 B per point
+        assert rx[0] > 0 and rx[1] > 0, rx
+        assert rx[2] >= 0.5 * 8 * 2 * c["n"] * (n - 1) / n, rx
         np.testing.assert_array_equal(bits(T), bits(T0))
         for Tx in Tb:
             np.testing.assert_array_equal(bits(Tx), bits(T0))
