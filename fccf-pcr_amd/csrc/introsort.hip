@@ -939,6 +939,21 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
   uint32_t j, f, l, m, P, kf;
   uint32_t tile0;
   uint32_t kk[IS_TC];
+  if (r > 0) {
+    // The grid is sized for the first rounds (maxtiles), and every workgroup derives the
+    // plan before it knows whether it has a tile.  Round r's large segments are children
+    // of round r-1's (which partitioned `pad` elements in nseg segments), so it has at
+    // most pad / IS_TILE + 2 nseg tiles: a workgroup past that bound leaves at once
+    // (the late rounds hold a few segments; their launches were all plan derivation).
+    const IsRound pr = W.rounds[r - 1];
+    if (t >= pr.pad / IS_TILE + 2u * pr.nseg + 1u) {
+      if (threadIdx.x == 0) {
+        W.tseg[t] = IS_NONE;
+        W.tdesc[t].j = IS_NONE;
+      }
+      return;
+    }
+  }
   {
     const uint32_t nsort = W.ctl[0];
     uint32_t* tf = dyn;
