@@ -152,11 +152,17 @@ __global__ void __launch_bounds__(ST) k_rs_hist(B4<RsRing<K>> R2, B4<const uint3
   const RsPlan pl = rs_plan(*d_nbits2[e]);
   if ((uint32_t)pass >= pl.passes) return;
   const uint32_t shift = (uint32_t)pass * pl.width, W = pl.width, nd = 1u << W, mask = nd - 1u;
+  const uint32_t n = *d_n2[e];
+  const uint32_t base = blockIdx.x * SORT_TILE;
+  // grids are sized for the capacity (the face stage sorts the downsampled cloud, a fifth
+  // of it at c3): a tile past n only zeroes its histogram column
+  if (base >= n) {
+    if (threadIdx.x < nd) hist[threadIdx.x * nblocks + blockIdx.x] = 0u;
+    return;
+  }
   __shared__ uint32_t cnt[RS_MAXD];
   if (threadIdx.x < RS_MAXD) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t n = *d_n2[e];
-  const uint32_t base = blockIdx.x * SORT_TILE;
   const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
   // all loads of the tile are issued before any is consumed (clamped indices, no
   // branches), then one LDS atomic per distinct digit per 64 keys (ballot match):
