@@ -342,14 +342,15 @@ struct fccf_ctx {
   // match mailbox (HostMail::match / match2) and completion event (ev_match).  The
   // fine-verification launches of both chains share sa[1] under fine_mutex.
   fccf::AsyncTask b1w;
-  std::unique_ptr<fccf::Pool> bpool[4];
+  std::unique_ptr<fccf::Pool> bpool[5];
   fccf::Arena arena2b;
-  hipEvent_t ev_match[4] = {nullptr, nullptr, nullptr, nullptr};
-  // The batch's last stage group drains with four chains: its third and fourth pairs run
-  // phase B on b1w2 / b1w3 with pools of a quarter of the host threads (bpool[2..3]),
-  // matching scratch arena2c / arena2d and mailboxes HostMail::match3 / match4.
-  fccf::AsyncTask b1w2, b1w3;
-  fccf::Arena arena2c, arena2d;
+  hipEvent_t ev_match[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  // The batch's last stage group drains with a chain per pair: its third to fifth pairs
+  // run phase B on b1w2 / b1w3 / b1w4 with pools of a quarter of the host threads
+  // (bpool[2..4]), matching scratch arena2c / arena2d / arena2e and mailboxes
+  // HostMail::match3 / match4 / match5.
+  fccf::AsyncTask b1w2, b1w3, b1w4;
+  fccf::Arena arena2c, arena2d, arena2e;
   std::mutex fine_mutex;
   fccf::Probe probe;
   fccf::Ingest ingest;  // pinned upload ring + copy stream (ingest.cpp)

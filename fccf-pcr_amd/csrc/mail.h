@@ -58,8 +58,9 @@ struct HostMail {
   CloudMail clouds[10];  // per pair slot; a stage group's slots are adjacent (k_compact_planar)
   MatchMail match;      // phase-B chain 0 (pipeline.cpp Chain)
   MatchMail match2;     // chain 1: a pipelined batch's second host thread
-  MatchMail match3;     // chains 2 and 3: the batch's last stage group (four chains)
+  MatchMail match3;     // chains 2 to 4: the batch's last stage group (a chain per pair)
   MatchMail match4;
+  MatchMail match5;
   FineMail fine[10];  // per pair slot: a pair's fine verification overlaps the next pair's phase B
 };
 

@@ -321,14 +321,20 @@ struct PhaseB {
 // two chains on two host threads (alternate pairs), so two pairs' host stages (growth,
 // clustering, the LM) overlap, and its last stage group drains with four (chains 2 and 3
 // on two more threads, quarter pools); a single registration, or a batch whose ctx needs
-// the one-chain form (group, probe, debug, the device growth/LM forms), uses chain 0.  The
-// matching stream sb is shared: each chain waits for its own work by its event.
+// the one-chain form (group, probe, debug, the device growth/LM forms), uses chain 0.
+// Chains 0 and 1 share the matching stream sb (each waits for its own work by its event)
+// and the fine stream sa[1] (under fine_mutex).  The drain's chains 2 to 4 run after the
+// batch's last cloud stage, when the cloud-stage streams sa[0], sa[2] and sa[3] are idle:
+// each takes one of them for its matching and fine verification, so the drain's pairs
+// spread over the hardware queues instead of queueing on two.
 struct Chain {
   Pool* pool;
   Arena* arena2;     // matching scratch
   MatchMail* mm;     // pinned match mailbox
-  hipEvent_t ev;     // this chain's matching work on sb is complete
+  hipEvent_t ev;     // this chain's matching work on its matching stream is complete
   bool may_redo;     // the stage redo (VG_REDO) runs in place (one chain only)
+  hipStream_t sm = nullptr;  // matching stream (null: c->sb)
+  hipStream_t sf = nullptr;  // fine-verification stream (null: c->sa[1], shared under fine_mutex)
 };
 
 struct BatchRestart {};  // two-chain batch: a stage needs its redo -> the batch again with one chain
@@ -611,7 +617,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   if (c->debug) c->dbg.clear();
   const auto t_all = ps.t_enq;
   auto t0 = ps.t_enq;
-  hipStream_t st0 = c->sb;
+  hipStream_t st0 = ch.sm ? ch.sm : c->sb;
   // counts and planar records of both clouds: written by k_compact_planar into
   // this set's pinned mailbox, visible once the clouds-done event has completed
   CloudMail& cm = host_mail(c)->clouds[s];
@@ -1082,7 +1088,7 @@ void phase_b1(fccf_ctx* c, int s, const fccf_params& P, float T_out[16], fccf_st
   int flo = 0, fhi = E;
   if (FG) shard_range(E, FG->rank, FG->n, &flo, &fhi);
   const int El = fhi - flo;
-  hipStream_t sf = c->sa[1];
+  hipStream_t sf = ch.sf ? ch.sf : c->sa[1];
   // the fine stream is shared by the chains: one chain's launch sequence (waits, graph
   // replay or capture, event records) at a time
   std::unique_lock<std::mutex> flk(c->fine_mutex);
@@ -1484,13 +1490,14 @@ void pipeline_release(fccf_ctx* c) {
 Chain chain_of(fccf_ctx* c, int k, int nchains) {
   HostMail* hm = host_mail(c);
   if (nchains <= 1) return Chain{&c->pool, &c->arena2, &hm->match, c->ev_match[0], true};
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 5; ++i)
     if (!c->bpool[i]) c->bpool[i].reset(new Pool(std::max(1, c->pool.size() / (i < 2 ? 2 : 4))));
   switch (k) {
     case 0: return Chain{c->bpool[0].get(), &c->arena2, &hm->match, c->ev_match[0], false};
     case 1: return Chain{c->bpool[1].get(), &c->arena2b, &hm->match2, c->ev_match[1], false};
-    case 2: return Chain{c->bpool[2].get(), &c->arena2c, &hm->match3, c->ev_match[2], false};
-    default: return Chain{c->bpool[3].get(), &c->arena2d, &hm->match4, c->ev_match[3], false};
+    case 2: return Chain{c->bpool[2].get(), &c->arena2c, &hm->match3, c->ev_match[2], false, c->sa[0], c->sa[0]};
+    case 3: return Chain{c->bpool[3].get(), &c->arena2d, &hm->match4, c->ev_match[3], false, c->sa[2], c->sa[2]};
+    default: return Chain{c->bpool[4].get(), &c->arena2e, &hm->match5, c->ev_match[4], false, c->sa[3], c->sa[3]};
   }
 }
 
@@ -1637,16 +1644,18 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       }
       sy.cv.notify_all();
     };
-    const Chain chains[4] = {chain_of(c, 0, 2), chain_of(c, 1, 2), chain_of(c, 2, 4), chain_of(c, 3, 4)};
-    // The last stage group drains with four chains: after its stage nothing else is left
-    // for the GPU, and its pairs' phase B would otherwise run two after two on each chain
-    // (FCCF_DRAIN4=0: two chains throughout, dev A/B)
+    const Chain chains[5] = {chain_of(c, 0, 2), chain_of(c, 1, 2), chain_of(c, 2, 5), chain_of(c, 3, 5),
+                             chain_of(c, 4, 5)};
+    // The last stage group drains with a chain per pair: after its stage nothing else is
+    // left for the GPU, and its pairs' phase B would otherwise run two after two on each
+    // chain (FCCF_DRAIN4=0: two chains throughout, tests)
     const char* d4e = std::getenv("FCCF_DRAIN4");  // (read per batch: tests switch it)
     const bool drain4_env = !(d4e && d4e[0] == '0');
     const int glast = ng - 1;
     const bool drain4 = drain4_env && ng >= 2 && cnt(glast) >= 3;
-    // pairs 2 and 3 of the last group go to workers 2 and 3; a fifth stays with worker 0 or 1
-    auto drained = [&](int i) { return drain4 && i / PP == glast && (i % PP == 2 || i % PP == 3); };
+    const int nextra = drain4 ? cnt(glast) - 2 : 0;  // workers 2 .. 1 + nextra
+    // pairs 2 to 4 of the last group go to workers 2 to 4
+    auto drained = [&](int i) { return drain4 && i / PP == glast && i % PP >= 2; };
     auto worker = [&](int k) {
       HIP_CHECK(hipSetDevice(c->device));
       const Chain& ch = chains[k];
@@ -1712,18 +1721,15 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
       }
     };
     c->b1w.submit([&guarded_worker] { guarded_worker(1); });
-    if (drain4) {
-      c->b1w2.submit([&guarded_worker] { guarded_worker(2); });
-      c->b1w3.submit([&guarded_worker] { guarded_worker(3); });
-    }
-    std::exception_ptr err[4];
+    AsyncTask* helpers[4] = {&c->b1w, &c->b1w2, &c->b1w3, &c->b1w4};
+    for (int k = 2; k < 2 + nextra; ++k) helpers[k - 1]->submit([&guarded_worker, k] { guarded_worker(k); });
+    std::exception_ptr err[5];
     try {
       guarded_worker(0);
     } catch (...) {
       err[0] = std::current_exception();
     }
-    AsyncTask* helpers[3] = {&c->b1w, &c->b1w2, &c->b1w3};
-    for (int h = 0; h < (drain4 ? 3 : 1); ++h) {
+    for (int h = 0; h < 1 + nextra; ++h) {
       try {
         helpers[h]->wait();  // (always joined before this frame unwinds)
       } catch (...) {
@@ -1747,7 +1753,7 @@ void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64
     }
     if (first) std::rethrow_exception(first);
     if (restart) throw BatchRestart();
-    if (err[0] || err[1] || err[2] || err[3]) throw Error(FCCF_E_INTERNAL, "pipelined batch: a phase-B worker stopped");
+    if (err[0] || err[1] || err[2] || err[3] || err[4]) throw Error(FCCF_E_INTERNAL, "pipelined batch: a phase-B worker stopped");
     c->enq.wait();
     std::sort(redo.begin(), redo.end());
   }

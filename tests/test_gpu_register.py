@@ -529,14 +529,15 @@ def test_mailbox_flags_and_event_waits_agree(ctx, oracle, fccf, monkeypatch):
 
 @pytest.mark.parametrize("drain4", ["1", "0"])
 @pytest.mark.parametrize("pp,ns", [("4", (11, 12)), ("5", (13, 14, 15))])
-def test_batch_drain_with_four_chains(ctx, oracle, fccf, monkeypatch, drain4, pp, ns):
-    """A batch whose last stage group holds three to five pairs drains with four phase-B
-    chains (pipeline.cpp; FCCF_DRAIN4=0: two).  Its third and fourth pairs go to the
-    drain's own workers and reuse the slots of pairs two groups back, whose phase B2 ran
-    on the other workers; a fifth stays with the first two workers.  Every T equals the
-    oracle's, for groups 4 + 4 + 3 and 4 + 4 + 4 at four pairs per stage, and 5 + 5 + 3,
-    5 + 5 + 4 and 5 + 5 + 5 at five (the default).  Distinct pairs, so a result read from
-    another pair's slot, or a pair left out, would show."""
+def test_batch_drain_with_a_chain_per_pair(oracle, fccf, monkeypatch, drain4, pp, ns):
+    """A batch whose last stage group holds three to five pairs drains with a phase-B
+    chain per pair (pipeline.cpp; FCCF_DRAIN4=0: two chains throughout).  Its third to
+    fifth pairs go to the drain's own workers, on the idle cloud-stage streams, and reuse
+    the slots of pairs two groups back, whose phase B2 ran on the other workers.  Every
+    T equals the oracle's, for groups 4 + 4 + 3 and 4 + 4 + 4 at four pairs per stage,
+    and 5 + 5 + 3, 5 + 5 + 4 and 5 + 5 + 5 at five (the default).  Distinct pairs, so a
+    result read from another pair's slot, or a pair left out, would show.  A ctx of its
+    own: the session's debug ctx runs batches on one chain."""
     monkeypatch.setenv("FCCF_DRAIN4", drain4)
     monkeypatch.setenv("FCCF_PAIR_BATCH", pp)
     base_src, base_tar, _ = fccf.synth_pair(40_000)
@@ -547,8 +548,9 @@ def test_batch_drain_with_four_chains(ctx, oracle, fccf, monkeypatch, drain4, pp
         s, t = (base_src + jit).astype(np.float32), base_tar[: 34_000 + 500 * k]
         pairs.append((s, t))
         refs.append(oracle.Run(s, t, 0.1, oracle.INTROSORT).T)
-    for n in ns:
-        Tb, sb = ctx.register_batch(pairs[:n], 0.1)
-        for i, (T, ref) in enumerate(zip(Tb, refs)):
-            np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"n={n} pair {i}")
-        assert all(x.K > 0 for x in sb)
+    with fccf.Ctx(0) as c:
+        for n in ns:
+            Tb, sb = c.register_batch(pairs[:n], 0.1)
+            for i, (T, ref) in enumerate(zip(Tb, refs)):
+                np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"n={n} pair {i}")
+            assert all(x.K > 0 for x in sb)

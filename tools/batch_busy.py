@@ -44,7 +44,8 @@ def report(trace_dir, out=None):
     rows = []
     for f in glob.glob(os.path.join(trace_dir, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+                         int(r.get("Queue_Id", 0) or 0), int(r.get("Grid_Size_Y", 1) or 1)))
     rows.sort()
     # last burst: after the last gap of > 50 ms between a kernel's start and the previous end
     cut = 0
@@ -54,9 +55,12 @@ def report(trace_dir, out=None):
             cut = i
         last_end = max(last_end, rows[i][1])
     b = rows[cut:]
-    t0, t1 = b[0][0], max(e for _, e, _ in b)
+    t0, t1 = b[0][0], max(x[1] for x in b)
+    b3 = [(x[0], x[1], x[2]) for x in b]
     busy, gaps = 0, []
     cs, ce, prev = b[0][0], b[0][1], b[0][2]
+    full = b
+    b = b3
     for s, e, k in b[1:]:
         if s > ce:
             busy += ce - cs
@@ -77,6 +81,23 @@ def report(trace_dir, out=None):
              "(length us, at us, kernel before -> after):")
     for g in big[:40]:
         L.append(f"  {g[0] / 1e3:8.1f} {g[1] / 1e3:10.1f}  {g[2]} -> {g[3]}")
+    L.append("")
+    # the cloud stages: main VoxelGrid's k_is_prep (the sort's first launch) to the stage's
+    # k_mail_done (its last kernel before the S1 replay); fill = batch start -> first
+    # stage end, drain = last stage end -> batch end
+    preps = [s for s, e, k in b if k == "k_is_prep"]
+    dones = [e for s, e, k in b if k == "k_mail_done"]
+    L.append("stages (us from the batch's first kernel): sort start -> clouds done")
+    for i, ps in enumerate(preps):
+        de = [d for d in dones if d > ps]
+        L.append(f"  stage {i}: {(ps - t0) / 1e3:9.1f} -> {((de[0] if de else ps) - t0) / 1e3:9.1f}"
+                 f"  ({((de[0] if de else ps) - ps) / 1e3:.1f} us)")
+    if dones:
+        L.append(f"  drain after the last stage: {(t1 - max(dones)) / 1e3:.1f} us of {(t1 - t0) / 1e3:.1f}")
+        L.append("  the drain's kernels (start, end us from the batch's first kernel, queue, grid y):")
+        for s_, e_, k_, q_, y_ in full:
+            if e_ > max(dones):
+                L.append(f"    {(s_ - t0) / 1e3:9.1f} {(e_ - t0) / 1e3:9.1f}  q{q_} y{y_}  {k_}")
     L.append("")
     L.append("kernel time by name (sum of durations, may overlap):")
     for k, v in fam.most_common(30):
