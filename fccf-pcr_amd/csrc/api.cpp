@@ -323,6 +323,97 @@ extern "C" int fccf_debug_sort_keys(fccf_ctx* c, const uint32_t* keys, int64_t n
   });
 }
 
+namespace {
+// the batched form's per-copy parameters (blockIdx.y = copy), and the point source the
+// finish kernels gather sorted points from (null: no sorted points)
+__global__ void k_sortkeys_params_batch(B4<const uint32_t*> keys2, B4<const uint32_t*> d_n2, B4<VGParams*> P2,
+                                        const float* pts) {
+  __shared__ uint32_t cnt;
+  const int e = blockIdx.y;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  const uint32_t* keys = keys2[e];
+  for (uint32_t i = threadIdx.x; i < *d_n2[e]; i += blockDim.x) c += keys[i] != 0xFFFFFFFFu ? 1u : 0u;
+  atomicAdd(&cnt, c);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    VGParams* P = P2[e];
+    P->overflow = 0;
+    P->nfinite = cnt;
+    P->unsorted = 1;
+    P->src = pts;
+  }
+}
+}  // namespace
+
+// Dev / tests: K1's sort of `copies` copies of the same keys in one batched launch
+// sequence (grid y = copies, as a pipelined stage group runs it), optionally writing the
+// sorted points of xyz as VoxelGrid's first pass does.  perm: copy 0's order;
+// dev_ms: the device span of the whole sort.
+extern "C" int fccf_debug_sort_keys_batch(fccf_ctx* c, const uint32_t* keys, int64_t n, int copies, const float* xyz,
+                                          uint32_t* perm, double* dev_ms) {
+  if (!c || !keys || !perm || n < 1 || n > (int64_t)0x7FFFFFFF || copies < 1 || copies > BMAX) return FCCF_E_ARG;
+  return guarded(c, [&] {
+    hipStream_t st = c->sb;
+    const uint32_t cap = (uint32_t)n;
+    c->arena2.ensure((size_t)copies * (voxel_grid_bytes(cap) + 4096) + 12 * (size_t)n + (1 << 20));
+    c->arena2.reset();
+    VGBufs b[BMAX];
+    uint32_t* d_sc[BMAX];
+    for (int e = 0; e < copies; ++e) {
+      d_sc[e] = c->arena2.take_n<uint32_t>(64);
+      b[e] = voxel_grid_carve(c->arena2, cap);
+    }
+    float* pts = xyz ? c->arena2.take_n<float>(3 * (size_t)n) : nullptr;
+    if (pts) HIP_CHECK(hipMemcpyAsync(pts, xyz, 12 * (size_t)n, hipMemcpyHostToDevice, st));
+    std::vector<uint32_t> iota((size_t)n);
+    for (uint32_t i = 0; i < (uint32_t)n; ++i) iota[i] = i;
+    const uint32_t hn = (uint32_t)n;
+    for (int e = 0; e < copies; ++e) {
+      HIP_CHECK(hipMemcpyAsync(d_sc[e], &hn, 4, hipMemcpyHostToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(b[e].k0, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(b[e].v0, iota.data(), 4 * (size_t)n, hipMemcpyHostToDevice, st));
+      b[e].is.xyzs = pts ? b[e].xyzs : nullptr;
+    }
+    auto all = [&](auto f) {
+      using T = decltype(f(b[0]));
+      T a[BMAX];
+      for (int e = 0; e < copies; ++e) a[e] = f(b[e]);
+      return B4<T>(a, copies);
+    };
+    k_sortkeys_params_batch<<<dim3(1, copies), 1024, 0, st>>>(all([](const VGBufs& x) { return (const uint32_t*)x.k0; }),
+                                                              B4<const uint32_t*>((const uint32_t* const*)d_sc, copies),
+                                                              all([](const VGBufs& x) { return x.params; }), pts);
+    struct Ev {
+      hipEvent_t e = nullptr;
+      ~Ev() {
+        if (e) (void)hipEventDestroy(e);
+      }
+    } e0, e1;
+    HIP_CHECK(hipEventCreate(&e0.e));
+    HIP_CHECK(hipEventCreate(&e1.e));
+    HIP_CHECK(hipEventRecord(e0.e, st));
+    introsort_u32(all([](const VGBufs& x) { return x.k0; }), all([](const VGBufs& x) { return x.v0; }),
+                  all([](const VGBufs& x) { return x.k1; }), all([](const VGBufs& x) { return x.v1; }),
+                  B4<const uint32_t*>((const uint32_t* const*)d_sc, copies),
+                  all([](const VGBufs& x) { return (const VGParams*)x.params; }), cap,
+                  all([](const VGBufs& x) { return x.is; }), st, copies, false);
+    HIP_CHECK(hipEventRecord(e1.e, st));
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(perm, b[0].v0, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    uint32_t ctl[BMAX][4];
+    for (int e = 0; e < copies; ++e) HIP_CHECK(hipMemcpyAsync(ctl[e], b[e].is.ctl, 16, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0.e, e1.e));
+    if (dev_ms) *dev_ms = ms;
+    for (int e = 0; e < copies; ++e)
+      if (ctl[e][2] & IS_FAULT_MASK)
+        throw Error(FCCF_E_INTERNAL, "K1 sort invariant violated (flags " + std::to_string(ctl[e][2]) + ")");
+  });
+}
+
 extern "C" int fccf_debug_graph_mismatch(fccf_ctx* c) {
   if (!c) return FCCF_E_ARG;
   c->graph_mismatch = true;

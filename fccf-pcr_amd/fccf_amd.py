@@ -112,6 +112,8 @@ _sig("fccf_debug_group_fail", ctypes.c_int, _P, ctypes.c_int, ctypes.c_int)
 _sig("fccf_group_aborted", ctypes.c_int, _P)
 _sig("fccf_debug_get", ctypes.c_int, _P, ctypes.c_char_p, _P, _I64, ctypes.POINTER(_I64))
 _sig("fccf_debug_sort_keys", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P)
+if hasattr(_lib, "fccf_debug_sort_keys_batch"):  # (dev A/B runs load older builds through FCCF_LIB)
+    _sig("fccf_debug_sort_keys_batch", ctypes.c_int, _P, _P, _I64, ctypes.c_int, _P, _P, ctypes.POINTER(ctypes.c_double))
 _sig("fccf_debug_sort_stats", ctypes.c_int, _P, _P)
 if hasattr(_lib, "fccf_debug_sort_rounds"):  # (dev A/B runs load older builds through FCCF_LIB)
     _sig("fccf_debug_sort_rounds", ctypes.c_int, _P, _P)
@@ -326,6 +328,19 @@ class Ctx:
         _check(_lib.fccf_debug_sort_keys(self._h, k.ctypes.data, k.size, int(exact_gate), perm.ctypes.data),
                "fccf_debug_sort_keys", self._h)
         return perm[:int(np.count_nonzero(k != 0xFFFFFFFF))].copy()
+
+    def sort_keys_batch(self, keys, copies: int, xyz=None):
+        """K1's sort of `copies` copies of keys in one batched launch sequence (the
+        stage group's grid), writing sorted points of xyz if given.  Returns (copy 0's
+        permutation, device ms)."""
+        k = np.ascontiguousarray(keys, np.uint32)
+        perm = np.zeros(k.size, np.uint32)
+        ms = ctypes.c_double()
+        x = None if xyz is None else np.ascontiguousarray(xyz, np.float32)
+        _check(_lib.fccf_debug_sort_keys_batch(self._h, k.ctypes.data, k.size, int(copies),
+                                               None if x is None else x.ctypes.data, perm.ctypes.data,
+                                               ctypes.byref(ms)), "fccf_debug_sort_keys_batch", self._h)
+        return perm, ms.value
 
     def graph_mismatch(self):
         """Test hook: the next cloud-stage graph replay is patched with a wrong layout

@@ -301,6 +301,12 @@ int fccf_debug_get(fccf_ctx* ctx, const char* name, void* buf, int64_t cap_bytes
  * order; perm_out[0..n) receives the values in sorted order (the finite ones first).
  * exact_gate != 0 runs the presorted second pass's single-workgroup form. */
 int fccf_debug_sort_keys(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int exact_gate, uint32_t* perm_out);
+/* Dev / tests: the same sort of `copies` (1..10) copies of the keys in one batched launch
+ * sequence, as a pipelined stage group runs it (grid y = copies), writing the sorted points
+ * of xyz (may be NULL) as VoxelGrid's first pass does; perm_out: copy 0's order; dev_ms:
+ * the sort's device span. */
+int fccf_debug_sort_keys_batch(fccf_ctx* ctx, const uint32_t* keys, int64_t n, int copies, const float* xyz,
+                               uint32_t* perm_out, double* dev_ms);
 /* Path counters of the last fccf_debug_sort_keys: [0] sort length, [2] slow-path flags
  * (1 global partitions, 2 a sequential heap sort beyond the LDS, 4 a depth-limit segment
  * beyond the LDS with distinct keys), [3] global partitions, [4] LDS segments, [5]

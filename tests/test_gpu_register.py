@@ -527,6 +527,28 @@ def test_mailbox_flags_and_event_waits_agree(ctx, oracle, fccf, monkeypatch):
             assert 0.0 < x.dev_ms[3] < 1000.0, (spin, list(x.dev_ms))
 
 
+def test_event_waits_while_other_chains_capture(oracle, fccf, monkeypatch):
+    """with FCCF_SPIN_US=0 phase B2 waits on the fine-verification event
+    instead of the mailbox flag, and that event is recorded on a stream the other chains
+    capture their fine graphs on whenever a pair's sizes change the graph key.  Pairs of
+    different sizes in a multi-chain batch (a non-debug ctx: the chains run) make those
+    captures overlap the event waits; every T must equal the oracle's."""
+    monkeypatch.setenv("FCCF_SPIN_US", "0")
+    base_src, base_tar, _ = fccf.synth_pair(40_000)
+    rng = np.random.default_rng(57)
+    pairs, refs = [], []
+    for k in range(12):
+        jit = rng.normal(0, 0.003, base_src.shape).astype(np.float32)
+        s, t = (base_src + jit).astype(np.float32)[: 40_000 - 700 * k], base_tar[: 33_000 + 600 * k]
+        pairs.append((s, t))
+        refs.append(oracle.Run(s, t, 0.1, oracle.INTROSORT).T)
+    with fccf.Ctx(0) as c:
+        for _ in range(2):
+            Tb, sb = c.register_batch(pairs, 0.1)
+            for i, (T, ref) in enumerate(zip(Tb, refs)):
+                np.testing.assert_array_equal(T.view(np.uint32), ref.view(np.uint32), err_msg=f"pair {i}")
+
+
 @pytest.mark.parametrize("drain4", ["1", "0"])
 @pytest.mark.parametrize("pp,ns", [("4", (11, 12)), ("5", (13, 14, 15))])
 def test_batch_drain_with_a_chain_per_pair(oracle, fccf, monkeypatch, drain4, pp, ns):
