@@ -76,6 +76,9 @@ constexpr int IS_WT = 256;           // wave kernel: threads per block
 constexpr uint32_t IS_TASK_BIG = 128;  // wave tasks above this are dequeued first
 constexpr uint32_t IS_THRESHOLD = 16;  // libstdc++ _S_threshold
 constexpr int IS_STACK = 96;  // a wave's stack also holds its register-mode subtree (depth <= 48 each)
+#ifndef IS_SEGT_MINC
+#define IS_SEGT_MINC 2  // wave_task_level: per-segment table from this many chunks per lane up
+#endif
 // packed u32 subtree of at most IS_WCAP elements: off (13 bits) | len (11) | depth (6)
 __device__ __forceinline__ uint32_t wpack(uint32_t off, uint32_t len, int d) { return off | (len << 13) | ((uint32_t)d << 24); }
 constexpr uint32_t IS_NONE = 0xFFFFFFFFu;
@@ -1291,12 +1294,15 @@ static_assert(IS_LCAP <= 8192 && IS_WCAP <= 1024, "task packing: 13-bit offsets,
 
 // One wave's slice of the wave kernel
 struct WaveLds {
-  uint32_t k[IS_WCAP], v[IS_WCAP];
+  uint32_t k[IS_WCAP + IS_THRESHOLD], v[IS_WCAP];  // (k: IS_NONE past the task, leaf_rank)
   uint16_t lg[IS_WCAP], ll[IS_WCAP];   // a level's >= / <= positions, in position order
   uint32_t cutv[IS_WCAP];              // per segment (at its first position): its cut, or its end
   uint64_t bw[2][IS_WC + 1];           // the level's >= / <= ballots per chunk
   uint32_t pc[2][IS_WC + 1];           // and their exclusive prefix counts
-  uint16_t xch[IS_WCAP / 2];
+  union {
+    uint16_t xch[IS_WCAP / 2];         // wave_partition's exchange
+    uint32_t seg[IS_WCAP / 4];         // wave_task_level: a level's segments to partition, a | b << 16
+  };
   uint32_t heads[IS_WCAP / 32];
   uint32_t stk[IS_STACK];
   uint32_t lstat[4];
@@ -1623,6 +1629,20 @@ __device__ __forceinline__ void wave_sort(SL& S, uint32_t packed, uint32_t* stk,
   }
 }
 
+// The rank of position p (key k[p]) in its leaf [a, b) of a finished wave task, ties
+// by position: # of q in [a, b) with (k[q], q) < (key, p).  b - a <= 16, and the scan
+// runs over the fixed window [a, a + 16): the positions in [b, a + 16) belong to later
+// segments, whose keys are >= every key of the leaf (the partitions' invariant), equal
+// ones at q > p, and the 16 positions past the task hold IS_NONE, so none of them
+// counts -- sixteen unrolled reads at immediate offsets, no per-lane loop bound.
+__device__ __forceinline__ uint32_t leaf_rank(const uint32_t* k, uint32_t a, uint32_t p, uint32_t key) {
+  const uint64_t me = (uint64_t)key << 32 | p;
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < IS_THRESHOLD; ++j) r += ((uint64_t)k[a + j] << 32 | (a + j)) < me ? 1u : 0u;
+  return r;
+}
+
 // # of the level's >= (s = 0) / <= (s = 1) elements before position x (0 <= x <= 64 C)
 __device__ __forceinline__ uint32_t level_rank(const WaveLds& S, int s, uint32_t x) {
   const uint32_t c = x >> 6, bit = x & 63u;
@@ -1712,6 +1732,34 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       }
       break;
     }
+    // Per-segment work once per segment instead of once per position: lane s takes
+    // the level's s-th segment (its median, pivot and whole-window ranks) and leaves
+    // them in the segment's own cutv slots a+1..a+3 (a segment here has > 16
+    // positions, so they are its own), which its positions then read.
+    constexpr bool SEGT = C >= IS_SEGT_MINC;
+    static_assert(IS_WCAP / (IS_THRESHOLD + 1) < 64 && IS_WCAP <= 1023, "one lane per segment; 10-bit ranks");
+    uint32_t sa = 0, sb = 0, nsg = 0;
+    if constexpr (SEGT) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const bool head = ((actm >> c) & 1u) && c * 64 + lane == (ab[c] & 0xFFFFu);
+        const uint64_t hm = __ballot(head);
+        if (head) S.seg[nsg + mbcnt(hm)] = ab[c];
+        nsg += (uint32_t)__popcll(hm);
+      }
+      wsync();
+      if (lane < nsg) {
+        const uint32_t s = S.seg[lane];
+        sa = s & 0xFFFFu;
+        sb = s >> 16;
+        // __move_median_to_first(a, a+1, mid, b-1): a receives the pivot, m the old first
+        const uint32_t m = median_pos(S.k, sa, sb);
+        S.cutv[sa] = IS_NONE;
+        S.cutv[sa + 1] = S.k[m];
+        S.cutv[sa + 2] = m;
+      }
+      wsync();
+    }
     uint32_t kk[C], vv[C];
     uint64_t bg[C], bl[C];
     uint32_t moved = 0;  // bit c: chunk c's position is the segment's first or its median (rewritten in place)
@@ -1726,12 +1774,18 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
         kk[c] = S.k[p];
         vv[c] = S.v[p];
         // __move_median_to_first(a, a+1, mid, b-1): a receives the pivot, m the old first
-        const uint32_t m = median_pos(S.k, a, b);
-        const uint32_t P = S.k[m];
+        uint32_t m, P;
+        if constexpr (SEGT) {
+          P = S.cutv[a + 1];
+          m = S.cutv[a + 2];
+        } else {
+          m = median_pos(S.k, a, b);
+          P = S.k[m];
+        }
         if (p == a) {
           kk[c] = P;
           vv[c] = S.v[m];
-          S.cutv[a] = IS_NONE;
+          if constexpr (!SEGT) S.cutv[a] = IS_NONE;
           moved |= 1u << c;
         } else {
           if (p == m) {
@@ -1761,6 +1815,13 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       }
     }
     wsync();  // (every read of S.k above precedes every write below)
+    if constexpr (SEGT) {
+      if (lane < nsg) {
+        const uint32_t g0 = level_rank(S, 0, sa + 1), l0 = level_rank(S, 1, sa + 1);
+        S.cutv[sa + 3] = g0 | l0 << 10 | (level_rank(S, 1, sb) - l0) << 20;
+      }
+      wsync();
+    }
     uint32_t li[C];  // 1 + index into S.ll (a swapped >=) or S.lg | 1 << 16 (a swapped <=), 0: stays
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -1769,8 +1830,17 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
       const uint32_t p = c * 64 + lane, a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
       if (p == a) continue;
       const bool ge = (bg[c] >> lane) & 1ull, le = (bl[c] >> lane) & 1ull;
-      const uint32_t g0 = level_rank(S, 0, a + 1), l0 = level_rank(S, 1, a + 1);
-      const uint32_t le_tot = level_rank(S, 1, b) - l0;
+      uint32_t g0, l0, le_tot;
+      if constexpr (SEGT) {
+        const uint32_t r = S.cutv[a + 3];
+        g0 = r & 0x3FFu;
+        l0 = (r >> 10) & 0x3FFu;
+        le_tot = r >> 20;
+      } else {
+        g0 = level_rank(S, 0, a + 1);
+        l0 = level_rank(S, 1, a + 1);
+        le_tot = level_rank(S, 1, b) - l0;
+      }
       const uint32_t ga = S.pc[0][c] + mbcnt(bg[c]), la = S.pc[1][c] + mbcnt(bl[c]);
       const uint32_t g = ga - g0, h = la - l0;  // # >= / # <= of the segment before p
       const bool sg = ge && le_tot - h - (le ? 1u : 0u) >= g + 1;
@@ -1814,13 +1884,18 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
     dpos[c] = IS_NONE;
     dval[c] = 0u;
     if (p >= n) continue;
-    const uint32_t a = ab[c] & 0xFFFFu, b = ab[c] >> 16;
+    const uint32_t a = ab[c] & 0xFFFFu;
     const uint32_t key = S.k[p];
+#ifdef IS_LEAF_LOOP
+    const uint32_t b = ab[c] >> 16;
     uint32_t rank = 0;
     for (uint32_t q = a; q < b; ++q) {
       const uint32_t kq = S.k[q];
       rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
     }
+#else
+    const uint32_t rank = leaf_rank(S.k, a, p, key);
+#endif
     dpos[c] = f + a + rank;
     dval[c] = S.v[p];
     K[dpos[c]] = key;
@@ -2432,6 +2507,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
         S.v[q] = V[f + q];
       }
     }
+    if (lane < IS_THRESHOLD) S.k[n + lane] = IS_NONE;  // (leaf_rank's window past the task)
     if (lane < IS_WCAP / 32) S.heads[lane] = 0;
     wsync();
     const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
@@ -2444,6 +2520,18 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
     {
     wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
     wsync();
+#ifndef IS_LEAF_LOOP
+    // (n <= 64: a task of more than 16 positions comes back from wave_sort sorted, every
+    // position its own leaf (wave_sort_regs or the depth-limit path); one of at most 16
+    // is one leaf, ranked here)
+    if (lane < n) {
+      const uint32_t key = S.k[lane], val = S.v[lane];
+      const uint32_t dst = f + (n <= IS_THRESHOLD ? leaf_rank(S.k, 0u, lane, key) : lane);
+      K[dst] = key;
+      V[dst] = val;
+      if (xsrc) put_xyz(W, xsrc, dst, val);
+    }
+#else
 #pragma unroll
     for (int c = 0; c < IS_WC; ++c) {
       const uint32_t p = c * 64 + lane;
@@ -2469,6 +2557,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
       V[f + a + rank] = S.v[p];
       if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);
     }
+#endif
     }
     wsync();
     if (W.trace && lane == 0) {
