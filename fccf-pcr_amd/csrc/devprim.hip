@@ -153,43 +153,43 @@ __global__ void __launch_bounds__(ST) k_rs_hist(B4<RsRing<K>> R2, B4<const uint3
   if ((uint32_t)pass >= pl.passes) return;
   const uint32_t shift = (uint32_t)pass * pl.width, W = pl.width, nd = 1u << W, mask = nd - 1u;
   const uint32_t n = *d_n2[e];
-  const uint32_t base = blockIdx.x * SORT_TILE;
-  // grids are sized for the capacity (the face stage sorts the downsampled cloud, a fifth
-  // of it at c3): a tile past n only zeroes its histogram column
-  if (base >= n) {
-    if (threadIdx.x < nd) hist[threadIdx.x * nblocks + blockIdx.x] = 0u;
-    return;
-  }
   __shared__ uint32_t cnt[RS_MAXD];
-  if (threadIdx.x < RS_MAXD) cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
-  // all loads of the tile are issued before any is consumed (clamped indices, no
-  // branches), then one LDS atomic per distinct digit per 64 keys (ballot match):
-  // neighbouring keys share their high digits
-  K kk[SORT_CHUNKS];
-  const uint32_t last = n ? n - 1u : 0u;
+  // the grid is capped (rs_grid), not sized for the capacity: each workgroup takes the
+  // problem's tiles blockIdx.x, + gridDim.x, ... (the face stage sorts the downsampled
+  // cloud, a fifth of the capacity at c3; tiles past n are neither counted nor scanned)
+  for (uint32_t t = blockIdx.x; t * (uint32_t)SORT_TILE < n; t += gridDim.x) {
+    const uint32_t base = t * SORT_TILE;
+    if (threadIdx.x < RS_MAXD) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t end = min(base + (uint32_t)SORT_TILE, n);
+    // all loads of the tile are issued before any is consumed (clamped indices, no
+    // branches), then one LDS atomic per distinct digit per 64 keys (ballot match):
+    // neighbouring keys share their high digits
+    K kk[SORT_CHUNKS];
+    const uint32_t last = n ? n - 1u : 0u;
 #pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) kk[c] = keys[min(base + c * ST + threadIdx.x, last)];
+    for (int c = 0; c < SORT_CHUNKS; ++c) kk[c] = keys[min(base + c * ST + threadIdx.x, last)];
 #pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) {
-    const bool ok = base + c * ST + threadIdx.x < end;
-    const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
-    uint64_t m = __ballot(ok);
-    for (uint32_t b = 0; b < W; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
+    for (int c = 0; c < SORT_CHUNKS; ++c) {
+      const bool ok = base + c * ST + threadIdx.x < end;
+      const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
+      uint64_t m = __ballot(ok);
+      for (uint32_t b = 0; b < W; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+      }
+      if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
     }
-    if (ok && mbcnt(m) == 0) atomicAdd(&cnt[d], (uint32_t)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x < nd) hist[threadIdx.x * nblocks + t] = cnt[threadIdx.x];
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x < nd) hist[threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
 // One block per digit: exclusive scan of that digit's per-block counts in place.
-__global__ void __launch_bounds__(T) k_rs_rowscan(B4<SortScratch> ss, uint32_t nblocks, B4<const uint32_t*> d_nbits2,
-                                                  int pass) {
+__global__ void __launch_bounds__(T) k_rs_rowscan(B4<SortScratch> ss, uint32_t nblocks, B4<const uint32_t*> d_n2,
+                                                  B4<const uint32_t*> d_nbits2, int pass) {
   KT();
   const int e = blockIdx.y;
   uint32_t* __restrict__ hist = ss[e].hist;
@@ -198,13 +198,14 @@ __global__ void __launch_bounds__(T) k_rs_rowscan(B4<SortScratch> ss, uint32_t n
   if ((uint32_t)pass >= pl.passes || blockIdx.x >= (1u << pl.width)) return;
   __shared__ uint32_t sh[4];
   const uint32_t d = blockIdx.x;
+  const uint32_t ntl = min(nblocks, (*d_n2[e] + SORT_TILE - 1u) / SORT_TILE);  // the problem's tiles
   uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nblocks; b0 += T) {
+  for (uint32_t b0 = 0; b0 < ntl; b0 += T) {
     const uint32_t i = b0 + threadIdx.x;
-    const uint32_t v = i < nblocks ? hist[d * nblocks + i] : 0u;
+    const uint32_t v = i < ntl ? hist[d * nblocks + i] : 0u;
     uint32_t t;
     const uint32_t ex = block_scan_256(v, sh, &t);
-    if (i < nblocks) hist[d * nblocks + i] = carry + ex;
+    if (i < ntl) hist[d * nblocks + i] = carry + ex;
     carry += t;
   }
   if (threadIdx.x == 0) tot[d] = carry;
@@ -239,8 +240,7 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B4<RsRing<K>> R2, B4<const ui
     *active = any ? 1u : 0u;
   }
   const uint32_t n = *d_n2[e];
-  const uint32_t tile0 = blockIdx.x * SORT_TILE;
-  if (!run || tile0 >= n) return;  // grids are sized for the capacity; tiles past n are empty
+  if (!run) return;
   const uint32_t shift = (uint32_t)pass * pl.width, W = pl.width, nd = 1u << W, mask = nd - 1u;
   __shared__ uint32_t gofs[RS_MAXD];     // global slot of the tile's first key of each digit
   __shared__ uint32_t tex[RS_MAXD];      // exclusive digit offsets inside the tile
@@ -249,73 +249,78 @@ __global__ void __launch_bounds__(ST) k_rs_scatter(B4<RsRing<K>> R2, B4<const ui
   __shared__ K sk[SORT_TILE];
   __shared__ uint32_t sv[SORT_TILE];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
-  K kk[SORT_CHUNKS];
-  uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
-  const uint32_t last = n - 1u;  // n > tile0 >= 0
   const bool hv = vout != nullptr;  // keys-only sorts pass no value buffers
+  // (capped grid: the problem's tiles blockIdx.x, + gridDim.x, ..., as in k_rs_hist)
+  for (uint32_t tl = blockIdx.x; tl * (uint32_t)SORT_TILE < n; tl += gridDim.x) {
+    const uint32_t tile0 = tl * SORT_TILE;
+    const uint32_t base = tile0 + wave * (SORT_CHUNKS * 64);
+    K kk[SORT_CHUNKS];
+    uint32_t vv[SORT_CHUNKS], rk[SORT_CHUNKS], dg[SORT_CHUNKS];
+    const uint32_t last = n - 1u;  // n > tile0 >= 0
 #pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) {  // all loads in flight before the ranking
-    const uint32_t i = min(base + c * 64 + lane, last);
-    kk[c] = kin[i];
-    vv[c] = (iota || !hv) ? i : vin[i];
-  }
-  {
-    uint32_t t;
-    const uint32_t g = tid < nd ? tot[tid] : 0u;
-    const uint32_t h = tid < nd ? hist[tid * nblocks + blockIdx.x] : 0u;
-    const uint32_t ex = scan_digits_of(g, sh, &t);
-    if (tid < nd) gofs[tid] = ex + h;
-  }
-  for (uint32_t j = tid; j < SW * RS_MAXD; j += ST) (&wcnt[0][0])[j] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) {
-    const uint32_t i = base + c * 64 + lane;
-    const bool ok = i < n;
-    const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
-    dg[c] = ok ? d : RS_MAXD;
-    uint64_t m = __ballot(ok);
-    for (uint32_t b = 0; b < W; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
+    for (int c = 0; c < SORT_CHUNKS; ++c) {  // all loads in flight before the ranking
+      const uint32_t i = min(base + c * 64 + lane, last);
+      kk[c] = kin[i];
+      vv[c] = (iota || !hv) ? i : vin[i];
     }
-    const uint32_t r = mbcnt(m);
-    const uint32_t pre = ok ? wcnt[wave][d] : 0u;
-    rk[c] = pre + r;
-    if (ok && r == 0) wcnt[wave][d] = (uint16_t)(pre + (uint32_t)__popcll(m));
-  }
-  __syncthreads();
-  {  // per-wave offsets within a digit, tile digit totals, their exclusive scan
-    uint32_t acc = 0;
-    if (tid < nd)
-      for (int w = 0; w < SW; ++w) {
-        const uint32_t t = wcnt[w][tid];
-        wcnt[w][tid] = (uint16_t)acc;
-        acc += t;
-      }
-    uint32_t t;
-    const uint32_t ex = scan_digits_of(acc, sh, &t);
-    if (tid < nd) tex[tid] = ex;
-  }
-  __syncthreads();
+    {
+      uint32_t t;
+      const uint32_t g = tid < nd ? tot[tid] : 0u;
+      const uint32_t h = tid < nd ? hist[tid * nblocks + tl] : 0u;
+      const uint32_t ex = scan_digits_of(g, sh, &t);
+      if (tid < nd) gofs[tid] = ex + h;
+    }
+    for (uint32_t j = tid; j < SW * RS_MAXD; j += ST) (&wcnt[0][0])[j] = 0;
+    __syncthreads();
 #pragma unroll
-  for (int c = 0; c < SORT_CHUNKS; ++c) {
-    const uint32_t d = dg[c];
-    if (d >= (uint32_t)RS_MAXD) continue;
-    const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
-    sk[lp] = kk[c];
-    if (hv) sv[lp] = vv[c];
-  }
-  __syncthreads();
-  const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
-  for (uint32_t j = tid; j < m; j += ST) {
-    const K k = sk[j];
-    const uint32_t d = (uint32_t)(k >> shift) & mask;
-    const uint32_t pos = gofs[d] + (j - tex[d]);
-    kout[pos] = k;
-    if (hv) vout[pos] = sv[j];
+    for (int c = 0; c < SORT_CHUNKS; ++c) {
+      const uint32_t i = base + c * 64 + lane;
+      const bool ok = i < n;
+      const uint32_t d = (uint32_t)(kk[c] >> shift) & mask;
+      dg[c] = ok ? d : RS_MAXD;
+      uint64_t m = __ballot(ok);
+      for (uint32_t b = 0; b < W; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+      }
+      const uint32_t r = mbcnt(m);
+      const uint32_t pre = ok ? wcnt[wave][d] : 0u;
+      rk[c] = pre + r;
+      if (ok && r == 0) wcnt[wave][d] = (uint16_t)(pre + (uint32_t)__popcll(m));
+    }
+    __syncthreads();
+    {  // per-wave offsets within a digit, tile digit totals, their exclusive scan
+      uint32_t acc = 0;
+      if (tid < nd)
+        for (int w = 0; w < SW; ++w) {
+          const uint32_t t = wcnt[w][tid];
+          wcnt[w][tid] = (uint16_t)acc;
+          acc += t;
+        }
+      uint32_t t;
+      const uint32_t ex = scan_digits_of(acc, sh, &t);
+      if (tid < nd) tex[tid] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < SORT_CHUNKS; ++c) {
+      const uint32_t d = dg[c];
+      if (d >= (uint32_t)RS_MAXD) continue;
+      const uint32_t lp = tex[d] + wcnt[wave][d] + rk[c];
+      sk[lp] = kk[c];
+      if (hv) sv[lp] = vv[c];
+    }
+    __syncthreads();
+    const uint32_t m = min((uint32_t)SORT_TILE, n - tile0);
+    for (uint32_t j = tid; j < m; j += ST) {
+      const K k = sk[j];
+      const uint32_t d = (uint32_t)(k >> shift) & mask;
+      const uint32_t pos = gofs[d] + (j - tex[d]);
+      kout[pos] = k;
+      if (hv) vout[pos] = sv[j];
+    }
+    __syncthreads();  // (the tile's LDS reads before the next tile's writes)
   }
 }
 
@@ -476,6 +481,17 @@ __global__ void k_rs_copyback(B4<RsRing<K>> R2, B4<const uint32_t*> d_n2, B4<con
   }
 }
 
+// Workgroups per problem of the radix passes: the capacity's tiles, at most ~1024
+// workgroups per launch over the batch (two 1024-thread tiles fit a CU, so that is two
+// rounds of the chip).  Grids sized for the capacity launched ~2,000 workgroups per
+// ten-cloud face sort of which a fifth had a tile.
+#ifndef RS_GRID_MAX
+#define RS_GRID_MAX 1024
+#endif
+static uint32_t rs_grid(uint32_t nb, int nbatch) {
+  return std::max(1u, std::min(nb, (uint32_t)RS_GRID_MAX / (uint32_t)std::max(1, nbatch)));
+}
+
 template <class K>
 void radix_sort(B4<K*> k0, B4<uint32_t*> v0, B4<K*> k1, B4<uint32_t*> v1, B4<const uint32_t*> d_n, uint32_t cap,
                 B4<const uint32_t*> d_nbits, int fast_bits, bool iota, B4<SortScratch> s, hipStream_t st,
@@ -489,13 +505,14 @@ void radix_sort(B4<K*> k0, B4<uint32_t*> v0, B4<K*> k1, B4<uint32_t*> v1, B4<con
   const int fast_passes = fast_bits / 8;
   B4<RsRing<K>> R;
   for (int e = 0; e < BMAX; ++e) R.v[e] = RsRing<K>{{k0[e], k1[e], k2[e]}, {v0[e], v1[e], v2[e]}};  // host side
+  const uint32_t g = rs_grid(nb, nbatch);
   for (int p = 0; p < fast_passes; ++p) {  // pass p: digit p of the device-side plan (rs_plan)
-    k_rs_hist<K><<<dim3(nb, nbatch), ST, 0, st>>>(R, d_n, d_nbits, p, s, nb, fast_passes);
-    k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_nbits, p);
+    k_rs_hist<K><<<dim3(g, nbatch), ST, 0, st>>>(R, d_n, d_nbits, p, s, nb, fast_passes);
+    k_rs_rowscan<<<dim3(RS_MAXD, nbatch), T, 0, st>>>(s, nb, d_n, d_nbits, p);
     const double eb = 2.0 * (sizeof(K) + (v0[0] ? 4 : 0));  // algorithmic bytes per element
     ProbeBytes pb;
     for (int e = 0; e < nbatch; ++e) pb.add(d_n[e], eb);
-    FCCF_LAUNCH("k_rs_scatter", (pb), k_rs_scatter<K>, dim3(nb, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
+    FCCF_LAUNCH("k_rs_scatter", (pb), k_rs_scatter<K>, dim3(g, nbatch), ST, 0, st, R, d_n, d_nbits, p, s, nb, (iota && p == 0) ? 1 : 0, _probe.active(), fast_passes);
   }
   // With a third buffer every plan but a single pass ends in buffer 0 (an even pass
   // count by ping-pong, three passes by rotation), so no copy-back kernel is launched
