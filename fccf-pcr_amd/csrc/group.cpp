@@ -23,8 +23,10 @@
 // sequential and deterministic, so every rank computes the same T with no further
 // exchange.
 //
-// Transports: RCCL (RcclTransport: an all-gather-v is one ncclGroupStart/End of
-// per-root ncclBroadcasts), or virtual ranks (LocalTransport, test hook): n contexts
+// Transports: RCCL (RcclTransport: an exchange's all-gather-v ops are packed into one
+// count-padded block per rank, moved by ONE ncclAllGather, and unpacked by one batched
+// copy kernel -- Transport::allgatherv_multi), or virtual ranks (LocalTransport, test
+// hook): n contexts
 // of one process on one device exchange through a shared device staging buffer under
 // host barriers -- the same gather logic with n > 1, where RCCL itself would refuse
 // two ranks on one GPU.

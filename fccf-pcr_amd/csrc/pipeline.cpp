@@ -1501,9 +1501,24 @@ Chain chain_of(fccf_ctx* c, int k, int nchains) {
   }
 }
 
+// Bytes this rank has received through its group's exchanges so far, per channel
+// (fccf_stats.xch_bytes: the difference over a call).
+void group_rx(const Group* g, int64_t rx[3]) {
+  for (int k = 0; k < 3; ++k) rx[k] = g && g->tr ? g->tr->rx_bytes[k].load() : 0;
+}
+void put_xch_bytes(const Group* g, const int64_t rx0[3], fccf_stats* stats, int n) {
+  if (!stats) return;
+  int64_t rx1[3];
+  group_rx(g, rx1);
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) stats[i].xch_bytes[k] = rx1[k] - rx0[k];
+}
+
 void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar, int64_t n_tar, bool on_device,
                   float leaf, const fccf_params& P, float T_out[16], fccf_stats* stats) {
   group_check(c->group);
+  int64_t rx0[3];
+  group_rx(c->group, rx0);
   ProbeGuard probe_guard(&c->probe);
   reset_capture_counts(c);
   if (c->group) order_reset(c->group);
@@ -1515,6 +1530,7 @@ void run_register(fccf_ctx* c, const float* src, int64_t n_src, const float* tar
   clouds_enqueue(c, 0, src, n_src, tar, n_tar, !on_device, leaf, P);
   phase_b1(c, 0, P, T_out, stats, [] {}, chain_of(c, 0, 1));
   phase_b2(c, 0);
+  put_xch_bytes(c->group, rx0, stats, 1);
 }
 
 void run_register_batch(fccf_ctx* c, int n, const float* const* src, const int64_t* n_src, const float* const* tar,
@@ -1777,14 +1793,18 @@ void run_register_batch_any(fccf_ctx* c, int n, const float* const* src, const i
   const int pp = pb_env ? std::atoi(pb_env) : PAIRS_DEFAULT;
   const bool two = pp >= 2 && n >= 2 && !c->group && !c->probe.on() && !c->debug &&
                    !c->grow_device && !c->lm_device;
+  int64_t rx0[3];
+  group_rx(c->group, rx0);
   if (two) {
     try {
       run_register_batch(c, n, src, n_src, tar, n_tar, on_device, leaf, P, T_out, stats, 2);
+      put_xch_bytes(c->group, rx0, stats, n);
       return;
     } catch (const BatchRestart&) {
     }
   }
   run_register_batch(c, n, src, n_src, tar, n_tar, on_device, leaf, P, T_out, stats, 1);
+  put_xch_bytes(c->group, rx0, stats, n);
 }
 
 }  // namespace fccf

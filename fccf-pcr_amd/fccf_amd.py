@@ -49,11 +49,13 @@ class Stats(ctypes.Structure):
         ("ms", ctypes.c_double * 10), ("ms_total", ctypes.c_double),
         ("m1_src", ctypes.c_int64), ("m1_tar", ctypes.c_int64), ("leaves1", ctypes.c_int64), ("leaves2", ctypes.c_int64),
         ("fine_evals", ctypes.c_int64), ("dev_ms", ctypes.c_double * 4), ("stage_redos", ctypes.c_int64),
-        ("shard_ranks", ctypes.c_int32), ("sharded", ctypes.c_uint32), ("fine_reruns", ctypes.c_int64)]
+        ("shard_ranks", ctypes.c_int32), ("sharded", ctypes.c_uint32), ("fine_reruns", ctypes.c_int64),
+        ("xch_bytes", ctypes.c_int64 * 3)]
     SHARDED = {"search": 1, "fine": 2, "sort": 4, "faces": 8}  # fccf_stats.sharded bits (FCCF_SHARDED_*)
 
     def as_dict(self):
-        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "dev_ms")}
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("cand", "fine", "ms", "dev_ms", "xch_bytes")}
+        d["xch_bytes"] = dict(zip(("match", "fine", "cloud"), list(self.xch_bytes)))
         d["dev_ms"] = dict(zip(("vg_main", "vg_driver", "faces", "fine"), list(self.dev_ms)))
         d["cand"] = list(self.cand)
         d["fine"] = list(self.fine)

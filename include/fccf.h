@@ -107,6 +107,13 @@ typedef struct fccf_stats {
                                     pipelined batch such a pair is registered again
                                     after the batch's last pair (its stage arena may
                                     be recycled by then)                           */
+  /* appended in round 6 */
+  int64_t xch_bytes[3];          /* bytes this rank received through its group's
+                                    exchanges during the call, per channel: matching
+                                    (K5 counts and lists), fine (F scores), clouds (D
+                                    sorted slices, P face records); a pipelined batch
+                                    reports its whole call on every pair.  0 without
+                                    a group (fccf_group_bytes: the running totals)  */
 } fccf_stats;
 /* fccf_stats.sharded bits */
 enum {

@@ -255,7 +255,7 @@ def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
     with fccf.Ctx(0) as ctx:
         T0, s0 = ctx.register(src, tar, leaf)
     np.testing.assert_array_equal(bits(T0), bits(T_orc))
-    assert s0.shard_ranks == 1 and s0.sharded == 0
+    assert s0.shard_ranks == 1 and s0.sharded == 0 and list(s0.xch_bytes) == [0, 0, 0]
     ctxs = [fccf.Ctx(0) for _ in range(n)]
     try:
         groups = fccf.local_groups(ctxs)
@@ -278,6 +278,10 @@ def test_virtual_ranks_baseline_multi_gpu_configs(fccf, oracle, n, cfg):
         # other ranks' sorted (key, value) slices of both clouds, ~(n-1)/n of 8 B per point
         assert rx[0] > 0 and rx[1] > 0, rx
         assert rx[2] >= 0.5 * 8 * 2 * c["n"] * (n - 1) / n, rx
+        # fccf_stats.xch_bytes: the same per-call difference, in the registration's stats
+        assert list(s.xch_bytes) == rx, (list(s.xch_bytes), rx)
+        for st in sb:
+            assert st.xch_bytes[2] >= 2 * rx[2] * 0.9, (list(st.xch_bytes), rx)
         np.testing.assert_array_equal(bits(T), bits(T0))
         for Tx in Tb:
             np.testing.assert_array_equal(bits(Tx), bits(T0))
