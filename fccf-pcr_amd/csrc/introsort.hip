@@ -1997,6 +1997,7 @@ __device__ __forceinline__ uint32_t block_partition(BlockLds& S, uint32_t f, uin
 // to (Ko, Vo) (task ranges in their current order, for the wave kernel).
 __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const uint32_t* Ki, const uint32_t* Vi,
                                           uint32_t* Ko, uint32_t* Vo, uint32_t f, uint32_t len, int d) {
+  IS_PH_START();
   for (uint32_t q = threadIdx.x; q < len; q += IS_OT) {
     S.k[q] = Ki[f + q];
     S.v[q] = Vi[f + q];
@@ -2107,6 +2108,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     pop();
     __syncthreads();
   }
+  IS_PH(11);  // block item: load and partitions
   // the segment's wave tasks into the global list: one slot reservation per class
   if (threadIdx.x == 0) {
     S.bc[1] = S.ntb ? atomicAdd(&W.ctl[16], S.ntb) : 0u;
@@ -2121,6 +2123,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     if (big) W.tasks[S.bc[1] + i] = t;
     else W.tasks[W.taskmax - 1u - (S.bc[2] + i - S.ntb)] = t;
   }
+  IS_PH(12);  // block item: tasks listed
   // leaves: stable sort in place (the final insertion sort); task ranges as they are
   const float* __restrict__ xsrc = W.xyzs ? W.vgp->src : nullptr;
   for (uint32_t p = threadIdx.x; p < len; p += IS_OT) {
@@ -2158,6 +2161,7 @@ __device__ __forceinline__ void lds_block(BlockLds& S, const IsBufs& W, const ui
     if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);  // (the block's leaf elements are few: most go to wave tasks)
   }
   __syncthreads();
+  IS_PH(13);  // block item: leaves and write-back
 }
 
 // One partition of [f, l) (l - f > IS_LCAP) in global memory by the whole block,
@@ -2754,7 +2758,11 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
 #ifdef IS_PHASES
 // Development export (variant builds only): the instrumented kernel's phase sums since
 // the last call (cycles [0..15], counts [16..31]), then reset.
+#ifdef IS_KERNEL_VARIANT
+extern "C" int fccf_debug_is_phases_b2(unsigned long long out[32]) {  // (the second form's own counters)
+#else
 extern "C" int fccf_debug_is_phases(unsigned long long out[32]) {
+#endif
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fccf::g_is_ph), 32 * sizeof(unsigned long long)) != hipSuccess) return -2;
   unsigned long long z[32] = {};
   if (hipMemcpyToSymbol(HIP_SYMBOL(fccf::g_is_ph), z, sizeof z) != hipSuccess) return -2;
