@@ -1098,7 +1098,13 @@ __global__ void __launch_bounds__(IS_TT) k_is_count_plan_s(B4<const uint32_t*> K
 
 // Every element of the round's large segments to its place after the partition,
 // written to the other buffer; the cut by atomicMin.  Dynamic LDS: 2 * maxtiles u32.
-__global__ void __launch_bounds__(IS_TT) k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
+// seven waves per SIMD: 67 VGPRs and no scratch instead of 79 (six waves); 44.7 ->
+// 43.0 us per ten-cloud launch (eight: 64 VGPRs with spills, 49.7 us; profiles/r06l)
+#ifndef IS_SCATTER_S_WPE
+#define IS_SCATTER_S_WPE 7
+#endif
+__global__ void __launch_bounds__(IS_TT) __attribute__((amdgpu_waves_per_eu(IS_SCATTER_S_WPE)))
+k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
                                                       B4<uint32_t*> Ko2, B4<uint32_t*> Vo2, B4<IsBufs> W2, int r) {
   KT();
   IS_PH_START();
