@@ -18,7 +18,10 @@ inline uint32_t rs_blocks(uint32_t cap) { return (cap + RS_TILE - 1) / RS_TILE; 
 
 // Radix sort tiles: 4096 keys per block of 1024 threads (hist and scatter).
 constexpr int SORT_THREADS = 1024;
-constexpr int SORT_CHUNKS = 4;
+#ifndef SORT_CHUNKS_VAL
+#define SORT_CHUNKS_VAL 4
+#endif
+constexpr int SORT_CHUNKS = SORT_CHUNKS_VAL;
 constexpr int SORT_TILE = SORT_THREADS * SORT_CHUNKS;
 inline uint32_t sort_blocks(uint32_t cap) { return (cap + SORT_TILE - 1) / SORT_TILE; }
 
