@@ -175,3 +175,22 @@ def test_sharded_sort_rank_ranges(ctx, fccf, oracle, world, monkeypatch):
             prev = hi
         assert prev == ref.size, name
         monkeypatch.delenv("FCCF_SHARD_D_SIM")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("copies", [2, 6, 10])
+def test_batched_sort_equals_std_sort(ctx, fccf, oracle, copies):
+    """The sort as a pipelined stage group runs it: `copies` clouds per launch (grid y;
+    the block kernel's second form from six on), with the sorted points written by the
+    finish kernels (fccf_debug_sort_keys_batch).  Copy 0's order equals std::sort on
+    structured, duplicate-heavy and adversarial keys."""
+    cases = _keys_cases(fccf, oracle)
+    rng = np.random.default_rng(5)
+    for name in ("room_200k", "room_200k_nan", "dups_300k", "adversary_20000", "adversary_ties_5000",
+                 "rand8_40000", "randbig_15000"):
+        k = cases[name]
+        pts = rng.random((k.size, 3), dtype=np.float32)
+        perm, ms = ctx.sort_keys_batch(k, copies, pts)
+        ref = oracle.sort_pairs(k)
+        assert ms > 0.0
+        assert np.array_equal(perm[:ref.size], ref), name
