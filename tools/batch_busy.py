@@ -98,6 +98,17 @@ def report(trace_dir, out=None):
         for s_, e_, k_, q_, y_ in full:
             if e_ > max(dones):
                 L.append(f"    {(s_ - t0) / 1e3:9.1f} {(e_ - t0) / 1e3:9.1f}  q{q_} y{y_}  {k_}")
+    # between stages: every kernel overlapping [stage i clouds done, stage i+1 sort start]
+    for i in range(len(preps) - 1):
+        de = [d for d in dones if d > preps[i]]
+        if not de:
+            continue
+        a, z = de[0], preps[i + 1]
+        L.append(f"  transition {i} -> {i + 1}: {(a - t0) / 1e3:.1f} -> {(z - t0) / 1e3:.1f} us "
+                 f"({(z - a) / 1e3:.1f} us); kernels in it (start, end, queue, grid y):")
+        for s_, e_, k_, q_, y_ in full:
+            if e_ > a and s_ < z:
+                L.append(f"    {(s_ - t0) / 1e3:9.1f} {(e_ - t0) / 1e3:9.1f}  q{q_} y{y_}  {k_}")
     L.append("")
     L.append("kernel time by name (sum of durations, may overlap):")
     for k, v in fam.most_common(30):
