@@ -1892,16 +1892,9 @@ __device__ __forceinline__ void wave_task_level(WaveLds& S, uint32_t* __restrict
     if (p >= n) continue;
     const uint32_t a = ab[c] & 0xFFFFu;
     const uint32_t key = S.k[p];
-#ifdef IS_LEAF_LOOP
-    const uint32_t b = ab[c] >> 16;
-    uint32_t rank = 0;
-    for (uint32_t q = a; q < b; ++q) {
-      const uint32_t kq = S.k[q];
-      rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
-    }
-#else
-    const uint32_t rank = leaf_rank(S.k, a, p, key);
-#endif
+    // (< b - a whenever the partitions' invariant holds; the clamp keeps every store
+    // inside the task whatever the data)
+    const uint32_t rank = min(leaf_rank(S.k, a, p, key), (ab[c] >> 16) - a - 1u);
     dpos[c] = f + a + rank;
     dval[c] = S.v[p];
     K[dpos[c]] = key;
@@ -2530,44 +2523,16 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
     {
     wave_sort(S, wpack(0u, n, d), S.stk, S.xch);
     wsync();
-#ifndef IS_LEAF_LOOP
     // (n <= 64: a task of more than 16 positions comes back from wave_sort sorted, every
     // position its own leaf (wave_sort_regs or the depth-limit path); one of at most 16
     // is one leaf, ranked here)
     if (lane < n) {
       const uint32_t key = S.k[lane], val = S.v[lane];
-      const uint32_t dst = f + (n <= IS_THRESHOLD ? leaf_rank(S.k, 0u, lane, key) : lane);
+      const uint32_t dst = f + (n <= IS_THRESHOLD ? min(leaf_rank(S.k, 0u, lane, key), n - 1u) : lane);
       K[dst] = key;
       V[dst] = val;
       if (xsrc) put_xyz(W, xsrc, dst, val);
     }
-#else
-#pragma unroll
-    for (int c = 0; c < IS_WC; ++c) {
-      const uint32_t p = c * 64 + lane;
-      if (p >= n) continue;
-      uint32_t a = 0, b = n;
-      {
-        uint32_t wi = p >> 5, m = S.heads[wi] & (0xFFFFFFFFu >> (31 - (p & 31)));
-        while (!m && wi > 0) m = S.heads[--wi];
-        if (m) a = (wi << 5) + 31 - __clz((int)m);
-        uint32_t wj = (p + 1) >> 5;
-        const uint32_t nw = (n + 31) >> 5, q = (p + 1) & 31;
-        uint32_t mm = wj < nw ? (S.heads[wj] & (0xFFFFFFFFu << q)) : 0u;
-        while (!mm && ++wj < nw) mm = S.heads[wj];
-        if (mm) b = min(n, (wj << 5) + (uint32_t)__ffs((int)mm) - 1);
-      }
-      const uint32_t key = S.k[p];
-      uint32_t rank = 0;
-      for (uint32_t q = a; q < b; ++q) {
-        const uint32_t kq = S.k[q];
-        rank += (kq < key || (kq == key && q < p)) ? 1u : 0u;
-      }
-      K[f + a + rank] = key;
-      V[f + a + rank] = S.v[p];
-      if (xsrc) put_xyz(W, xsrc, f + a + rank, S.v[p]);
-    }
-#endif
     }
     wsync();
     if (W.trace && lane == 0) {
