@@ -2515,8 +2515,11 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
     wsync();
     const unsigned long long t_task = W.trace ? wall_clock64() : 0ull;
     if (n > 64) {
+      // (chunk counts 2, 4, 6, 8: 6 for 257-384 elements saved ~2 %; every count from 2 to
+      // 8 made the kernel's code 164 KB and it slower, profiles/r06l)
       if (n <= 128) wave_task_level<2>(S, K, V, f, n, d, W, xsrc);
       else if (n <= 256) wave_task_level<4>(S, K, V, f, n, d, W, xsrc);
+      else if (n <= 384) wave_task_level<6>(S, K, V, f, n, d, W, xsrc);
       else wave_task_level<IS_WC>(S, K, V, f, n, d, W, xsrc);
       if (S.son && lane == 0) atomicAdd(&S.lstat[2], 1u);
     } else
