@@ -938,93 +938,75 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
   __shared__ uint32_t cg[IS_TC * 4], cl[IS_TC * 4], pg[IS_TC * 4], pl[IS_TC * 4];
   __shared__ uint32_t bsh[4];
   __shared__ uint64_t sh64[16];
-  const uint32_t t = blockIdx.x;
-  uint32_t j, f, l, m, P, kf;
-  uint32_t tile0;
-  uint32_t kk[IS_TC];
+  // Tiles blockIdx.x, + gridDim.x, ... of the round (the grid is capped, is_round_grid):
+  // the plan is derived once per workgroup, not once per tile.
   if (r > 0) {
-    // The grid is sized for the first rounds (maxtiles), and every workgroup derives the
-    // plan before it knows whether it has a tile.  Round r's large segments are children
-    // of round r-1's (which partitioned `pad` elements in nseg segments), so it has at
-    // most pad / IS_TILE + 2 nseg tiles: a workgroup past that bound leaves at once
-    // (the late rounds hold a few segments; their launches were all plan derivation).
+    // Round r's large segments are children of round r-1's (which partitioned `pad`
+    // elements in nseg segments), so it has at most pad / IS_TILE + 2 nseg tiles: a
+    // workgroup whose first tile lies past that bound leaves at once (the late rounds
+    // hold a few segments; their launches were all plan derivation).
     const IsRound pr = W.rounds[r - 1];
-    if (t >= pr.pad / IS_TILE + 2u * pr.nseg + 1u) {
-      if (threadIdx.x == 0) {
-        W.tseg[t] = IS_NONE;
-        W.tdesc[t].j = IS_NONE;
-      }
-      return;
-    }
+    if (blockIdx.x >= pr.pad / IS_TILE + 2u * pr.nseg + 1u) return;
   }
-  {
-    const uint32_t nsort = W.ctl[0];
-    uint32_t* tf = dyn;
-    uint32_t* tl = tf + W.segmax;
-    int32_t* td = (int32_t*)(tl + W.segmax);
-    uint32_t* t0 = (uint32_t*)(td + W.segmax);
-    const uint32_t nch = nchildren(W, r);
-    const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
-    uint32_t nseg = 0, ntiles = 0, nown = 0;
-    for (uint32_t b = 0; b < nch; b += blockDim.x) {
-      const uint32_t i = b + threadIdx.x;
-      Child c = {0u, 0u, 0};
-      if (i < nch) c = child_of(W, r, nsort, i);
-      const bool lg = i < nch && is_large(c, W.tier);
-      const bool ow = i < nch && !lg && c.l > c.f;
-      const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
-      // one scan of the three counters packed: large (21 bits) | owned (21) | tiles (22)
-      uint64_t s_all;
-      const uint64_t p_all =
-          block_excl_scan64((lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)nt << 42), sh64, &s_all);
-      const uint32_t p_lg = (uint32_t)(p_all & 0x1FFFFFu), p_ow = (uint32_t)((p_all >> 21) & 0x1FFFFFu),
-                     p_nt = (uint32_t)(p_all >> 42);
-      const uint32_t s_lg = (uint32_t)(s_all & 0x1FFFFFu), s_ow = (uint32_t)((s_all >> 21) & 0x1FFFFFu),
-                     s_nt = (uint32_t)(s_all >> 42);
-      if (lg) {
-        tf[nseg + p_lg] = c.f;
-        tl[nseg + p_lg] = c.l;
-        td[nseg + p_lg] = c.d;
-        t0[nseg + p_lg] = ntiles + p_nt;
-      }
-      if (ow && t == 0) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
-      nseg += s_lg;
-      ntiles += s_nt;
-      nown += s_ow;
+  const uint32_t nsort = W.ctl[0];
+  uint32_t* tf = dyn;
+  uint32_t* tl = tf + W.segmax;
+  int32_t* td = (int32_t*)(tl + W.segmax);
+  uint32_t* t0 = (uint32_t*)(td + W.segmax);
+  const uint32_t nch = nchildren(W, r);
+  const uint32_t own_base = r ? W.rounds[r - 1].nown : 0u;
+  uint32_t nseg = 0, ntiles = 0, nown = 0;
+  for (uint32_t b = 0; b < nch; b += blockDim.x) {
+    const uint32_t i = b + threadIdx.x;
+    Child c = {0u, 0u, 0};
+    if (i < nch) c = child_of(W, r, nsort, i);
+    const bool lg = i < nch && is_large(c, W.tier);
+    const bool ow = i < nch && !lg && c.l > c.f;
+    const uint32_t nt = lg ? tiles_of(c.l - c.f) : 0u;
+    // one scan of the three counters packed: large (21 bits) | owned (21) | tiles (22)
+    uint64_t s_all;
+    const uint64_t p_all =
+        block_excl_scan64((lg ? 1ull : 0ull) | ((ow ? 1ull : 0ull) << 21) | ((uint64_t)nt << 42), sh64, &s_all);
+    const uint32_t p_lg = (uint32_t)(p_all & 0x1FFFFFu), p_ow = (uint32_t)((p_all >> 21) & 0x1FFFFFu),
+                   p_nt = (uint32_t)(p_all >> 42);
+    const uint32_t s_lg = (uint32_t)(s_all & 0x1FFFFFu), s_ow = (uint32_t)((s_all >> 21) & 0x1FFFFFu),
+                   s_nt = (uint32_t)(s_all >> 42);
+    if (lg) {
+      tf[nseg + p_lg] = c.f;
+      tl[nseg + p_lg] = c.l;
+      td[nseg + p_lg] = c.d;
+      t0[nseg + p_lg] = ntiles + p_nt;
     }
-    __syncthreads();
-    IS_PH(5);  // count: the round's plan
-    // (pad: elements partitioned this round, the scatter probe's unit count, summed by
-    // the scatter's first tiles)
-    if (t == 0 && threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
-    if (t >= ntiles) {
-      if (threadIdx.x == 0 && t < W.maxtiles) {
-        W.tseg[t] = IS_NONE;
-        W.tdesc[t].j = IS_NONE;
-      }
-      return;
-    }
-    j = upper_index(t0, nseg, t);
-    f = tf[j];
-    l = tl[j];
-    tile0 = t0[j];
+    if (ow && blockIdx.x == 0) W.own[own_base + nown + p_ow] = IsOwn{c.f, c.l, c.d, (uint32_t)(r & 1)};
+    nseg += s_lg;
+    ntiles += s_nt;
+    nown += s_ow;
+  }
+  __syncthreads();
+  IS_PH(5);  // count: the round's plan
+  // (pad: elements partitioned this round, the scatter probe's unit count, summed by
+  // the scatter's first tiles)
+  if (blockIdx.x == 0 && threadIdx.x == 0) W.rounds[r] = IsRound{nseg, ntiles, own_base + nown, 0u};
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t j = upper_index(t0, nseg, t);
+    const uint32_t f = tf[j], l = tl[j], tile0 = t0[j];
+    const uint32_t a = f + 1 + (t - tile0) * IS_TILE, b = min(l, a + IS_TILE);
     // the tile's keys are loaded before the pivot, so their latency overlaps thread 0's
     // dependent median reads below
-    {
-      const uint32_t a0 = f + 1 + (t - tile0) * IS_TILE, b0 = min(l, a0 + IS_TILE);
+    uint32_t kk[IS_TC];
 #pragma unroll
-      for (int c = 0; c < IS_TC; ++c) {
-        const uint32_t p = a0 + c * IS_TT + threadIdx.x;
-        kk[c] = p < b0 ? K[p] : 0u;
-      }
+    for (int c = 0; c < IS_TC; ++c) {
+      const uint32_t p = a + c * IS_TT + threadIdx.x;
+      kk[c] = p < b ? K[p] : 0u;
     }
     if (threadIdx.x == 0) {
-      uint32_t Pm, vm, kf0, vf0;
-      median_load(K, V, f, l, m, Pm, vm, kf0, vf0);
-      bsh[0] = m;
+      uint32_t m0, Pm, vm, kf0, vf0;
+      median_load(K, V, f, l, m0, Pm, vm, kf0, vf0);
+      bsh[0] = m0;
       bsh[1] = Pm;
       bsh[2] = kf0;
-      const IsSeg rec{f, l, td[j], tile0, m, Pm, kf0, vf0, vm};
+      const IsSeg rec{f, l, td[j], tile0, m0, Pm, kf0, vf0, vm};
       W.tseg[t] = j;
       W.tdesc[t] = IsTile{j, rec};  // the scatter's one-load view of this tile's segment
       if (t == tile0) {  // the segment's record, once
@@ -1034,56 +1016,52 @@ __device__ __forceinline__ void is_count_body_s(const uint32_t* __restrict__ K, 
     }
     __syncthreads();
     IS_PH(6);  // count: tile keys, median, descriptor
-    m = bsh[0];
-    P = bsh[1];
-    kf = bsh[2];
-  }
-  const uint32_t i = t - tile0;
-  const uint32_t a = f + 1 + i * IS_TILE, b = min(l, a + IS_TILE);
-  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t m = bsh[0], P = bsh[1], kf = bsh[2];
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c)
-    if (a + c * IS_TT + threadIdx.x == m) kk[c] = kf;  // the median-to-first swap
+    for (int c = 0; c < IS_TC; ++c)
+      if (a + c * IS_TT + threadIdx.x == m) kk[c] = kf;  // the median-to-first swap
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
-    const bool ok = a + c * IS_TT + threadIdx.x < b;
-    const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
-    if (lane == 0) {
-      cg[c * 4 + w] = (uint32_t)__popcll(bg);
-      cl[c * 4 + w] = (uint32_t)__popcll(bl);
+    for (int c = 0; c < IS_TC; ++c) {
+      const bool ok = a + c * IS_TT + threadIdx.x < b;
+      const uint64_t bg = __ballot(ok && kk[c] >= P), bl = __ballot(ok && kk[c] <= P);
+      if (lane == 0) {
+        cg[c * 4 + w] = (uint32_t)__popcll(bg);
+        cl[c * 4 + w] = (uint32_t)__popcll(bl);
+      }
     }
-  }
-  __syncthreads();
-  IS_PH(7);  // count: ballots
-  if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
-    const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
-    uint32_t xg = xg0, xl = xl0;
+    __syncthreads();
+    IS_PH(7);  // count: ballots
+    if (w == 0) {  // IS_TC * 4 (chunk, wave) entries in position order
+      const uint32_t xg0 = lane < IS_TC * 4 ? cg[lane] : 0u, xl0 = lane < IS_TC * 4 ? cl[lane] : 0u;
+      uint32_t xg = xg0, xl = xl0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
-      if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yg = __shfl_up(xg, o, 64), yl = __shfl_up(xl, o, 64);
+        if (lane >= (uint32_t)o) { xg += yg; xl += yl; }
+      }
+      if (lane < IS_TC * 4) {
+        pg[lane] = xg - xg0;
+        pl[lane] = xl - xl0;
+      }
+      if (lane == IS_TC * 4 - 1) {
+        W.cnt[2 * (size_t)t] = xg;
+        W.cnt[2 * (size_t)t + 1] = xl;
+      }
     }
-    if (lane < IS_TC * 4) {
-      pg[lane] = xg - xg0;
-      pl[lane] = xl - xl0;
-    }
-    if (lane == IS_TC * 4 - 1) {
-      W.cnt[2 * (size_t)t] = xg;
-      W.cnt[2 * (size_t)t + 1] = xl;
-    }
-  }
-  __syncthreads();
-  IS_PH(8);  // count: chunk scan
+    __syncthreads();
+    IS_PH(8);  // count: chunk scan
 #pragma unroll
-  for (int c = 0; c < IS_TC; ++c) {
-    const uint32_t p = a + c * IS_TT + threadIdx.x;
-    const bool ok = p < b;
-    const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
-    const uint64_t bg = __ballot(ge), bl = __ballot(le);
-    if (ge) W.gel[a + pg[c * 4 + w] + mbcnt(bg)] = (uint16_t)(p - a);
-    if (le) W.lel[a + pl[c * 4 + w] + mbcnt(bl)] = (uint16_t)(p - a);
+    for (int c = 0; c < IS_TC; ++c) {
+      const uint32_t p = a + c * IS_TT + threadIdx.x;
+      const bool ok = p < b;
+      const bool ge = ok && kk[c] >= P, le = ok && kk[c] <= P;
+      const uint64_t bg = __ballot(ge), bl = __ballot(le);
+      if (ge) W.gel[a + pg[c * 4 + w] + mbcnt(bg)] = (uint16_t)(p - a);
+      if (le) W.lel[a + pl[c * 4 + w] + mbcnt(bl)] = (uint16_t)(p - a);
+    }
+    IS_PH(9);  // count: lists written
+    __syncthreads();  // (this tile's LDS reads before the next tile's writes)
   }
-  IS_PH(9);  // count: lists written
 }
 
 // Dynamic LDS: 4 * segmax u32 (the round's segment table).
@@ -1115,9 +1093,12 @@ k_is_scatter_s(B4<const uint32_t*> Ki2, B4<const uint32_t*> Vi2,
   const int e = blockIdx.y;
   const IsBufs W = W2[e];
   const uint32_t t = blockIdx.x;
+  // (the count kernel wrote the round's tile count; descriptors past it are stale, both
+  // loads in flight together)
+  const uint32_t ntl = W.rounds[r].ntiles;
   const IsTile td = W.tdesc[t];
+  if (t >= ntl) return;
   const uint32_t j = td.j;
-  if (j == IS_NONE) return;
   const IsSeg s = td.s;
   const uint32_t f = s.f, l = s.l, nt = tiles_of(l - f), i = t - s.tile0, m = s.m, P = s.P;
   uint32_t* preg = dyn;
@@ -2572,6 +2553,16 @@ void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4
 // the rounds split segments longer than this (8192 / 6144 / 2048 with 13-17 rounds
 // measured slower)
 uint32_t introsort_tier() { return 4096u; }
+// Workgroups per cloud of the small-cloud count kernel, which takes its tiles in a
+// grid-stride loop (the plan derived once per workgroup): 1024 over the batch, at most a
+// cloud's tile capacity (profiles/r06o).
+#ifndef IS_COUNT_GRID
+#define IS_COUNT_GRID 1024
+#endif
+static uint32_t is_round_grid(uint32_t maxtiles, int nbatch, uint32_t total) {
+  return std::max(1u, std::min(maxtiles, total / (uint32_t)std::max(1, nbatch)));
+}
+
 uint32_t introsort_segmax(uint32_t cap) { return cap / introsort_tier() + 2; }
 uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
 uint32_t introsort_maxtiles_l(uint32_t cap) { return cap / IS_TILE_L + introsort_segmax(cap) + 1; }
@@ -2686,8 +2677,8 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
     } else {
       FCCF_LAUNCH("k_is_count_plan",
                   (pb_round(r, 8.0)),
-                  k_is_count_plan_s, dim3(maxtiles, nbatch), IS_TT, 16 * (size_t)segmax, st, B4<const uint32_t*>(ki),
-                  B4<const uint32_t*>(vi), b, r);
+                  k_is_count_plan_s, dim3(is_round_grid(maxtiles, nbatch, IS_COUNT_GRID), nbatch), IS_TT,
+                  16 * (size_t)segmax, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), b, r);
       step("count", r);
       FCCF_LAUNCH("k_is_scatter", (pb_round(r, 18.0)), k_is_scatter_s, dim3(maxtiles, nbatch), IS_TT,
                   8 * (size_t)maxtiles, st, B4<const uint32_t*>(ki), B4<const uint32_t*>(vi), ko, vo, b, r);
