@@ -2,6 +2,8 @@
 # Dev: SQ / SQC counters of the batched sort in isolation (tools/sort_bench10.py, ten
 # copies of a c3 cloud per launch), one pass per counter set, per library variant.
 # Usage (via gpurun): bash tools/gpu_sortpmc.sh TAG name...   ("base" = lib/)
+# SETS="A B;C D" replaces the SQ/SQC counter sets (one pass per ';'-separated set),
+# e.g. SETS="FETCH_SIZE;WRITE_SIZE" for the memory-side bytes.
 TAG=$1
 shift
 OUT=gpurun_out/$TAG
@@ -11,9 +13,9 @@ for v in "$@"; do
   if [ "$v" = base ]; then L=fccf-pcr_amd/lib/libfccf.so; else L=fccf-pcr_amd/lib_$v/libfccf.so; fi
   i=0
   D=""
-  for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
-           "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_IFETCH SQ_INSTS_VMEM_RD" \
-           "SQC_ICACHE_REQ SQC_ICACHE_MISSES"; do
+  SETS=${SETS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS;SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_IFETCH SQ_INSTS_VMEM_RD;SQC_ICACHE_REQ SQC_ICACHE_MISSES"}
+  IFS=';' read -ra PASSES <<< "$SETS"
+  for P in "${PASSES[@]}"; do
     i=$((i+1))
     FCCF_LIB=$L timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace -f csv -d $OUT/${v}_p$i -o run -- python3 -u tools/sort_bench10.py 3 > $OUT/${v}_p$i.log 2>&1 || { echo "$v pass $i failed"; tail -3 $OUT/${v}_p$i.log; exit 1; }
     D="$D $OUT/${v}_p$i"
