@@ -28,41 +28,39 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // quantum count Q_l[p] (and so to the end parity p + Q_l[p]); lane l ends with
 // the count of units 0..l for each parity at unit 0.  Two int32 per lane per
 // step instead of a whole summary: this is the chain's critical path.
+// Every DPP step reads 0 where its source lane is out of range or its row is masked
+// off (update_dpp's old value): 0 is the identity map (no quanta, parity kept), so no
+// step needs a lane condition.
 // Wrap-around in lanes past the first invalid unit is harmless (never read).
 __device__ __forceinline__ void pmap_scan(uint32_t& q0, uint32_t& q1) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
-  auto step = [&](uint32_t o0, uint32_t o1, bool take) {
+  auto step = [&](uint32_t o0, uint32_t o1) {
     // earlier run o, then this run: Q[p] = o[p] + this[(p + o[p]) & 1]
     const uint32_t m0 = 0u - (o0 & 1u), m1 = 0u - ((o1 + 1u) & 1u);
     const uint32_t n0 = o0 + (q0 ^ ((q0 ^ q1) & m0));
     const uint32_t n1 = o1 + (q0 ^ ((q0 ^ q1) & m1));
-    if (take) { q0 = n0; q1 = n1; }
+    q0 = n0;
+    q1 = n1;
   };
-#define XS_PSTEP(CTRL, ROWS, COND)                                                        \
-  {                                                                                        \
-    const uint32_t o0 = __builtin_amdgcn_update_dpp(q0, q0, CTRL, ROWS, 0xf, false);       \
-    const uint32_t o1 = __builtin_amdgcn_update_dpp(q1, q1, CTRL, ROWS, 0xf, false);       \
-    step(o0, o1, COND);                                                                    \
-  }
-  XS_PSTEP(0x111, 0xf, r >= 1)
-  XS_PSTEP(0x112, 0xf, r >= 2)
-  XS_PSTEP(0x114, 0xf, r >= 4)
-  XS_PSTEP(0x118, 0xf, r >= 8)
-  XS_PSTEP(0x142, 0xa, (lane & 16) != 0)
-  XS_PSTEP(0x143, 0xc, lane >= 32)
+#define XS_PSTEP(CTRL, ROWS)                                                     \
+  step((uint32_t)__builtin_amdgcn_update_dpp(0, (int)q0, CTRL, ROWS, 0xf, false), \
+       (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q1, CTRL, ROWS, 0xf, false));
+  XS_PSTEP(0x111, 0xf)  // row_shr:1
+  XS_PSTEP(0x112, 0xf)  // row_shr:2
+  XS_PSTEP(0x114, 0xf)  // row_shr:4
+  XS_PSTEP(0x118, 0xf)  // row_shr:8
+  XS_PSTEP(0x142, 0xa)  // row_bcast:15 into rows 1, 3
+  XS_PSTEP(0x143, 0xc)  // row_bcast:31 into rows 2, 3
 #undef XS_PSTEP
 }
 
-// parity-free form (no unit of the scan depends on the start parity)
+// parity-free form (no unit of the scan depends on the start parity; 0 is the identity)
 __device__ __forceinline__ uint32_t add_scan(uint32_t q) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
-  uint32_t o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x111, 0xf, 0xf, false); if (r >= 1) q += o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x112, 0xf, 0xf, false); if (r >= 2) q += o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x114, 0xf, 0xf, false); if (r >= 4) q += o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x118, 0xf, 0xf, false); if (r >= 8) q += o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x142, 0xa, 0xf, false); if (lane & 16) q += o;
-  o = __builtin_amdgcn_update_dpp(q, q, 0x143, 0xc, 0xf, false); if (lane >= 32) q += o;
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x111, 0xf, 0xf, false);
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x112, 0xf, 0xf, false);
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x114, 0xf, 0xf, false);
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x118, 0xf, 0xf, false);
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x142, 0xa, 0xf, false);
+  q += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x143, 0xc, 0xf, false);
   return q;
 }
 
@@ -71,20 +69,23 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
-// Inclusive ordered min / max over the wave (lane 63 ends with the total).
+// Inclusive ordered min / max over the wave (lane 63 ends with the total).  Lanes
+// without a source read the operation's identity (INT32_MAX / INT32_MIN), so no step
+// needs a lane condition.
 template <bool MAX>
 __device__ __forceinline__ int32_t mm_scan(int32_t q) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
-  int32_t o;
-#define XS_MM(CTRL, ROWS, COND)                                          \
-  o = __builtin_amdgcn_update_dpp(q, q, CTRL, ROWS, 0xf, false);         \
-  if (COND) q = MAX ? (o > q ? o : q) : (o < q ? o : q);
-  XS_MM(0x111, 0xf, r >= 1)
-  XS_MM(0x112, 0xf, r >= 2)
-  XS_MM(0x114, 0xf, r >= 4)
-  XS_MM(0x118, 0xf, r >= 8)
-  XS_MM(0x142, 0xa, (lane & 16) != 0)
-  XS_MM(0x143, 0xc, lane >= 32)
+  constexpr int32_t I = MAX ? INT32_MIN : INT32_MAX;
+#define XS_MM(CTRL, ROWS)                                                  \
+  {                                                                        \
+    const int32_t o = __builtin_amdgcn_update_dpp(I, q, CTRL, ROWS, 0xf, false); \
+    q = MAX ? max(q, o) : min(q, o);                                       \
+  }
+  XS_MM(0x111, 0xf)
+  XS_MM(0x112, 0xf)
+  XS_MM(0x114, 0xf)
+  XS_MM(0x118, 0xf)
+  XS_MM(0x142, 0xa)
+  XS_MM(0x143, 0xc)
 #undef XS_MM
   return q;
 }
@@ -225,6 +226,53 @@ __global__ void __launch_bounds__(256) k_xs_prefix(XsIn in, int K, double* __res
   }
 }
 
+// The lane's run of (up to) four inputs under inv_u = 2^(23-E): the left fold
+// xs_compose(...xs_compose(xs_identity(), xs_elem(x0)), ...) over the present inputs,
+// computed directly.  Both start parities share each input's y, floor f and fraction;
+// with e = Q + f (the input's envelope point), the input adds f + 1 when its fraction
+// is above 1/2, or exactly 1/2 with p + e odd (the tie goes to the even quantum), and
+// f otherwise.  The bounds are checked after every input, as each xs_compose checks
+// its result, so the accepted summaries and the bad ones are those of the fold.
+template <int S>
+__device__ __forceinline__ XsSum xs_lane4(const float (&v)[4][S], int k, const bool (&ok)[4], double inv_u) {
+  int32_t Q0 = 0, Q1 = 0, lo0 = XS_INF, lo1 = XS_INF, hi0 = -XS_INF, hi1 = -XS_INF;
+  bool good = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x = v[j][k];
+    const double y = (double)x * inv_u;
+    const bool fin = isfinite(x) && fabs(y) < XS_YMAX;
+    const double fl = floor(y);
+    const int32_t f = fin ? (int32_t)fl : 0;
+    const double fr = y - fl;
+    const uint32_t up = fr > 0.5 ? 1u : 0u, tie = fr == 0.5 ? 1u : 0u;
+    // (unsigned arithmetic: a run already out of bounds keeps going without overflow)
+    const int32_t e0 = (int32_t)((uint32_t)Q0 + (uint32_t)f), e1 = (int32_t)((uint32_t)Q1 + (uint32_t)f);
+    const int32_t n0 = (int32_t)((uint32_t)e0 + (up | (tie & (uint32_t)e0 & 1u)));
+    const int32_t n1 = (int32_t)((uint32_t)e1 + (up | (tie & ~(uint32_t)e1 & 1u)));
+    const bool in = ok[j];
+    Q0 = in ? n0 : Q0;
+    Q1 = in ? n1 : Q1;
+    lo0 = in ? min(lo0, e0) : lo0;
+    lo1 = in ? min(lo1, e1) : lo1;
+    hi0 = in ? max(hi0, e0) : hi0;
+    hi1 = in ? max(hi1, e1) : hi1;
+    good = good && (!in || (fin && Q0 > -XS_LIM && Q0 < XS_LIM && Q1 > -XS_LIM && Q1 < XS_LIM &&
+                            lo0 > -XS_LIM && lo1 > -XS_LIM && hi0 < XS_LIM && hi1 < XS_LIM));
+  }
+  if (!good) return xs_bad();
+  XsSum a;
+  a.Q[0] = Q0;
+  a.Q[1] = Q1;
+  a.lo[0] = lo0;
+  a.lo[1] = lo1;
+  a.hi[0] = hi0;
+  a.hi[1] = hi1;
+  a.ok = 1;
+  a.pad = 0;
+  return a;
+}
+
 template <int S>
 __global__ void __launch_bounds__(256) k_xs_chunk(XsIn in, int K, const double* __restrict__ pre,
                                                   XsSum* __restrict__ ctab, int32_t* __restrict__ cE, uint32_t NC) {
@@ -244,11 +292,7 @@ __global__ void __launch_bounds__(256) k_xs_chunk(XsIn in, int K, const double* 
       if (Eb == XS_NOE) continue;
       for (int h = 0; h < XS_NE; ++h) {
         const double inv_u = ldexp(1.0, 23 - (Eb + h));
-        XsSum a = xs_identity();
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (ok[j]) a = xs_compose(a, xs_elem(v[j][k], inv_u));
-        a = wave_total(a);
+        const XsSum a = wave_total(xs_lane4<S>(v, k, ok, inv_u));
         if (lane == 63) ctab[(row * NC + c) * XS_NE + h] = a;
       }
     }
