@@ -59,7 +59,10 @@ constexpr int IS_NSH = 64;                       // round kernels: completion co
 constexpr int IS_DONE_WORDS = (IS_NSH + 1) * 32;  // u32 per launch: shards + top, 128 B apart
 constexpr int IS_TT = 256;           // round kernels: threads per block
 constexpr int IS_TC = IS_TILE / IS_TT;  // 8 elements per thread
-constexpr uint32_t IS_LCAP = 8192;   // largest segment a block kernel workgroup holds in LDS
+#ifndef IS_LCAP_VAL
+#define IS_LCAP_VAL 8192
+#endif
+constexpr uint32_t IS_LCAP = IS_LCAP_VAL;  // largest segment a block kernel workgroup holds in LDS
 #ifndef IS_OT_VAL
 #define IS_OT_VAL 1024
 #endif
@@ -2546,7 +2549,7 @@ void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4
                         hipStream_t st, int nbatch) {
   ProbeBytes pb;  // algorithmic bytes: see introsort_u32 (block_probe_bytes)
   for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0).add(b[e].ctl + 21, 24.0);
-  const int blocks = std::max(1, 2 * IS_OWN_BLOCKS / nbatch);
+  const int blocks = std::max(1, IS_B2_PER_CU * IS_OWN_BLOCKS / nbatch);
   FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
 }
 #else
