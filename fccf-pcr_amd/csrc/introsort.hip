@@ -2570,6 +2570,9 @@ uint32_t introsort_segmax(uint32_t cap) { return cap / introsort_tier() + 2; }
 uint32_t introsort_maxtiles(uint32_t cap) { return cap / IS_TILE + introsort_segmax(cap) + 1; }
 uint32_t introsort_maxtiles_l(uint32_t cap) { return cap / IS_TILE_L + introsort_segmax(cap) + 1; }
 
+#ifndef IS_RPLUS
+#define IS_RPLUS 7
+#endif
 int introsort_rounds(uint32_t cap) {
   int r = 0;
   const uint32_t tier = introsort_tier();
@@ -2577,7 +2580,7 @@ int introsort_rounds(uint32_t cap) {
     // ceil(log2(cap / tier)) balanced levels, plus the deeper tail of unbalanced
     // splits (structured clouds: ~15 rounds at 1M points before all segments are <= 4096)
     while ((uint64_t)tier << r < cap) ++r;
-    r += 7;
+    r += IS_RPLUS;
   }
   return r > IS_RMAX ? IS_RMAX : r;
 }
