@@ -2543,8 +2543,8 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
 }  // namespace
 
 #ifdef IS_KERNEL_VARIANT
-// introsort_b2.hip: this file's kernels again with 512-thread block-kernel workgroups at
-// two per CU; only the block kernel's launch is taken from this form
+// introsort_b2.hip: this file's kernels again with 256-thread block-kernel workgroups over
+// 4,096-element segments, three per CU; only the block kernel's launch is taken from this form
 void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint32_t*> v1, B4<IsBufs> b, int R,
                         hipStream_t st, int nbatch) {
   ProbeBytes pb;  // algorithmic bytes: see introsort_u32 (block_probe_bytes)
@@ -2702,10 +2702,12 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // streams (matching, fine verification); profiles/r03r
   const int own_blocks = std::max(1, IS_OWN_BLOCKS / nbatch);
   // Stage groups of three to five pairs (six to ten clouds per launch): the block
-  // kernel's second form, 512-thread workgroups at two per CU (introsort_b2.hip), whose
-  // items interleave their partition chains on each CU: pipelined 0.650-0.654 against
-  // 0.658-0.665 ms per registration; single registrations (two clouds: few items per
-  // workgroup) keep the 1024-thread form, 0.726 against 0.778 ms (profiles/r05ap).
+  // kernel's second form, 256-thread workgroups at three per CU (introsort_b2.hip), whose
+  // items interleave their partition chains on each CU: pipelined 0.548 against 0.593 ms
+  // per registration (profiles/r06u; the earlier 512-thread form read 0.650-0.654 against
+  // 0.658-0.665 for the 1024-thread form, r05ap).  Single registrations (two clouds: few
+  // items per workgroup) keep the 1024-thread form: main VoxelGrid 0.733 against 0.843 ms
+  // with the second form (r06u).
   // FCCF_IS_BLOCK_B2=0 / 1: never / always (dev, tests)
   const char* b2e = std::getenv("FCCF_IS_BLOCK_B2");
   const bool b2 = b2e ? b2e[0] == '1' : nbatch >= 6;
