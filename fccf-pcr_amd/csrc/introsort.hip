@@ -2300,13 +2300,57 @@ __device__ bool distinct_keys(BlockLds& S, const uint32_t* K, uint32_t* T0, uint
   return r;
 }
 
-// One workgroup per remaining segment: the final children of the last round first
-// (they may exceed IS_LCAP), then the owned list, dequeued from ctl[1].
+// The block kernel's items -- the last round's final children (index i < nfin), then the
+// owned list -- in descending size, as indices into that list (W.ord), so that the
+// workgroups dequeue the longest items first and the launch does not end on a long item
+// started late (longest-first list scheduling).  One workgroup per cloud: 64 size classes
+// of 128 elements, counted and placed with LDS atomics (the order inside a class is free:
+// items are disjoint segments, so the result does not depend on it).
+constexpr int IS_ORD_CLASSES = 64;
+__device__ __forceinline__ uint32_t item_len(const IsBufs& W, int R, uint32_t nsort, uint32_t nfin, uint32_t i) {
+  if (i < nfin) {
+    const Child c = child_of(W, R, nsort, i);
+    return c.l > c.f ? c.l - c.f : 0u;
+  }
+  const IsOwn o = W.own[i - nfin];
+  return o.l > o.f ? o.l - o.f : 0u;
+}
+__global__ void __launch_bounds__(1024) k_is_order(B4<IsBufs> W2, int R) {
+  KT();
+  const IsBufs W = W2[blockIdx.y];
+  const uint32_t nsort = W.ctl[0];
+  if (nsort == 0) return;
+  const uint32_t nfin = nchildren(W, R), n = nfin + (R ? W.rounds[R - 1].nown : 0u);
+  __shared__ uint32_t cnt[IS_ORD_CLASSES];
+  if (threadIdx.x < IS_ORD_CLASSES) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  auto slot = [&](uint32_t i) {  // descending: the longest class first
+    return (uint32_t)IS_ORD_CLASSES - 1u - min(item_len(W, R, nsort, nfin, i) >> 7, (uint32_t)IS_ORD_CLASSES - 1u);
+  };
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[slot(i)], 1u);
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 64 class counts (one wave)
+    const uint32_t v = cnt[threadIdx.x];
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if ((int)threadIdx.x >= o) x += y;
+    }
+    cnt[threadIdx.x] = x - v;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) W.ord[atomicAdd(&cnt[slot(i)], 1u)] = i;
+}
+
+// One workgroup per remaining segment, dequeued from ctl[1]: in W.ord's order (the longest
+// first) when `ordered`, else the final children of the last round (which may exceed
+// IS_LCAP), then the owned list.
 #ifndef IS_BLOCK_WPE
 #define IS_BLOCK_WPE 1
 #endif
 __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_BLOCK_WPE))) k_is_block(B4<uint32_t*> K02, B4<uint32_t*> V02, B4<uint32_t*> K12,
-                                                    B4<uint32_t*> V12, B4<IsBufs> W2, int R) {
+                                                    B4<uint32_t*> V12, B4<IsBufs> W2, int R, int ordered) {
   KT();
   __shared__ BlockLds S;
   __shared__ uint32_t s_idx;
@@ -2338,7 +2382,8 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
     if (threadIdx.x == 0) {
       // look before taking: once the list is drained, leave without another atomic
       const uint32_t seen = __hip_atomic_load(&W.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_idx = seen >= nfin + nown ? seen : atomicAdd(&W.ctl[1], 1u);
+      const uint32_t q = seen >= nfin + nown ? seen : atomicAdd(&W.ctl[1], 1u);
+      s_idx = q < nfin + nown ? (ordered ? W.ord[q] : q) : IS_NONE;
     }
     __syncthreads();
     const uint32_t idx = s_idx;
@@ -2550,7 +2595,7 @@ void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4
   ProbeBytes pb;  // algorithmic bytes: see introsort_u32 (block_probe_bytes)
   for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0).add(b[e].ctl + 21, 24.0);
   const int blocks = std::max(1, IS_B2_PER_CU * IS_OWN_BLOCKS / nbatch);
-  FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+  FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R, 0);
 }
 #else
 // the rounds split segments longer than this (8192 / 6144 / 2048 with 13-17 rounds
@@ -2589,7 +2634,7 @@ size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
   return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + sizeof(IsTile) * mt + 256 + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
-         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 4 * (IS_SHARD_MAX + 1) + 13 * 256;
+         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 4 * (IS_SHARD_MAX + 1) + 4 * (own + 2 * sm + 4) + 14 * 256;
 }
 
 IsBufs introsort_carve(void* base, uint32_t cap) {
@@ -2618,6 +2663,7 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.ptab = (uint4*)take(sizeof(uint4) * (size_t)b.segmax);
   b.pre = (uint32_t*)take(8 * (size_t)b.maxtiles);
   b.letot = (uint32_t*)take(4 * (size_t)b.segmax);
+  b.ord = (uint32_t*)take(4 * ((size_t)b.ownmax + 2 * (size_t)b.segmax + 4));
   b.done = (uint32_t*)take(4 * 2 * (size_t)IS_RMAX * IS_DONE_WORDS);
   b.bounds = (uint32_t*)take(4 * (IS_SHARD_MAX + 1));
   b.shard_n = 1;
@@ -2711,11 +2757,18 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   // FCCF_IS_BLOCK_B2=0 / 1: never / always (dev, tests)
   const char* b2e = std::getenv("FCCF_IS_BLOCK_B2");
   const bool b2 = b2e ? b2e[0] == '1' : nbatch >= 6;
-  if (b2)
+  if (b2) {
     introsort_block_b2(k0, v0, k1, v1, b, R, st, nbatch);
-  else
+  } else {
+    // One 1024-thread workgroup per CU takes 3-4 items per launch: the longest first
+    // (k_is_order), so that none starts late: main VoxelGrid 0.727-0.731 -> 0.703-0.707
+    // ms.  The second form keeps the list order: its launch in a pipelined batch read
+    // 388-405 us ordered against 342-344 us (profiles/r06x).
+    k_is_order<<<dim3(1, nbatch), 1024, 0, st>>>(b, R);
+    step("order", R);
     FCCF_LAUNCH("k_is_block", (pb_block()), k_is_block,
-                dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R);
+                dim3(own_blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R, 1);
+  }
   step("block", R);
   // (other wave grids at ten clouds per launch: no gain, profiles/r05au/ab_wave_grid_width10.txt)
   const int wave_blocks = IS_WAVE_BLOCKS;

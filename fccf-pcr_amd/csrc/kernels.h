@@ -72,6 +72,7 @@ struct IsBufs {
   uint4* ptab;          // the current round's plan: per segment {f, l, depth, first tile} (plan_round)
   uint32_t* pre;        // per round tile: exclusive (>=, <=) prefix within its segment (k_is_count_plan's last workgroup)
   uint32_t* letot;      // per segment of the round: its <= count
+  uint32_t* ord;        // the block kernel's items (final children, then owned) in descending size (k_is_order)
   uint32_t* done;       // per round, count and scatter: sharded completion counters (last-workgroup hand-offs)
   // Row D sharding (group.cpp): from round shard_r0 on, this rank partitions and finishes
   // only the segments starting in its range [bounds[shard_rank], bounds[shard_rank + 1]);
