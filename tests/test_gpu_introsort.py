@@ -74,9 +74,11 @@ def test_sort_keys_equals_std_sort(ctx, fccf, oracle):
 
 @pytest.mark.gpu
 def test_block_kernel_second_form_equals_std_sort(ctx, fccf, oracle, monkeypatch):
-    """The block kernel's second form (introsort_b2.hip: 512-thread workgroups, two per CU;
-    stage groups of three to five pairs use it) forced for every sort (FCCF_IS_BLOCK_B2=1)
-    on every case and a c3 downsample, against the oracle's std::sort."""
+    """The block kernel's second form (introsort_b2.hip: 256-thread workgroups over
+    segments of up to 4,096 elements, three per CU; stage groups of three to five pairs use
+    it) forced for every sort (FCCF_IS_BLOCK_B2=1) on every case and a c3 downsample (whose
+    last round leaves a segment above 4,096 for the global-memory partition), against the
+    oracle's std::sort."""
     monkeypatch.setenv("FCCF_IS_BLOCK_B2", "1")
     bad = [name for name, k in _keys_cases(fccf, oracle).items()
            if not np.array_equal(ctx.sort_keys(k), oracle.sort_pairs(k))]
