@@ -2498,8 +2498,39 @@ __global__ void __launch_bounds__(IS_OT) __attribute__((amdgpu_waves_per_eu(IS_B
   if (threadIdx.x == 0 && xunits) atomicAdd(&W.ctl[21], xunits);
 }
 
+// The wave tasks' slots (the large list from the front, the small list from the end of
+// W.tasks) in descending size (64 classes of 8 elements), for k_is_wave's longest-first
+// dequeue.  One workgroup per cloud; the order inside a class is free (disjoint subtrees).
+__global__ void __launch_bounds__(1024) k_is_torder(B4<IsBufs> W2) {
+  KT();
+  const IsBufs W = W2[blockIdx.y];
+  const uint32_t nbig = W.ctl[16], n = nbig + W.ctl[18];
+  __shared__ uint32_t cnt[64];
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  auto slot_of = [&](uint32_t i) { return i < nbig ? i : W.taskmax - 1u - (i - nbig); };
+  auto cls = [&](uint32_t i) { return 63u - min(W.tasks[slot_of(i)].y >> 3, 63u); };
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[cls(i)], 1u);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const uint32_t v = cnt[threadIdx.x];
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if ((int)threadIdx.x >= o) x += y;
+    }
+    cnt[threadIdx.x] = x - v;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) W.tord[atomicAdd(&cnt[cls(i)], 1u)] = slot_of(i);
+}
+
 // Every wave takes its share of the wave tasks: the subtree in its LDS slice,
 // finished and stably leaf-sorted, written back in place in buffer 0.
+#ifndef IS_WAVE_DYN
+#define IS_WAVE_DYN 1
+#endif
 #ifndef IS_WAVE_LB
 #define IS_WAVE_LB 4  // 4 waves per SIMD: 128 VGPRs, no spill (1.19 vs 1.21 ms pipelined, profiles/r02j)
 #endif
@@ -2518,6 +2549,19 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
   }
   if (blockIdx.x == 0 && e == 0 && threadIdx.x == 0) is_inject(W, IS_FAULT_WAVE);
   wsync();
+#if IS_WAVE_DYN
+  // Longest first (W.tord, k_is_torder): wave g of the grid (which is sized to be
+  // resident at once) takes task g, then the next one from a per-cloud counter when it
+  // has finished one (greedy list scheduling; the static first task keeps the grid's
+  // start free of contention on the counter).
+  const uint32_t nbig = W.ctl[16], ntasks = nbig + W.ctl[18];
+  const float* __restrict__ xsrc = W.xyzs ? W.vgp->src : nullptr;
+  uint32_t* __restrict__ K = K02[e];
+  uint32_t* __restrict__ V = V02[e];
+  const uint32_t nw = gridDim.x * (IS_WT / 64);
+  for (uint32_t idx = blockIdx.x * (IS_WT / 64) + w; idx < ntasks;) {
+    const uint4 tk = W.tasks[W.tord[idx]];
+#else
   // Static assignment, no queue: wave g of the grid takes tasks g, g + NW, g + 2 NW ...
   // of the list, which holds the large tasks first, so the largest ones are spread
   // one per wave (a dynamic dequeue from one counter serialises on that counter:
@@ -2529,6 +2573,7 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
   const uint32_t nw = gridDim.x * (IS_WT / 64);
   for (uint32_t idx = blockIdx.x * (IS_WT / 64) + w; idx < ntasks; idx += nw) {
     const uint4 tk = W.tasks[idx < nbig ? idx : W.taskmax - 1u - (idx - nbig)];
+#endif
     const uint32_t f = __builtin_amdgcn_readfirstlane(tk.x), n = __builtin_amdgcn_readfirstlane(tk.y);
     const int d = (int)__builtin_amdgcn_readfirstlane(tk.z);
 #pragma unroll
@@ -2577,6 +2622,11 @@ __global__ void __launch_bounds__(IS_WT, IS_WAVE_LB) k_is_wave(B4<uint32_t*> K02
         r[3] = blockIdx.x * (IS_WT / 64) + w;
       }
     }
+#if IS_WAVE_DYN
+    uint32_t nxt = 0;
+    if (lane == 0) nxt = nw + atomicAdd(&W.ctl[26], 1u);
+    idx = __builtin_amdgcn_readfirstlane(nxt);
+#endif
   }
   if (S.son && lane == 0) {
     atomicAdd(&W.ctl[6], S.lstat[2]);
@@ -2634,7 +2684,7 @@ size_t introsort_bytes(uint32_t cap) {
   const size_t sm = introsort_segmax(cap), mt = introsort_maxtiles(cap);
   const size_t own = 2 * sm * (IS_RMAX + 1) + 4;
   return 256 + 256 + 16 * ((size_t)cap / 16 + 64) + 12 * mt + sizeof(IsTile) * mt + 256 + 2 * 2 * ((size_t)cap + 64) + sizeof(IsRound) * IS_RMAX +
-         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 4 * (IS_SHARD_MAX + 1) + 4 * (own + 2 * sm + 4) + 14 * 256;
+         (sizeof(IsSeg) + 4) * sm * IS_RMAX + sizeof(IsOwn) * own + 16 * sm + 8 * mt + 4 * sm + 8 * (size_t)IS_RMAX * IS_DONE_WORDS + 4 * (IS_SHARD_MAX + 1) + 4 * (own + 2 * sm + 4) + 4 * ((size_t)cap / 16 + 64) + 15 * 256;
 }
 
 IsBufs introsort_carve(void* base, uint32_t cap) {
@@ -2660,6 +2710,7 @@ IsBufs introsort_carve(void* base, uint32_t cap) {
   b.own = (IsOwn*)take(sizeof(IsOwn) * (size_t)b.ownmax);
   b.taskmax = cap / 16 + 64;
   b.tasks = (uint4*)take(sizeof(uint4) * (size_t)b.taskmax);
+  b.tord = (uint32_t*)take(4 * (size_t)b.taskmax);
   b.ptab = (uint4*)take(sizeof(uint4) * (size_t)b.segmax);
   b.pre = (uint32_t*)take(8 * (size_t)b.maxtiles);
   b.letot = (uint32_t*)take(4 * (size_t)b.segmax);
@@ -2771,7 +2822,14 @@ void introsort_u32(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4<uint
   }
   step("block", R);
   // (other wave grids at ten clouds per launch: no gain, profiles/r05au/ab_wave_grid_width10.txt)
+#if IS_WAVE_DYN
+  // (the tasks longest first; a grid that is resident at once: four workgroups per CU)
+  k_is_torder<<<dim3(1, nbatch), 1024, 0, st>>>(b);
+  step("torder", R);
+  const int wave_blocks = std::max(1, IS_WAVE_RESIDENT / nbatch);
+#else
   const int wave_blocks = IS_WAVE_BLOCKS;
+#endif
   FCCF_LAUNCH("k_is_wave", (pb_wave()), k_is_wave,
               dim3(wave_blocks, nbatch), IS_WT, 0, st, k0, v0, b);
   step("wave", R);

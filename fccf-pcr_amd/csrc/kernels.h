@@ -36,7 +36,8 @@ constexpr int VG_KEY_BLOCKS = 512;
 // K1's sort in libstdc++ std::sort order (introsort.hip): workspace of one cloud.
 constexpr int IS_RMAX = 24;          // most partition rounds before the owner kernel
 constexpr int IS_OWN_BLOCKS = 248;   // block-kernel workgroups of a launch, split over its clouds (one per CU)
-constexpr int IS_WAVE_BLOCKS = 512;  // wave-kernel workgroups per cloud (4 waves each)
+constexpr int IS_WAVE_BLOCKS = 512;  // wave-kernel workgroups per cloud (4 waves each; static task assignment)
+constexpr int IS_WAVE_RESIDENT = 1024;  // wave-kernel workgroups of a launch (dynamic dequeue): 4 per CU
 constexpr int IS_SHARD_MAX = 64;     // most ranks of a sharded sort (row D)
 struct IsRound {
   uint32_t nseg, ntiles, nown, pad;  // large segments, their tiles, owned entries so far
@@ -69,6 +70,7 @@ struct IsBufs {
   uint32_t* cuts;       // IS_RMAX x segmax
   IsOwn* own;           // ownmax
   uint4* tasks;         // wave tasks {f, n, depth, -} (count in ctl[16])
+  uint32_t* tord;       // the wave tasks' slots in descending size (k_is_torder), dequeued by k_is_wave
   uint4* ptab;          // the current round's plan: per segment {f, l, depth, first tile} (plan_round)
   uint32_t* pre;        // per round tile: exclusive (>=, <=) prefix within its segment (k_is_count_plan's last workgroup)
   uint32_t* letot;      // per segment of the round: its <= count
