@@ -2645,7 +2645,11 @@ void introsort_block_b2(B4<uint32_t*> k0, B4<uint32_t*> v0, B4<uint32_t*> k1, B4
   ProbeBytes pb;  // algorithmic bytes: see introsort_u32 (block_probe_bytes)
   for (int e = 0; e < nbatch; ++e) pb.add(b[e].ctl + 20, 16.0).add(b[e].ctl + 21, 24.0);
   const int blocks = std::max(1, IS_B2_PER_CU * IS_OWN_BLOCKS / nbatch);
-  FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R, 0);
+#ifndef IS_B2_ORDERED
+#define IS_B2_ORDERED 0  // (ordered, its launch in a pipelined batch read 388-405 against 342-344 us, r06x)
+#endif
+  if (IS_B2_ORDERED) k_is_order<<<dim3(1, nbatch), 1024, 0, st>>>(b, R);
+  FCCF_LAUNCH("k_is_block", (pb), k_is_block, dim3(blocks, nbatch), IS_OT, 0, st, k0, v0, k1, v1, b, R, IS_B2_ORDERED);
 }
 #else
 // the rounds split segments longer than this (8192 / 6144 / 2048 with 13-17 rounds
