@@ -24,11 +24,13 @@
 //              k_is_count (pivot, per-tile ge/le counts and tile-local position
 //              lists) and k_is_scatter (ranks from the tile prefix, every element
 //              written to its destination in the other buffer, cut by atomicMin);
-//  k_is_block  one workgroup per remaining segment (dequeued): partitions in global
-//              memory while a segment exceeds IS_LCAP, then in LDS down to subtrees
-//              of <= IS_WCAP, which become wave tasks; leaves are finished here;
-//  k_is_wave   every wave of the GPU finishes tasks in its own LDS slice (wave
-//              partitions, register-resident subtrees of <= 64, stable leaf sort).
+//  k_is_block  one workgroup per remaining segment (dequeued; single registrations take
+//              them longest first, k_is_order): partitions in global memory while a
+//              segment exceeds IS_LCAP, then in LDS down to subtrees of <= IS_WCAP,
+//              which become wave tasks; leaves are finished here;
+//  k_is_wave   every wave of a resident grid finishes tasks in its own LDS slice, the
+//              longest first (k_is_torder) from a per-cloud counter (wave partitions,
+//              register-resident subtrees of <= 64, stable leaf sort).
 // HBM per round: 4 B/elem (count) + 4 B lists + 16 B (scatter); the block and wave
 // kernels read and write each element once more each (8 + 8 B).
 #ifndef KT_TU
